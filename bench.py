@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched trace merge on MI355X.
+
+A "step" = one merge pass of the hot path over every document resident on the GPU: the four
+josephg traces (automerge-paper, rustcode, sveltecomponent, seph-blog1), resolved once on the
+host into anchor op logs (untimed, like the reference's load at main.rs:19), materialised as
+`--replicas` independent relabelled HBM copies each (4 x 4096 = 16,384 documents, 4.14 G items
+per GPU by default), merged by the gfx950 kernels to per-document text + digest.
+
+value = patches merged per second, whole job: sum over ranks of (patches per replica set x
+replicas) / max-over-ranks step time; the reference's accounting unit is criterion's
+Throughput::Elements(trace.len()) = patches (/root/reference/src/main.rs:25,58).
+
+Multi-GPU (torchrun, one process per GPU): replicas shard with no data-path collective (weak
+scaling); after timing, the per-document digests are all-gathered over RCCL through the
+engine's C ABI (crdt_hip_allgather_u64) and rank 0 checks every one against the golden digest
+of the trace's endContent.
+
+cpu_baseline: the oracle's sequential RGA merge (oracle/oracle.c orc_merge_many), one document
+per thread over the box's host cores, on a bounded sample of the same documents.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "crdt-benches_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import crdt_hip  # noqa: E402
+
+TRACES = ["automerge-paper", "rustcode", "sveltecomponent", "seph-blog1"]
+METRIC = "merged CRDT ops/sec (whole node) + achieved HBM GB/s, batched trace merge"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# SURVEY.md §8(d) algorithmic-bytes contract: 117 B per op-log item + survivor bytes
+PIPE_B_PER_ITEM = 117.0
+# Per-kernel algorithmic bytes per slot (declared before tuning).
+STAGE_B_PER_ITEM = {"count": 8.0, "scan": 8.0, "place": 12.0, "link": 29.0, "walk1": 16.0,
+                    "walk2": 16.0}
+
+
+def log(msg: str) -> None:
+    print(msg, file=sys.stderr, flush=True)
+
+
+def load_bases():
+    with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
+        golden = json.load(f)
+    bases, patches, items, survivors, digests = [], [], [], [], []
+    for name in TRACES:
+        t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
+        bases.append(t.resolve().arrays())
+        patches.append(len(t))
+        items.append(bases[-1].n)
+        survivors.append(golden[name]["end_bytes"])
+        digests.append(int(golden[name]["tree_digest"], 16))
+    return bases, patches, items, survivors, digests
+
+
+def cpu_baseline(bases, patches, seconds: float, threads: int) -> dict:
+    """Oracle RGA merge (orc_merge_many) over a bounded sample: rounds of `threads` x 4 docs."""
+    from oracle_bind import AnchorLog, Oracle
+
+    oracle = Oracle()
+    logs = []
+    for b in bases:
+        a = AnchorLog(b.n)
+        for f in ("parent", "lamport", "agent", "deleted", "cp"):
+            getattr(a, f)[: b.n] = getattr(b, f)
+        logs.append(a)
+    batch = logs * threads
+    per_round = sum(patches) * threads
+    done, t0 = 0, time.perf_counter()
+    rounds = 0
+    while True:
+        oracle.merge_many(batch, threads)
+        rounds += 1
+        done += per_round
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"{rounds} rounds x {len(batch)} documents ({threads} copies of the 4 "
+                      f"resolved traces), {el:.1f} s, oracle/oracle.c orc_merge_rga, one "
+                      "document per thread"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--replicas", type=int, default=4096, help="replicas of each trace per GPU")
+    ap.add_argument("--relabel", default="rotate", choices=["none", "rotate", "shuffle"])
+    ap.add_argument("--splitter-stride", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_setup = time.perf_counter()
+    bases, patches, items, survivors, golden_dig = load_bases()
+    ctx = crdt_hip.Context(local)
+    if args.splitter_stride:
+        ctx.set_param("splitter_stride", args.splitter_stride)
+    batch = ctx.batch(bases, replicas=args.replicas, relabel=args.relabel,
+                      seed=0x5EED0003 + 7919 * rank)
+    if rank == 0:
+        log(f"[bench] rank0: {batch.docs} docs, {batch.items} items, "
+            f"{batch.device_bytes / 1e9:.1f} GB resident, setup {time.perf_counter() - t_setup:.1f} s")
+
+    for i in range(args.warmup):
+        dig, lens, st = batch.merge()
+        if rank == 0:
+            log(f"[bench] warmup {i}: device {st['total_ns'] / 1e6:.1f} ms")
+    barrier()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        dig, lens, st = batch.merge()  # synchronous: returns after the device finished
+        stats.append(st)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = allmax(elapsed)
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # correctness: every document's digest must equal its trace's endContent digest
+    expect = np.array([golden_dig[d % 4] for d in range(batch.docs)], np.uint64)
+    ok_local = bool(np.array_equal(dig, expect)) and bool(
+        np.array_equal(lens, np.array([survivors[d % 4] for d in range(batch.docs)], np.uint64)))
+    if world > 1:
+        # digest exchange over RCCL/xGMI through the engine's C ABI
+        import torch
+        uid = [crdt_hip.Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
+        all_dig = ctx.allgather_u64(dig, world)
+        ok = bool(np.array_equal(all_dig, np.tile(expect, world)))
+        flag = torch.tensor([1 if (ok and ok_local) else 0], device=f"cuda:{local}")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        digests_ok = bool(flag.item())
+    else:
+        digests_ok = ok_local
+
+    patches_per_gpu = sum(patches) * args.replicas
+    items_per_gpu = batch.items
+    value = patches_per_gpu * world / (elapsed / args.steps)
+
+    # per-stage device times (HIP events on the engine stream), mean over timed steps
+    stage_ns = {k: float(np.mean([s["stage_ns"][k] for s in stats])) for k in stats[0]["stage_ns"]}
+    launches = stats[0]["stage_launches"]
+    dev_ns = float(np.mean([s["total_ns"] for s in stats]))
+    kern_ns = sum(stage_ns.values())
+    dom = max((k for k in STAGE_B_PER_ITEM), key=lambda k: stage_ns[k])
+    slots = items_per_gpu + batch.docs  # items + one document-start node per document
+    dom_launch_ns = stage_ns[dom] / max(1, launches[dom])
+    dom_bytes_per_launch = STAGE_B_PER_ITEM[dom] * slots / max(1, launches[dom])
+    achieved = dom_bytes_per_launch / dom_launch_ns  # bytes/ns == GB/s
+    surv_per_item = sum(survivors) / sum(items)
+    pipe_bytes = (PIPE_B_PER_ITEM + surv_per_item) * items_per_gpu
+    pipe_gbps = pipe_bytes / kern_ns
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "patches/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic replicas of the 4 real josephg traces (resolved on host, "
+                    f"relabel={args.relabel}, resident in HBM)",
+            "config": {
+                "workload": "config 3: 4 traces x %d replicas per GPU" % args.replicas,
+                "docs_per_gpu": batch.docs,
+                "items_per_gpu": items_per_gpu,
+                "patches_per_gpu": patches_per_gpu,
+                "relabel": args.relabel,
+                "waves": stats[0]["waves"],
+                "parallelism": f"replicas x{world} (no data-path collective)",
+            },
+            "items_per_s": items_per_gpu * world / (elapsed / args.steps),
+            "hbm_gbps_alg_pipeline": pipe_gbps,
+            "device_ms_per_step": dev_ns / 1e6,
+            "kernel_ms_per_step": {k: v / 1e6 for k, v in stage_ns.items()},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": None,
+                "alg_bytes_per_launch": dom_bytes_per_launch,
+                "launch_us": dom_launch_ns / 1e3,
+            },
+            "roofline_pipeline": {
+                "bound": "hbm", "achieved": pipe_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": pipe_gbps / HBM_PEAK_GBPS,
+                "alg_bytes_per_item": PIPE_B_PER_ITEM + surv_per_item,
+            },
+            "digests_ok": digests_ok,
+        }
+        if not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(bases, patches, args.cpu_seconds, threads)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0 if digests_ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,523 @@
+"""Python ctypes binding of libcrdt_hip.so (include/crdt_hip.h).
+
+Host plumbing for the tests and bench.py.  The merge itself always runs in the HIP kernels of
+libcrdt_hip.so; there is no Python or CPU fallback: if the library is missing, or no device is
+present, calls raise.
+
+Mirrors the reference's per-CRDT interface (/root/reference/src/rope.rs:6-33 `Upstream`,
+:185-191 `Downstream`) through `HipMerge`, so tests read like the reference's bench loop
+(/root/reference/src/main.rs:28-36, :63-69).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libcrdt_hip.so")
+
+OK = 0
+ERRORS = {
+    -1: "EINVAL", -2: "ERANGE", -3: "ENOMEM", -4: "EDEVICE", -5: "EBADLOG", -6: "ESPACE",
+    -7: "EIO", -8: "ECOMM",
+}
+STAGES = ["count", "scan", "place", "link", "walk1", "rank", "walk2", "digest"]
+
+# Every symbol include/crdt_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "crdt_hip_abi_version", "crdt_hip_device_count", "crdt_hip_init", "crdt_hip_destroy",
+    "crdt_hip_last_error", "crdt_hip_set_param", "crdt_hip_oplog_new", "crdt_hip_oplog_clone",
+    "crdt_hip_oplog_free", "crdt_hip_oplog_insert", "crdt_hip_oplog_remove",
+    "crdt_hip_oplog_replace", "crdt_hip_oplog_visible_len", "crdt_hip_oplog_get_view",
+    "crdt_hip_oplog_version", "crdt_hip_oplog_encode_from", "crdt_hip_oplog_apply_update",
+    "crdt_hip_trace_load", "crdt_hip_trace_free", "crdt_hip_trace_len", "crdt_hip_trace_txns",
+    "crdt_hip_trace_patch", "crdt_hip_trace_start_content", "crdt_hip_trace_end_content",
+    "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_synth_agents",
+    "crdt_hip_synth_tree", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
+    "crdt_hip_batch_create", "crdt_hip_batch_free", "crdt_hip_batch_info",
+    "crdt_hip_batch_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
+    "crdt_hip_allgather_u64", "crdt_hip_comm_destroy", "crdt_hip_xxh64",
+    "crdt_hip_tree_digest",
+]
+
+
+class CrdtHipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class View(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32),
+        ("parent", C.POINTER(C.c_uint32)),
+        ("origin_right", C.POINTER(C.c_uint32)),
+        ("lamport", C.POINTER(C.c_uint32)),
+        ("agent", C.POINTER(C.c_uint16)),
+        ("deleted", C.POINTER(C.c_uint8)),
+        ("cp", C.POINTER(C.c_uint32)),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("items", C.c_uint64),
+        ("docs", C.c_uint64),
+        ("text_bytes", C.c_uint64),
+        ("waves", C.c_uint32),
+        ("nstages", C.c_uint32),
+        ("stage_ns", C.c_uint64 * 16),
+        ("stage_launches", C.c_uint32 * 16),
+        ("total_ns", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {
+            "items": self.items, "docs": self.docs, "text_bytes": self.text_bytes,
+            "waves": self.waves, "total_ns": self.total_ns,
+            "stage_ns": {STAGES[i]: int(self.stage_ns[i]) for i in range(self.nstages)},
+            "stage_launches": {STAGES[i]: int(self.stage_launches[i]) for i in range(self.nstages)},
+        }
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load libcrdt_hip.so from the package directory (fails loudly if it is not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is not built: run `make -C {PKG_DIR}` "
+                           "(or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, sz, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
+    P = C.POINTER
+    sig = {
+        "crdt_hip_abi_version": (i32, []),
+        "crdt_hip_device_count": (i32, [P(i32)]),
+        "crdt_hip_init": (i32, [i32, P(vp)]),
+        "crdt_hip_destroy": (i32, [vp]),
+        "crdt_hip_last_error": (C.c_char_p, [vp]),
+        "crdt_hip_set_param": (i32, [vp, C.c_char_p, u64]),
+        "crdt_hip_oplog_new": (i32, [P(vp)]),
+        "crdt_hip_oplog_clone": (i32, [vp, P(vp)]),
+        "crdt_hip_oplog_free": (None, [vp]),
+        "crdt_hip_oplog_insert": (i32, [vp, sz, C.c_char_p, sz]),
+        "crdt_hip_oplog_remove": (i32, [vp, sz, sz]),
+        "crdt_hip_oplog_replace": (i32, [vp, sz, sz, C.c_char_p, sz]),
+        "crdt_hip_oplog_visible_len": (sz, [vp]),
+        "crdt_hip_oplog_get_view": (i32, [vp, P(View)]),
+        "crdt_hip_oplog_version": (u64, [vp]),
+        "crdt_hip_oplog_encode_from": (i32, [vp, u64, vp, sz, P(sz)]),
+        "crdt_hip_oplog_apply_update": (i32, [vp, vp, sz]),
+        "crdt_hip_trace_load": (i32, [C.c_char_p, P(vp)]),
+        "crdt_hip_trace_free": (None, [vp]),
+        "crdt_hip_trace_len": (sz, [vp]),
+        "crdt_hip_trace_txns": (sz, [vp]),
+        "crdt_hip_trace_patch": (i32, [vp, sz, P(sz), P(sz), P(C.c_char_p), P(sz)]),
+        "crdt_hip_trace_start_content": (i32, [vp, P(vp), P(sz)]),
+        "crdt_hip_trace_end_content": (i32, [vp, P(vp), P(sz)]),
+        "crdt_hip_trace_chars_to_bytes": (i32, [vp]),
+        "crdt_hip_trace_resolve": (i32, [vp, P(vp)]),
+        "crdt_hip_synth_agents": (i32, [u32, u32, u64, P(vp)]),
+        "crdt_hip_synth_tree": (i32, [u32, u32, u32, u64, P(vp)]),
+        "crdt_hip_merge": (i32, [vp, P(View), vp, sz, P(sz), P(u64)]),
+        "crdt_hip_merge_batch": (i32, [vp, P(View), u32, vp, vp, P(Stats)]),
+        "crdt_hip_merge_order": (i32, [vp, P(View), vp]),
+        "crdt_hip_batch_create": (i32, [vp, P(View), u32, u32, u32, u64, P(vp)]),
+        "crdt_hip_batch_free": (i32, [vp]),
+        "crdt_hip_batch_info": (i32, [vp, P(u64), P(u64), P(u64)]),
+        "crdt_hip_batch_merge": (i32, [vp, vp, vp, vp, P(Stats)]),
+        "crdt_hip_comm_unique_id": (i32, [vp]),
+        "crdt_hip_comm_init": (i32, [vp, i32, i32, vp]),
+        "crdt_hip_allgather_u64": (i32, [vp, vp, sz, vp]),
+        "crdt_hip_comm_destroy": (i32, [vp]),
+        "crdt_hip_xxh64": (u64, [vp, sz, u64]),
+        "crdt_hip_tree_digest": (u64, [vp, sz]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def _check(rc: int, ctx=None) -> None:
+    if rc != OK:
+        msg = lib().crdt_hip_last_error(ctx)
+        raise CrdtHipError(rc, msg.decode("utf-8", "replace") if msg else "")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().crdt_hip_device_count(C.byref(n))
+    return int(n.value) if rc == OK else 0
+
+
+def xxh64(data: bytes, seed: int = 0) -> int:
+    return int(lib().crdt_hip_xxh64(data, len(data), seed))
+
+
+def tree_digest(data: bytes) -> int:
+    return int(lib().crdt_hip_tree_digest(data, len(data)))
+
+
+# ------------------------------------------------------------------------------------------------
+class LogArrays:
+    """Anchor op log as numpy SoA (ids 1..n).  Keeps the arrays alive for a View."""
+
+    FIELDS = ("parent", "origin_right", "lamport", "agent", "deleted", "cp")
+
+    def __init__(self, parent, lamport, agent, deleted, cp, origin_right=None):
+        self.parent = np.ascontiguousarray(parent, dtype=np.uint32)
+        n = self.parent.size
+        self.lamport = np.ascontiguousarray(lamport, dtype=np.uint32)
+        self.agent = np.ascontiguousarray(agent, dtype=np.uint16)
+        self.deleted = np.ascontiguousarray(deleted, dtype=np.uint8)
+        self.cp = np.ascontiguousarray(cp, dtype=np.uint32)
+        self.origin_right = (np.full(n, 0xFFFFFFFF, np.uint32) if origin_right is None
+                             else np.ascontiguousarray(origin_right, dtype=np.uint32))
+        for f in self.FIELDS:
+            assert getattr(self, f).size == n, f
+
+    @property
+    def n(self) -> int:
+        return int(self.parent.size)
+
+    def view(self) -> View:
+        def p(a, t):
+            return a.ctypes.data_as(C.POINTER(t)) if a.size else None
+        return View(self.n, p(self.parent, C.c_uint32), p(self.origin_right, C.c_uint32),
+                    p(self.lamport, C.c_uint32), p(self.agent, C.c_uint16),
+                    p(self.deleted, C.c_uint8), p(self.cp, C.c_uint32))
+
+    def copy(self) -> "LogArrays":
+        return LogArrays(self.parent.copy(), self.lamport.copy(), self.agent.copy(),
+                         self.deleted.copy(), self.cp.copy(), self.origin_right.copy())
+
+
+class OpLog:
+    """Host-side resolver (positional patches -> anchor op log), crdt_hip_oplog_*."""
+
+    def __init__(self, handle=None):
+        if handle is None:
+            h = C.c_void_p()
+            _check(lib().crdt_hip_oplog_new(C.byref(h)))
+            handle = h
+        self._h = handle
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_oplog_free(self._h)
+            self._h = None
+
+    def clone(self) -> "OpLog":
+        h = C.c_void_p()
+        _check(lib().crdt_hip_oplog_clone(self._h, C.byref(h)))
+        return OpLog(h)
+
+    def insert(self, pos: int, text: str) -> None:
+        b = text.encode("utf-8")
+        _check(lib().crdt_hip_oplog_insert(self._h, pos, b, len(b)))
+
+    def remove(self, start: int, end: int) -> None:
+        _check(lib().crdt_hip_oplog_remove(self._h, start, end))
+
+    def replace(self, start: int, end: int, text: str) -> None:
+        b = text.encode("utf-8")
+        _check(lib().crdt_hip_oplog_replace(self._h, start, end, b, len(b)))
+
+    def visible_len(self) -> int:
+        return int(lib().crdt_hip_oplog_visible_len(self._h))
+
+    def view(self) -> View:
+        v = View()
+        _check(lib().crdt_hip_oplog_get_view(self._h, C.byref(v)))
+        return v
+
+    def arrays(self) -> LogArrays:
+        v = self.view()
+        n = v.n
+
+        def arr(ptr, dt):
+            if n == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
+        return LogArrays(arr(v.parent, np.uint32), arr(v.lamport, np.uint32),
+                         arr(v.agent, np.uint16), arr(v.deleted, np.uint8),
+                         arr(v.cp, np.uint32), arr(v.origin_right, np.uint32))
+
+    def version(self) -> int:
+        return int(lib().crdt_hip_oplog_version(self._h))
+
+    def encode_from(self, version: int) -> bytes:
+        need = C.c_size_t(0)
+        rc = lib().crdt_hip_oplog_encode_from(self._h, version, None, 0, C.byref(need))
+        if rc not in (OK, -6):
+            _check(rc)
+        buf = C.create_string_buffer(max(need.value, 1))
+        _check(lib().crdt_hip_oplog_encode_from(self._h, version, buf, need.value,
+                                                C.byref(need)))
+        return buf.raw[: need.value]
+
+    def apply_update(self, update: bytes) -> None:
+        _check(lib().crdt_hip_oplog_apply_update(self._h, update, len(update)))
+
+    @staticmethod
+    def synth_agents(n_items: int, agents: int, seed: int) -> "OpLog":
+        h = C.c_void_p()
+        _check(lib().crdt_hip_synth_agents(n_items, agents, seed, C.byref(h)))
+        return OpLog(h)
+
+    @staticmethod
+    def synth_tree(n_items: int, p_chain_pct: int, del_pct: int, seed: int) -> "OpLog":
+        h = C.c_void_p()
+        _check(lib().crdt_hip_synth_tree(n_items, p_chain_pct, del_pct, seed, C.byref(h)))
+        return OpLog(h)
+
+
+class Trace:
+    """josephg trace loaded by the native loader (crdt_hip_trace_*)."""
+
+    def __init__(self, path: str):
+        h = C.c_void_p()
+        _check(lib().crdt_hip_trace_load(path.encode(), C.byref(h)))
+        self._h = h
+        self.path = path
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_trace_free(self._h)
+            self._h = None
+
+    def __len__(self) -> int:
+        return int(lib().crdt_hip_trace_len(self._h))
+
+    @property
+    def txns(self) -> int:
+        return int(lib().crdt_hip_trace_txns(self._h))
+
+    def patch(self, i: int):
+        pos, dele, n = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        ins = C.c_char_p()
+        _check(lib().crdt_hip_trace_patch(self._h, i, C.byref(pos), C.byref(dele),
+                                          C.byref(ins), C.byref(n)))
+        return int(pos.value), int(dele.value), C.string_at(ins, n.value).decode("utf-8")
+
+    def _content(self, fn) -> str:
+        p, n = C.c_void_p(), C.c_size_t()
+        _check(fn(self._h, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value).decode("utf-8") if n.value else ""
+
+    @property
+    def start_content(self) -> str:
+        return self._content(lib().crdt_hip_trace_start_content)
+
+    @property
+    def end_content(self) -> str:
+        return self._content(lib().crdt_hip_trace_end_content)
+
+    def chars_to_bytes(self) -> None:
+        _check(lib().crdt_hip_trace_chars_to_bytes(self._h))
+
+    def resolve(self) -> OpLog:
+        h = C.c_void_p()
+        _check(lib().crdt_hip_trace_resolve(self._h, C.byref(h)))
+        return OpLog(h)
+
+
+def _as_view(log) -> tuple:
+    """(View, keepalive) for an OpLog or LogArrays."""
+    if isinstance(log, OpLog):
+        return log.view(), log
+    if isinstance(log, LogArrays):
+        return log.view(), log
+    raise TypeError(type(log))
+
+
+class Context:
+    """One HIP device + its merge engine (crdt_hip_init)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(lib().crdt_hip_init(device, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def set_param(self, key: str, value: int) -> None:
+        _check(lib().crdt_hip_set_param(self._h, key.encode(), value), self._h)
+
+    def merge(self, log) -> tuple:
+        """Merged document: (utf8 bytes, tree digest)."""
+        v, keep = _as_view(log)
+        cap = 4 * v.n + 16
+        buf = C.create_string_buffer(cap)
+        n, dig = C.c_size_t(), C.c_uint64()
+        _check(lib().crdt_hip_merge(self._h, C.byref(v), buf, cap, C.byref(n), C.byref(dig)),
+               self._h)
+        del keep
+        return buf.raw[: n.value], int(dig.value)
+
+    def merge_digest(self, log) -> tuple:
+        v, keep = _as_view(log)
+        n, dig = C.c_size_t(), C.c_uint64()
+        _check(lib().crdt_hip_merge(self._h, C.byref(v), None, 0, C.byref(n), C.byref(dig)),
+               self._h)
+        return int(n.value), int(dig.value)
+
+    def merge_batch(self, logs: list, stats: bool = False):
+        views = []
+        keep = []
+        for lg in logs:
+            v, k = _as_view(lg)
+            views.append(v)
+            keep.append(k)
+        arr = (View * len(views))(*views)
+        dig = np.zeros(len(views), np.uint64)
+        lens = np.zeros(len(views), np.uint64)
+        st = Stats()
+        _check(lib().crdt_hip_merge_batch(self._h, arr, len(views), dig.ctypes.data,
+                                          lens.ctypes.data, C.byref(st)), self._h)
+        return (dig, lens, st.as_dict()) if stats else (dig, lens)
+
+    def merge_order(self, log) -> np.ndarray:
+        v, keep = _as_view(log)
+        out = np.zeros(max(v.n, 1), np.uint32)
+        _check(lib().crdt_hip_merge_order(self._h, C.byref(v), out.ctypes.data), self._h)
+        return out[: v.n]
+
+    def batch(self, bases: list, replicas: int, relabel: int = 0, seed: int = 0) -> "Batch":
+        return Batch(self, bases, replicas, relabel, seed)
+
+    # RCCL
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        _check(lib().crdt_hip_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        _check(lib().crdt_hip_comm_init(self._h, nranks, rank, uid), self._h)
+
+    def allgather_u64(self, values: np.ndarray, nranks: int) -> np.ndarray:
+        v = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.zeros(v.size * nranks, np.uint64)
+        _check(lib().crdt_hip_allgather_u64(self._h, v.ctypes.data, v.size, out.ctypes.data),
+               self._h)
+        return out
+
+
+class Batch:
+    """Device-resident replica batch (crdt_hip_batch_*)."""
+
+    RELABEL = {"none": 0, "rotate": 1, "shuffle": 2}
+
+    def __init__(self, ctx: Context, bases: list, replicas: int, relabel=0, seed: int = 0):
+        if isinstance(relabel, str):
+            relabel = self.RELABEL[relabel]
+        views = []
+        keep = []
+        for b in bases:
+            v, k = _as_view(b)
+            views.append(v)
+            keep.append(k)
+        arr = (View * len(views))(*views)
+        h = C.c_void_p()
+        _check(lib().crdt_hip_batch_create(ctx._h, arr, len(views), replicas, relabel, seed,
+                                           C.byref(h)), ctx._h)
+        self._h = h
+        self.ctx = ctx
+        docs, items, dev = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().crdt_hip_batch_info(h, C.byref(docs), C.byref(items), C.byref(dev)))
+        self.docs, self.items, self.device_bytes = int(docs.value), int(items.value), int(dev.value)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_batch_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def merge(self):
+        dig = np.zeros(self.docs, np.uint64)
+        lens = np.zeros(self.docs, np.uint64)
+        st = Stats()
+        _check(lib().crdt_hip_batch_merge(self.ctx._h, self._h, dig.ctypes.data,
+                                          lens.ctypes.data, C.byref(st)), self.ctx._h)
+        return dig, lens, st.as_dict()
+
+
+class HipMerge:
+    """Mirror of the reference's per-CRDT adapter for the GPU engine.
+
+    `Upstream` (/root/reference/src/rope.rs:6-33): NAME, EDITS_USE_BYTE_OFFSETS, from_str,
+    insert, remove, replace, len.  `Downstream` (:185-191): upstream_updates, apply_update.
+    len() is where the merge happens (as Dt::len -> checkout_tip, rope.rs:133-136): it calls
+    crdt_hip_merge on the shared device context.
+    """
+
+    NAME = "mi355x"
+    EDITS_USE_BYTE_OFFSETS = False
+    _ctx: Context | None = None
+
+    def __init__(self, log: OpLog):
+        self.log = log
+
+    @classmethod
+    def context(cls) -> Context:
+        if cls._ctx is None:
+            cls._ctx = Context(0)
+        return cls._ctx
+
+    @classmethod
+    def from_str(cls, s: str) -> "HipMerge":
+        log = OpLog()
+        if s:
+            log.insert(0, s)
+        return cls(log)
+
+    def insert(self, at: int, text: str) -> None:
+        self.log.insert(at, text)
+
+    def remove(self, start: int, end: int) -> None:
+        self.log.remove(start, end)
+
+    def replace(self, start: int, end: int, text: str) -> None:
+        self.log.replace(start, end, text)
+
+    def clone(self) -> "HipMerge":
+        return HipMerge(self.log.clone())
+
+    def text(self) -> str:
+        data, _ = self.context().merge(self.log)
+        return data.decode("utf-8")
+
+    def len(self) -> int:
+        data, _ = self.context().merge(self.log)
+        return len(data.decode("utf-8"))  # codepoints (EDITS_USE_BYTE_OFFSETS = false)
+
+    # Downstream
+    @classmethod
+    def upstream_updates(cls, start_content: str, patches) -> tuple:
+        up = cls.from_str(start_content)
+        updates = []
+        for pos, dele, ins in patches:
+            v = up.log.version()
+            up.replace(pos, pos + dele, ins)
+            updates.append(up.log.encode_from(v))
+        return cls.from_str(start_content), updates
+
+    def apply_update(self, update: bytes) -> None:
+        self.log.apply_update(update)

@@ -1,0 +1,478 @@
+// capi.cpp — the extern "C" boundary declared in include/crdt_hip.h.  Nothing throws across it:
+// every entry point catches, records the message and returns a CRDT_HIP_E* code.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <exception>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "crdt_hip.h"
+#include "engine.hpp"
+#include "oplog.hpp"
+#include "synth.hpp"
+#include "trace.hpp"
+#include "util.hpp"
+
+struct crdt_hip_ctx {
+    crdt::Engine eng;
+    std::string last_err;
+    crdt::DeviceLogs staging;
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0;
+};
+struct crdt_hip_oplog {
+    crdt::OpLog log;
+};
+struct crdt_hip_trace {
+    crdt::Trace t;
+};
+struct crdt_hip_batch {
+    crdt_hip_ctx* ctx = nullptr;
+    crdt::DeviceLogs logs;
+    uint64_t device_bytes = 0;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int set_err(crdt_hip_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->last_err = msg;
+    else g_err = msg;
+    return code;
+}
+int from_engine(crdt_hip_ctx* ctx, int rc) {
+    if (rc) ctx->last_err = ctx->eng.err;
+    return rc;
+}
+
+template <class F>
+int guard(crdt_hip_ctx* ctx, F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return set_err(ctx, CRDT_HIP_ENOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return set_err(ctx, CRDT_HIP_EINVAL, e.what());
+    } catch (...) {
+        return set_err(ctx, CRDT_HIP_EINVAL, "unknown exception");
+    }
+}
+
+uint64_t visible_bytes(const crdt_hip_oplog_view& v) {
+    uint64_t b = 0;
+    for (uint32_t i = 0; i < v.n; ++i)
+        if (!v.deleted[i]) b += crdt::utf8_len_cp(v.cp[i] & 0x1FFFFFu);
+    return b;
+}
+
+int check_view(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* v) {
+    if (!v) return set_err(ctx, CRDT_HIP_EINVAL, "null op log view");
+    if (v->n && (!v->parent || !v->lamport || !v->agent || !v->deleted || !v->cp))
+        return set_err(ctx, CRDT_HIP_EINVAL, "op log view has null arrays");
+    if (v->n > 0x7FFFFF00u) return set_err(ctx, CRDT_HIP_ERANGE, "op log too large");
+    return 0;
+}
+
+int stage_views(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* logs, uint32_t n) {
+    std::vector<crdt::DocInfo> docs(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        int rc = check_view(ctx, &logs[i]);
+        if (rc) return rc;
+        docs[i] = crdt::DocInfo{logs[i].n, visible_bytes(logs[i])};
+    }
+    int rc = ctx->eng.plan(ctx->staging, docs);
+    if (rc) return from_engine(ctx, rc);
+    return from_engine(ctx, ctx->eng.upload(ctx->staging, logs, n));
+}
+}  // namespace
+
+extern "C" {
+
+int crdt_hip_abi_version(void) { return CRDT_HIP_ABI_VERSION; }
+
+int crdt_hip_device_count(int* out) {
+    if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *out = e == hipSuccess ? n : 0;
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(nullptr, CRDT_HIP_EDEVICE, hipGetErrorString(e));
+    }
+    return 0;
+}
+
+int crdt_hip_init(int device, crdt_hip_ctx** out) {
+    if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
+    *out = nullptr;
+    return guard(nullptr, [&] {
+        crdt_hip_ctx* c = new crdt_hip_ctx();
+        std::string e = c->eng.init(device);
+        if (!e.empty()) {
+            delete c;
+            return set_err(nullptr, CRDT_HIP_EDEVICE, e);
+        }
+        *out = c;
+        return 0;
+    });
+}
+
+int crdt_hip_destroy(crdt_hip_ctx* ctx) {
+    if (!ctx) return 0;
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    delete ctx;
+    return 0;
+}
+
+const char* crdt_hip_last_error(const crdt_hip_ctx* ctx) {
+    return ctx ? ctx->last_err.c_str() : g_err.c_str();
+}
+
+int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
+    if (!ctx || !key) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    std::string k = key;
+    if (k == "splitter_stride") {
+        if (value < 16 || value > 4096 || (value & (value - 1)))
+            return set_err(ctx, CRDT_HIP_EINVAL, "splitter_stride must be a power of two in [16, 4096]");
+        uint32_t l = 0;
+        while ((1ull << l) < value) ++l;
+        ctx->eng.log2m = l;
+        return 0;
+    }
+    if (k == "max_wave_slots") {
+        if (value < 4096 || value > (1ull << 31))
+            return set_err(ctx, CRDT_HIP_EINVAL, "max_wave_slots out of range");
+        ctx->eng.max_wave_slots = value;
+        return 0;
+    }
+    return set_err(ctx, CRDT_HIP_EINVAL, "unknown parameter " + k);
+}
+
+// ---- op log ----------------------------------------------------------------------------------
+int crdt_hip_oplog_new(crdt_hip_oplog** out) {
+    if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
+    return guard(nullptr, [&] { *out = new crdt_hip_oplog(); return 0; });
+}
+int crdt_hip_oplog_clone(const crdt_hip_oplog* src, crdt_hip_oplog** out) {
+    if (!src || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] { *out = new crdt_hip_oplog(*src); return 0; });
+}
+void crdt_hip_oplog_free(crdt_hip_oplog* log) { delete log; }
+
+int crdt_hip_oplog_insert(crdt_hip_oplog* log, size_t pos, const char* utf8, size_t nbytes) {
+    if (!log || (!utf8 && nbytes)) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::string e = log->log.insert_utf8(pos, utf8, nbytes);
+        return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_ERANGE, e);
+    });
+}
+int crdt_hip_oplog_remove(crdt_hip_oplog* log, size_t start, size_t end) {
+    if (!log) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::string e = log->log.remove(start, end);
+        return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_ERANGE, e);
+    });
+}
+int crdt_hip_oplog_replace(crdt_hip_oplog* log, size_t start, size_t end, const char* utf8,
+                           size_t nbytes) {
+    if (end > start) {
+        int rc = crdt_hip_oplog_remove(log, start, end);
+        if (rc) return rc;
+    }
+    if (nbytes) return crdt_hip_oplog_insert(log, start, utf8, nbytes);
+    return 0;
+}
+size_t crdt_hip_oplog_visible_len(const crdt_hip_oplog* log) { return log ? log->log.visible() : 0; }
+
+int crdt_hip_oplog_get_view(const crdt_hip_oplog* log, crdt_hip_oplog_view* out) {
+    if (!log || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    const crdt::OpLog& L = log->log;
+    out->n = L.size();
+    out->parent = L.parent.data();
+    out->origin_right = L.oright.data();
+    out->lamport = L.lamport.data();
+    out->agent = L.agent.data();
+    out->deleted = L.deleted.data();
+    out->cp = L.cp.data();
+    return 0;
+}
+uint64_t crdt_hip_oplog_version(const crdt_hip_oplog* log) { return log ? log->log.version() : 0; }
+
+int crdt_hip_oplog_encode_from(const crdt_hip_oplog* log, uint64_t version, uint8_t* buf,
+                               size_t cap, size_t* out_len) {
+    if (!log || !out_len) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::vector<uint8_t> u = log->log.encode_from(version);
+        *out_len = u.size();
+        if (!buf || cap < u.size()) return set_err(nullptr, CRDT_HIP_ESPACE, "buffer too small");
+        std::memcpy(buf, u.data(), u.size());
+        return 0;
+    });
+}
+int crdt_hip_oplog_apply_update(crdt_hip_oplog* log, const uint8_t* buf, size_t len) {
+    if (!log || (!buf && len)) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::string e = log->log.apply_update(buf, len);
+        return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EINVAL, e);
+    });
+}
+
+// ---- traces ----------------------------------------------------------------------------------
+int crdt_hip_trace_load(const char* path, crdt_hip_trace** out) {
+    if (!path || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    *out = nullptr;
+    return guard(nullptr, [&] {
+        crdt_hip_trace* t = new crdt_hip_trace();
+        std::string e = crdt::load_trace(path, t->t);
+        if (!e.empty()) {
+            delete t;
+            return set_err(nullptr, CRDT_HIP_EIO, e);
+        }
+        *out = t;
+        return 0;
+    });
+}
+void crdt_hip_trace_free(crdt_hip_trace* t) { delete t; }
+size_t crdt_hip_trace_len(const crdt_hip_trace* t) { return t ? t->t.len() : 0; }
+size_t crdt_hip_trace_txns(const crdt_hip_trace* t) { return t ? t->t.txn_end.size() : 0; }
+
+int crdt_hip_trace_patch(const crdt_hip_trace* t, size_t i, size_t* pos, size_t* del,
+                         const char** ins, size_t* ins_len) {
+    if (!t || i >= t->t.patches.size()) return set_err(nullptr, CRDT_HIP_ERANGE, "patch index");
+    const crdt::Patch& p = t->t.patches[i];
+    if (pos) *pos = p.pos;
+    if (del) *del = p.del;
+    if (ins) *ins = t->t.ins.data() + p.ins_off;
+    if (ins_len) *ins_len = p.ins_len;
+    return 0;
+}
+int crdt_hip_trace_start_content(const crdt_hip_trace* t, const char** s, size_t* len) {
+    if (!t || !s || !len) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    *s = t->t.start_content.data();
+    *len = t->t.start_content.size();
+    return 0;
+}
+int crdt_hip_trace_end_content(const crdt_hip_trace* t, const char** s, size_t* len) {
+    if (!t || !s || !len) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    *s = t->t.end_content.data();
+    *len = t->t.end_content.size();
+    return 0;
+}
+int crdt_hip_trace_chars_to_bytes(crdt_hip_trace* t) {
+    if (!t) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::string e = crdt::chars_to_bytes(t->t);
+        return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_ERANGE, e);
+    });
+}
+int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out) {
+    if (!t || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    if (t->t.byte_offsets)
+        return set_err(nullptr, CRDT_HIP_EINVAL, "resolve needs codepoint offsets (EDITS_USE_BYTE_OFFSETS = false)");
+    *out = nullptr;
+    return guard(nullptr, [&] {
+        crdt_hip_oplog* L = new crdt_hip_oplog();
+        const crdt::Trace& T = t->t;
+        std::string e;
+        // from_str(start_content), then replace() every patch (main.rs:29-33, rope.rs:21-32)
+        if (!T.start_content.empty())
+            e = L->log.insert_utf8(0, T.start_content.data(), T.start_content.size());
+        for (size_t i = 0; e.empty() && i < T.patches.size(); ++i) {
+            const crdt::Patch& p = T.patches[i];
+            if (p.del) e = L->log.remove(p.pos, p.pos + p.del);
+            if (e.empty() && p.ins_len) e = L->log.insert_utf8(p.pos, T.ins.data() + p.ins_off, p.ins_len);
+        }
+        if (!e.empty()) {
+            delete L;
+            return set_err(nullptr, CRDT_HIP_ERANGE, e);
+        }
+        *out = L;
+        return 0;
+    });
+}
+
+// ---- synthetic -------------------------------------------------------------------------------
+int crdt_hip_synth_agents(uint32_t n_items, uint32_t agents, uint64_t seed, crdt_hip_oplog** out) {
+    if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
+    return guard(nullptr, [&] {
+        crdt::OpLog* L = crdt::synth_agents(n_items, agents, seed);
+        crdt_hip_oplog* o = new crdt_hip_oplog();
+        o->log = std::move(*L);
+        delete L;
+        *out = o;
+        return 0;
+    });
+}
+int crdt_hip_synth_tree(uint32_t n_items, uint32_t p_chain_pct, uint32_t del_pct, uint64_t seed,
+                        crdt_hip_oplog** out) {
+    if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
+    if (p_chain_pct > 100 || del_pct > 100) return set_err(nullptr, CRDT_HIP_EINVAL, "percent > 100");
+    return guard(nullptr, [&] {
+        crdt::OpLog* L = crdt::synth_tree(n_items, p_chain_pct, del_pct, seed);
+        crdt_hip_oplog* o = new crdt_hip_oplog();
+        o->log = std::move(*L);
+        delete L;
+        *out = o;
+        return 0;
+    });
+}
+
+// ---- merge -----------------------------------------------------------------------------------
+int crdt_hip_merge(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint8_t* out, size_t cap,
+                   size_t* out_len, uint64_t* digest) {
+    if (!ctx) return set_err(nullptr, CRDT_HIP_EINVAL, "null context");
+    return guard(ctx, [&] {
+        int rc = stage_views(ctx, log, 1);
+        if (rc) return rc;
+        std::vector<uint8_t> text;
+        std::vector<uint64_t> offs;
+        uint64_t dig = 0, len = 0;
+        rc = ctx->eng.merge(ctx->staging, crdt::Engine::TEXT, &dig, &len, nullptr,
+                            out ? &text : nullptr, nullptr);
+        if (rc) return from_engine(ctx, rc);
+        if (out_len) *out_len = (size_t)len;
+        if (digest) *digest = dig;
+        if (out) {
+            if (cap < len) return set_err(ctx, CRDT_HIP_ESPACE, "output buffer too small");
+            if (len) std::memcpy(out, text.data(), (size_t)len);
+        }
+        return 0;
+    });
+}
+
+int crdt_hip_merge_batch(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* logs, uint32_t n,
+                         uint64_t* digests, uint64_t* lens, crdt_hip_stats* stats) {
+    if (!ctx || (!logs && n)) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    return guard(ctx, [&] {
+        if (n == 0) return 0;
+        int rc = stage_views(ctx, logs, n);
+        if (rc) return rc;
+        return from_engine(ctx, ctx->eng.merge(ctx->staging, crdt::Engine::TEXT, digests, lens, stats));
+    });
+}
+
+int crdt_hip_merge_order(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint32_t* order) {
+    if (!ctx || !order) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    return guard(ctx, [&] {
+        int rc = stage_views(ctx, log, 1);
+        if (rc) return rc;
+        std::vector<uint8_t> raw;
+        rc = ctx->eng.merge(ctx->staging, crdt::Engine::ORDER, nullptr, nullptr, nullptr, &raw, nullptr);
+        if (rc) return from_engine(ctx, rc);
+        if (raw.size() != (size_t)log->n * 4)
+            return set_err(ctx, CRDT_HIP_EBADLOG, "order output size mismatch");
+        if (!raw.empty()) std::memcpy(order, raw.data(), raw.size());
+        return 0;
+    });
+}
+
+// ---- resident batches ------------------------------------------------------------------------
+int crdt_hip_batch_create(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* bases, uint32_t nbases,
+                          uint32_t replicas, uint32_t relabel, uint64_t seed,
+                          crdt_hip_batch** out) {
+    if (!ctx || !bases || !out || nbases == 0 || replicas == 0)
+        return set_err(ctx, CRDT_HIP_EINVAL, "bad batch arguments");
+    if (relabel > 2) return set_err(ctx, CRDT_HIP_EINVAL, "relabel must be 0, 1 or 2");
+    *out = nullptr;
+    return guard(ctx, [&] {
+        int rc = stage_views(ctx, bases, nbases);
+        if (rc) return rc;
+        crdt_hip_batch* b = new crdt_hip_batch();
+        b->ctx = ctx;
+        rc = ctx->eng.replicate(ctx->staging, b->logs, replicas, relabel, seed);
+        if (rc) {
+            delete b;
+            return from_engine(ctx, rc);
+        }
+        b->device_bytes = b->logs.total_slots * 15 + (b->logs.total_slots >> b->logs.log2m) * 4;
+        *out = b;
+        return 0;
+    });
+}
+int crdt_hip_batch_free(crdt_hip_batch* b) {
+    delete b;
+    return 0;
+}
+int crdt_hip_batch_info(const crdt_hip_batch* b, uint64_t* docs, uint64_t* items,
+                        uint64_t* device_bytes) {
+    if (!b) return set_err(nullptr, CRDT_HIP_EINVAL, "null batch");
+    if (docs) *docs = b->logs.docs.size();
+    if (items) *items = b->logs.items;
+    if (device_bytes) *device_bytes = b->device_bytes;
+    return 0;
+}
+int crdt_hip_batch_merge(crdt_hip_ctx* ctx, crdt_hip_batch* b, uint64_t* digests, uint64_t* lens,
+                         crdt_hip_stats* stats) {
+    if (!ctx || !b) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (b->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "batch belongs to another context");
+    return guard(ctx, [&] {
+        return from_engine(ctx, ctx->eng.merge(b->logs, crdt::Engine::TEXT, digests, lens, stats));
+    });
+}
+
+// ---- RCCL ------------------------------------------------------------------------------------
+int crdt_hip_comm_unique_id(uint8_t id[128]) {
+    if (!id) return set_err(nullptr, CRDT_HIP_EINVAL, "null id");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return set_err(nullptr, CRDT_HIP_ECOMM, ncclGetErrorString(r));
+    std::memcpy(id, &u, 128);
+    return 0;
+}
+int crdt_hip_comm_init(crdt_hip_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks)
+        return set_err(ctx, CRDT_HIP_EINVAL, "bad comm arguments");
+    if (hipSetDevice(ctx->eng.device) != hipSuccess)
+        return set_err(ctx, CRDT_HIP_EDEVICE, "hipSetDevice failed");
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+    if (r != ncclSuccess) return set_err(ctx, CRDT_HIP_ECOMM, ncclGetErrorString(r));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return 0;
+}
+int crdt_hip_allgather_u64(crdt_hip_ctx* ctx, const uint64_t* send, size_t count, uint64_t* recv) {
+    if (!ctx || !ctx->comm || (!send && count) || (!recv && count))
+        return set_err(ctx, CRDT_HIP_EINVAL, "comm not initialised or null buffer");
+    if (count == 0) return 0;
+    uint64_t *ds = nullptr, *dr = nullptr;
+    hipStream_t s = ctx->eng.stream;
+    auto cleanup = [&] {
+        if (ds) (void)hipFree(ds);
+        if (dr) (void)hipFree(dr);
+    };
+    if (hipMalloc(&ds, count * 8) != hipSuccess ||
+        hipMalloc(&dr, count * 8 * (size_t)ctx->nranks) != hipSuccess) {
+        cleanup();
+        return set_err(ctx, CRDT_HIP_ENOMEM, "device allocation for all-gather");
+    }
+    hipError_t e = hipMemcpyAsync(ds, send, count * 8, hipMemcpyHostToDevice, s);
+    ncclResult_t r = ncclSuccess;
+    if (e == hipSuccess) r = ncclAllGather(ds, dr, count, ncclUint64, ctx->comm, s);
+    if (e == hipSuccess && r == ncclSuccess)
+        e = hipMemcpyAsync(recv, dr, count * 8 * (size_t)ctx->nranks, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    cleanup();
+    if (r != ncclSuccess) return set_err(ctx, CRDT_HIP_ECOMM, ncclGetErrorString(r));
+    if (e != hipSuccess) return set_err(ctx, CRDT_HIP_EDEVICE, hipGetErrorString(e));
+    return 0;
+}
+int crdt_hip_comm_destroy(crdt_hip_ctx* ctx) {
+    if (!ctx) return 0;
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    return 0;
+}
+
+// ---- helpers ---------------------------------------------------------------------------------
+uint64_t crdt_hip_xxh64(const void* data, size_t len, uint64_t seed) { return crdt::xxh64(data, len, seed); }
+uint64_t crdt_hip_tree_digest(const uint8_t* text, size_t len) { return crdt::tree_digest(text, len); }
+
+}  // extern "C"

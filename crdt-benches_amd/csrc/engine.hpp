@@ -1,0 +1,111 @@
+// engine.hpp — device merge engine: op logs resident in HBM in a slot layout, merged to their
+// documents by the gfx950 kernels in engine.hip.
+//
+// Slot layout (DESIGN.md §Data layout): every document d owns slots [base_d, base_d + n_d + 1)
+// of a wave, padded up to a multiple of the splitter stride M: slot base_d is the document-start
+// node (id 0), slot base_d + k holds item id k.  Input SoA arrays are indexed by slot.  Because
+// every document starts on a multiple of M, the chunk -> document table needs one entry per M
+// slots, and splitter indices are a pure function of the slot.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "crdt_hip.h"
+
+namespace crdt {
+
+struct DocInfo {
+    uint32_t n;          // items
+    uint64_t text_cap;   // exact visible UTF-8 bytes (host-computed upper bound)
+};
+
+struct Wave {
+    uint32_t first_doc, ndocs;
+    uint64_t slot0;      // first slot of the wave
+    uint32_t nslots;     // multiple of M
+    uint32_t max_splitters_per_doc;
+    uint64_t text_cap;   // bytes (docs aligned to 16)
+    uint64_t leaf_cap;   // 4 KiB leaves
+    uint64_t order_cap;  // u32 entries for ORDER mode
+};
+
+// Device-resident op logs in slot layout, planned into waves.
+struct DeviceLogs {
+    uint32_t log2m = 6;
+    uint64_t total_slots = 0, cap_slots = 0;
+    std::vector<DocInfo> docs;
+    std::vector<uint64_t> doc_slot;  // global slot base per doc
+    std::vector<Wave> waves;
+    uint64_t items = 0;
+    // device arrays (slot-indexed)
+    uint32_t* parent = nullptr;
+    uint32_t* lamport = nullptr;
+    uint16_t* agent = nullptr;
+    uint8_t* deleted = nullptr;
+    uint32_t* cp = nullptr;
+    uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
+    uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
+    uint64_t cap_docs = 0, cap_chunks = 0;
+
+    void release();
+    ~DeviceLogs() { release(); }
+};
+
+class Engine {
+public:
+    Engine() = default;
+    ~Engine();
+    std::string init(int device);
+
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t log2m = 6;                    // splitter stride M = 2^log2m
+    uint64_t max_wave_slots = 1ull << 30;
+    std::string err;
+
+    // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
+    int plan(DeviceLogs& L, const std::vector<DocInfo>& docs);
+    // Upload host views into `L` (plan first).  Synchronous.
+    int upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n);
+    // Build docs_rel / chunk_doc tables for L's plan.
+    int upload_tables(DeviceLogs& L);
+
+    enum Mode { TEXT = 0, ORDER = 1 };
+    // Merge every wave of L.  digests/lens: per doc (host, may be null).  If text_out is set
+    // (single-wave only), the merged bytes of the wave are copied back (docs concatenated,
+    // each 16-aligned; offsets in text_offsets).
+    int merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, crdt_hip_stats* st,
+              std::vector<uint8_t>* text_out = nullptr,
+              std::vector<uint64_t>* text_offsets = nullptr);
+
+    // Materialise `replicas` relabelled copies of `bases` (already uploaded in B) into R.
+    int replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,
+                  uint64_t seed);
+
+private:
+    // scratch, grown on demand
+    uint64_t cap_slots_ = 0, cap_splitters_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
+    uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
+             *bigl_ = nullptr, *scan_sums_ = nullptr, *ctl_ = nullptr;
+    uint2 *dn_ = nullptr, *up_ = nullptr;
+    uint32_t *sw_ = nullptr, *snext_ = nullptr, *pred_ = nullptr, *v0_ = nullptr, *v1_ = nullptr,
+             *p0_ = nullptr, *p1_ = nullptr;
+    uint32_t *tlen_ = nullptr, *icnt_ = nullptr, *loff_ = nullptr;
+    uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;
+    uint8_t* text_ = nullptr;
+    uint32_t* host_ctl_ = nullptr;       // pinned
+    uint64_t* host_dig_ = nullptr;       // pinned
+    uint32_t* host_len_ = nullptr;       // pinned
+    uint64_t cap_host_docs_ = 0;
+    std::vector<hipEvent_t> ev_;
+
+    int ensure_scratch(const Wave& w, uint32_t ndocs_total);
+    int run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
+                 std::vector<uint32_t>& stage_launches);
+    int fail(const char* what, hipError_t e);
+};
+
+}  // namespace crdt

@@ -1,0 +1,70 @@
+// oplog.hpp — host-side resolver: positional patches -> anchor op log (SoA).
+//
+// Replaces the positional half of diamond-types' OpLog::add_insert / add_delete_without_content
+// (called from the Dt adapter, /root/reference/src/rope.rs:116-131).  Conventions (SURVEY.md
+// §4.2): an insert at visible codepoint position p is anchored to the p-th visible item
+// (origin_left; id 0 = document start) and placed immediately after it, before any tombstones
+// that follow it; origin_right = the item that followed origin_left (tombstones included, NIL
+// at the end); char k > 0 of a multi-char insert is anchored to char k-1; every deleted
+// codepoint is tombstoned exactly once.  lamport = max lamport seen + 1 per item, agent =
+// the log's local agent.  With RGA ordering (siblings by (lamport, agent) descending) the
+// resolver's sequence equals the merged document order at every step.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace crdt {
+
+class OpLog {
+public:
+    // ---- SoA (index k holds item id k+1) ----
+    std::vector<uint32_t> parent, oright, lamport, cp;
+    std::vector<uint16_t> agent;
+    std::vector<uint8_t> deleted;
+    std::vector<uint32_t> del_ops;  // target id of every delete op, in op order
+    uint16_t local_agent = 0;
+    uint32_t max_lamport = 0;
+
+    OpLog();
+    uint32_t size() const { return (uint32_t)parent.size(); }
+    uint64_t visible() const { return nvis_; }
+
+    // Upstream::insert / remove (codepoint offsets).  Return "" or an error message.
+    std::string insert(uint64_t pos, const uint32_t* cps, size_t k);
+    std::string insert_utf8(uint64_t pos, const char* s, size_t nbytes);
+    std::string remove(uint64_t start, uint64_t end);
+
+    // Downstream wire format (see oplog.cpp for the layout).
+    uint64_t version() const { return ((uint64_t)size() << 32) | (uint32_t)del_ops.size(); }
+    std::vector<uint8_t> encode_from(uint64_t version) const;
+    std::string apply_update(const uint8_t* buf, size_t len);
+
+    // Append a fully-specified item (synthetic generators / decoding); marks the positional
+    // index stale.
+    void push_item(uint32_t par, uint32_t orr, uint32_t lam, uint16_t ag, uint8_t del,
+                   uint32_t c);
+    void mark_deleted(uint32_t id);
+    // For bulk builders that fill the SoA directly.
+    void mark_stale() { stale_ = true; }
+    void reset_visible(uint64_t v) { nvis_ = v; }
+
+private:
+    struct Chunk {
+        std::vector<uint32_t> ids;
+        uint32_t vis = 0;
+    };
+    std::vector<Chunk> chunks_;
+    std::vector<int64_t> fen_;  // Fenwick tree over chunks_[i].vis
+    uint64_t nvis_ = 0;
+    bool stale_ = false;  // positional index must be rebuilt (after remote items arrived)
+
+    void fen_build();
+    void fen_add(size_t i, int64_t d);
+    size_t fen_find(uint64_t& p) const;  // chunk holding the p-th visible item (p >= 1)
+    void split_chunk(size_t c);
+    std::string rebuild_index();
+    bool find_visible(uint64_t p, size_t& c, size_t& i) const;
+};
+
+}  // namespace crdt

@@ -1,0 +1,51 @@
+// util.cpp — host xxh64 (published XXH64 algorithm) and the document tree digest.
+#include "util.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace crdt {
+
+namespace {
+constexpr uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL,
+                   P3 = 0x165667B19E3779F9ULL, P4 = 0x85EBCA77C2B2AE63ULL,
+                   P5 = 0x27D4EB2F165667C5ULL;
+inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t load64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+inline uint32_t load32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+inline uint64_t round1(uint64_t acc, uint64_t x) { return rotl(acc + x * P2, 31) * P1; }
+inline uint64_t merge1(uint64_t acc, uint64_t v) { return (acc ^ round1(0, v)) * P1 + P4; }
+}  // namespace
+
+uint64_t xxh64(const void* data, size_t len, uint64_t seed) {
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    const uint8_t* const end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v[4] = {seed + P1 + P2, seed + P2, seed, seed - P1};
+        for (; end - p >= 32; p += 32)
+            for (int k = 0; k < 4; ++k) v[k] = round1(v[k], load64(p + 8 * k));
+        h = rotl(v[0], 1) + rotl(v[1], 7) + rotl(v[2], 12) + rotl(v[3], 18);
+        for (int k = 0; k < 4; ++k) h = merge1(h, v[k]);
+    } else {
+        h = seed + P5;
+    }
+    h += len;
+    for (; end - p >= 8; p += 8) h = rotl(h ^ round1(0, load64(p)), 27) * P1 + P4;
+    if (end - p >= 4) { h = rotl(h ^ (load32(p) * P1), 23) * P2 + P3; p += 4; }
+    for (; p < end; ++p) h = rotl(h ^ (*p * P5), 11) * P1;
+    h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+    return h;
+}
+
+uint64_t tree_digest(const uint8_t* text, size_t len) {
+    const size_t leaf = 4096;
+    std::vector<uint64_t> hs((len + leaf - 1) / leaf);
+    for (size_t i = 0; i < hs.size(); ++i) {
+        const size_t n = std::min(leaf, len - i * leaf);
+        hs[i] = xxh64(text + i * leaf, n, 0);
+    }
+    return xxh64(hs.data(), hs.size() * 8, (uint64_t)len);
+}
+
+}  // namespace crdt

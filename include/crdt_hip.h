@@ -1,0 +1,200 @@
+/*
+ * crdt_hip.h — C ABI of the MI355X-native merge engine (libcrdt_hip.so).
+ *
+ * This is the drop-in boundary for the replay-and-merge path of noib3/crdt-benches.  The
+ * reference binds CRDT engines through two Rust traits:
+ *   trait Upstream   /root/reference/src/rope.rs:6-33   (from_str, insert, remove, len, replace)
+ *   trait Downstream /root/reference/src/rope.rs:185-191 (upstream_updates, apply_update)
+ * and registers them in the bench at /root/reference/src/main.rs:43-46 and :78.  A Rust
+ * `crdt-hip-sys` crate binds exactly the entry points below; the
+ * `impl Upstream/Downstream for HipMerge` maps:
+ *   from_str(s)          -> crdt_hip_oplog_new + crdt_hip_oplog_insert(0, s)   (rope.rs:113-121)
+ *   insert(at, s)        -> crdt_hip_oplog_insert                               (rope.rs:124-126)
+ *   remove(a..b)         -> crdt_hip_oplog_remove                               (rope.rs:129-131)
+ *   len()                -> crdt_hip_merge  (replaces OpLog::checkout_tip().len(), rope.rs:134-136)
+ *   upstream_updates     -> crdt_hip_oplog_version + crdt_hip_oplog_encode_from (rope.rs:196-220)
+ *   apply_update(u)      -> crdt_hip_oplog_apply_update (replaces decode_and_add, rope.rs:222-224)
+ *   clone()              -> crdt_hip_oplog_clone (the device context is shared, never copied)
+ *
+ * Conventions
+ *   - Every function returns int status: 0 = ok, < 0 = error (CRDT_HIP_E*).  Nothing throws or
+ *     aborts across the ABI.  crdt_hip_last_error(ctx) returns the message of the last failure
+ *     on that context (ctx == NULL: the last failure of a context-free call on this thread).
+ *   - Host pointers are BORROWED for the duration of the call only.
+ *   - Positions are Unicode codepoints (EDITS_USE_BYTE_OFFSETS = false, rope.rs:8,16-19).
+ *   - A context is bound to one HIP device and must be used by one host thread at a time; calls
+ *     are synchronous at the ABI (the work runs on the context's own HIP stream).
+ *   - Op log ids: items are 1..n in creation order; id 0 is the document start (origin of an
+ *     insert at position 0).
+ */
+#ifndef CRDT_HIP_H
+#define CRDT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRDT_HIP_ABI_VERSION 1
+
+enum {
+    CRDT_HIP_OK = 0,
+    CRDT_HIP_EINVAL = -1,   /* bad argument */
+    CRDT_HIP_ERANGE = -2,   /* position / id out of range */
+    CRDT_HIP_ENOMEM = -3,   /* host or device allocation failed */
+    CRDT_HIP_EDEVICE = -4,  /* HIP runtime error (no device, launch failure, ...) */
+    CRDT_HIP_EBADLOG = -5,  /* malformed op log (bad parent, cycle) detected on device */
+    CRDT_HIP_ESPACE = -6,   /* caller's output buffer too small (*out_len says how much) */
+    CRDT_HIP_EIO = -7,      /* file / decompression / parse error */
+    CRDT_HIP_ECOMM = -8     /* RCCL error */
+};
+
+typedef struct crdt_hip_ctx crdt_hip_ctx;
+typedef struct crdt_hip_oplog crdt_hip_oplog;
+typedef struct crdt_hip_trace crdt_hip_trace;
+typedef struct crdt_hip_batch crdt_hip_batch;
+
+/* Anchor op log, structure of arrays (borrowed view).  Item k (0-based) has id k+1.
+ * parent = origin_left id (0 = document start).  Document order (RGA): pre-order of the tree
+ * parent -> children, siblings by (lamport, agent) descending.  cp = Unicode codepoint. */
+typedef struct {
+    uint32_t n;
+    const uint32_t* parent;
+    const uint32_t* origin_right; /* optional (may be NULL); not used by the RGA merge */
+    const uint32_t* lamport;
+    const uint16_t* agent;
+    const uint8_t* deleted;
+    const uint32_t* cp;
+} crdt_hip_oplog_view;
+
+/* Per-stage device time of the last merge (HIP events on the context's stream), in ns,
+ * summed over every wave of the call, plus work counters. */
+typedef struct {
+    uint64_t items;        /* op-log items merged */
+    uint64_t docs;         /* documents merged */
+    uint64_t text_bytes;   /* merged bytes produced */
+    uint32_t waves;        /* device waves the call was split into */
+    uint32_t nstages;      /* valid entries in stage_ns / stage_launches */
+    uint64_t stage_ns[16];
+    uint32_t stage_launches[16];
+    uint64_t total_ns;     /* first event to last event of the call */
+} crdt_hip_stats;
+
+/* Stage indices of crdt_hip_stats.stage_ns. */
+enum {
+    CRDT_HIP_STAGE_COUNT = 0,   /* child counting per parent               */
+    CRDT_HIP_STAGE_SCAN = 1,    /* exclusive scan of child counts           */
+    CRDT_HIP_STAGE_PLACE = 2,   /* children scattered into parent segments  */
+    CRDT_HIP_STAGE_LINK = 3,    /* sibling sort + first-child/next-sibling  */
+    CRDT_HIP_STAGE_WALK1 = 4,   /* Euler-tour sublist sums                  */
+    CRDT_HIP_STAGE_RANK = 5,    /* ranking of the splitter lists            */
+    CRDT_HIP_STAGE_WALK2 = 6,   /* Euler-tour re-walk: UTF-8 scatter         */
+    CRDT_HIP_STAGE_DIGEST = 7,  /* per-document tree digest                 */
+    CRDT_HIP_NSTAGES = 8
+};
+
+/* ---- library / context ----------------------------------------------------------------- */
+int crdt_hip_abi_version(void);
+int crdt_hip_device_count(int* out);
+int crdt_hip_init(int device, crdt_hip_ctx** out);
+int crdt_hip_destroy(crdt_hip_ctx* ctx);
+const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
+/* Tuning: splitter stride of the list ranking (power of two, 16..4096; default 64) and the
+ * maximum slots per device wave (default 2^30). */
+int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
+
+/* ---- op log: host-side resolver (positional patch -> anchor op) ---------------------------- */
+int crdt_hip_oplog_new(crdt_hip_oplog** out);
+int crdt_hip_oplog_clone(const crdt_hip_oplog* src, crdt_hip_oplog** out);
+void crdt_hip_oplog_free(crdt_hip_oplog* log);
+/* insert `nbytes` of UTF-8 at codepoint position `pos` (Upstream::insert). */
+int crdt_hip_oplog_insert(crdt_hip_oplog* log, size_t pos, const char* utf8, size_t nbytes);
+/* delete codepoints [start, end) (Upstream::remove). */
+int crdt_hip_oplog_remove(crdt_hip_oplog* log, size_t start, size_t end);
+/* Upstream::replace default (rope.rs:21-32): remove if end > start, then insert if non-empty. */
+int crdt_hip_oplog_replace(crdt_hip_oplog* log, size_t start, size_t end, const char* utf8,
+                           size_t nbytes);
+/* Visible codepoints tracked by the resolver (host side; NOT the merged result). */
+size_t crdt_hip_oplog_visible_len(const crdt_hip_oplog* log);
+/* Borrowed SoA view, valid until the next mutation of `log`. */
+int crdt_hip_oplog_get_view(const crdt_hip_oplog* log, crdt_hip_oplog_view* out);
+/* Version token (items and delete ops so far) for encode_from. */
+uint64_t crdt_hip_oplog_version(const crdt_hip_oplog* log);
+/* Encode every op after `version` as one update (Downstream::upstream_updates, rope.rs:210-216).
+ * If buf is NULL or cap too small, *out_len gets the needed size and ESPACE is returned. */
+int crdt_hip_oplog_encode_from(const crdt_hip_oplog* log, uint64_t version, uint8_t* buf,
+                               size_t cap, size_t* out_len);
+/* Decode and append an update (Downstream::apply_update / decode_and_add, rope.rs:222-224). */
+int crdt_hip_oplog_apply_update(crdt_hip_oplog* log, const uint8_t* buf, size_t len);
+
+/* ---- trace loader (crdt-testdata load_testing_data / chars_to_bytes, main.rs:19-23) ---------- */
+int crdt_hip_trace_load(const char* path, crdt_hip_trace** out);
+void crdt_hip_trace_free(crdt_hip_trace* t);
+/* Number of patches (TestData::len, main.rs:25) / txns. */
+size_t crdt_hip_trace_len(const crdt_hip_trace* t);
+size_t crdt_hip_trace_txns(const crdt_hip_trace* t);
+/* Patch i: codepoint position, deleted codepoints, inserted UTF-8 (borrowed). */
+int crdt_hip_trace_patch(const crdt_hip_trace* t, size_t i, size_t* pos, size_t* del,
+                         const char** ins, size_t* ins_len);
+int crdt_hip_trace_start_content(const crdt_hip_trace* t, const char** s, size_t* len);
+int crdt_hip_trace_end_content(const crdt_hip_trace* t, const char** s, size_t* len);
+/* Rewrite every patch from codepoint to UTF-8 byte offsets (TestData::chars_to_bytes). */
+int crdt_hip_trace_chars_to_bytes(crdt_hip_trace* t);
+/* Replay every patch into a fresh op log (the upstream loop body of main.rs:29-34). */
+int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out);
+
+/* ---- synthetic op logs -------------------------------- */
+/* 64-agent concurrent interleaved edits; `n_items` inserts, ~20% deletes, splitmix64 seed. */
+int crdt_hip_synth_agents(uint32_t n_items, uint32_t agents, uint64_t seed, crdt_hip_oplog** out);
+/* single document: parent of item i is i-1 with probability p_chain_pct/100, else uniform in
+ * [0, i-1]; deleted ~ Bernoulli(del_pct/100); cp = 'a' + h % 26; lamport = i; agent = i % 64. */
+int crdt_hip_synth_tree(uint32_t n_items, uint32_t p_chain_pct, uint32_t del_pct, uint64_t seed,
+                        crdt_hip_oplog** out);
+
+/* ---- merge (device) --------------------------------------------------------------------- */
+/* Merge one op log to its document: UTF-8 into out[0..cap), byte length in *out_len, tree
+ * digest in *digest (either may be NULL).  If out is NULL only length/digest are produced. */
+int crdt_hip_merge(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint8_t* out, size_t cap,
+                   size_t* out_len, uint64_t* digest);
+/* Merge n independent op logs; digests[i], lens[i] per log.  stats may be NULL. */
+int crdt_hip_merge_batch(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* logs, uint32_t n,
+                         uint64_t* digests, uint64_t* lens, crdt_hip_stats* stats);
+/* Pre-order of every item (tombstones included), ids 1..n, into order[0..n) (test hook for
+ * the Euler-tour + list-ranking kernels). */
+int crdt_hip_merge_order(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint32_t* order);
+
+/* ---- device-resident replica batches (bench config 3) ------------------------------------- */
+/* Upload `nbases` base logs once, then materialise `replicas` independent HBM copies of each
+ * (document r uses base r % nbases).  relabel: 0 = ids kept, 1 = per-replica rotation of item
+ * ids (locality kept), 2 = per-replica pseudo-random permutation of item ids (seeded by seed
+ * and the replica index).  Parents are relabelled; lamport/agent kept, so every replica of a
+ * base must merge to the base's document. */
+int crdt_hip_batch_create(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* bases, uint32_t nbases,
+                          uint32_t replicas, uint32_t relabel, uint64_t seed,
+                          crdt_hip_batch** out);
+int crdt_hip_batch_free(crdt_hip_batch* b);
+int crdt_hip_batch_info(const crdt_hip_batch* b, uint64_t* docs, uint64_t* items,
+                        uint64_t* device_bytes);
+/* Merge every document of the batch (resident inputs); digests/lens sized to docs (may be
+ * NULL). */
+int crdt_hip_batch_merge(crdt_hip_ctx* ctx, crdt_hip_batch* b, uint64_t* digests,
+                         uint64_t* lens, crdt_hip_stats* stats);
+
+/* ---- multi-GPU (RCCL over xGMI): digest/counter exchange only ----------------------------- */
+int crdt_hip_comm_unique_id(uint8_t id[128]);
+int crdt_hip_comm_init(crdt_hip_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
+/* All-gather `count` u64 from every rank into recv[nranks * count] (rank-major). */
+int crdt_hip_allgather_u64(crdt_hip_ctx* ctx, const uint64_t* send, size_t count,
+                           uint64_t* recv);
+int crdt_hip_comm_destroy(crdt_hip_ctx* ctx);
+
+/* ---- helpers ------------------------------------------------------------------------------ */
+uint64_t crdt_hip_xxh64(const void* data, size_t len, uint64_t seed);
+uint64_t crdt_hip_tree_digest(const uint8_t* text, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

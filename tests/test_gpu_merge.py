@@ -1,0 +1,211 @@
+"""GPU parity tests: device merge through the C ABI vs the oracle (bit-exact bytes / ids).
+
+Every test runs the gfx950 kernels of libcrdt_hip.so; there is no CPU fallback in the product.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import crdt_hip
+from conftest import TESTS, TRACES, trace_path
+from oracle_bind import AnchorLog
+
+pytestmark = pytest.mark.gpu
+
+
+def arrays_from_anchor(a: AnchorLog) -> crdt_hip.LogArrays:
+    n = a.n
+    return crdt_hip.LogArrays(a.parent[:n], a.lamport[:n], a.agent[:n], a.deleted[:n], a.cp[:n])
+
+
+def to_anchor(arrs: crdt_hip.LogArrays) -> AnchorLog:
+    a = AnchorLog(arrs.n)
+    for f in ("parent", "lamport", "agent", "deleted", "cp"):
+        getattr(a, f)[: arrs.n] = getattr(arrs, f)
+    return a
+
+
+_RESOLVED = {}
+
+
+def resolved(name) -> crdt_hip.LogArrays:
+    if name not in _RESOLVED:
+        _RESOLVED[name] = crdt_hip.Trace(trace_path(name)).resolve().arrays()
+    return _RESOLVED[name]
+
+
+@pytest.mark.parametrize("name", TRACES)
+def test_trace_merge_byte_exact(ctx, oracle, golden, name):
+    """Config 2 for every trace: resolved anchor log -> one MI355X -> byte-exact endContent."""
+    log = resolved(name)
+    text, dig = ctx.merge(log)
+    end_hash = golden[name]["sha256"]
+    import hashlib
+    assert hashlib.sha256(text).hexdigest() == end_hash
+    assert text == oracle.merge(to_anchor(log))
+    assert "%016x" % dig == golden[name]["tree_digest"]
+    assert dig == oracle.tree_digest(text)
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "automerge-paper"])
+def test_merge_order_matches_oracle_preorder(ctx, oracle, name):
+    log = resolved(name)
+    order = ctx.merge_order(log)
+    _, ref = oracle.merge(to_anchor(log), want_order=True)
+    assert np.array_equal(order, ref)
+
+
+def test_upstream_bench_loop_semantics(ctx, golden, py_trace):
+    """The reference's upstream closure (main.rs:28-36) with HipMerge as R."""
+    name = "sveltecomponent"
+    t = crdt_hip.Trace(trace_path(name))
+    rope = crdt_hip.HipMerge.from_str(t.start_content)
+    for i in range(len(t)):
+        pos, dele, ins = t.patch(i)
+        rope.replace(pos, pos + dele, ins)
+    assert rope.len() == len(t.end_content)  # main.rs:35
+    assert rope.text() == t.end_content
+
+
+def test_downstream_bench_loop_semantics(golden, py_trace):
+    """The reference's downstream closure (main.rs:60-69): clone + apply_update* + len()."""
+    t = py_trace("sveltecomponent")
+    patches = [(int(t.pos[i]), int(t.dele[i]),
+                t.ins_cp[int(t.ins_off[i]): int(t.ins_off[i] + t.ins_len[i])].tobytes().decode("utf-32-le"))
+               for i in range(len(t))]
+    crdt0, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
+    for _ in range(2):
+        crdt = crdt0.clone()
+        for u in updates:
+            crdt.apply_update(u)
+        assert crdt.len() == len(t.end_content)
+        assert crdt.text() == t.end_content
+
+
+def test_concurrent_fixtures_on_device(ctx):
+    with open(os.path.join(TESTS, "golden", "concurrent.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        log = crdt_hip.LogArrays(c["parent"], c["lamport"], c["agent"], c["deleted"], c["cp"])
+        text, _ = ctx.merge(log)
+        assert text.decode() == c["expected"], c["name"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_synth_agents_vs_oracle(ctx, oracle, seed):
+    log = crdt_hip.OpLog.synth_agents(200000, 64, 0x5EED0000 + seed).arrays()
+    text, dig = ctx.merge(log)
+    assert text == oracle.merge(to_anchor(log))
+    order = ctx.merge_order(log)
+    _, ref = oracle.merge(to_anchor(log), want_order=True)
+    assert np.array_equal(order, ref)
+
+
+def test_synth_agents_naive_prefix(ctx, oracle):
+    """Causal prefix of the 64-agent log: device == tree oracle == O(n^2) integrator."""
+    log = crdt_hip.OpLog.synth_agents(10000, 64, 0x5EED0001).arrays()
+    text, _ = ctx.merge(log)
+    a = to_anchor(log)
+    assert text == oracle.merge(a) == oracle.merge_naive(a)
+
+
+@pytest.mark.parametrize("p_chain", [90, 0])
+def test_synth_tree_vs_oracle(ctx, oracle, p_chain):
+    log = crdt_hip.OpLog.synth_tree(1_000_000, p_chain, 50, 0x5EED0002).arrays()
+    text, dig = ctx.merge(log)
+    ref = oracle.merge(to_anchor(log))
+    assert text == ref
+    assert dig == oracle.tree_digest(ref)
+
+
+def fanout_log(n_children, depth_extra=0):
+    """Every item anchored at the document start (typing backwards at position 0)."""
+    n = n_children + depth_extra
+    parent = np.zeros(n, np.uint32)
+    if depth_extra:
+        parent[n_children:] = np.arange(n_children, n, dtype=np.uint32)  # a chain under the last
+    lam = np.arange(1, n + 1, dtype=np.uint32)
+    rng = np.random.default_rng(n)
+    cp = rng.integers(0x61, 0x7B, n).astype(np.uint32)
+    deleted = (rng.random(n) < 0.2).astype(np.uint8)
+    return crdt_hip.LogArrays(parent, lam, np.zeros(n, np.uint16), deleted, cp)
+
+
+@pytest.mark.parametrize("k", [2, 3, 17, 64, 65, 1000, 4096, 4097, 20000])
+def test_sibling_groups_every_sort_path(ctx, oracle, k):
+    """2 inline, 3..64 wave rank sort, 65..4096 LDS bitonic, >4096 global bitonic."""
+    log = fanout_log(k, depth_extra=50)
+    order = ctx.merge_order(log)
+    _, ref = oracle.merge(to_anchor(log), want_order=True)
+    assert np.array_equal(order, ref)
+    text, _ = ctx.merge(log)
+    assert text == oracle.merge(to_anchor(log))
+
+
+def test_ragged_batch_with_edge_cases(ctx, oracle):
+    rng = np.random.default_rng(7)
+    logs = []
+    logs.append(crdt_hip.LogArrays([], [], [], [], []))                   # empty document
+    logs.append(crdt_hip.LogArrays([0], [1], [0], [0], [0x1F600]))         # one 4-byte char
+    logs.append(crdt_hip.LogArrays([0, 1, 2], [1, 2, 3], [0, 0, 0], [1, 1, 1], [97, 98, 99]))  # all deleted
+    logs.append(resolved("sveltecomponent"))
+    for n in (63, 64, 65, 127, 128, 4095, 4097):
+        logs.append(fanout_log(n // 2, n - n // 2))
+    logs.append(crdt_hip.OpLog.synth_agents(50000, 64, 99).arrays())
+    wide = crdt_hip.OpLog.synth_agents(3000, 8, 5).arrays()
+    wide.cp[:] = rng.choice([0x41, 0xE9, 0x2019, 0x4E2D, 0x1F600], wide.n)  # every UTF-8 width
+    logs.append(wide)
+    dig, lens = ctx.merge_batch(logs)
+    for i, lg in enumerate(logs):
+        ref = oracle.merge(to_anchor(lg)) if lg.n else b""
+        assert lens[i] == len(ref), i
+        assert dig[i] == oracle.tree_digest(ref), i
+
+
+@pytest.mark.parametrize("stride", [16, 256, 4096])
+def test_splitter_stride_and_waves_do_not_change_results(oracle, stride):
+    c = crdt_hip.Context(0)
+    c.set_param("splitter_stride", stride)
+    c.set_param("max_wave_slots", 1 << 20)  # forces several waves
+    logs = [resolved(n) for n in TRACES]
+    dig, lens = c.merge_batch(logs)
+    for i, n in enumerate(TRACES):
+        ref = oracle.merge(to_anchor(logs[i]))
+        assert lens[i] == len(ref) and dig[i] == oracle.tree_digest(ref)
+    c.close()
+
+
+@pytest.mark.parametrize("relabel", ["none", "rotate", "shuffle"])
+def test_replica_batch_relabel_invariance(ctx, oracle, golden, relabel):
+    """Config 3 shape at small scale: relabelled HBM replicas merge to the trace documents."""
+    bases = [resolved(n) for n in TRACES]
+    b = ctx.batch(bases, replicas=3, relabel=relabel, seed=1234)
+    assert b.docs == 12
+    dig, lens, st = b.merge()
+    for r in range(b.docs):
+        name = TRACES[r % 4]
+        assert "%016x" % dig[r] == golden[name]["tree_digest"], (relabel, r)
+        assert lens[r] == golden[name]["end_bytes"]
+    assert st["items"] == 3 * sum(golden[n]["items"] for n in TRACES)
+
+
+def test_malformed_logs_are_rejected(ctx):
+    bad_parent = crdt_hip.LogArrays([0, 5], [1, 2], [0, 0], [0, 0], [97, 98])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        ctx.merge(bad_parent)
+    assert e.value.code == -5
+    cycle = crdt_hip.LogArrays([0, 3, 2], [1, 2, 3], [0, 0, 0], [0, 0, 0], [97, 98, 99])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        ctx.merge(cycle)
+    assert e.value.code == -5
+    ok = crdt_hip.LogArrays([0, 1], [1, 2], [0, 0], [0, 0], [97, 98])
+    assert ctx.merge(ok)[0] == b"ab"  # the engine recovers after an error
+
+
+def test_repeated_merges_are_deterministic(ctx):
+    log = crdt_hip.OpLog.synth_agents(300000, 64, 42).arrays()
+    d0 = ctx.merge_digest(log)
+    for _ in range(3):
+        assert ctx.merge_digest(log) == d0

@@ -1,0 +1,138 @@
+"""Host-side product code vs the oracle (CPU only): native trace loader (crdt-testdata
+restatement), resolver (positional patches -> anchor op log), update wire format, synthetic
+generators."""
+import numpy as np
+import pytest
+
+import crdt_hip
+from conftest import TRACES, trace_path
+from oracle_bind import AnchorLog
+
+
+def to_anchor(arrs: crdt_hip.LogArrays) -> AnchorLog:
+    a = AnchorLog(arrs.n)
+    for f in ("parent", "lamport", "agent", "deleted", "cp"):
+        getattr(a, f)[: arrs.n] = getattr(arrs, f)
+    a.oright[: arrs.n] = arrs.origin_right
+    return a
+
+
+@pytest.mark.parametrize("name", TRACES)
+def test_native_loader_matches_python_loader(name, py_trace):
+    t = crdt_hip.Trace(trace_path(name))
+    p = py_trace(name)
+    assert len(t) == len(p)  # TestData::len (main.rs:25)
+    assert t.end_content == p.end_content and t.start_content == p.start_content
+    rng = np.random.default_rng(0)
+    idx = set(rng.integers(0, len(p), 2000).tolist()) | {0, len(p) - 1}
+    for i in sorted(idx):
+        pos, dele, ins = t.patch(i)
+        assert pos == int(p.pos[i]) and dele == int(p.dele[i])
+        off, n = int(p.ins_off[i]), int(p.ins_len[i])
+        exp = p.ins_cp[off: off + n].tobytes().decode("utf-32-le") if n else ""
+        assert ins == exp
+
+
+@pytest.mark.parametrize("name", ["rustcode", "seph-blog1", "sveltecomponent"])
+def test_chars_to_bytes_replay(name, py_trace):
+    """After chars_to_bytes, a byte-offset replay reproduces endContent."""
+    t = crdt_hip.Trace(trace_path(name))
+    t.chars_to_bytes()
+    doc = bytearray(t.start_content.encode())
+    for i in range(len(t)):
+        pos, dele, ins = t.patch(i)
+        doc[pos: pos + dele] = ins.encode()
+    assert bytes(doc) == t.end_content.encode()
+
+
+def test_chars_to_bytes_changes_expected_patch_counts():
+    """exactly 7 rustcode and 2 seph-blog1 patches change coordinates."""
+    for name, exp in (("rustcode", 7), ("seph-blog1", 2), ("sveltecomponent", 0)):
+        a = crdt_hip.Trace(trace_path(name))
+        b = crdt_hip.Trace(trace_path(name))
+        b.chars_to_bytes()
+        changed = sum(a.patch(i)[:2] != b.patch(i)[:2] for i in range(len(a)))
+        assert changed == exp, name
+
+
+@pytest.mark.parametrize("name", TRACES)
+def test_native_resolver_matches_oracle_bit_exact(name, oracle, py_trace):
+    t = crdt_hip.Trace(trace_path(name))
+    log = t.resolve().arrays()
+    ref = oracle.resolve(py_trace(name))
+    assert log.n == ref.n
+    for f, g in (("parent", "parent"), ("lamport", "lamport"), ("agent", "agent"),
+                 ("deleted", "deleted"), ("cp", "cp"), ("origin_right", "oright")):
+        assert np.array_equal(getattr(log, f), getattr(ref, g)[: ref.n]), f
+    # and the oracle merges the product's resolved log to endContent
+    assert oracle.merge(to_anchor(log)) == py_trace(name).end_content.encode()
+
+
+def test_resolver_upstream_api_semantics(oracle):
+    log = crdt_hip.OpLog()
+    log.insert(0, "hello")
+    log.insert(5, " world")
+    log.replace(0, 1, "J")           # Upstream::replace: remove then insert
+    log.remove(5, 11)
+    log.insert(5, "!€\U0001F600")
+    assert log.visible_len() == 8
+    assert oracle.merge(to_anchor(log.arrays())) == "Jello!€\U0001F600".encode()
+    with pytest.raises(crdt_hip.CrdtHipError):
+        log.remove(3, 100)
+    assert crdt_hip.lib().crdt_hip_oplog_insert(log._h, 0, b"\xff", 1) == -2  # invalid UTF-8
+
+
+def test_update_wire_roundtrip(oracle, py_trace):
+    """Downstream: upstream_updates (one update per patch) + apply_update == the upstream log."""
+    t = py_trace("sveltecomponent")
+    patches = [(int(t.pos[i]), int(t.dele[i]),
+                t.ins_cp[int(t.ins_off[i]): int(t.ins_off[i] + t.ins_len[i])].tobytes().decode("utf-32-le"))
+               for i in range(2000)]
+    down, updates = crdt_hip.HipMerge.upstream_updates("", patches)
+    assert len(updates) == len(patches)
+    for u in updates:
+        down.apply_update(u)
+    up = crdt_hip.OpLog()
+    for pos, dele, ins in patches:
+        up.replace(pos, pos + dele, ins)
+    a, b = down.log.arrays(), up.arrays()
+    for f in crdt_hip.LogArrays.FIELDS:
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    # re-applying is idempotent, a gap is rejected
+    down.log.apply_update(updates[-1])
+    fresh = crdt_hip.OpLog()
+    with pytest.raises(crdt_hip.CrdtHipError):
+        fresh.apply_update(updates[5])
+    # positional edits after remote updates rebuild the resolver index from the log
+    down.log.insert(0, "Z")
+    up.insert(0, "Z")
+    assert oracle.merge(to_anchor(down.log.arrays())) == oracle.merge(to_anchor(up.arrays()))
+
+
+def test_synth_agents_is_valid_and_oracles_agree(oracle):
+    log = crdt_hip.OpLog.synth_agents(20000, 64, 0x5EED0001).arrays()
+    assert log.n == 20000
+    ids = np.arange(1, log.n + 1)
+    assert np.all(log.parent < ids)  # causal
+    par = log.parent.astype(np.int64)
+    has_p = par > 0
+    assert np.all(log.lamport[has_p] > log.lamport[par[has_p] - 1])
+    keys = log.lamport.astype(np.uint64) << np.uint64(16) | log.agent.astype(np.uint64)
+    assert np.unique(keys).size == log.n  # (lamport, agent) unique
+    assert len(set(log.agent.tolist())) == 64
+    a = to_anchor(log)
+    assert oracle.merge(a) == oracle.merge_naive(a)
+    # heavy sibling conflicts exist
+    counts = np.bincount(log.parent, minlength=log.n + 1)
+    assert counts.max() >= 3
+
+
+def test_synth_tree_shape():
+    log = crdt_hip.OpLog.synth_tree(100000, 90, 50, 0x5EED0002).arrays()
+    ids = np.arange(1, log.n + 1)
+    chain = np.mean(log.parent == ids - 1)
+    assert 0.88 < chain < 0.93
+    assert 0.48 < log.deleted.mean() < 0.52
+    assert np.all(log.lamport == ids) and np.all(log.agent == ids % 64)
+    log2 = crdt_hip.OpLog.synth_tree(1000, 90, 50, 0x5EED0002).arrays()
+    assert np.array_equal(log2.parent, log.parent[:1000])  # counter-based: prefix-stable
