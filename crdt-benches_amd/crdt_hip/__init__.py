@@ -23,7 +23,8 @@ ERRORS = {
     -1: "EINVAL", -2: "ERANGE", -3: "ENOMEM", -4: "EDEVICE", -5: "EBADLOG", -6: "ESPACE",
     -7: "EIO", -8: "ECOMM",
 }
-STAGES = ["count", "scan", "place", "link", "walk1", "rank", "walk2", "digest"]
+STAGES = ["jump", "tile_reduce", "tile_top", "tile_apply", "run_parent", "count", "scan", "place",
+          "link", "walk1", "rank", "walk2", "expand", "digest"]
 
 # Every symbol include/crdt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -66,6 +67,7 @@ class Stats(C.Structure):
         ("items", C.c_uint64),
         ("docs", C.c_uint64),
         ("text_bytes", C.c_uint64),
+        ("runs", C.c_uint64),
         ("waves", C.c_uint32),
         ("nstages", C.c_uint32),
         ("stage_ns", C.c_uint64 * 16),
@@ -76,7 +78,7 @@ class Stats(C.Structure):
     def as_dict(self) -> dict:
         return {
             "items": self.items, "docs": self.docs, "text_bytes": self.text_bytes,
-            "waves": self.waves, "total_ns": self.total_ns,
+            "runs": self.runs, "waves": self.waves, "total_ns": self.total_ns,
             "stage_ns": {STAGES[i]: int(self.stage_ns[i]) for i in range(self.nstages)},
             "stage_launches": {STAGES[i]: int(self.stage_launches[i]) for i in range(self.nstages)},
         }

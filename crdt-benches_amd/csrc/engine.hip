@@ -3,21 +3,32 @@
 // Replaces diamond-types' OpLog::checkout_tip (/root/reference/src/rope.rs:134-136): anchor
 // op log -> merged document.  Document order is the RGA order: pre-order of the tree
 // item -> children (children = items whose origin_left is the item), siblings by (lamport,
-// agent) descending.  Pipeline per wave:
-//   count   k_count      child count per parent                      (atomics, L2-local)
-//   scan    k_scan_*     exclusive scan of counts -> segment starts    (DPP wave scans)
-//   place   k_place      children scattered into parent segments
-//   link    k_link       sibling order (inline for <= 2 children), first-child / next-sibling
-//           k_sortmid    wave-per-segment rank sort (3..64 children, ds_permute/shuffles)
-//           k_sortbig    workgroup bitonic sort (> 64 children; LDS <= 4096, else global)
-//   walk1   k_walk1      Euler-tour sublist sums from every splitter (node id % M == 0)
-//   rank    k_pred/k_winit/k_wstep  prefix ranks of the splitter lists (pointer jumping)
-//   walk2   k_doctotals + k_walk2   re-walk; every visible item's UTF-8 lands at its offset
-//   digest  k_leafhash + k_docdigest  xxh64 tree digest per document
+// agent) descending.
+//
+// Two levels:
+//  Level 0 streams over item slots in 4096-slot tiles.  A slot continues the run of the slot
+//  before it iff its parent is that slot and that slot has no other child ("jump" child).  Such
+//  runs are unary chains of the tree with consecutive ids, so their items are consecutive in
+//  the document; on the josephg traces they hold 93-98 % of all items.  Run heads are recorded
+//  in a rank bitvector (1 bit/slot + a u32 rank per 64 slots) and every run gets its parent run,
+//  its key (lamport, agent of the head) and its weight (visible UTF-8 bytes).
+//    k_jump        flag slots that have a non-consecutive child
+//    k_tile_reduce per-tile head count + weight sum, per-document run counts
+//    k_tile_top    tile bases; per-document run bases (each document padded to M runs)
+//    k_tile_apply  head bitvector + rank words; run records (head slot, key, weight prefix)
+//    k_run_parent  parent run (rank lookup) and weight of every run
+//  Level 1 merges the tree of runs:
+//    k_count / k_scan_* / k_place        children grouped by parent run
+//    k_link / k_sortmid / k_sortbig      sibling order -> first-child / next-sibling
+//    k_walk1 / k_pred / k_winit / k_wstep / k_walk2
+//                                        Euler-tour list ranking (sublists from splitters
+//                                        run id % M == 0, pointer jumping over the splitter
+//                                        lists); weighted so the rank is each run's byte offset
+//  Expansion and digest:
+//    k_expand      every visible item's UTF-8 lands at run offset + in-run prefix (coalesced)
+//    k_leafhash / k_docdigest  xxh64 tree digest per document
 // The Euler tour is never materialised: succ(down v) = down(first_child v) or up v;
-// succ(up v) = down(next_sibling v) or up(parent v).  Weighted list ranking (down arc of a
-// visible item = its UTF-8 length, every other arc 0) yields each item's byte offset directly,
-// which fuses the tombstone scan and compaction into the ranking.
+// succ(up v) = down(next_sibling v) or up(parent v).
 #include "engine.hpp"
 
 #include <algorithm>
@@ -30,49 +41,31 @@ namespace crdt {
 namespace {
 
 constexpr uint32_t kNil = 0xFFFFFFFFu;
-constexpr uint32_t kVis = 0x80000000u;   // meta: visible item
-constexpr uint32_t kItem = 0x40000000u;  // meta: real item (not the document-start node)
 constexpr uint32_t kCpMask = 0x001FFFFFu;
 constexpr int kBlock = 256;
 constexpr int kScanItems = 16;
-constexpr int kScanTile = kBlock * kScanItems;
+constexpr int kScanTile = kBlock * kScanItems;  // also the level-0 tile
 constexpr uint32_t kLeaf = 4096;
 constexpr int kMidGrid = 2048;
 constexpr int kBigGrid = 256;
 constexpr int kBigThreads = 1024;
 constexpr int kBigLds = 4096;
 
-enum Stage { S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK, S_WALK2, S_DIGEST, S_N };
-
-struct WaveArgs {
-    uint32_t nslots, log2m, ndocs, S;
-    uint32_t step_limit;
-    const uint32_t* chunk_doc;
-    const uint2* docs;  // {wave-relative base slot, n}
-    const uint32_t* in_parent;
-    const uint32_t* in_lamport;
-    const uint16_t* in_agent;
-    const uint8_t* in_deleted;
-    const uint32_t* in_cp;
-    uint32_t* deg;
-    uint32_t* cstart;
-    uint32_t* child;
-    uint2* dn;  // {first_child, meta}
-    uint2* up;  // {next_sibling, parent}
-    uint32_t* defer;
-    uint32_t* bigl;
-    uint32_t* ctl;  // [0] deferred segments, [1] big segments, [2] error bits
-    uint32_t* sw;
-    uint32_t* snext;
-    uint32_t* tlen;
-    uint32_t* icnt;  // items reached by walk2, per document (reachability check)
-    uint64_t* toff;
-    uint32_t* loff;
-    uint64_t* leafh;
-    uint64_t* dig;
-    uint8_t* text;
-    uint64_t text_cap;
+// ctl words (device, zeroed per wave)
+enum Ctl {
+    C_NDEFER = 0,   // deferred sibling segments (3..64 children)
+    C_NBIG = 1,     // sibling segments with > 64 children
+    C_ERR = 2,      // error bits: 1 bad parent, 2 walk overrun, 4 text overflow, 8 write out
+                    //   of range, 16 unreachable runs (cycle)
+    C_RSLOTS = 3,   // level-1 run slots of the wave
+    C_RMAX = 4,     // largest per-document run slot count
+    C_WTOTAL = 5,   // wave weight total
+    C_HTOTAL = 6,   // wave head total
 };
+
+// Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
+enum Stage { S_JUMP, S_TREDUCE, S_TTOP, S_TAPPLY, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK,
+             S_WALK1, S_RANK, S_WALK2, S_EXPAND, S_DIGEST, S_N };
 
 // ---------------------------------------------------------------------------------------------
 // wave / block primitives
@@ -91,6 +84,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x = dpp_add<0x142, 0xa>(x);
     x = dpp_add<0x143, 0xc>(x);
     return x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
 }
 
 // Exclusive scan over the block's threads (NW waves); returns the block total in `total`.
@@ -112,29 +108,408 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* lds, u
     return off + inc - x;
 }
 
+// Per-document counter add, one atomic per wave when the wave's lanes share the document.
+__device__ __forceinline__ void doc_add(uint32_t* ctr, uint32_t d, uint32_t v) {
+    const uint64_t act = __ballot(v != 0);
+    if (!act) return;
+    const int first = __ffsll((unsigned long long)act) - 1;
+    const uint32_t d0 = (uint32_t)__shfl((int)d, first);
+    if (__all(v == 0 || d == d0)) {
+        const uint32_t tot = wave_sum(v);
+        if ((threadIdx.x & 63) == (uint32_t)first) atomicAdd(&ctr[d0], tot);
+    } else if (v) {
+        atomicAdd(&ctr[d], v);
+    }
+}
+
 __device__ __forceinline__ uint32_t utf8_len(uint32_t c) {
     return c < 0x80u ? 1u : c < 0x800u ? 2u : c < 0x10000u ? 3u : 4u;
 }
 
-__device__ __forceinline__ uint64_t sib_key(const WaveArgs& a, uint32_t c) {
+// ---------------------------------------------------------------------------------------------
+// Level 0: runs
+// ---------------------------------------------------------------------------------------------
+struct L0Args {
+    uint32_t nslots, log2m, ndocs, mode;  // mode: 0 text, 1 order
+    const uint32_t* chunk_doc;  // per M slots: wave-local document
+    const uint2* docs;          // per document {wave-relative base slot, n items}
+    const uint32_t* in_parent;
+    const uint32_t* in_lamport;
+    const uint16_t* in_agent;
+    const uint8_t* in_deleted;
+    const uint32_t* in_cp;
+    uint8_t* jump;              // per slot: has a non-consecutive child
+    uint64_t* hbits;            // per 64 slots: run-head bits
+    uint32_t* hrank;            // per 64 slots: heads before the word (wave-relative)
+    uint32_t* tsum_h;           // per tile: head count -> exclusive base
+    uint32_t* tsum_w;           // per tile: weight sum -> exclusive base
+    uint32_t ntiles;
+    uint32_t* doc_runs;         // per document: runs (the document-start run included)
+    uint32_t* doc_rank0;        // per document: heads before the document
+    uint32_t* run_base;         // per document: first run slot (multiple of M)
+    uint32_t* doc_pend;         // per document: weight prefix at the document's end
+    uint2* docs1;               // per document {run_base, runs - 1}: level-1 document table
+    uint32_t* r_head;           // per run slot: head slot
+    uint32_t* r_pstart;         // per run slot: weight prefix at the head
+    uint32_t* r_lam;
+    uint16_t* r_ag;
+    uint32_t* r_parent;         // per run slot: parent run, document-local
+    uint32_t* r_w;              // per run slot: weight
+    uint32_t* chunk_doc1;       // per M run slots: document
+    const uint32_t* roff;       // per run slot: offset of the run in its document (level 1)
+    const uint64_t* toff;       // per document: output offset
+    uint8_t* text;
+    uint32_t* ctl;
+};
+
+// The 16 slots [gs, gs+16) of one thread (always inside one document: 16 | M).
+struct Slots16 {
+    uint32_t hmask;   // run-head bits
+    uint32_t w[16];   // weights
+    uint32_t d;       // document (kNil when gs is past the wave)
+    uint2 doc;
+};
+
+__device__ __forceinline__ void load_slots16(const L0Args& a, uint32_t gs, bool need_heads,
+                                             Slots16& o) {
+    o.hmask = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o.w[k] = 0;
+    o.d = kNil;
+    o.doc = make_uint2(0, 0);
+    if (gs >= a.nslots) return;
+    o.d = a.chunk_doc[gs >> a.log2m];
+    o.doc = a.docs[o.d];
+    const uint32_t base = o.doc.x, n = o.doc.y;
+    const uint32_t l0 = gs - base;  // local id of slot gs
+    if (l0 > n) return;             // all padding
+    if (a.mode == 0) {
+        const uint4 dl = *reinterpret_cast<const uint4*>(a.in_deleted + gs);
+        const uint32_t dw[4] = {dl.x, dl.y, dl.z, dl.w};
+        const uint4* cpv = reinterpret_cast<const uint4*>(a.in_cp + gs);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 c = cpv[q];
+            const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = 4 * q + j;
+                const uint32_t local = l0 + k;
+                const bool item = (local - 1u) < n;
+                const bool del = (dw[q] >> (8 * j)) & 0xFFu;
+                o.w[k] = (item && !del) ? utf8_len(cc[j] & kCpMask) : 0u;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o.w[k] = ((l0 + k - 1u) < n) ? 1u : 0u;
+    }
+    if (!need_heads) return;
+    const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+    const uint4 jv = *reinterpret_cast<const uint4*>(a.jump + gs);
+    const uint32_t jw[4] = {jv.x, jv.y, jv.z, jv.w};
+    uint32_t prevj = (l0 > 0) ? a.jump[gs - 1] : 0u;
+    uint32_t bad = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 pp = pv[q];
+        const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * q + j;
+            const uint32_t local = l0 + k;
+            const uint32_t p = pa[j];
+            const uint32_t jk = (jw[q] >> (8 * j)) & 0xFFu;
+            bool head;
+            if (local == 0) {
+                head = true;
+            } else if (local <= n) {
+                const bool b = p > n || p == local;
+                bad |= b;
+                head = b || p != local - 1 || prevj;
+            } else {
+                head = false;
+            }
+            o.hmask |= (head ? 1u : 0u) << k;
+            prevj = jk;
+        }
+    }
+    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_jump(L0Args a) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.nslots) return;
+    const uint2 doc = a.docs[a.chunk_doc[g >> a.log2m]];
+    const uint32_t local = g - doc.x;
+    if (local - 1u >= doc.y) return;
+    const uint32_t p = a.in_parent[g];
+    if (p <= doc.y && p != local - 1u && p != local) a.jump[doc.x + p] = 1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_reduce(L0Args a) {
+    __shared__ uint32_t lds[kBlock / 64];
+    const uint32_t gs = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    Slots16 s;
+    load_slots16(a, gs, true, s);
+    uint32_t W = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) W += s.w[k];
+    const uint32_t H = __popc(s.hmask);
+    doc_add(a.doc_runs, s.d, H);
+    uint32_t th, tw;
+    block_excl_scan<kBlock / 64>(H, lds, th);
+    block_excl_scan<kBlock / 64>(W, lds, tw);
+    if (threadIdx.x == 0) {
+        a.tsum_h[blockIdx.x] = th;
+        a.tsum_w[blockIdx.x] = tw;
+    }
+}
+
+// Single workgroup: tile bases, per-document run bases (M-aligned), level-1 document table.
+__global__ __launch_bounds__(1024) void k_tile_top(L0Args a) {
+    __shared__ uint32_t lds[16];
+    __shared__ uint32_t mx;
+    if (threadIdx.x == 0) mx = 0;
+    uint32_t ch = 0, cw = 0;
+    for (uint32_t b0 = 0; b0 < a.ntiles; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t h = i < a.ntiles ? a.tsum_h[i] : 0u;
+        const uint32_t w = i < a.ntiles ? a.tsum_w[i] : 0u;
+        uint32_t th, tw;
+        const uint32_t eh = block_excl_scan<16>(h, lds, th);
+        const uint32_t ew = block_excl_scan<16>(w, lds, tw);
+        if (i < a.ntiles) {
+            a.tsum_h[i] = ch + eh;
+            a.tsum_w[i] = cw + ew;
+        }
+        ch += th;
+        cw += tw;
+    }
+    const uint32_t M = 1u << a.log2m;
+    uint32_t crank = 0, cbase = 0, rmax = 0;
+    for (uint32_t d0 = 0; d0 < a.ndocs; d0 += 1024) {
+        const uint32_t d = d0 + threadIdx.x;
+        const uint32_t r = d < a.ndocs ? a.doc_runs[d] : 0u;
+        const uint32_t rs = (r + M - 1) & ~(M - 1);
+        uint32_t tr, ts;
+        const uint32_t er = block_excl_scan<16>(r, lds, tr);
+        const uint32_t es = block_excl_scan<16>(rs, lds, ts);
+        if (d < a.ndocs) {
+            a.doc_rank0[d] = crank + er;
+            a.run_base[d] = cbase + es;
+            a.docs1[d] = make_uint2(cbase + es, r - 1);
+        }
+        rmax = max(rmax, rs);
+        crank += tr;
+        cbase += ts;
+    }
+    atomicMax(&mx, rmax);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.ctl[C_RSLOTS] = cbase;
+        a.ctl[C_RMAX] = mx;
+        a.ctl[C_WTOTAL] = cw;
+        a.ctl[C_HTOTAL] = ch;
+        if (a.ndocs) a.doc_pend[a.ndocs - 1] = cw;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_apply(L0Args a) {
+    __shared__ uint32_t lds[kBlock / 64];
+    const uint32_t gs = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    Slots16 s;
+    load_slots16(a, gs, true, s);
+    uint32_t W = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) W += s.w[k];
+    const uint32_t H = __popc(s.hmask);
+    uint32_t th, tw;
+    const uint32_t rank = a.tsum_h[blockIdx.x] + block_excl_scan<kBlock / 64>(H, lds, th);
+    uint32_t P = a.tsum_w[blockIdx.x] + block_excl_scan<kBlock / 64>(W, lds, tw);
+    // 64-bit head word from 4 consecutive lanes
+    const uint32_t q = threadIdx.x & 3u;
+    uint64_t word = (uint64_t)s.hmask << (16 * q);
+    word |= (uint64_t)__shfl_xor((long long)word, 1);
+    word |= (uint64_t)__shfl_xor((long long)word, 2);
+    if (gs >= a.nslots) return;
+    if (q == 0) {
+        a.hbits[gs >> 6] = word;
+        a.hrank[gs >> 6] = rank;
+    }
+    if (!s.hmask) return;
+    const uint32_t d = s.d;
+    const uint32_t rb = a.run_base[d] - a.doc_rank0[d];
+    uint32_t r = rank;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (s.hmask & (1u << k)) {
+            const uint32_t g = gs + k;
+            const uint32_t rho = rb + r;
+            const bool root = g == s.doc.x;
+            a.r_head[rho] = g;
+            a.r_pstart[rho] = P;
+            a.r_lam[rho] = root ? 0u : a.in_lamport[g];
+            a.r_ag[rho] = root ? (uint16_t)0 : a.in_agent[g];
+            if (root && d > 0) a.doc_pend[d - 1] = P;
+            ++r;
+        }
+        P += s.w[k];
+    }
+}
+
+// Heads at or before slot g (wave-relative), from the rank bitvector.
+__device__ __forceinline__ uint32_t rank_incl(const uint64_t* hbits, const uint32_t* hrank,
+                                              uint32_t g) {
+    const uint32_t w = g >> 6, b = g & 63u;
+    const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
+    return hrank[w] + (uint32_t)__popcll(hbits[w] & mask);
+}
+
+__global__ __launch_bounds__(1024) void k_chunk_doc1(L0Args a, uint32_t nchunks) {
+    const uint32_t c = blockIdx.x * 1024 + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint32_t slot = c << a.log2m;
+    uint32_t lo = 0, hi = a.ndocs;  // last d with run_base[d] <= slot
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.run_base[mid] <= slot) lo = mid; else hi = mid;
+    }
+    a.chunk_doc1[c] = lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t rslots) {
+    const uint32_t rho = blockIdx.x * kBlock + threadIdx.x;
+    if (rho >= rslots) return;
+    const uint32_t d = a.chunk_doc1[rho >> a.log2m];
+    const uint2 d1 = a.docs1[d];
+    const uint32_t r = rho - d1.x;
+    if (r > d1.y) return;  // run padding
+    const uint32_t ps = a.r_pstart[rho];
+    const uint32_t next = (r < d1.y) ? a.r_pstart[rho + 1] : a.doc_pend[d];
+    a.r_w[rho] = next - ps;
+    uint32_t pr = 0;
+    if (r != 0) {
+        const uint32_t h = a.r_head[rho];
+        const uint2 doc = a.docs[d];
+        uint32_t p = a.in_parent[h];
+        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_tile_reduce
+        pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u - a.doc_rank0[d];
+    }
+    a.r_parent[rho] = pr;
+}
+
+// Expansion: item slot -> its run -> output position; TEXT writes UTF-8, ORDER writes ids.
+__global__ __launch_bounds__(kBlock) void k_expand(L0Args a) {
+    __shared__ uint32_t lds[kBlock / 64];
+    const uint32_t gs = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    Slots16 s;
+    load_slots16(a, gs, false, s);
+    uint32_t W = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) W += s.w[k];
+    uint32_t tw;
+    uint32_t P = a.tsum_w[blockIdx.x] + block_excl_scan<kBlock / 64>(W, lds, tw);
+    if (!W) return;
+    const uint32_t d = s.d;
+    const uint32_t wi = gs >> 6, sh = gs & 63u;
+    const uint64_t hw = a.hbits[wi];
+    const uint32_t hm = (uint32_t)(hw >> sh) & 0xFFFFu;
+    uint32_t heads = a.hrank[wi] + (uint32_t)__popcll(sh ? (hw & ((1ull << sh) - 1ull)) : 0ull);
+    const uint32_t rb = a.run_base[d] - a.doc_rank0[d] - 1u;
+    const uint64_t obase = a.toff[d];
+    const uint64_t olim = a.toff[d + 1];
+    uint32_t cur = kNil, roff = 0, pst = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        heads += (hm >> k) & 1u;
+        const uint32_t w = s.w[k];
+        if (w) {
+            const uint32_t rho = rb + heads;
+            if (rho != cur) {
+                cur = rho;
+                roff = a.roff[rho];
+                pst = a.r_pstart[rho];
+            }
+            const uint64_t o = obase + roff + (P - pst);
+            if (a.mode == 0) {
+                if (o + w > olim) { atomicOr(&a.ctl[C_ERR], 8u); return; }
+                const uint32_t c = a.in_cp[gs + k] & kCpMask;
+                uint8_t* p = a.text + o;
+                if (c < 0x80u) {
+                    p[0] = (uint8_t)c;
+                } else if (c < 0x800u) {
+                    p[0] = (uint8_t)(0xC0u | (c >> 6));
+                    p[1] = (uint8_t)(0x80u | (c & 63u));
+                } else if (c < 0x10000u) {
+                    p[0] = (uint8_t)(0xE0u | (c >> 12));
+                    p[1] = (uint8_t)(0x80u | ((c >> 6) & 63u));
+                    p[2] = (uint8_t)(0x80u | (c & 63u));
+                } else {
+                    p[0] = (uint8_t)(0xF0u | (c >> 18));
+                    p[1] = (uint8_t)(0x80u | ((c >> 12) & 63u));
+                    p[2] = (uint8_t)(0x80u | ((c >> 6) & 63u));
+                    p[3] = (uint8_t)(0x80u | (c & 63u));
+                }
+            } else {
+                if (o >= olim) { atomicOr(&a.ctl[C_ERR], 8u); return; }
+                reinterpret_cast<uint32_t*>(a.text)[o] = gs + k - s.doc.x;
+            }
+        }
+        P += w;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Level 1: the tree of runs.  Node = run slot; local 0 of a document = its document-start run.
+// ---------------------------------------------------------------------------------------------
+struct TreeArgs {
+    uint32_t nslots, log2m, ndocs, S;
+    uint32_t step_limit;
+    const uint32_t* chunk_doc;
+    const uint2* docs;  // {base run slot, runs - 1}
+    const uint32_t* in_parent;
+    const uint32_t* in_lamport;
+    const uint16_t* in_agent;
+    const uint32_t* in_w;
+    uint32_t* deg;
+    uint32_t* cstart;
+    uint32_t* child;
+    uint2* dn;  // {first_child, weight}
+    uint2* up;  // {next_sibling, parent}
+    uint32_t* defer;
+    uint32_t* bigl;
+    uint32_t* ctl;
+    uint32_t* sw;
+    uint32_t* snext;
+    uint32_t* roff;
+    uint32_t* tlen;
+    uint32_t* icnt;
+    uint64_t* toff;
+    uint32_t* loff;
+    uint64_t* leafh;
+    uint64_t* dig;
+    uint8_t* text;
+    uint64_t text_cap;
+    uint32_t align;  // per-document output alignment (16 for text, 1 for order)
+};
+
+__device__ __forceinline__ uint64_t sib_key(const TreeArgs& a, uint32_t c) {
     return ((uint64_t)a.in_lamport[c] << 16) | (uint64_t)a.in_agent[c];
 }
 
-__device__ __forceinline__ uint2 doc_of(const WaveArgs& a, uint32_t g) {
+__device__ __forceinline__ uint2 doc_of(const TreeArgs& a, uint32_t g) {
     return a.docs[a.chunk_doc[g >> a.log2m]];
 }
 
-// ---------------------------------------------------------------------------------------------
-// count / scan / place
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_count(WaveArgs a) {
+__global__ __launch_bounds__(kBlock) void k_count(TreeArgs a) {
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
     if (g >= a.nslots) return;
     const uint2 doc = doc_of(a, g);
     const uint32_t local = g - doc.x;
-    if (local - 1u >= doc.y) return;  // document-start node or padding
+    if (local - 1u >= doc.y) return;  // document-start run or padding
     uint32_t p = a.in_parent[g];
-    if (p > doc.y || p == local) { atomicOr(&a.ctl[2], 1u); p = 0; }
+    if (p > doc.y || p == local) { atomicOr(&a.ctl[C_ERR], 1u); p = 0; }
     atomicAdd(&a.deg[doc.x + p], 1u);
 }
 
@@ -210,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* __restric
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_place(WaveArgs a) {
+__global__ __launch_bounds__(kBlock) void k_place(TreeArgs a) {
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
     if (g >= a.nslots) return;
     const uint2 doc = doc_of(a, g);
@@ -224,50 +599,56 @@ __global__ __launch_bounds__(kBlock) void k_place(WaveArgs a) {
     a.child[a.cstart[gp] + r] = g;
 }
 
-// ---------------------------------------------------------------------------------------------
-// link: sibling order -> first_child / next_sibling
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_link(WaveArgs a) {
+__global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
+    __shared__ uint32_t nblk, bbase;
+    if (threadIdx.x == 0) nblk = 0;
+    __syncthreads();
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.nslots) return;
-    const uint2 doc = doc_of(a, g);
-    const uint32_t local = g - doc.x;
-    if (local > doc.y) return;  // padding
-    uint32_t meta = 0;
-    if (local != 0) {
-        meta = (a.in_cp[g] & kCpMask) | kItem | (a.in_deleted[g] ? 0u : kVis);
-    } else {
-        a.up[g] = make_uint2(kNil, kNil);  // document start: no sibling, no parent
+    bool defer = false;
+    if (g < a.nslots) {
+        const uint2 doc = doc_of(a, g);
+        const uint32_t local = g - doc.x;
+        if (local <= doc.y) {
+            const uint32_t w = a.in_w[g];
+            if (local == 0) a.up[g] = make_uint2(kNil, kNil);  // no sibling, no parent
+            const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
+            uint32_t fc = kNil;
+            if (cnt == 1) {
+                const uint32_t c0 = a.child[s0];
+                fc = c0;
+                a.up[c0] = make_uint2(kNil, g);
+            } else if (cnt == 2) {
+                uint32_t c0 = a.child[s0], c1 = a.child[s0 + 1];
+                if (sib_key(a, c0) < sib_key(a, c1)) { uint32_t t = c0; c0 = c1; c1 = t; }
+                fc = c0;
+                a.up[c0] = make_uint2(c1, g);
+                a.up[c1] = make_uint2(kNil, g);
+            } else if (cnt > 2) {
+                defer = true;  // first_child written by the sort kernels
+            }
+            a.dn[g] = make_uint2(fc, w);
+        }
     }
-    const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
-    uint32_t fc = kNil;
-    if (cnt == 1) {
-        const uint32_t c0 = a.child[s0];
-        fc = c0;
-        a.up[c0] = make_uint2(kNil, g);
-    } else if (cnt == 2) {
-        uint32_t c0 = a.child[s0], c1 = a.child[s0 + 1];
-        if (sib_key(a, c0) < sib_key(a, c1)) { uint32_t t = c0; c0 = c1; c1 = t; }
-        fc = c0;
-        a.up[c0] = make_uint2(c1, g);
-        a.up[c1] = make_uint2(kNil, g);
-    } else if (cnt > 2) {
-        a.defer[atomicAdd(&a.ctl[0], 1u)] = g;  // first_child written by the sort kernels
-    }
-    a.dn[g] = make_uint2(fc, meta);
+    // deferred segments: one global atomic per block
+    uint32_t slot = 0;
+    if (defer) slot = atomicAdd(&nblk, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && nblk) bbase = atomicAdd(&a.ctl[C_NDEFER], nblk);
+    __syncthreads();
+    if (defer) a.defer[bbase + slot] = g;
 }
 
 // One wave per deferred segment of 3..64 children: rank = #siblings with a greater key, then
 // ds_permute scatters ids into rank order and shuffles hand each lane its successor.
-__global__ __launch_bounds__(kBlock) void k_sortmid(WaveArgs a) {
+__global__ __launch_bounds__(kBlock) void k_sortmid(TreeArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nw = (gridDim.x * kBlock) >> 6;
-    const uint32_t nd = a.ctl[0];
+    const uint32_t nd = a.ctl[C_NDEFER];
     for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6; i < nd; i += nw) {
         const uint32_t p = a.defer[i];
         const uint32_t s0 = a.cstart[p], cnt = a.cstart[p + 1] - s0;
         if (cnt > 64) {
-            if (lane == 0) a.bigl[atomicAdd(&a.ctl[1], 1u)] = p;
+            if (lane == 0) a.bigl[atomicAdd(&a.ctl[C_NBIG], 1u)] = p;
             continue;
         }
         const bool on = lane < cnt;
@@ -296,10 +677,10 @@ __global__ __launch_bounds__(kBlock) void k_sortmid(WaveArgs a) {
 // Bitonic sort (descending by key) of one sibling segment with the "flip" formulation: every
 // compare-exchange has the same direction, so the virtual -inf padding up to a power of two
 // never has to be stored.
-__global__ __launch_bounds__(kBigThreads) void k_sortbig(WaveArgs a) {
+__global__ __launch_bounds__(kBigThreads) void k_sortbig(TreeArgs a) {
     __shared__ uint64_t skey[kBigLds];
     __shared__ uint32_t sid[kBigLds];
-    const uint32_t nb = a.ctl[1];
+    const uint32_t nb = a.ctl[C_NBIG];
     for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
         const uint32_t p = a.bigl[bi];
         const uint32_t s0 = a.cstart[p], cnt = a.cstart[p + 1] - s0;
@@ -351,19 +732,10 @@ __global__ __launch_bounds__(kBigThreads) void k_sortbig(WaveArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Euler-tour walks (sublist list ranking).  Splitters: both arcs of every node whose wave slot
-// is a multiple of M (every document-start node is one).  Splitter s <-> node (s>>1)<<log2m,
-// arc (s&1) (0 = down, 1 = up).
-// ---------------------------------------------------------------------------------------------
-template <bool ORDER>
-__device__ __forceinline__ uint32_t arc_weight(uint32_t meta) {
-    if (ORDER) return (meta >> 30) & 1u;
-    return (meta & kVis) ? utf8_len(meta & kCpMask) : 0u;
-}
-
-template <bool ORDER>
-__global__ __launch_bounds__(kBlock) void k_walk1(WaveArgs a) {
+// Euler-tour walks (sublist list ranking).  Splitters: both arcs of every run slot that is a
+// multiple of M (every document-start run is one).  Splitter s <-> node (s>>1)<<log2m, arc
+// (s&1) (0 = down, 1 = up).
+__global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= a.S) return;
     const uint32_t m = a.log2m, mask = (1u << m) - 1u;
@@ -375,18 +747,18 @@ __global__ __launch_bounds__(kBlock) void k_walk1(WaveArgs a) {
         bool nup;
         if (!up) {
             const uint2 r = a.dn[v];
-            sum += arc_weight<ORDER>(r.y);
+            sum += r.y;
             if (r.x != kNil) { nv = r.x; nup = false; } else { nv = v; nup = true; }
         } else {
             const uint2 r = a.up[v];
             if (r.x != kNil) { nv = r.x; nup = false; }
             else if (r.y != kNil) { nv = r.y; nup = true; }
-            else break;  // up arc of the document start: end of this document's tour
+            else break;  // up arc of the document-start run: end of this document's tour
         }
         if ((nv & mask) == 0) { nxt = ((nv >> m) << 1) | (nup ? 1u : 0u); break; }
         v = nv;
         up = nup;
-        if (++steps > a.step_limit) { atomicOr(&a.ctl[2], 2u); break; }
+        if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
     }
     a.sw[s] = sum;
     a.snext[s] = nxt;
@@ -427,23 +799,23 @@ __global__ __launch_bounds__(kBlock) void k_wstep(const uint32_t* __restrict__ v
     pout[s] = q;
 }
 
-// Single workgroup: per-document length, 16-aligned text offsets, leaf offsets.
-template <bool ORDER>
-__global__ __launch_bounds__(1024) void k_doctotals(WaveArgs a, const uint32_t* __restrict__ spref) {
+// Single workgroup: per-document length, aligned output offsets, leaf offsets.
+__global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a, const uint32_t* __restrict__ spref) {
     __shared__ uint64_t st[1024];
     __shared__ uint32_t sl[1024];
     uint64_t carry_t = 0;
     uint32_t carry_l = 0;
+    const uint64_t am = (uint64_t)a.align - 1u;
     for (uint32_t d0 = 0; d0 < a.ndocs; d0 += 1024) {
         const uint32_t d = d0 + threadIdx.x;
         uint32_t tl = 0;
         if (d < a.ndocs) {
             const uint2 doc = a.docs[d];
-            tl = ORDER ? doc.y : spref[((doc.x >> a.log2m) << 1) | 1u];
+            tl = spref[((doc.x >> a.log2m) << 1) | 1u];
             a.tlen[d] = tl;
         }
-        const uint64_t sz = ORDER ? (uint64_t)tl : (((uint64_t)tl + 15u) & ~15ull);
-        const uint32_t nl = ORDER ? 0u : (tl + kLeaf - 1u) / kLeaf;
+        const uint64_t sz = ((uint64_t)tl + am) & ~am;
+        const uint32_t nl = a.align > 1 ? (tl + kLeaf - 1u) / kLeaf : 0u;
         st[threadIdx.x] = sz;
         sl[threadIdx.x] = nl;
         __syncthreads();
@@ -466,65 +838,29 @@ __global__ __launch_bounds__(1024) void k_doctotals(WaveArgs a, const uint32_t* 
     if (threadIdx.x == 0) {
         a.toff[a.ndocs] = carry_t;
         a.loff[a.ndocs] = carry_l;
-        if (carry_t > a.text_cap) atomicOr(&a.ctl[2], 4u);
+        if (carry_t > a.text_cap) atomicOr(&a.ctl[C_ERR], 4u);
     }
 }
 
-template <bool ORDER>
-__global__ __launch_bounds__(kBlock) void k_walk2(WaveArgs a, const uint32_t* __restrict__ spref) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= a.S) return;
-    if (a.ctl[2] & 4u) return;  // text capacity exceeded: never write out of bounds
+// Re-walk: every run passed on a down arc gets its offset inside its document.
+__global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __restrict__ spref) {
+    const uint32_t s0 = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = s0 < a.S;
+    const uint32_t s = live ? s0 : a.S - 1;  // keep every lane for the wave reduction below
     const uint32_t m = a.log2m, mask = (1u << m) - 1u;
     uint32_t v = (s >> 1) << m;
     bool up = s & 1u;
     const uint32_t d = a.chunk_doc[v >> m];
-    const uint64_t obase = a.toff[d];
-    const uint64_t lim = a.toff[d + 1] - obase;  // this document's own output range
-    const uint32_t docbase = a.docs[d].x;
     uint32_t off = spref[s];
-    uint32_t steps = 0, items = 0;
-    uint8_t* __restrict__ text = a.text;
-    uint32_t* __restrict__ order = reinterpret_cast<uint32_t*>(a.text);
-    for (;;) {
+    uint32_t steps = 0, runs = 0;
+    for (; live;) {
         uint32_t nv;
         bool nup;
         if (!up) {
             const uint2 r = a.dn[v];
-            const uint32_t meta = r.y;
-            items += (meta >> 30) & 1u;
-            if (ORDER) {
-                if (meta & kItem) {
-                    if (off >= lim) { atomicOr(&a.ctl[2], 8u); break; }
-                    order[obase + off++] = v - docbase;
-                }
-            } else if (meta & kVis) {
-                const uint32_t c = meta & kCpMask;
-                if (off + (uint64_t)utf8_len(c) > lim) {
-                    atomicOr(&a.ctl[2], 8u);
-                    break;
-                }
-                uint8_t* o = text + obase + off;
-                if (c < 0x80u) {
-                    o[0] = (uint8_t)c;
-                    off += 1;
-                } else if (c < 0x800u) {
-                    o[0] = (uint8_t)(0xC0u | (c >> 6));
-                    o[1] = (uint8_t)(0x80u | (c & 63u));
-                    off += 2;
-                } else if (c < 0x10000u) {
-                    o[0] = (uint8_t)(0xE0u | (c >> 12));
-                    o[1] = (uint8_t)(0x80u | ((c >> 6) & 63u));
-                    o[2] = (uint8_t)(0x80u | (c & 63u));
-                    off += 3;
-                } else {
-                    o[0] = (uint8_t)(0xF0u | (c >> 18));
-                    o[1] = (uint8_t)(0x80u | ((c >> 12) & 63u));
-                    o[2] = (uint8_t)(0x80u | ((c >> 6) & 63u));
-                    o[3] = (uint8_t)(0x80u | (c & 63u));
-                    off += 4;
-                }
-            }
+            a.roff[v] = off;
+            off += r.y;
+            ++runs;
             if (r.x != kNil) { nv = r.x; nup = false; } else { nv = v; nup = true; }
         } else {
             const uint2 r = a.up[v];
@@ -535,9 +871,9 @@ __global__ __launch_bounds__(kBlock) void k_walk2(WaveArgs a, const uint32_t* __
         if ((nv & mask) == 0) break;
         v = nv;
         up = nup;
-        if (++steps > a.step_limit) { atomicOr(&a.ctl[2], 2u); break; }
+        if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
     }
-    if (items) atomicAdd(&a.icnt[d], items);
+    doc_add(a.icnt, d, runs);  // reachability: every run of the document must be visited
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -590,7 +926,7 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
     return h;
 }
 
-__global__ __launch_bounds__(kBlock) void k_leafhash(WaveArgs a, uint32_t leaf_cap) {
+__global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_cap) {
     const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
     if (L >= leaf_cap || L >= a.loff[a.ndocs]) return;
     uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
@@ -604,10 +940,10 @@ __global__ __launch_bounds__(kBlock) void k_leafhash(WaveArgs a, uint32_t leaf_c
     a.leafh[L] = xxh64_aligned(a.text + a.toff[d] + (uint64_t)j * kLeaf, len, 0);
 }
 
-__global__ __launch_bounds__(kBlock) void k_docdigest(WaveArgs a, bool hash) {
+__global__ __launch_bounds__(kBlock) void k_docdigest(TreeArgs a, bool hash) {
     const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
     if (d >= a.ndocs) return;
-    if (a.icnt[d] != a.docs[d].y) atomicOr(&a.ctl[2], 16u);  // unreachable items: a cycle
+    if (a.icnt[d] != a.docs[d].y + 1u) atomicOr(&a.ctl[C_ERR], 16u);  // unreachable runs: a cycle
     if (!hash) return;
     const uint32_t l0 = a.loff[d], l1 = a.loff[d + 1];
     a.dig[d] = xxh64_aligned(reinterpret_cast<const uint8_t*>(a.leafh + l0), (l1 - l0) * 8u,
@@ -706,10 +1042,14 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
+    dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(tsum_h_); dfree(tsum_w_);
+    dfree(doc_runs_); dfree(doc_rank0_); dfree(run_base_); dfree(doc_pend_); dfree(docs1_);
+    dfree(chunk_doc1_); dfree(r_head_); dfree(r_pstart_); dfree(r_lam_); dfree(r_ag_);
+    dfree(r_parent_); dfree(r_w_); dfree(roff_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(ctl_); dfree(dn_); dfree(up_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
-    dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(icnt_); dfree(loff_); dfree(toff_); dfree(dig_);
-    dfree(leafh_); dfree(text_);
+    dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(icnt_); dfree(loff_); dfree(toff_);
+    dfree(dig_); dfree(leafh_); dfree(text_);
     if (host_ctl_) (void)hipHostFree(host_ctl_);
     if (host_dig_) (void)hipHostFree(host_dig_);
     if (host_len_) (void)hipHostFree(host_len_);
@@ -723,9 +1063,9 @@ int Engine::fail(const char* what, hipError_t e) {
     return CRDT_HIP_EDEVICE;
 }
 
-#define HIPCHK(expr, what)                         \
-    do {                                           \
-        hipError_t _e = (expr);                    \
+#define HIPCHK(expr, what)                           \
+    do {                                             \
+        hipError_t _e = (expr);                      \
         if (_e != hipSuccess) return fail(what, _e); \
     } while (0)
 
@@ -738,7 +1078,7 @@ std::string Engine::init(int dev) {
     if ((e = hipSetDevice(dev)) != hipSuccess) return hipGetErrorString(e);
     if ((e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess)
         return hipGetErrorString(e);
-    ev_.resize(2 * S_N + 2);
+    ev_.resize(2 * S_N + 4);
     for (hipEvent_t& x : ev_)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hipGetErrorString(e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&host_ctl_), 64)) != hipSuccess)
@@ -758,6 +1098,10 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     for (uint32_t d = 0; d < docs.size(); ++d) {
         const uint64_t ds = (docs[d].n + 1 + M - 1) / M * M;
         if (ds > hard_max) { err = "document too large for one wave"; return CRDT_HIP_ERANGE; }
+        if (docs[d].text_cap >= (1ull << 32)) {
+            err = "document text of 4 GiB or more is not supported";
+            return CRDT_HIP_ERANGE;
+        }
         if (L.waves.empty() || (uint64_t)L.waves.back().nslots + ds > max_wave_slots) {
             Wave w{};
             w.first_doc = d;
@@ -857,41 +1201,31 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 
 int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     const uint64_t slots = w.nslots;
-    if (slots > cap_slots_) {
-        dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_);
-        dfree(scan_sums_); dfree(dn_); dfree(up_);
-        HIPCHK(dalloc(&deg_, slots + 16), "hipMalloc deg");
-        HIPCHK(hipMemset(deg_, 0, (slots + 16) * 4), "memset deg");
-        HIPCHK(dalloc(&cstart_, slots + 16), "hipMalloc cstart");
-        HIPCHK(dalloc(&child_, slots), "hipMalloc child");
-        HIPCHK(dalloc(&defer_, slots / 3 + 64), "hipMalloc defer");
-        HIPCHK(dalloc(&bigl_, slots / 65 + 64), "hipMalloc bigl");
-        HIPCHK(dalloc(&scan_sums_, slots / kScanTile + 2), "hipMalloc scan sums");
-        HIPCHK(dalloc(&dn_, slots), "hipMalloc dn");
-        HIPCHK(dalloc(&up_, slots), "hipMalloc up");
-        cap_slots_ = slots;
+    if (slots > cap_slots0_) {
+        dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(tsum_h_); dfree(tsum_w_);
+        HIPCHK(dalloc(&jump_, slots + 64), "hipMalloc jump");
+        HIPCHK(dalloc(&hbits_, slots / 64 + 2), "hipMalloc hbits");
+        HIPCHK(dalloc(&hrank_, slots / 64 + 2), "hipMalloc hrank");
+        HIPCHK(dalloc(&tsum_h_, slots / kScanTile + 2), "hipMalloc tsum_h");
+        HIPCHK(dalloc(&tsum_w_, slots / kScanTile + 2), "hipMalloc tsum_w");
+        cap_slots0_ = slots;
     }
     if (!ctl_) HIPCHK(dalloc(&ctl_, 16), "hipMalloc ctl");
-    const uint64_t S = 2 * (slots >> log2m);
-    if (S > cap_splitters_) {
-        dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_); dfree(v1_); dfree(p0_); dfree(p1_);
-        HIPCHK(dalloc(&sw_, S), "hipMalloc sw");
-        HIPCHK(dalloc(&snext_, S), "hipMalloc snext");
-        HIPCHK(dalloc(&pred_, S), "hipMalloc pred");
-        HIPCHK(dalloc(&v0_, S), "hipMalloc v0");
-        HIPCHK(dalloc(&v1_, S), "hipMalloc v1");
-        HIPCHK(dalloc(&p0_, S), "hipMalloc p0");
-        HIPCHK(dalloc(&p1_, S), "hipMalloc p1");
-        cap_splitters_ = S;
-    }
     if (w.ndocs + 1 > cap_docs_) {
         dfree(tlen_); dfree(icnt_); dfree(loff_); dfree(toff_); dfree(dig_);
-        HIPCHK(dalloc(&tlen_, w.ndocs + 1), "hipMalloc tlen");
-        HIPCHK(dalloc(&icnt_, w.ndocs + 1), "hipMalloc icnt");
-        HIPCHK(dalloc(&loff_, w.ndocs + 1), "hipMalloc loff");
-        HIPCHK(dalloc(&toff_, w.ndocs + 1), "hipMalloc toff");
-        HIPCHK(dalloc(&dig_, w.ndocs + 1), "hipMalloc dig");
-        cap_docs_ = w.ndocs + 1;
+        dfree(doc_runs_); dfree(doc_rank0_); dfree(run_base_); dfree(doc_pend_); dfree(docs1_);
+        const uint64_t nd = w.ndocs + 1;
+        HIPCHK(dalloc(&tlen_, nd), "hipMalloc tlen");
+        HIPCHK(dalloc(&icnt_, nd), "hipMalloc icnt");
+        HIPCHK(dalloc(&loff_, nd), "hipMalloc loff");
+        HIPCHK(dalloc(&toff_, nd), "hipMalloc toff");
+        HIPCHK(dalloc(&dig_, nd), "hipMalloc dig");
+        HIPCHK(dalloc(&doc_runs_, nd), "hipMalloc doc_runs");
+        HIPCHK(dalloc(&doc_rank0_, nd), "hipMalloc doc_rank0");
+        HIPCHK(dalloc(&run_base_, nd), "hipMalloc run_base");
+        HIPCHK(dalloc(&doc_pend_, nd), "hipMalloc doc_pend");
+        HIPCHK(dalloc(&docs1_, nd), "hipMalloc docs1");
+        cap_docs_ = nd;
     }
     const uint64_t tb = std::max<uint64_t>(w.text_cap, w.order_cap * 4) + 64;
     if (tb > cap_text_) {
@@ -914,54 +1248,172 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     return CRDT_HIP_OK;
 }
 
+// Level-1 scratch, sized by the run slots of the wave (known after k_tile_top).
+int Engine::ensure_runs(uint64_t rslots) {
+    if (rslots > cap_runs_) {
+        dfree(chunk_doc1_); dfree(r_head_); dfree(r_pstart_); dfree(r_lam_); dfree(r_ag_);
+        dfree(r_parent_); dfree(r_w_); dfree(roff_);
+        dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_);
+        dfree(scan_sums_); dfree(dn_); dfree(up_);
+        const uint64_t r = rslots + (rslots >> 3) + 4096;  // headroom against regrowth
+        HIPCHK(dalloc(&chunk_doc1_, (r >> log2m) + 2), "hipMalloc chunk_doc1");
+        HIPCHK(dalloc(&r_head_, r), "hipMalloc r_head");
+        HIPCHK(dalloc(&r_pstart_, r), "hipMalloc r_pstart");
+        HIPCHK(dalloc(&r_lam_, r), "hipMalloc r_lam");
+        HIPCHK(dalloc(&r_ag_, r), "hipMalloc r_ag");
+        HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
+        HIPCHK(dalloc(&r_w_, r), "hipMalloc r_w");
+        HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
+        HIPCHK(dalloc(&deg_, r + 16), "hipMalloc deg");
+        HIPCHK(hipMemset(deg_, 0, (r + 16) * 4), "memset deg");
+        HIPCHK(dalloc(&cstart_, r + 16), "hipMalloc cstart");
+        HIPCHK(dalloc(&child_, r), "hipMalloc child");
+        HIPCHK(dalloc(&defer_, r / 3 + 64), "hipMalloc defer");
+        HIPCHK(dalloc(&bigl_, r / 65 + 64), "hipMalloc bigl");
+        HIPCHK(dalloc(&scan_sums_, r / kScanTile + 2), "hipMalloc scan sums");
+        HIPCHK(dalloc(&dn_, r), "hipMalloc dn");
+        HIPCHK(dalloc(&up_, r), "hipMalloc up");
+        cap_runs_ = r;
+    }
+    const uint64_t S = 2 * (cap_runs_ >> log2m) + 2;
+    if (S > cap_splitters_) {
+        dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_); dfree(v1_); dfree(p0_); dfree(p1_);
+        HIPCHK(dalloc(&sw_, S), "hipMalloc sw");
+        HIPCHK(dalloc(&snext_, S), "hipMalloc snext");
+        HIPCHK(dalloc(&pred_, S), "hipMalloc pred");
+        HIPCHK(dalloc(&v0_, S), "hipMalloc v0");
+        HIPCHK(dalloc(&v1_, S), "hipMalloc v1");
+        HIPCHK(dalloc(&p0_, S), "hipMalloc p0");
+        HIPCHK(dalloc(&p1_, S), "hipMalloc p1");
+        cap_splitters_ = S;
+    }
+    return CRDT_HIP_OK;
+}
+
 int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
                      std::vector<uint32_t>& stage_launches) {
-    WaveArgs a{};
-    a.nslots = w.nslots;
+    hipStream_t s = stream;
+    const bool ord = mode == ORDER;
+    const uint32_t ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
+
+    L0Args a0{};
+    a0.nslots = w.nslots;
+    a0.log2m = log2m;
+    a0.ndocs = w.ndocs;
+    a0.mode = ord ? 1u : 0u;
+    a0.chunk_doc = L.chunk_doc + (w.slot0 >> log2m);
+    a0.docs = L.docs_rel + w.first_doc;
+    a0.in_parent = L.parent + w.slot0;
+    a0.in_lamport = L.lamport + w.slot0;
+    a0.in_agent = L.agent + w.slot0;
+    a0.in_deleted = L.deleted + w.slot0;
+    a0.in_cp = L.cp + w.slot0;
+    a0.jump = jump_;
+    a0.hbits = hbits_;
+    a0.hrank = hrank_;
+    a0.tsum_h = tsum_h_;
+    a0.tsum_w = tsum_w_;
+    a0.ntiles = ntiles;
+    a0.doc_runs = doc_runs_;
+    a0.doc_rank0 = doc_rank0_;
+    a0.run_base = run_base_;
+    a0.doc_pend = doc_pend_;
+    a0.docs1 = docs1_;
+    a0.toff = toff_;
+    a0.text = text_;
+    a0.ctl = ctl_;
+
+#define BEGIN(st) HIPCHK(hipEventRecord(ev_[2 * (st)], s), "event record")
+#define END(st) HIPCHK(hipEventRecord(ev_[2 * (st) + 1], s), "event record")
+    // ---- level 0: runs -------------------------------------------------------------------
+    HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
+    HIPCHK(hipMemsetAsync(jump_, 0, w.nslots + 64ull, s), "memset jump");
+    HIPCHK(hipMemsetAsync(doc_runs_, 0, w.ndocs * 4ull, s), "memset doc_runs");
+    HIPCHK(hipMemsetAsync(icnt_, 0, w.ndocs * 4ull, s), "memset icnt");
+    BEGIN(S_JUMP);
+    k_jump<<<grid_for(w.nslots), kBlock, 0, s>>>(a0);
+    END(S_JUMP);
+    BEGIN(S_TREDUCE);
+    k_tile_reduce<<<ntiles, kBlock, 0, s>>>(a0);
+    END(S_TREDUCE);
+    BEGIN(S_TTOP);
+    k_tile_top<<<1, 1024, 0, s>>>(a0);
+    END(S_TTOP);
+    HIPCHK(hipGetLastError(), "level-0 launch");
+    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
+    HIPCHK(hipStreamSynchronize(s), "level-0 sync");
+    const uint32_t rslots = host_ctl_[C_RSLOTS];
+    const uint32_t rmax = host_ctl_[C_RMAX];
+    if (host_ctl_[C_ERR] & 1u) {
+        err = "malformed op log: parent id out of range";
+        return CRDT_HIP_EBADLOG;
+    }
+    int rc = ensure_runs(rslots);
+    if (rc) return rc;
+    a0.r_head = r_head_;
+    a0.r_pstart = r_pstart_;
+    a0.r_lam = r_lam_;
+    a0.r_ag = r_ag_;
+    a0.r_parent = r_parent_;
+    a0.r_w = r_w_;
+    a0.chunk_doc1 = chunk_doc1_;
+    a0.roff = roff_;
+    BEGIN(S_TAPPLY);
+    k_tile_apply<<<ntiles, kBlock, 0, s>>>(a0);
+    END(S_TAPPLY);
+    const uint32_t nchunks1 = rslots >> log2m;
+    BEGIN(S_RPARENT);
+    k_chunk_doc1<<<grid_for(nchunks1, 1024), 1024, 0, s>>>(a0, nchunks1);
+    k_run_parent<<<grid_for(rslots), kBlock, 0, s>>>(a0, rslots);
+    END(S_RPARENT);
+
+    // ---- level 1: the tree of runs -------------------------------------------------------
+    TreeArgs a{};
+    a.nslots = rslots;
     a.log2m = log2m;
     a.ndocs = w.ndocs;
-    a.S = 2 * (w.nslots >> log2m);
-    a.step_limit = 2u * w.nslots + 4u;
-    a.chunk_doc = L.chunk_doc + (w.slot0 >> log2m);
-    a.docs = L.docs_rel + w.first_doc;
-    a.in_parent = L.parent + w.slot0;
-    a.in_lamport = L.lamport + w.slot0;
-    a.in_agent = L.agent + w.slot0;
-    a.in_deleted = L.deleted + w.slot0;
-    a.in_cp = L.cp + w.slot0;
+    a.S = 2 * (rslots >> log2m);
+    a.step_limit = 2u * rslots + 4u;
+    a.chunk_doc = chunk_doc1_;
+    a.docs = docs1_;
+    a.in_parent = r_parent_;
+    a.in_lamport = r_lam_;
+    a.in_agent = r_ag_;
+    a.in_w = r_w_;
     a.deg = deg_; a.cstart = cstart_; a.child = child_; a.dn = dn_; a.up = up_;
     a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;
+    a.roff = roff_;
     a.tlen = tlen_; a.icnt = icnt_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.dig = dig_;
     a.text = text_;
-    a.text_cap = mode == ORDER ? w.order_cap : cap_text_ - 64;
-    const bool ord = mode == ORDER;
-    const uint32_t gs = grid_for(w.nslots), gS = grid_for(a.S);
-    const uint32_t nb = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
-    hipStream_t s = stream;
+    a.text_cap = ord ? w.order_cap : cap_text_ - 64;
+    a.align = ord ? 1u : 16u;
+    const uint32_t gs = grid_for(rslots), gS = grid_for(a.S);
+    const uint32_t nb = (uint32_t)((rslots + kScanTile - 1) / kScanTile);
 
-#define REC(i) HIPCHK(hipEventRecord(ev_[i], s), "event record")
-    HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
-    HIPCHK(hipMemsetAsync(icnt_, 0, w.ndocs * 4ull, s), "memset icnt");
-    REC(0);
+    BEGIN(S_COUNT);
     k_count<<<gs, kBlock, 0, s>>>(a);
-    REC(1);
-    k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, w.nslots, scan_sums_);
-    k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, w.nslots);
-    k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, w.nslots, scan_sums_, cstart_);
-    REC(2);
+    END(S_COUNT);
+    BEGIN(S_SCAN);
+    k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, rslots, scan_sums_);
+    k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, rslots);
+    k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, rslots, scan_sums_, cstart_);
+    END(S_SCAN);
+    BEGIN(S_PLACE);
     k_place<<<gs, kBlock, 0, s>>>(a);
-    REC(3);
+    END(S_PLACE);
+    BEGIN(S_LINK);
     k_link<<<gs, kBlock, 0, s>>>(a);
     k_sortmid<<<kMidGrid, kBlock, 0, s>>>(a);
     k_sortbig<<<kBigGrid, kBigThreads, 0, s>>>(a);
-    REC(4);
-    if (ord) k_walk1<true><<<gS, kBlock, 0, s>>>(a);
-    else k_walk1<false><<<gS, kBlock, 0, s>>>(a);
-    REC(5);
+    END(S_LINK);
+    BEGIN(S_WALK1);
+    k_walk1<<<gS, kBlock, 0, s>>>(a);
+    END(S_WALK1);
+    BEGIN(S_RANK);
     HIPCHK(hipMemsetAsync(pred_, 0xFF, a.S * 4ull, s), "memset pred");
     k_pred<<<gS, kBlock, 0, s>>>(snext_, a.S, pred_);
     k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, a.S, v0_, p0_);
-    const uint32_t rounds = ceil_log2(std::max<uint32_t>(w.max_splitters_per_doc, 2));
+    const uint32_t rounds = ceil_log2(std::max<uint32_t>(2 * (rmax >> log2m), 2));
     uint32_t *vi = v0_, *pi = p0_, *vo = v1_, *po = p1_;
     for (uint32_t r = 0; r < rounds; ++r) {
         k_wstep<<<gS, kBlock, 0, s>>>(vi, pi, a.S, vo, po);
@@ -969,40 +1421,41 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
         std::swap(pi, po);
     }
     const uint32_t* spref = vi;
-    REC(6);
-    if (ord) {
-        k_doctotals<true><<<1, 1024, 0, s>>>(a, spref);
-        k_walk2<true><<<gS, kBlock, 0, s>>>(a, spref);
-    } else {
-        k_doctotals<false><<<1, 1024, 0, s>>>(a, spref);
-        k_walk2<false><<<gS, kBlock, 0, s>>>(a, spref);
-    }
-    REC(7);
+    END(S_RANK);
+    BEGIN(S_WALK2);
+    k_doctotals<<<1, 1024, 0, s>>>(a, spref);
+    k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
+    END(S_WALK2);
+
+    // ---- expansion + digest --------------------------------------------------------------
+    BEGIN(S_EXPAND);
+    k_expand<<<ntiles, kBlock, 0, s>>>(a0);
+    END(S_EXPAND);
+    BEGIN(S_DIGEST);
     if (!ord) k_leafhash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
     k_docdigest<<<grid_for(w.ndocs), kBlock, 0, s>>>(a, !ord);
-    REC(8);
-#undef REC
+    END(S_DIGEST);
     HIPCHK(hipGetLastError(), "kernel launch");
     HIPCHK(hipMemcpyAsync(host_len_ + w.first_doc, tlen_, w.ndocs * 4ull, hipMemcpyDeviceToHost, s),
            "copy lens");
     if (!ord)
         HIPCHK(hipMemcpyAsync(host_dig_ + w.first_doc, dig_, w.ndocs * 8ull, hipMemcpyDeviceToHost, s),
                "copy digests");
-    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 16, hipMemcpyDeviceToHost, s), "copy ctl");
+    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "merge wave");
-    static const int stage_of_interval[8] = {S_COUNT, S_SCAN, S_PLACE, S_LINK,
-                                             S_WALK1, S_RANK, S_WALK2, S_DIGEST};
-    static const uint32_t launches[8] = {1, 3, 1, 3, 1, 0, 2, 2};
-    for (int i = 0; i < 8; ++i) {
+    const uint32_t launches[S_N] = {1, 1, 1, 1, 2, 1, 3, 1, 3, 1, 2 + rounds, 2, 1, ord ? 1u : 2u};
+    for (int i = 0; i < S_N; ++i) {
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, ev_[i], ev_[i + 1]), "event time");
-        stage_ms[stage_of_interval[i]] += ms;
-        stage_launches[stage_of_interval[i]] += launches[i];
+        HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");
+        stage_ms[i] += ms;
+        stage_launches[i] += launches[i];
     }
-    stage_launches[S_RANK] += 2 + rounds;
-    if (host_ctl_[2]) {
-        (void)hipMemset(deg_, 0, (cap_slots_ + 16) * 4);  // restore the all-zero invariant
-        err = "malformed op log detected on device (flags " + std::to_string(host_ctl_[2]) + ")";
+#undef BEGIN
+#undef END
+    runs_ += host_ctl_[C_HTOTAL];
+    if (host_ctl_[C_ERR]) {
+        (void)hipMemset(deg_, 0, (cap_runs_ + 16) * 4);  // restore the all-zero invariant
+        err = "malformed op log detected on device (flags " + std::to_string(host_ctl_[C_ERR]) + ")";
         return CRDT_HIP_EBADLOG;
     }
     return CRDT_HIP_OK;
@@ -1018,26 +1471,26 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
     std::vector<float> stage_ms(S_N, 0.f);
     std::vector<uint32_t> stage_launches(S_N, 0);
     const uint32_t ndocs = (uint32_t)L.docs.size();
-    HIPCHK(hipEventRecord(ev_[2 * S_N], stream), "event record");
+    runs_ = 0;
+    HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
     for (const Wave& w : L.waves) {
         int rc = ensure_scratch(w, ndocs);
         if (rc) return rc;
         rc = run_wave(L, w, mode, stage_ms, stage_launches);
         if (rc) return rc;
         if (text_out) {
-            uint64_t total = 0;
             std::vector<uint64_t> offs(w.ndocs + 1);
             HIPCHK(hipMemcpy(offs.data(), toff_, (w.ndocs + 1) * 8ull, hipMemcpyDeviceToHost),
                    "copy offsets");
-            total = offs[w.ndocs] * (mode == ORDER ? 4 : 1);
+            const uint64_t total = offs[w.ndocs] * (mode == ORDER ? 4 : 1);
             text_out->resize(total);
             if (total)
                 HIPCHK(hipMemcpy(text_out->data(), text_, total, hipMemcpyDeviceToHost), "copy text");
             if (text_offsets) *text_offsets = offs;
         }
     }
-    HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
-    HIPCHK(hipEventSynchronize(ev_[2 * S_N + 1]), "event sync");
+    HIPCHK(hipEventRecord(ev_[2 * S_N + 2], stream), "event record");
+    HIPCHK(hipEventSynchronize(ev_[2 * S_N + 2]), "event sync");
     uint64_t text_bytes = 0;
     for (uint32_t d = 0; d < ndocs; ++d) {
         if (lens) lens[d] = host_len_[d];
@@ -1049,6 +1502,7 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         st->items = L.items;
         st->docs = ndocs;
         st->text_bytes = text_bytes;
+        st->runs = runs_;
         st->waves = (uint32_t)L.waves.size();
         st->nstages = S_N;
         for (int i = 0; i < S_N; ++i) {
@@ -1056,7 +1510,7 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
             st->stage_launches[i] = stage_launches[i];
         }
         float tot = 0;
-        HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N], ev_[2 * S_N + 1]), "event time");
+        HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N + 1], ev_[2 * S_N + 2]), "event time");
         st->total_ns = (uint64_t)((double)tot * 1e6);
     }
     return CRDT_HIP_OK;

@@ -86,22 +86,36 @@ public:
                   uint64_t seed);
 
 private:
-    // scratch, grown on demand
-    uint64_t cap_slots_ = 0, cap_splitters_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
+    // level-0 scratch (per slot / per tile), grown on demand
+    uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
+    uint8_t* jump_ = nullptr;
+    uint64_t* hbits_ = nullptr;
+    uint32_t *hrank_ = nullptr, *tsum_h_ = nullptr, *tsum_w_ = nullptr;
+    // per document
+    uint32_t *doc_runs_ = nullptr, *doc_rank0_ = nullptr, *run_base_ = nullptr,
+             *doc_pend_ = nullptr;
+    uint2* docs1_ = nullptr;
+    uint32_t *tlen_ = nullptr, *icnt_ = nullptr, *loff_ = nullptr;
+    uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;
+    uint8_t* text_ = nullptr;
+    // level-1 scratch (per run slot), grown on demand
+    uint64_t cap_runs_ = 0, cap_splitters_ = 0;
+    uint32_t *chunk_doc1_ = nullptr, *r_head_ = nullptr, *r_pstart_ = nullptr, *r_lam_ = nullptr,
+             *r_parent_ = nullptr, *r_w_ = nullptr, *roff_ = nullptr;
+    uint16_t* r_ag_ = nullptr;
     uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
              *bigl_ = nullptr, *scan_sums_ = nullptr, *ctl_ = nullptr;
     uint2 *dn_ = nullptr, *up_ = nullptr;
     uint32_t *sw_ = nullptr, *snext_ = nullptr, *pred_ = nullptr, *v0_ = nullptr, *v1_ = nullptr,
              *p0_ = nullptr, *p1_ = nullptr;
-    uint32_t *tlen_ = nullptr, *icnt_ = nullptr, *loff_ = nullptr;
-    uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;
-    uint8_t* text_ = nullptr;
     uint32_t* host_ctl_ = nullptr;       // pinned
     uint64_t* host_dig_ = nullptr;       // pinned
     uint32_t* host_len_ = nullptr;       // pinned
     uint64_t cap_host_docs_ = 0;
+    uint64_t runs_ = 0;
     std::vector<hipEvent_t> ev_;
 
+    int ensure_runs(uint64_t rslots);
     int ensure_scratch(const Wave& w, uint32_t ndocs_total);
     int run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
                  std::vector<uint32_t>& stage_launches);

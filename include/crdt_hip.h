@@ -75,6 +75,7 @@ typedef struct {
     uint64_t items;        /* op-log items merged */
     uint64_t docs;         /* documents merged */
     uint64_t text_bytes;   /* merged bytes produced */
+    uint64_t runs;         /* runs (unary chains of consecutive items) the items collapsed to */
     uint32_t waves;        /* device waves the call was split into */
     uint32_t nstages;      /* valid entries in stage_ns / stage_launches */
     uint64_t stage_ns[16];
@@ -82,17 +83,23 @@ typedef struct {
     uint64_t total_ns;     /* first event to last event of the call */
 } crdt_hip_stats;
 
-/* Stage indices of crdt_hip_stats.stage_ns. */
+/* Stage indices of crdt_hip_stats.stage_ns (one HIP-event interval per kernel group). */
 enum {
-    CRDT_HIP_STAGE_COUNT = 0,   /* child counting per parent               */
-    CRDT_HIP_STAGE_SCAN = 1,    /* exclusive scan of child counts           */
-    CRDT_HIP_STAGE_PLACE = 2,   /* children scattered into parent segments  */
-    CRDT_HIP_STAGE_LINK = 3,    /* sibling sort + first-child/next-sibling  */
-    CRDT_HIP_STAGE_WALK1 = 4,   /* Euler-tour sublist sums                  */
-    CRDT_HIP_STAGE_RANK = 5,    /* ranking of the splitter lists            */
-    CRDT_HIP_STAGE_WALK2 = 6,   /* Euler-tour re-walk: UTF-8 scatter         */
-    CRDT_HIP_STAGE_DIGEST = 7,  /* per-document tree digest                 */
-    CRDT_HIP_NSTAGES = 8
+    CRDT_HIP_STAGE_JUMP = 0,     /* level 0: flag items with a non-consecutive child          */
+    CRDT_HIP_STAGE_TREDUCE = 1,  /* level 0: per-tile run-head counts and weight sums         */
+    CRDT_HIP_STAGE_TTOP = 2,     /* level 0: tile bases, per-document run bases               */
+    CRDT_HIP_STAGE_TAPPLY = 3,   /* level 0: rank bitvector + run records                     */
+    CRDT_HIP_STAGE_RPARENT = 4,  /* level 0: parent run and weight of every run               */
+    CRDT_HIP_STAGE_COUNT = 5,    /* level 1: child count per parent run                       */
+    CRDT_HIP_STAGE_SCAN = 6,     /* level 1: exclusive scan of child counts                   */
+    CRDT_HIP_STAGE_PLACE = 7,    /* level 1: children scattered into parent segments          */
+    CRDT_HIP_STAGE_LINK = 8,     /* level 1: sibling sort + first-child / next-sibling        */
+    CRDT_HIP_STAGE_WALK1 = 9,    /* level 1: Euler-tour sublist sums                          */
+    CRDT_HIP_STAGE_RANK = 10,    /* level 1: ranking of the splitter lists                    */
+    CRDT_HIP_STAGE_WALK2 = 11,   /* level 1: Euler-tour re-walk, run offsets                  */
+    CRDT_HIP_STAGE_EXPAND = 12,  /* items -> UTF-8 at run offset + in-run prefix              */
+    CRDT_HIP_STAGE_DIGEST = 13,  /* per-document tree digest                                  */
+    CRDT_HIP_NSTAGES = 14
 };
 
 /* ---- library / context ----------------------------------------------------------------- */
