@@ -45,10 +45,8 @@ PIPE_B_PER_ITEM = 117.0
 # "s" = survivor (visible UTF-8) bytes per slot is added where the kernel touches the text.
 KERNEL_BYTES = {
     "jump": (4.0, 0.0),          # parent
-    "tile_reduce": (10.0, 0.0),  # parent, jump flag, cp, deleted
-    "tile_top": (0.0, 0.0),
-    "tile_apply": (10.19, 20.0),  # as tile_reduce + head bits/ranks; run records
-    "run_parent": (0.0, 32.0),   # run head/prefix/parent lookups, run weight + parent run
+    "tile_scan": (10.19, 8.0),   # parent, jump flag, cp, deleted; head bits/ranks; run records
+    "run_parent": (0.0, 28.0),   # run head/prefix, parent lookup (+ rank word); weight, parent
     "count": (0.0, 8.0),
     "scan": (0.0, 8.0),
     "place": (0.0, 12.0),

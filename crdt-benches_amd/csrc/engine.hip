@@ -44,28 +44,31 @@ constexpr uint32_t kNil = 0xFFFFFFFFu;
 constexpr uint32_t kCpMask = 0x001FFFFFu;
 constexpr int kBlock = 256;
 constexpr int kScanItems = 16;
-constexpr int kScanTile = kBlock * kScanItems;  // also the level-0 tile
+constexpr int kScanTile = kBlock * kScanItems;
+constexpr uint32_t kDocAlignLog2 = 6;  // slot-level document alignment (chunk table: 1/64)
+constexpr int kTileThreads = 1024;                       // level-0 tile: 1024 threads x 16 slots
+constexpr int kTile = kTileThreads * kScanItems;
 constexpr uint32_t kLeaf = 4096;
-constexpr int kMidGrid = 2048;
+constexpr int kMidGrid = 16384;
 constexpr int kBigGrid = 256;
 constexpr int kBigThreads = 1024;
 constexpr int kBigLds = 4096;
 
 // ctl words (device, zeroed per wave)
 enum Ctl {
-    C_NDEFER = 0,   // deferred sibling segments (3..64 children)
+    C_NDEFER = 0,   // deferred sibling segments (9..64 children)
     C_NBIG = 1,     // sibling segments with > 64 children
     C_ERR = 2,      // error bits: 1 bad parent, 2 walk overrun, 4 text overflow, 8 write out
-                    //   of range, 16 unreachable runs (cycle)
-    C_RSLOTS = 3,   // level-1 run slots of the wave
-    C_RMAX = 4,     // largest per-document run slot count
-    C_WTOTAL = 5,   // wave weight total
-    C_HTOTAL = 6,   // wave head total
+                    //   of range, 16 unreachable runs (cycle), 32 look-back timeout
+    C_RTOTAL = 3,   // runs of the wave
+    C_WTOTAL = 4,   // weight total of the wave
+    C_RMAX = 5,     // most runs in one document
+    C_VISITED = 6,  // runs visited by k_walk2
 };
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
-enum Stage { S_JUMP, S_TREDUCE, S_TTOP, S_TAPPLY, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK,
-             S_WALK1, S_RANK, S_WALK2, S_EXPAND, S_DIGEST, S_N };
+enum Stage { S_JUMP, S_TSCAN, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
+             S_WALK2, S_EXPAND, S_DIGEST, S_N };
 
 // ---------------------------------------------------------------------------------------------
 // wave / block primitives
@@ -108,20 +111,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* lds, u
     return off + inc - x;
 }
 
-// Per-document counter add, one atomic per wave when the wave's lanes share the document.
-__device__ __forceinline__ void doc_add(uint32_t* ctr, uint32_t d, uint32_t v) {
-    const uint64_t act = __ballot(v != 0);
-    if (!act) return;
-    const int first = __ffsll((unsigned long long)act) - 1;
-    const uint32_t d0 = (uint32_t)__shfl((int)d, first);
-    if (__all(v == 0 || d == d0)) {
-        const uint32_t tot = wave_sum(v);
-        if ((threadIdx.x & 63) == (uint32_t)first) atomicAdd(&ctr[d0], tot);
-    } else if (v) {
-        atomicAdd(&ctr[d], v);
-    }
-}
-
 __device__ __forceinline__ uint32_t utf8_len(uint32_t c) {
     return c < 0x80u ? 1u : c < 0x800u ? 2u : c < 0x10000u ? 3u : 4u;
 }
@@ -129,6 +118,9 @@ __device__ __forceinline__ uint32_t utf8_len(uint32_t c) {
 // ---------------------------------------------------------------------------------------------
 // Level 0: runs
 // ---------------------------------------------------------------------------------------------
+// Runs are numbered by global head rank within the wave (run rho = number of heads before its
+// head slot), so a run's weight is pstart[rho+1] - pstart[rho] and no per-document padding is
+// needed: documents are contiguous ranges of runs starting at doc_root[d].
 struct L0Args {
     uint32_t nslots, log2m, ndocs, mode;  // mode: 0 text, 1 order
     const uint32_t* chunk_doc;  // per M slots: wave-local document
@@ -141,22 +133,19 @@ struct L0Args {
     uint8_t* jump;              // per slot: has a non-consecutive child
     uint64_t* hbits;            // per 64 slots: run-head bits
     uint32_t* hrank;            // per 64 slots: heads before the word (wave-relative)
-    uint32_t* tsum_h;           // per tile: head count -> exclusive base
-    uint32_t* tsum_w;           // per tile: weight sum -> exclusive base
     uint32_t ntiles;
-    uint32_t* doc_runs;         // per document: runs (the document-start run included)
-    uint32_t* doc_rank0;        // per document: heads before the document
-    uint32_t* run_base;         // per document: first run slot (multiple of M)
-    uint32_t* doc_pend;         // per document: weight prefix at the document's end
-    uint2* docs1;               // per document {run_base, runs - 1}: level-1 document table
-    uint32_t* r_head;           // per run slot: head slot
-    uint32_t* r_pstart;         // per run slot: weight prefix at the head
-    uint32_t* r_lam;
-    uint16_t* r_ag;
-    uint32_t* r_parent;         // per run slot: parent run, document-local
-    uint32_t* r_w;              // per run slot: weight
-    uint32_t* chunk_doc1;       // per M run slots: document
-    const uint32_t* roff;       // per run slot: offset of the run in its document (level 1)
+    uint64_t* look;             // per tile: 4 look-back granules {epoch, value}
+    uint32_t* ticket;           // tile ticket counter (zeroed per launch)
+    uint32_t* tile_exw;         // per 4096-slot sub-tile: exclusive weight prefix (k_expand)
+    uint32_t epoch;             // nonzero, unique per launch
+    uint32_t* doc_root;         // per document: its document-start run
+    uint32_t* doc_p0;           // per document: weight prefix at its start
+    uint32_t* r_head;           // per run: head slot
+    uint32_t* r_pstart;         // per run: weight prefix at the head
+    uint32_t* r_parent;         // per run: parent run (kNil for a document-start run)
+    uint32_t* r_w;              // per run: weight
+    uint64_t* r_key;            // per run: sibling key (lamport, agent) of its head
+    const uint32_t* roff;       // per run: offset of the run inside its document (level 1)
     const uint64_t* toff;       // per document: output offset
     uint8_t* text;
     uint32_t* ctl;
@@ -237,87 +226,51 @@ __device__ __forceinline__ void load_slots16(const L0Args& a, uint32_t gs, bool 
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
+// 16 slots per thread (one document: 16 | M), 4 x 16-byte parent loads.
 __global__ __launch_bounds__(kBlock) void k_jump(L0Args a) {
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.nslots) return;
-    const uint2 doc = a.docs[a.chunk_doc[g >> a.log2m]];
-    const uint32_t local = g - doc.x;
-    if (local - 1u >= doc.y) return;
-    const uint32_t p = a.in_parent[g];
-    if (p <= doc.y && p != local - 1u && p != local) a.jump[doc.x + p] = 1;
-}
-
-__global__ __launch_bounds__(kBlock) void k_tile_reduce(L0Args a) {
-    __shared__ uint32_t lds[kBlock / 64];
-    const uint32_t gs = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
-    Slots16 s;
-    load_slots16(a, gs, true, s);
-    uint32_t W = 0;
+    const uint32_t gs = (blockIdx.x * kBlock + threadIdx.x) * kScanItems;
+    if (gs >= a.nslots) return;
+    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+    const uint32_t l0 = gs - doc.x;
+    if (l0 > doc.y) return;
+    const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) W += s.w[k];
-    const uint32_t H = __popc(s.hmask);
-    doc_add(a.doc_runs, s.d, H);
-    uint32_t th, tw;
-    block_excl_scan<kBlock / 64>(H, lds, th);
-    block_excl_scan<kBlock / 64>(W, lds, tw);
-    if (threadIdx.x == 0) {
-        a.tsum_h[blockIdx.x] = th;
-        a.tsum_w[blockIdx.x] = tw;
+    for (int q = 0; q < 4; ++q) {
+        const uint4 pp = pv[q];
+        const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t local = l0 + 4 * q + j, p = pa[j];
+            if ((local - 1u) < doc.y && p <= doc.y && p != local - 1u && p != local)
+                a.jump[doc.x + p] = 1;
+        }
     }
 }
 
-// Single workgroup: tile bases, per-document run bases (M-aligned), level-1 document table.
-__global__ __launch_bounds__(1024) void k_tile_top(L0Args a) {
-    __shared__ uint32_t lds[16];
-    __shared__ uint32_t mx;
-    if (threadIdx.x == 0) mx = 0;
-    uint32_t ch = 0, cw = 0;
-    for (uint32_t b0 = 0; b0 < a.ntiles; b0 += 1024) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint32_t h = i < a.ntiles ? a.tsum_h[i] : 0u;
-        const uint32_t w = i < a.ntiles ? a.tsum_w[i] : 0u;
-        uint32_t th, tw;
-        const uint32_t eh = block_excl_scan<16>(h, lds, th);
-        const uint32_t ew = block_excl_scan<16>(w, lds, tw);
-        if (i < a.ntiles) {
-            a.tsum_h[i] = ch + eh;
-            a.tsum_w[i] = cw + ew;
-        }
-        ch += th;
-        cw += tw;
-    }
-    const uint32_t M = 1u << a.log2m;
-    uint32_t crank = 0, cbase = 0, rmax = 0;
-    for (uint32_t d0 = 0; d0 < a.ndocs; d0 += 1024) {
-        const uint32_t d = d0 + threadIdx.x;
-        const uint32_t r = d < a.ndocs ? a.doc_runs[d] : 0u;
-        const uint32_t rs = (r + M - 1) & ~(M - 1);
-        uint32_t tr, ts;
-        const uint32_t er = block_excl_scan<16>(r, lds, tr);
-        const uint32_t es = block_excl_scan<16>(rs, lds, ts);
-        if (d < a.ndocs) {
-            a.doc_rank0[d] = crank + er;
-            a.run_base[d] = cbase + es;
-            a.docs1[d] = make_uint2(cbase + es, r - 1);
-        }
-        rmax = max(rmax, rs);
-        crank += tr;
-        cbase += ts;
-    }
-    atomicMax(&mx, rmax);
+// Look-back granules (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms R2): every shared
+// word is an 8-byte {epoch, value} granule written by ONE relaxed agent-scope atomic store and
+// read by relaxed agent-scope atomic loads, so the value is its own flag and no fence is needed.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ void granule_store(uint64_t* p, uint32_t epoch, uint32_t v) {
+    __hip_atomic_store((gu64*)p, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t granule_load(const uint64_t* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+// Single-pass tile scan with decoupled look-back (tiles ordered by an atomic ticket, so every
+// predecessor a tile waits on is already running and publishes its aggregate without waiting).
+// Per tile: run-head bits + weights of 4096 slots, then the tile's exclusive (heads, weight)
+// prefix, then the rank bitvector words and one record per run head.
+__global__ __launch_bounds__(kTileThreads) void k_tile_scan(L0Args a) {
+    __shared__ uint32_t lds[kTileThreads / 64];
+    __shared__ uint32_t s_tile, s_exh, s_exw;
+    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        a.ctl[C_RSLOTS] = cbase;
-        a.ctl[C_RMAX] = mx;
-        a.ctl[C_WTOTAL] = cw;
-        a.ctl[C_HTOTAL] = ch;
-        if (a.ndocs) a.doc_pend[a.ndocs - 1] = cw;
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_tile_apply(L0Args a) {
-    __shared__ uint32_t lds[kBlock / 64];
-    const uint32_t gs = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    const uint32_t tile = s_tile;
+    const uint32_t gs = tile * kTile + threadIdx.x * kScanItems;
     Slots16 s;
     load_slots16(a, gs, true, s);
     uint32_t W = 0;
@@ -325,8 +278,63 @@ __global__ __launch_bounds__(kBlock) void k_tile_apply(L0Args a) {
     for (int k = 0; k < 16; ++k) W += s.w[k];
     const uint32_t H = __popc(s.hmask);
     uint32_t th, tw;
-    const uint32_t rank = a.tsum_h[blockIdx.x] + block_excl_scan<kBlock / 64>(H, lds, th);
-    uint32_t P = a.tsum_w[blockIdx.x] + block_excl_scan<kBlock / 64>(W, lds, tw);
+    const uint32_t exh_t = block_excl_scan<kTileThreads / 64>(H, lds, th);
+    const uint32_t exw_t = block_excl_scan<kTileThreads / 64>(W, lds, tw);
+    uint64_t* look = a.look + 4ull * tile;
+    if (threadIdx.x == 0) {  // aggregate first: never waits on anything
+        granule_store(look + 0, a.epoch, th);
+        granule_store(look + 1, a.epoch, tw);
+    }
+    if (threadIdx.x < 64) {  // wave 0: parallel look-back, 64 predecessors per round
+        const uint32_t lane = threadIdx.x;
+        uint32_t exh = 0, exw = 0, spins = 0;
+        bool fail = false;
+        for (int base = (int)tile - 1; base >= 0; base -= 64) {
+            const int j = base - (int)lane;
+            uint32_t vh = 0, vw = 0;
+            bool inc = true;  // j < 0: the virtual inclusive prefix 0
+            if (j >= 0) {
+                const uint64_t* lj = a.look + 4ull * (uint32_t)j;
+                uint64_t gh = granule_load(lj + 0), gw = granule_load(lj + 1);
+                while (((gh >> 32) != a.epoch || (gw >> 32) != a.epoch) && !fail) {
+                    __builtin_amdgcn_s_sleep(1);
+                    gh = granule_load(lj + 0);
+                    gw = granule_load(lj + 1);
+                    if (++spins > kSpinLimit) fail = true;
+                }
+                const uint64_t ih = granule_load(lj + 2), iw = granule_load(lj + 3);
+                inc = (ih >> 32) == a.epoch && (iw >> 32) == a.epoch;
+                vh = (uint32_t)(inc ? ih : gh);
+                vw = (uint32_t)(inc ? iw : gw);
+            }
+            const uint64_t incm = __ballot(inc);
+            if (incm) {
+                const uint32_t f = (uint32_t)(__ffsll((unsigned long long)incm) - 1);
+                exh += wave_sum(lane <= f ? vh : 0u);
+                exw += wave_sum(lane <= f ? vw : 0u);
+                break;
+            }
+            exh += wave_sum(vh);
+            exw += wave_sum(vw);
+        }
+        if (__ballot(fail)) {
+            if (lane == 0) atomicOr(&a.ctl[C_ERR], 32u);
+        }
+        if (lane == 0) {
+            granule_store(look + 2, a.epoch, exh + th);
+            granule_store(look + 3, a.epoch, exw + tw);
+            s_exh = exh;
+            s_exw = exw;
+        }
+    }
+    __syncthreads();
+    const uint32_t rank = s_exh + exh_t;
+    uint32_t P = s_exw + exw_t;
+    if ((threadIdx.x & (kBlock - 1)) == 0) a.tile_exw[tile * (kTile / kScanTile) + threadIdx.x / kBlock] = P;
+    if (tile == a.ntiles - 1 && threadIdx.x == 0) {
+        a.ctl[C_RTOTAL] = s_exh + th;
+        a.ctl[C_WTOTAL] = s_exw + tw;
+    }
     // 64-bit head word from 4 consecutive lanes
     const uint32_t q = threadIdx.x & 3u;
     uint64_t word = (uint64_t)s.hmask << (16 * q);
@@ -338,24 +346,36 @@ __global__ __launch_bounds__(kBlock) void k_tile_apply(L0Args a) {
         a.hrank[gs >> 6] = rank;
     }
     if (!s.hmask) return;
-    const uint32_t d = s.d;
-    const uint32_t rb = a.run_base[d] - a.doc_rank0[d];
     uint32_t r = rank;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         if (s.hmask & (1u << k)) {
             const uint32_t g = gs + k;
-            const uint32_t rho = rb + r;
-            const bool root = g == s.doc.x;
-            a.r_head[rho] = g;
-            a.r_pstart[rho] = P;
-            a.r_lam[rho] = root ? 0u : a.in_lamport[g];
-            a.r_ag[rho] = root ? (uint16_t)0 : a.in_agent[g];
-            if (root && d > 0) a.doc_pend[d - 1] = P;
+            a.r_head[r] = g;
+            a.r_pstart[r] = P;
+            if (g == s.doc.x) {
+                a.doc_root[s.d] = r;
+                a.doc_p0[s.d] = P;
+            }
             ++r;
         }
         P += s.w[k];
     }
+}
+
+// Single workgroup: the most runs any document of the wave has (sizes the pointer jumping).
+__global__ __launch_bounds__(1024) void k_docmax(L0Args a) {
+    __shared__ uint32_t mx;
+    if (threadIdx.x == 0) mx = 0;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t d = threadIdx.x; d < a.ndocs; d += 1024) {
+        const uint32_t end = d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL];
+        m = max(m, end - a.doc_root[d]);
+    }
+    atomicMax(&mx, m);
+    __syncthreads();
+    if (threadIdx.x == 0) a.ctl[C_RMAX] = mx;
 }
 
 // Heads at or before slot g (wave-relative), from the rank bitvector.
@@ -366,37 +386,26 @@ __device__ __forceinline__ uint32_t rank_incl(const uint64_t* hbits, const uint3
     return hrank[w] + (uint32_t)__popcll(hbits[w] & mask);
 }
 
-__global__ __launch_bounds__(1024) void k_chunk_doc1(L0Args a, uint32_t nchunks) {
-    const uint32_t c = blockIdx.x * 1024 + threadIdx.x;
-    if (c >= nchunks) return;
-    const uint32_t slot = c << a.log2m;
-    uint32_t lo = 0, hi = a.ndocs;  // last d with run_base[d] <= slot
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.run_base[mid] <= slot) lo = mid; else hi = mid;
-    }
-    a.chunk_doc1[c] = lo;
-}
-
-__global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t rslots) {
+// Per run: weight (next run's prefix - own prefix) and parent run (rank lookup of the head's
+// parent item; the parent item is always the last item of its run).
+__global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uint32_t wtotal) {
     const uint32_t rho = blockIdx.x * kBlock + threadIdx.x;
-    if (rho >= rslots) return;
-    const uint32_t d = a.chunk_doc1[rho >> a.log2m];
-    const uint2 d1 = a.docs1[d];
-    const uint32_t r = rho - d1.x;
-    if (r > d1.y) return;  // run padding
+    if (rho >= R) return;
+    const uint32_t h = a.r_head[rho];
     const uint32_t ps = a.r_pstart[rho];
-    const uint32_t next = (r < d1.y) ? a.r_pstart[rho + 1] : a.doc_pend[d];
+    const uint32_t next = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
     a.r_w[rho] = next - ps;
-    uint32_t pr = 0;
-    if (r != 0) {
-        const uint32_t h = a.r_head[rho];
-        const uint2 doc = a.docs[d];
+    const uint2 doc = a.docs[a.chunk_doc[h >> a.log2m]];
+    uint32_t pr = kNil;
+    uint64_t key = 0;
+    if (h != doc.x) {
         uint32_t p = a.in_parent[h];
-        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_tile_reduce
-        pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u - a.doc_rank0[d];
+        key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
+        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_tile_scan
+        pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u;
     }
     a.r_parent[rho] = pr;
+    a.r_key[rho] = key;
 }
 
 // Expansion: item slot -> its run -> output position; TEXT writes UTF-8, ORDER writes ids.
@@ -409,23 +418,21 @@ __global__ __launch_bounds__(kBlock) void k_expand(L0Args a) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) W += s.w[k];
     uint32_t tw;
-    uint32_t P = a.tsum_w[blockIdx.x] + block_excl_scan<kBlock / 64>(W, lds, tw);
+    uint32_t P = a.tile_exw[blockIdx.x] + block_excl_scan<kBlock / 64>(W, lds, tw);
     if (!W) return;
-    const uint32_t d = s.d;
     const uint32_t wi = gs >> 6, sh = gs & 63u;
     const uint64_t hw = a.hbits[wi];
     const uint32_t hm = (uint32_t)(hw >> sh) & 0xFFFFu;
-    uint32_t heads = a.hrank[wi] + (uint32_t)__popcll(sh ? (hw & ((1ull << sh) - 1ull)) : 0ull);
-    const uint32_t rb = a.run_base[d] - a.doc_rank0[d] - 1u;
-    const uint64_t obase = a.toff[d];
-    const uint64_t olim = a.toff[d + 1];
+    // run of slot gs-1: heads strictly before gs, minus one
+    uint32_t rho = a.hrank[wi] + (uint32_t)__popcll(sh ? (hw & ((1ull << sh) - 1ull)) : 0ull) - 1u;
+    const uint64_t obase = a.toff[s.d];
+    const uint64_t olim = a.toff[s.d + 1];
     uint32_t cur = kNil, roff = 0, pst = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        heads += (hm >> k) & 1u;
+        rho += (hm >> k) & 1u;
         const uint32_t w = s.w[k];
         if (w) {
-            const uint32_t rho = rb + heads;
             if (rho != cur) {
                 cur = rho;
                 roff = a.roff[rho];
@@ -461,17 +468,17 @@ __global__ __launch_bounds__(kBlock) void k_expand(L0Args a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Level 1: the tree of runs.  Node = run slot; local 0 of a document = its document-start run.
+// Level 1: the tree of runs.  Runs 0..R-1 of the wave; r_parent = kNil marks a document start.
 // ---------------------------------------------------------------------------------------------
 struct TreeArgs {
-    uint32_t nslots, log2m, ndocs, S;
+    uint32_t R, log2m, ndocs, Sreg, S;
     uint32_t step_limit;
-    const uint32_t* chunk_doc;
-    const uint2* docs;  // {base run slot, runs - 1}
-    const uint32_t* in_parent;
-    const uint32_t* in_lamport;
-    const uint16_t* in_agent;
-    const uint32_t* in_w;
+    const uint32_t* in_parent;   // parent run (kNil: document start)
+    const uint64_t* key;         // sibling key: (lamport, agent) of the run's head
+    const uint32_t* in_w;        // run weight
+    const uint32_t* doc_root;    // per document: its document-start run
+    const uint32_t* doc_p0;      // per document: weight prefix at its start
+    uint32_t wtotal;
     uint32_t* deg;
     uint32_t* cstart;
     uint32_t* child;
@@ -484,7 +491,6 @@ struct TreeArgs {
     uint32_t* snext;
     uint32_t* roff;
     uint32_t* tlen;
-    uint32_t* icnt;
     uint64_t* toff;
     uint32_t* loff;
     uint64_t* leafh;
@@ -494,23 +500,15 @@ struct TreeArgs {
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
 };
 
-__device__ __forceinline__ uint64_t sib_key(const TreeArgs& a, uint32_t c) {
-    return ((uint64_t)a.in_lamport[c] << 16) | (uint64_t)a.in_agent[c];
-}
-
-__device__ __forceinline__ uint2 doc_of(const TreeArgs& a, uint32_t g) {
-    return a.docs[a.chunk_doc[g >> a.log2m]];
-}
+__device__ __forceinline__ uint64_t sib_key(const TreeArgs& a, uint32_t c) { return a.key[c]; }
 
 __global__ __launch_bounds__(kBlock) void k_count(TreeArgs a) {
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.nslots) return;
-    const uint2 doc = doc_of(a, g);
-    const uint32_t local = g - doc.x;
-    if (local - 1u >= doc.y) return;  // document-start run or padding
-    uint32_t p = a.in_parent[g];
-    if (p > doc.y || p == local) { atomicOr(&a.ctl[C_ERR], 1u); p = 0; }
-    atomicAdd(&a.deg[doc.x + p], 1u);
+    if (g >= a.R) return;
+    const uint32_t p = a.in_parent[g];
+    if (p == kNil) return;
+    if (p >= a.R || p == g) { atomicOr(&a.ctl[C_ERR], 1u); return; }
+    atomicAdd(&a.deg[p], 1u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n,
@@ -587,16 +585,45 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* __restric
 
 __global__ __launch_bounds__(kBlock) void k_place(TreeArgs a) {
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.nslots) return;
-    const uint2 doc = doc_of(a, g);
-    const uint32_t local = g - doc.x;
-    if (local - 1u >= doc.y) return;
-    uint32_t p = a.in_parent[g];
-    if (p > doc.y || p == local) p = 0;  // flagged by k_count
-    const uint32_t gp = doc.x + p;
+    if (g >= a.R) return;
+    const uint32_t p = a.in_parent[g];
+    if (p == kNil || p >= a.R || p == g) return;  // flagged by k_count
     // decrementing restores deg[] to all-zero for the next wave (no memset needed)
-    const uint32_t r = atomicSub(&a.deg[gp], 1u) - 1u;
-    a.child[a.cstart[gp] + r] = g;
+    const uint32_t r = atomicSub(&a.deg[p], 1u) - 1u;
+    a.child[a.cstart[p] + r] = g;
+}
+
+// Compare-exchange for a descending sort of (key, id) pairs held in registers.
+__device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uint32_t& ib) {
+    if (ka < kb) {
+        const uint64_t tk = ka; ka = kb; kb = tk;
+        const uint32_t ti = ia; ia = ib; ib = ti;
+    }
+}
+
+// Up to 8 siblings: Batcher's 19-comparator odd-even merge network (verified on all 0-1
+// inputs), padding key 0 sorts last (every child key has lamport >= 1).
+__device__ __forceinline__ uint32_t link_small(const TreeArgs& a, uint32_t g, uint32_t s0,
+                                               uint32_t cnt) {
+    uint64_t k[8];
+    uint32_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = (uint32_t)i < cnt ? a.child[s0 + i] : kNil;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = (uint32_t)i < cnt ? a.key[c[i]] : 0ull;
+    cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
+    cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
+    cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
+    cx(k[4], c[4], k[6], c[6]); cx(k[5], c[5], k[7], c[7]);
+    cx(k[1], c[1], k[2], c[2]); cx(k[5], c[5], k[6], c[6]);
+    cx(k[0], c[0], k[4], c[4]); cx(k[1], c[1], k[5], c[5]);
+    cx(k[2], c[2], k[6], c[6]); cx(k[3], c[3], k[7], c[7]);
+    cx(k[2], c[2], k[4], c[4]); cx(k[3], c[3], k[5], c[5]);
+    cx(k[1], c[1], k[2], c[2]); cx(k[3], c[3], k[4], c[4]); cx(k[5], c[5], k[6], c[6]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if ((uint32_t)i < cnt) a.up[c[i]] = make_uint2((uint32_t)i + 1 < cnt ? c[i + 1 < 8 ? i + 1 : 7] : kNil, g);
+    return c[0];
 }
 
 __global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
@@ -605,29 +632,27 @@ __global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
     __syncthreads();
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
     bool defer = false;
-    if (g < a.nslots) {
-        const uint2 doc = doc_of(a, g);
-        const uint32_t local = g - doc.x;
-        if (local <= doc.y) {
-            const uint32_t w = a.in_w[g];
-            if (local == 0) a.up[g] = make_uint2(kNil, kNil);  // no sibling, no parent
-            const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
-            uint32_t fc = kNil;
-            if (cnt == 1) {
-                const uint32_t c0 = a.child[s0];
-                fc = c0;
-                a.up[c0] = make_uint2(kNil, g);
-            } else if (cnt == 2) {
-                uint32_t c0 = a.child[s0], c1 = a.child[s0 + 1];
-                if (sib_key(a, c0) < sib_key(a, c1)) { uint32_t t = c0; c0 = c1; c1 = t; }
-                fc = c0;
-                a.up[c0] = make_uint2(c1, g);
-                a.up[c1] = make_uint2(kNil, g);
-            } else if (cnt > 2) {
-                defer = true;  // first_child written by the sort kernels
-            }
-            a.dn[g] = make_uint2(fc, w);
+    if (g < a.R) {
+        const uint32_t w = a.in_w[g];
+        if (a.in_parent[g] == kNil) a.up[g] = make_uint2(kNil, kNil);  // no sibling, no parent
+        const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
+        uint32_t fc = kNil;
+        if (cnt == 1) {
+            const uint32_t c0 = a.child[s0];
+            fc = c0;
+            a.up[c0] = make_uint2(kNil, g);
+        } else if (cnt == 2) {
+            uint32_t c0 = a.child[s0], c1 = a.child[s0 + 1];
+            if (sib_key(a, c0) < sib_key(a, c1)) { uint32_t t = c0; c0 = c1; c1 = t; }
+            fc = c0;
+            a.up[c0] = make_uint2(c1, g);
+            a.up[c1] = make_uint2(kNil, g);
+        } else if (cnt <= 8) {
+            if (cnt) fc = link_small(a, g, s0, cnt);
+        } else {
+            defer = true;  // first_child written by the sort kernels
         }
+        a.dn[g] = make_uint2(fc, w);
     }
     // deferred segments: one global atomic per block
     uint32_t slot = 0;
@@ -638,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
     if (defer) a.defer[bbase + slot] = g;
 }
 
-// One wave per deferred segment of 3..64 children: rank = #siblings with a greater key, then
+// One wave per deferred segment of 9..64 children: rank = #siblings with a greater key, then
 // ds_permute scatters ids into rank order and shuffles hand each lane its successor.
 __global__ __launch_bounds__(kBlock) void k_sortmid(TreeArgs a) {
     const uint32_t lane = threadIdx.x & 63;
@@ -732,33 +757,50 @@ __global__ __launch_bounds__(kBigThreads) void k_sortbig(TreeArgs a) {
     }
 }
 
-// Euler-tour walks (sublist list ranking).  Splitters: both arcs of every run slot that is a
-// multiple of M (every document-start run is one).  Splitter s <-> node (s>>1)<<log2m, arc
-// (s&1) (0 = down, 1 = up).
+// Euler-tour walks (sublist list ranking).  Regular splitters: both arcs of every run that is
+// a multiple of M (splitter s <-> run (s>>1)<<log2m, arc s&1: 0 down, 1 up); plus one splitter
+// per document for the down arc of its document-start run (index Sreg + d), the head of that
+// document's list.  No arc leads into a document start's down arc, so walks only ever stop at
+// regular splitters.  Returns false for an inactive splitter slot.
+__device__ __forceinline__ bool splitter_arc(const TreeArgs& a, uint32_t s, uint32_t& v,
+                                             bool& up) {
+    if (s >= a.Sreg) {
+        v = a.doc_root[s - a.Sreg];
+        up = false;
+        return true;
+    }
+    v = (s >> 1) << a.log2m;
+    up = s & 1u;
+    if (v >= a.R) return false;
+    return up || a.in_parent[v] != kNil;  // a document start's down arc has its own splitter
+}
+
 __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= a.S) return;
     const uint32_t m = a.log2m, mask = (1u << m) - 1u;
-    uint32_t v = (s >> 1) << m;
-    bool up = s & 1u;
+    uint32_t v;
+    bool up;
     uint32_t sum = 0, steps = 0, nxt = kNil;
-    for (;;) {
-        uint32_t nv;
-        bool nup;
-        if (!up) {
-            const uint2 r = a.dn[v];
-            sum += r.y;
-            if (r.x != kNil) { nv = r.x; nup = false; } else { nv = v; nup = true; }
-        } else {
-            const uint2 r = a.up[v];
-            if (r.x != kNil) { nv = r.x; nup = false; }
-            else if (r.y != kNil) { nv = r.y; nup = true; }
-            else break;  // up arc of the document-start run: end of this document's tour
+    if (splitter_arc(a, s, v, up)) {
+        for (;;) {
+            uint32_t nv;
+            bool nup;
+            if (!up) {
+                const uint2 r = a.dn[v];
+                sum += r.y;
+                if (r.x != kNil) { nv = r.x; nup = false; } else { nv = v; nup = true; }
+            } else {
+                const uint2 r = a.up[v];
+                if (r.x != kNil) { nv = r.x; nup = false; }
+                else if (r.y != kNil) { nv = r.y; nup = true; }
+                else break;  // up arc of a document start: end of that document's tour
+            }
+            if ((nv & mask) == 0) { nxt = ((nv >> m) << 1) | (nup ? 1u : 0u); break; }
+            v = nv;
+            up = nup;
+            if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
         }
-        if ((nv & mask) == 0) { nxt = ((nv >> m) << 1) | (nup ? 1u : 0u); break; }
-        v = nv;
-        up = nup;
-        if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
     }
     a.sw[s] = sum;
     a.snext[s] = nxt;
@@ -799,8 +841,9 @@ __global__ __launch_bounds__(kBlock) void k_wstep(const uint32_t* __restrict__ v
     pout[s] = q;
 }
 
-// Single workgroup: per-document length, aligned output offsets, leaf offsets.
-__global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a, const uint32_t* __restrict__ spref) {
+// Single workgroup: per-document length (weight between consecutive document starts), aligned
+// output offsets, leaf offsets.
+__global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     __shared__ uint64_t st[1024];
     __shared__ uint32_t sl[1024];
     uint64_t carry_t = 0;
@@ -810,8 +853,8 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a, const uint32_t* 
         const uint32_t d = d0 + threadIdx.x;
         uint32_t tl = 0;
         if (d < a.ndocs) {
-            const uint2 doc = a.docs[d];
-            tl = spref[((doc.x >> a.log2m) << 1) | 1u];
+            const uint32_t end = d + 1 < a.ndocs ? a.doc_p0[d + 1] : a.wtotal;
+            tl = end - a.doc_p0[d];
             a.tlen[d] = tl;
         }
         const uint64_t sz = ((uint64_t)tl + am) & ~am;
@@ -844,14 +887,12 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a, const uint32_t* 
 
 // Re-walk: every run passed on a down arc gets its offset inside its document.
 __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __restrict__ spref) {
-    const uint32_t s0 = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = s0 < a.S;
-    const uint32_t s = live ? s0 : a.S - 1;  // keep every lane for the wave reduction below
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t m = a.log2m, mask = (1u << m) - 1u;
-    uint32_t v = (s >> 1) << m;
-    bool up = s & 1u;
-    const uint32_t d = a.chunk_doc[v >> m];
-    uint32_t off = spref[s];
+    uint32_t v = 0;
+    bool up = false;
+    const bool live = s < a.S && splitter_arc(a, s, v, up);
+    uint32_t off = live ? spref[s] : 0u;
     uint32_t steps = 0, runs = 0;
     for (; live;) {
         uint32_t nv;
@@ -873,7 +914,9 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
         up = nup;
         if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
     }
-    doc_add(a.icnt, d, runs);  // reachability: every run of the document must be visited
+    // reachability: every run of the wave must be visited exactly once
+    const uint32_t tot = wave_sum(runs);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -940,11 +983,9 @@ __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_c
     a.leafh[L] = xxh64_aligned(a.text + a.toff[d] + (uint64_t)j * kLeaf, len, 0);
 }
 
-__global__ __launch_bounds__(kBlock) void k_docdigest(TreeArgs a, bool hash) {
+__global__ __launch_bounds__(kBlock) void k_docdigest(TreeArgs a) {
     const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
     if (d >= a.ndocs) return;
-    if (a.icnt[d] != a.docs[d].y + 1u) atomicOr(&a.ctl[C_ERR], 16u);  // unreachable runs: a cycle
-    if (!hash) return;
     const uint32_t l0 = a.loff[d], l1 = a.loff[d + 1];
     a.dig[d] = xxh64_aligned(reinterpret_cast<const uint8_t*>(a.leafh + l0), (l1 - l0) * 8u,
                              a.tlen[d]);
@@ -1042,13 +1083,12 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(tsum_h_); dfree(tsum_w_);
-    dfree(doc_runs_); dfree(doc_rank0_); dfree(run_base_); dfree(doc_pend_); dfree(docs1_);
-    dfree(chunk_doc1_); dfree(r_head_); dfree(r_pstart_); dfree(r_lam_); dfree(r_ag_);
-    dfree(r_parent_); dfree(r_w_); dfree(roff_);
+    dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(ticket_); dfree(tile_exw_);
+    dfree(doc_root_); dfree(doc_p0_);
+    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(ctl_); dfree(dn_); dfree(up_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
-    dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(icnt_); dfree(loff_); dfree(toff_);
+    dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
     dfree(dig_); dfree(leafh_); dfree(text_);
     if (host_ctl_) (void)hipHostFree(host_ctl_);
     if (host_dig_) (void)hipHostFree(host_dig_);
@@ -1087,8 +1127,8 @@ std::string Engine::init(int dev) {
 }
 
 int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
-    const uint64_t M = 1ull << log2m;
-    L.log2m = log2m;
+    const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
+    L.log2m = kDocAlignLog2;
     L.docs = docs;
     L.doc_slot.resize(docs.size());
     L.waves.clear();
@@ -1202,29 +1242,27 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(tsum_h_); dfree(tsum_w_);
+        dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(tile_exw_);
+        const uint64_t tiles = slots / kTile + 2;
         HIPCHK(dalloc(&jump_, slots + 64), "hipMalloc jump");
         HIPCHK(dalloc(&hbits_, slots / 64 + 2), "hipMalloc hbits");
         HIPCHK(dalloc(&hrank_, slots / 64 + 2), "hipMalloc hrank");
-        HIPCHK(dalloc(&tsum_h_, slots / kScanTile + 2), "hipMalloc tsum_h");
-        HIPCHK(dalloc(&tsum_w_, slots / kScanTile + 2), "hipMalloc tsum_w");
+        HIPCHK(dalloc(&look_, 4 * tiles), "hipMalloc look-back");
+        HIPCHK(hipMemset(look_, 0, 4 * tiles * 8), "memset look-back");  // no stale epoch
+        HIPCHK(dalloc(&tile_exw_, tiles * (kTile / kScanTile)), "hipMalloc tile prefixes");
         cap_slots0_ = slots;
     }
     if (!ctl_) HIPCHK(dalloc(&ctl_, 16), "hipMalloc ctl");
+    if (!ticket_) HIPCHK(dalloc(&ticket_, 16), "hipMalloc ticket");
     if (w.ndocs + 1 > cap_docs_) {
-        dfree(tlen_); dfree(icnt_); dfree(loff_); dfree(toff_); dfree(dig_);
-        dfree(doc_runs_); dfree(doc_rank0_); dfree(run_base_); dfree(doc_pend_); dfree(docs1_);
+        dfree(tlen_); dfree(loff_); dfree(toff_); dfree(dig_); dfree(doc_root_); dfree(doc_p0_);
         const uint64_t nd = w.ndocs + 1;
         HIPCHK(dalloc(&tlen_, nd), "hipMalloc tlen");
-        HIPCHK(dalloc(&icnt_, nd), "hipMalloc icnt");
         HIPCHK(dalloc(&loff_, nd), "hipMalloc loff");
         HIPCHK(dalloc(&toff_, nd), "hipMalloc toff");
         HIPCHK(dalloc(&dig_, nd), "hipMalloc dig");
-        HIPCHK(dalloc(&doc_runs_, nd), "hipMalloc doc_runs");
-        HIPCHK(dalloc(&doc_rank0_, nd), "hipMalloc doc_rank0");
-        HIPCHK(dalloc(&run_base_, nd), "hipMalloc run_base");
-        HIPCHK(dalloc(&doc_pend_, nd), "hipMalloc doc_pend");
-        HIPCHK(dalloc(&docs1_, nd), "hipMalloc docs1");
+        HIPCHK(dalloc(&doc_root_, nd), "hipMalloc doc_root");
+        HIPCHK(dalloc(&doc_p0_, nd), "hipMalloc doc_p0");
         cap_docs_ = nd;
     }
     const uint64_t tb = std::max<uint64_t>(w.text_cap, w.order_cap * 4) + 64;
@@ -1248,21 +1286,16 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     return CRDT_HIP_OK;
 }
 
-// Level-1 scratch, sized by the run slots of the wave (known after k_tile_top).
-int Engine::ensure_runs(uint64_t rslots) {
-    if (rslots > cap_runs_) {
-        dfree(chunk_doc1_); dfree(r_head_); dfree(r_pstart_); dfree(r_lam_); dfree(r_ag_);
-        dfree(r_parent_); dfree(r_w_); dfree(roff_);
+// Level-1 scratch, sized by the runs of the wave (known after k_tile_scan).
+int Engine::ensure_runs(uint64_t R, uint64_t S) {
+    if (R > cap_runs_) {
+        dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
         dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_);
         dfree(scan_sums_); dfree(dn_); dfree(up_);
-        const uint64_t r = rslots + (rslots >> 3) + 4096;  // headroom against regrowth
-        HIPCHK(dalloc(&chunk_doc1_, (r >> log2m) + 2), "hipMalloc chunk_doc1");
-        HIPCHK(dalloc(&r_head_, r), "hipMalloc r_head");
-        HIPCHK(dalloc(&r_pstart_, r), "hipMalloc r_pstart");
-        HIPCHK(dalloc(&r_lam_, r), "hipMalloc r_lam");
-        HIPCHK(dalloc(&r_ag_, r), "hipMalloc r_ag");
+        const uint64_t r = R + (R >> 3) + 4096;  // headroom against regrowth
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
         HIPCHK(dalloc(&r_w_, r), "hipMalloc r_w");
+        HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
         HIPCHK(dalloc(&deg_, r + 16), "hipMalloc deg");
         HIPCHK(hipMemset(deg_, 0, (r + 16) * 4), "memset deg");
@@ -1275,17 +1308,17 @@ int Engine::ensure_runs(uint64_t rslots) {
         HIPCHK(dalloc(&up_, r), "hipMalloc up");
         cap_runs_ = r;
     }
-    const uint64_t S = 2 * (cap_runs_ >> log2m) + 2;
     if (S > cap_splitters_) {
         dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_); dfree(v1_); dfree(p0_); dfree(p1_);
-        HIPCHK(dalloc(&sw_, S), "hipMalloc sw");
-        HIPCHK(dalloc(&snext_, S), "hipMalloc snext");
-        HIPCHK(dalloc(&pred_, S), "hipMalloc pred");
-        HIPCHK(dalloc(&v0_, S), "hipMalloc v0");
-        HIPCHK(dalloc(&v1_, S), "hipMalloc v1");
-        HIPCHK(dalloc(&p0_, S), "hipMalloc p0");
-        HIPCHK(dalloc(&p1_, S), "hipMalloc p1");
-        cap_splitters_ = S;
+        const uint64_t sc = S + (S >> 3) + 1024;
+        HIPCHK(dalloc(&sw_, sc), "hipMalloc sw");
+        HIPCHK(dalloc(&snext_, sc), "hipMalloc snext");
+        HIPCHK(dalloc(&pred_, sc), "hipMalloc pred");
+        HIPCHK(dalloc(&v0_, sc), "hipMalloc v0");
+        HIPCHK(dalloc(&v1_, sc), "hipMalloc v1");
+        HIPCHK(dalloc(&p0_, sc), "hipMalloc p0");
+        HIPCHK(dalloc(&p1_, sc), "hipMalloc p1");
+        cap_splitters_ = sc;
     }
     return CRDT_HIP_OK;
 }
@@ -1294,14 +1327,17 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
                      std::vector<uint32_t>& stage_launches) {
     hipStream_t s = stream;
     const bool ord = mode == ORDER;
-    const uint32_t ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
+    const uint32_t ntiles = (uint32_t)((w.nslots + kTile - 1) / kTile);
+    const uint32_t njump = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
+#define BEGIN(st) HIPCHK(hipEventRecord(ev_[2 * (st)], s), "event record")
+#define END(st) HIPCHK(hipEventRecord(ev_[2 * (st) + 1], s), "event record")
 
     L0Args a0{};
     a0.nslots = w.nslots;
-    a0.log2m = log2m;
+    a0.log2m = L.log2m;
     a0.ndocs = w.ndocs;
     a0.mode = ord ? 1u : 0u;
-    a0.chunk_doc = L.chunk_doc + (w.slot0 >> log2m);
+    a0.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);
     a0.docs = L.docs_rel + w.first_doc;
     a0.in_parent = L.parent + w.slot0;
     a0.in_lamport = L.lamport + w.slot0;
@@ -1311,98 +1347,97 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.jump = jump_;
     a0.hbits = hbits_;
     a0.hrank = hrank_;
-    a0.tsum_h = tsum_h_;
-    a0.tsum_w = tsum_w_;
     a0.ntiles = ntiles;
-    a0.doc_runs = doc_runs_;
-    a0.doc_rank0 = doc_rank0_;
-    a0.run_base = run_base_;
-    a0.doc_pend = doc_pend_;
-    a0.docs1 = docs1_;
+    a0.look = look_;
+    a0.ticket = ticket_;
+    a0.tile_exw = tile_exw_;
+    a0.epoch = ++epoch_;
+    a0.doc_root = doc_root_;
+    a0.doc_p0 = doc_p0_;
     a0.toff = toff_;
     a0.text = text_;
     a0.ctl = ctl_;
+    // run records are written by the tile scan before the run count is known: runs <= slots
+    if (w.nslots > cap_heads_) {
+        dfree(r_head_); dfree(r_pstart_);
+        HIPCHK(dalloc(&r_head_, w.nslots + 64ull), "hipMalloc r_head");
+        HIPCHK(dalloc(&r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
+        cap_heads_ = w.nslots;
+    }
+    a0.r_head = r_head_;
+    a0.r_pstart = r_pstart_;
 
-#define BEGIN(st) HIPCHK(hipEventRecord(ev_[2 * (st)], s), "event record")
-#define END(st) HIPCHK(hipEventRecord(ev_[2 * (st) + 1], s), "event record")
     // ---- level 0: runs -------------------------------------------------------------------
     HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
+    HIPCHK(hipMemsetAsync(ticket_, 0, 16, s), "memset ticket");
     HIPCHK(hipMemsetAsync(jump_, 0, w.nslots + 64ull, s), "memset jump");
-    HIPCHK(hipMemsetAsync(doc_runs_, 0, w.ndocs * 4ull, s), "memset doc_runs");
-    HIPCHK(hipMemsetAsync(icnt_, 0, w.ndocs * 4ull, s), "memset icnt");
     BEGIN(S_JUMP);
-    k_jump<<<grid_for(w.nslots), kBlock, 0, s>>>(a0);
+    k_jump<<<njump, kBlock, 0, s>>>(a0);
     END(S_JUMP);
-    BEGIN(S_TREDUCE);
-    k_tile_reduce<<<ntiles, kBlock, 0, s>>>(a0);
-    END(S_TREDUCE);
-    BEGIN(S_TTOP);
-    k_tile_top<<<1, 1024, 0, s>>>(a0);
-    END(S_TTOP);
+    BEGIN(S_TSCAN);
+    k_tile_scan<<<ntiles, kTileThreads, 0, s>>>(a0);
+    k_docmax<<<1, 1024, 0, s>>>(a0);
+    END(S_TSCAN);
     HIPCHK(hipGetLastError(), "level-0 launch");
     HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "level-0 sync");
-    const uint32_t rslots = host_ctl_[C_RSLOTS];
-    const uint32_t rmax = host_ctl_[C_RMAX];
-    if (host_ctl_[C_ERR] & 1u) {
-        err = "malformed op log: parent id out of range";
-        return CRDT_HIP_EBADLOG;
+    if (host_ctl_[C_ERR]) {
+        err = host_ctl_[C_ERR] & 32u ? "tile look-back timed out"
+                                     : "malformed op log: parent id out of range";
+        return host_ctl_[C_ERR] & 32u ? CRDT_HIP_EDEVICE : CRDT_HIP_EBADLOG;
     }
-    int rc = ensure_runs(rslots);
+    const uint32_t R = host_ctl_[C_RTOTAL];
+    const uint32_t wtotal = host_ctl_[C_WTOTAL];
+    const uint32_t rmax = host_ctl_[C_RMAX];
+    const uint32_t Sreg = 2 * ((R + (1u << log2m) - 1) >> log2m);
+    const uint32_t S = Sreg + w.ndocs;
+    const int rc = ensure_runs(R, S);
     if (rc) return rc;
-    a0.r_head = r_head_;
-    a0.r_pstart = r_pstart_;
-    a0.r_lam = r_lam_;
-    a0.r_ag = r_ag_;
     a0.r_parent = r_parent_;
     a0.r_w = r_w_;
-    a0.chunk_doc1 = chunk_doc1_;
+    a0.r_key = r_key_;
     a0.roff = roff_;
-    BEGIN(S_TAPPLY);
-    k_tile_apply<<<ntiles, kBlock, 0, s>>>(a0);
-    END(S_TAPPLY);
-    const uint32_t nchunks1 = rslots >> log2m;
     BEGIN(S_RPARENT);
-    k_chunk_doc1<<<grid_for(nchunks1, 1024), 1024, 0, s>>>(a0, nchunks1);
-    k_run_parent<<<grid_for(rslots), kBlock, 0, s>>>(a0, rslots);
+    k_run_parent<<<grid_for(R), kBlock, 0, s>>>(a0, R, wtotal);
     END(S_RPARENT);
 
     // ---- level 1: the tree of runs -------------------------------------------------------
     TreeArgs a{};
-    a.nslots = rslots;
+    a.R = R;
     a.log2m = log2m;
     a.ndocs = w.ndocs;
-    a.S = 2 * (rslots >> log2m);
-    a.step_limit = 2u * rslots + 4u;
-    a.chunk_doc = chunk_doc1_;
-    a.docs = docs1_;
+    a.Sreg = Sreg;
+    a.S = S;
+    a.step_limit = 2u * R + 4u;
     a.in_parent = r_parent_;
-    a.in_lamport = r_lam_;
-    a.in_agent = r_ag_;
+    a.key = r_key_;
     a.in_w = r_w_;
+    a.doc_root = doc_root_;
+    a.doc_p0 = doc_p0_;
+    a.wtotal = wtotal;
     a.deg = deg_; a.cstart = cstart_; a.child = child_; a.dn = dn_; a.up = up_;
     a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;
     a.roff = roff_;
-    a.tlen = tlen_; a.icnt = icnt_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.dig = dig_;
+    a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.dig = dig_;
     a.text = text_;
     a.text_cap = ord ? w.order_cap : cap_text_ - 64;
     a.align = ord ? 1u : 16u;
-    const uint32_t gs = grid_for(rslots), gS = grid_for(a.S);
-    const uint32_t nb = (uint32_t)((rslots + kScanTile - 1) / kScanTile);
+    const uint32_t gR = grid_for(R), gS = grid_for(S);
+    const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
 
     BEGIN(S_COUNT);
-    k_count<<<gs, kBlock, 0, s>>>(a);
+    k_count<<<gR, kBlock, 0, s>>>(a);
     END(S_COUNT);
     BEGIN(S_SCAN);
-    k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, rslots, scan_sums_);
-    k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, rslots);
-    k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, rslots, scan_sums_, cstart_);
+    k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_);
+    k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, R);
+    k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_, cstart_);
     END(S_SCAN);
     BEGIN(S_PLACE);
-    k_place<<<gs, kBlock, 0, s>>>(a);
+    k_place<<<gR, kBlock, 0, s>>>(a);
     END(S_PLACE);
     BEGIN(S_LINK);
-    k_link<<<gs, kBlock, 0, s>>>(a);
+    k_link<<<gR, kBlock, 0, s>>>(a);
     k_sortmid<<<kMidGrid, kBlock, 0, s>>>(a);
     k_sortbig<<<kBigGrid, kBigThreads, 0, s>>>(a);
     END(S_LINK);
@@ -1410,30 +1445,33 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     k_walk1<<<gS, kBlock, 0, s>>>(a);
     END(S_WALK1);
     BEGIN(S_RANK);
-    HIPCHK(hipMemsetAsync(pred_, 0xFF, a.S * 4ull, s), "memset pred");
-    k_pred<<<gS, kBlock, 0, s>>>(snext_, a.S, pred_);
-    k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, a.S, v0_, p0_);
-    const uint32_t rounds = ceil_log2(std::max<uint32_t>(2 * (rmax >> log2m), 2));
+    HIPCHK(hipMemsetAsync(pred_, 0xFF, S * 4ull, s), "memset pred");
+    k_pred<<<gS, kBlock, 0, s>>>(snext_, S, pred_);
+    k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, S, v0_, p0_);
+    // a document's list holds at most 2 * (ceil(runs / M) + 1) + 1 splitters
+    const uint32_t rounds = ceil_log2(2ull * ((rmax + (1u << log2m) - 1) >> log2m) + 4);
     uint32_t *vi = v0_, *pi = p0_, *vo = v1_, *po = p1_;
     for (uint32_t r = 0; r < rounds; ++r) {
-        k_wstep<<<gS, kBlock, 0, s>>>(vi, pi, a.S, vo, po);
+        k_wstep<<<gS, kBlock, 0, s>>>(vi, pi, S, vo, po);
         std::swap(vi, vo);
         std::swap(pi, po);
     }
     const uint32_t* spref = vi;
     END(S_RANK);
     BEGIN(S_WALK2);
-    k_doctotals<<<1, 1024, 0, s>>>(a, spref);
+    k_doctotals<<<1, 1024, 0, s>>>(a);
     k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
     END(S_WALK2);
 
     // ---- expansion + digest --------------------------------------------------------------
     BEGIN(S_EXPAND);
-    k_expand<<<ntiles, kBlock, 0, s>>>(a0);
+    k_expand<<<njump, kBlock, 0, s>>>(a0);
     END(S_EXPAND);
     BEGIN(S_DIGEST);
-    if (!ord) k_leafhash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
-    k_docdigest<<<grid_for(w.ndocs), kBlock, 0, s>>>(a, !ord);
+    if (!ord) {
+        k_leafhash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
+        k_docdigest<<<grid_for(w.ndocs), kBlock, 0, s>>>(a);
+    }
     END(S_DIGEST);
     HIPCHK(hipGetLastError(), "kernel launch");
     HIPCHK(hipMemcpyAsync(host_len_ + w.first_doc, tlen_, w.ndocs * 4ull, hipMemcpyDeviceToHost, s),
@@ -1443,7 +1481,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
                "copy digests");
     HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "merge wave");
-    const uint32_t launches[S_N] = {1, 1, 1, 1, 2, 1, 3, 1, 3, 1, 2 + rounds, 2, 1, ord ? 1u : 2u};
+    const uint32_t launches[S_N] = {1, 2, 1, 1, 3, 1, 3, 1, 2 + rounds, 2, 1, ord ? 0u : 2u};
     for (int i = 0; i < S_N; ++i) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");
@@ -1452,10 +1490,12 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     }
 #undef BEGIN
 #undef END
-    runs_ += host_ctl_[C_HTOTAL];
-    if (host_ctl_[C_ERR]) {
+    runs_ += R;
+    uint32_t errs = host_ctl_[C_ERR];
+    if (!errs && host_ctl_[C_VISITED] != R) errs |= 16u;  // unreachable runs: a cycle
+    if (errs) {
         (void)hipMemset(deg_, 0, (cap_runs_ + 16) * 4);  // restore the all-zero invariant
-        err = "malformed op log detected on device (flags " + std::to_string(host_ctl_[C_ERR]) + ")";
+        err = "malformed op log detected on device (flags " + std::to_string(errs) + ")";
         return CRDT_HIP_EBADLOG;
     }
     return CRDT_HIP_OK;

@@ -2,10 +2,9 @@
 // documents by the gfx950 kernels in engine.hip.
 //
 // Slot layout (DESIGN.md §Data layout): every document d owns slots [base_d, base_d + n_d + 1)
-// of a wave, padded up to a multiple of the splitter stride M: slot base_d is the document-start
-// node (id 0), slot base_d + k holds item id k.  Input SoA arrays are indexed by slot.  Because
-// every document starts on a multiple of M, the chunk -> document table needs one entry per M
-// slots, and splitter indices are a pure function of the slot.
+// of a wave, padded up to a multiple of 64: slot base_d is the document-start node (id 0), slot
+// base_d + k holds item id k.  Input SoA arrays are indexed by slot.  Because every document
+// starts on a multiple of 64, the chunk -> document table needs one entry per 64 slots.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -62,7 +61,7 @@ public:
 
     int device = 0;
     hipStream_t stream = nullptr;
-    uint32_t log2m = 6;                    // splitter stride M = 2^log2m
+    uint32_t log2m = 4;                    // level-1 splitter stride M = 2^log2m
     uint64_t max_wave_slots = 1ull << 30;
     std::string err;
 
@@ -89,20 +88,18 @@ private:
     // level-0 scratch (per slot / per tile), grown on demand
     uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
     uint8_t* jump_ = nullptr;
-    uint64_t* hbits_ = nullptr;
-    uint32_t *hrank_ = nullptr, *tsum_h_ = nullptr, *tsum_w_ = nullptr;
+    uint64_t *hbits_ = nullptr, *look_ = nullptr;
+    uint32_t *hrank_ = nullptr, *ticket_ = nullptr, *tile_exw_ = nullptr;
+    uint32_t epoch_ = 0;  // look-back epoch, unique per tile-scan launch
     // per document
-    uint32_t *doc_runs_ = nullptr, *doc_rank0_ = nullptr, *run_base_ = nullptr,
-             *doc_pend_ = nullptr;
-    uint2* docs1_ = nullptr;
-    uint32_t *tlen_ = nullptr, *icnt_ = nullptr, *loff_ = nullptr;
+    uint32_t *doc_root_ = nullptr, *doc_p0_ = nullptr, *tlen_ = nullptr, *loff_ = nullptr;
     uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;
     uint8_t* text_ = nullptr;
-    // level-1 scratch (per run slot), grown on demand
-    uint64_t cap_runs_ = 0, cap_splitters_ = 0;
-    uint32_t *chunk_doc1_ = nullptr, *r_head_ = nullptr, *r_pstart_ = nullptr, *r_lam_ = nullptr,
-             *r_parent_ = nullptr, *r_w_ = nullptr, *roff_ = nullptr;
-    uint16_t* r_ag_ = nullptr;
+    // level-1 scratch (per run / per splitter), grown on demand
+    uint64_t cap_heads_ = 0, cap_runs_ = 0, cap_splitters_ = 0;
+    uint32_t *r_head_ = nullptr, *r_pstart_ = nullptr, *r_parent_ = nullptr, *r_w_ = nullptr,
+             *roff_ = nullptr;
+    uint64_t* r_key_ = nullptr;
     uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
              *bigl_ = nullptr, *scan_sums_ = nullptr, *ctl_ = nullptr;
     uint2 *dn_ = nullptr, *up_ = nullptr;
@@ -115,7 +112,7 @@ private:
     uint64_t runs_ = 0;
     std::vector<hipEvent_t> ev_;
 
-    int ensure_runs(uint64_t rslots);
+    int ensure_runs(uint64_t runs, uint64_t splitters);
     int ensure_scratch(const Wave& w, uint32_t ndocs_total);
     int run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
                  std::vector<uint32_t>& stage_launches);

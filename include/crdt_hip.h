@@ -86,20 +86,19 @@ typedef struct {
 /* Stage indices of crdt_hip_stats.stage_ns (one HIP-event interval per kernel group). */
 enum {
     CRDT_HIP_STAGE_JUMP = 0,     /* level 0: flag items with a non-consecutive child          */
-    CRDT_HIP_STAGE_TREDUCE = 1,  /* level 0: per-tile run-head counts and weight sums         */
-    CRDT_HIP_STAGE_TTOP = 2,     /* level 0: tile bases, per-document run bases               */
-    CRDT_HIP_STAGE_TAPPLY = 3,   /* level 0: rank bitvector + run records                     */
-    CRDT_HIP_STAGE_RPARENT = 4,  /* level 0: parent run and weight of every run               */
-    CRDT_HIP_STAGE_COUNT = 5,    /* level 1: child count per parent run                       */
-    CRDT_HIP_STAGE_SCAN = 6,     /* level 1: exclusive scan of child counts                   */
-    CRDT_HIP_STAGE_PLACE = 7,    /* level 1: children scattered into parent segments          */
-    CRDT_HIP_STAGE_LINK = 8,     /* level 1: sibling sort + first-child / next-sibling        */
-    CRDT_HIP_STAGE_WALK1 = 9,    /* level 1: Euler-tour sublist sums                          */
-    CRDT_HIP_STAGE_RANK = 10,    /* level 1: ranking of the splitter lists                    */
-    CRDT_HIP_STAGE_WALK2 = 11,   /* level 1: Euler-tour re-walk, run offsets                  */
-    CRDT_HIP_STAGE_EXPAND = 12,  /* items -> UTF-8 at run offset + in-run prefix              */
-    CRDT_HIP_STAGE_DIGEST = 13,  /* per-document tree digest                                  */
-    CRDT_HIP_NSTAGES = 14
+    CRDT_HIP_STAGE_TSCAN = 1,    /* level 0: one-pass tile scan (look-back): run heads, rank
+                                    bitvector, run records                                    */
+    CRDT_HIP_STAGE_RPARENT = 2,  /* level 0: parent run and weight of every run               */
+    CRDT_HIP_STAGE_COUNT = 3,    /* level 1: child count per parent run                       */
+    CRDT_HIP_STAGE_SCAN = 4,     /* level 1: exclusive scan of child counts                   */
+    CRDT_HIP_STAGE_PLACE = 5,    /* level 1: children scattered into parent segments          */
+    CRDT_HIP_STAGE_LINK = 6,     /* level 1: sibling sort + first-child / next-sibling        */
+    CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums                          */
+    CRDT_HIP_STAGE_RANK = 8,     /* level 1: ranking of the splitter lists                    */
+    CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets                  */
+    CRDT_HIP_STAGE_EXPAND = 10,  /* items -> UTF-8 at run offset + in-run prefix              */
+    CRDT_HIP_STAGE_DIGEST = 11,  /* per-document tree digest                                  */
+    CRDT_HIP_NSTAGES = 12
 };
 
 /* ---- library / context ----------------------------------------------------------------- */
@@ -108,7 +107,7 @@ int crdt_hip_device_count(int* out);
 int crdt_hip_init(int device, crdt_hip_ctx** out);
 int crdt_hip_destroy(crdt_hip_ctx* ctx);
 const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
-/* Tuning: splitter stride of the list ranking (power of two, 16..4096; default 64) and the
+/* Tuning: splitter stride of the list ranking (power of two, 16..4096; default 16) and the
  * maximum slots per device wave (default 2^30). */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 

@@ -133,9 +133,9 @@ def fanout_log(n_children, depth_extra=0):
     return crdt_hip.LogArrays(parent, lam, np.zeros(n, np.uint16), deleted, cp)
 
 
-@pytest.mark.parametrize("k", [2, 3, 17, 64, 65, 1000, 4096, 4097, 20000])
+@pytest.mark.parametrize("k", [2, 3, 4, 8, 9, 17, 64, 65, 1000, 4096, 4097, 20000])
 def test_sibling_groups_every_sort_path(ctx, oracle, k):
-    """2 inline, 3..64 wave rank sort, 65..4096 LDS bitonic, >4096 global bitonic."""
+    """2 inline, 3..8 register network, 9..64 wave rank sort, 65..4096 LDS bitonic, >4096 global."""
     log = fanout_log(k, depth_extra=50)
     order = ctx.merge_order(log)
     _, ref = oracle.merge(to_anchor(log), want_order=True)
