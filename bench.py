@@ -59,6 +59,21 @@ KERNEL_BYTES = {
 }
 TEXT_KERNELS = ("expand", "digest")
 
+def expected_digests(golden_dig, docs: int) -> np.ndarray:
+    """Document r of a replica batch is a copy of trace r % 4."""
+    return np.array([golden_dig[d % len(golden_dig)] for d in range(docs)], np.uint64)
+
+
+def verify_gathered(all_dig: np.ndarray, expect: np.ndarray, world: int) -> bool:
+    """Rank-major all-gathered digests: every rank's shard must equal the golden vector."""
+    return bool(np.array_equal(np.asarray(all_dig, np.uint64), np.tile(expect, world)))
+
+
+def whole_job_rate(units_per_rank: int, world: int, step_seconds: float) -> float:
+    """Weak scaling: every rank processes its own shard; value = all units / max-rank time."""
+    return units_per_rank * world / step_seconds
+
+
 def log(msg: str) -> None:
     print(msg, file=sys.stderr, flush=True)
 
@@ -168,7 +183,7 @@ def main() -> int:
     ms_per_step = elapsed / args.steps * 1e3
 
     # correctness: every document's digest must equal its trace's endContent digest
-    expect = np.array([golden_dig[d % 4] for d in range(batch.docs)], np.uint64)
+    expect = expected_digests(golden_dig, batch.docs)
     ok_local = bool(np.array_equal(dig, expect)) and bool(
         np.array_equal(lens, np.array([survivors[d % 4] for d in range(batch.docs)], np.uint64)))
     if world > 1:
@@ -178,7 +193,7 @@ def main() -> int:
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
         all_dig = ctx.allgather_u64(dig, world)
-        ok = bool(np.array_equal(all_dig, np.tile(expect, world)))
+        ok = verify_gathered(all_dig, expect, world)
         flag = torch.tensor([1 if (ok and ok_local) else 0], device=f"cuda:{local}")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         digests_ok = bool(flag.item())
@@ -187,7 +202,7 @@ def main() -> int:
 
     patches_per_gpu = sum(patches) * args.replicas
     items_per_gpu = batch.items
-    value = patches_per_gpu * world / (elapsed / args.steps)
+    value = whole_job_rate(patches_per_gpu, world, elapsed / args.steps)
 
     # per-kernel device times (HIP events on the engine stream), mean over timed steps
     stage_ns = {k: float(np.mean([s["stage_ns"][k] for s in stats])) for k in stats[0]["stage_ns"]}
