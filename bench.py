@@ -44,8 +44,8 @@ PIPE_B_PER_ITEM = 117.0
 # declared inputs read once + outputs written once, as (bytes per item slot, bytes per run);
 # "s" = survivor (visible UTF-8) bytes per slot is added where the kernel touches the text.
 KERNEL_BYTES = {
-    "jump": (4.0, 0.0),          # parent
-    "tile_scan": (10.19, 8.0),   # parent, jump flag, cp, deleted; head bits/ranks; run records
+    "jump": (4.125, 0.0),        # parent; sequential-parent bits
+    "tile_scan": (5.34, 8.0),    # cp, deleted, seq/jump bits; head bits/ranks; run records
     "run_parent": (0.0, 28.0),   # run head/prefix, parent lookup (+ rank word); weight, parent
     "count": (0.0, 8.0),
     "scan": (0.0, 8.0),

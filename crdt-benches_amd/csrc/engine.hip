@@ -130,7 +130,8 @@ struct L0Args {
     const uint16_t* in_agent;
     const uint8_t* in_deleted;
     const uint32_t* in_cp;
-    uint8_t* jump;              // per slot: has a non-consecutive child
+    uint32_t* jbits;            // per slot bit: has a non-consecutive ("jump") child
+    uint16_t* seqb;             // per slot bit (16 per thread): parent is the previous slot
     uint64_t* hbits;            // per 64 slots: run-head bits
     uint32_t* hrank;            // per 64 slots: heads before the word (wave-relative)
     uint32_t ntiles;
@@ -194,57 +195,53 @@ __device__ __forceinline__ void load_slots16(const L0Args& a, uint32_t gs, bool 
         for (int k = 0; k < 16; ++k) o.w[k] = ((l0 + k - 1u) < n) ? 1u : 0u;
     }
     if (!need_heads) return;
-    const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
-    const uint4 jv = *reinterpret_cast<const uint4*>(a.jump + gs);
-    const uint32_t jw[4] = {jv.x, jv.y, jv.z, jv.w};
-    uint32_t prevj = (l0 > 0) ? a.jump[gs - 1] : 0u;
-    uint32_t bad = 0;
+    // head(g) = document start, or an item that does not continue g-1's run:
+    //   continue(g) = seq(g) && !jump(g-1)   (both bitvectors written by k_jump)
+    const uint32_t seq = a.seqb[gs >> 4];
+    const uint32_t wj = (a.jbits[gs >> 5] >> (gs & 31u)) & 0xFFFFu;
+    const uint32_t pj = l0 > 0 ? (a.jbits[(gs - 1) >> 5] >> ((gs - 1) & 31u)) & 1u : 0u;
+    const uint32_t prevj = ((wj << 1) | pj) & 0xFFFFu;  // bit k = jump(gs + k - 1)
+    uint32_t item = 0, root = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 pp = pv[q];
-        const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k = 4 * q + j;
-            const uint32_t local = l0 + k;
-            const uint32_t p = pa[j];
-            const uint32_t jk = (jw[q] >> (8 * j)) & 0xFFu;
-            bool head;
-            if (local == 0) {
-                head = true;
-            } else if (local <= n) {
-                const bool b = p > n || p == local;
-                bad |= b;
-                head = b || p != local - 1 || prevj;
-            } else {
-                head = false;
-            }
-            o.hmask |= (head ? 1u : 0u) << k;
-            prevj = jk;
-        }
+    for (int k = 0; k < 16; ++k) {
+        item |= (((l0 + k - 1u) < n) ? 1u : 0u) << k;
+        root |= ((l0 + k == 0u) ? 1u : 0u) << k;
     }
-    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
+    o.hmask = root | (item & ~(seq & ~prevj));
 }
 
-// 16 slots per thread (one document: 16 | M), 4 x 16-byte parent loads.
+// 16 slots per thread (one document: 16 | 64), 4 x 16-byte parent loads.  Writes the
+// "parent is the previous slot" bits (16 per thread, one u16 store) and sets the jump bit of
+// every parent that has a non-consecutive child; a parent out of range is an error.
 __global__ __launch_bounds__(kBlock) void k_jump(L0Args a) {
     const uint32_t gs = (blockIdx.x * kBlock + threadIdx.x) * kScanItems;
     if (gs >= a.nslots) return;
     const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
     const uint32_t l0 = gs - doc.x;
-    if (l0 > doc.y) return;
-    const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+    uint32_t seq = 0, bad = 0;
+    if (l0 <= doc.y) {
+        const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 pp = pv[q];
-        const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
+        for (int q = 0; q < 4; ++q) {
+            const uint4 pp = pv[q];
+            const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t local = l0 + 4 * q + j, p = pa[j];
-            if ((local - 1u) < doc.y && p <= doc.y && p != local - 1u && p != local)
-                a.jump[doc.x + p] = 1;
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = 4 * q + j, local = l0 + k, p = pa[j];
+                if ((local - 1u) >= doc.y) continue;  // document start or padding
+                if (p > doc.y || p == local) {
+                    bad = 1;  // becomes a run head under the document start (flagged)
+                } else if (p == local - 1u) {
+                    seq |= 1u << k;
+                } else {
+                    const uint32_t ps = doc.x + p;
+                    atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+                }
+            }
         }
     }
+    a.seqb[gs >> 4] = (uint16_t)seq;
+    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
 // Look-back granules (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms R2): every shared
@@ -401,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uin
     if (h != doc.x) {
         uint32_t p = a.in_parent[h];
         key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
-        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_tile_scan
+        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_jump
         pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u;
     }
     a.r_parent[rho] = pr;
@@ -482,8 +479,7 @@ struct TreeArgs {
     uint32_t* deg;
     uint32_t* cstart;
     uint32_t* child;
-    uint2* dn;  // {first_child, weight}
-    uint2* up;  // {next_sibling, parent}
+    uint4* rec;  // per run {first_child, weight, next_sibling, parent}
     uint32_t* defer;
     uint32_t* bigl;
     uint32_t* ctl;
@@ -601,6 +597,18 @@ __device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uin
     }
 }
 
+// Run records: {first_child, weight} written by the run itself, {next_sibling, parent} by
+// whoever sorted its sibling group; one 16-byte load per arc in the walks.
+__device__ __forceinline__ void set_dn(const TreeArgs& a, uint32_t g, uint32_t fc, uint32_t w) {
+    reinterpret_cast<uint2*>(a.rec + g)[0] = make_uint2(fc, w);
+}
+__device__ __forceinline__ void set_up(const TreeArgs& a, uint32_t c, uint32_t ns, uint32_t p) {
+    reinterpret_cast<uint2*>(a.rec + c)[1] = make_uint2(ns, p);
+}
+__device__ __forceinline__ void set_fc(const TreeArgs& a, uint32_t p, uint32_t c) {
+    reinterpret_cast<uint32_t*>(a.rec + p)[0] = c;
+}
+
 // Up to 8 siblings: Batcher's 19-comparator odd-even merge network (verified on all 0-1
 // inputs), padding key 0 sorts last (every child key has lamport >= 1).
 __device__ __forceinline__ uint32_t link_small(const TreeArgs& a, uint32_t g, uint32_t s0,
@@ -622,7 +630,7 @@ __device__ __forceinline__ uint32_t link_small(const TreeArgs& a, uint32_t g, ui
     cx(k[1], c[1], k[2], c[2]); cx(k[3], c[3], k[4], c[4]); cx(k[5], c[5], k[6], c[6]);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        if ((uint32_t)i < cnt) a.up[c[i]] = make_uint2((uint32_t)i + 1 < cnt ? c[i + 1 < 8 ? i + 1 : 7] : kNil, g);
+        if ((uint32_t)i < cnt) set_up(a, c[i], (uint32_t)i + 1 < cnt ? c[i + 1 < 8 ? i + 1 : 7] : kNil, g);
     return c[0];
 }
 
@@ -634,25 +642,25 @@ __global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
     bool defer = false;
     if (g < a.R) {
         const uint32_t w = a.in_w[g];
-        if (a.in_parent[g] == kNil) a.up[g] = make_uint2(kNil, kNil);  // no sibling, no parent
+        if (a.in_parent[g] == kNil) set_up(a, g, kNil, kNil);  // no sibling, no parent
         const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
         uint32_t fc = kNil;
         if (cnt == 1) {
             const uint32_t c0 = a.child[s0];
             fc = c0;
-            a.up[c0] = make_uint2(kNil, g);
+            set_up(a, c0, kNil, g);
         } else if (cnt == 2) {
             uint32_t c0 = a.child[s0], c1 = a.child[s0 + 1];
             if (sib_key(a, c0) < sib_key(a, c1)) { uint32_t t = c0; c0 = c1; c1 = t; }
             fc = c0;
-            a.up[c0] = make_uint2(c1, g);
-            a.up[c1] = make_uint2(kNil, g);
+            set_up(a, c0, c1, g);
+            set_up(a, c1, kNil, g);
         } else if (cnt <= 8) {
             if (cnt) fc = link_small(a, g, s0, cnt);
         } else {
             defer = true;  // first_child written by the sort kernels
         }
-        a.dn[g] = make_uint2(fc, w);
+        set_dn(a, g, fc, w);
     }
     // deferred segments: one global atomic per block
     uint32_t slot = 0;
@@ -693,8 +701,8 @@ __global__ __launch_bounds__(kBlock) void k_sortmid(TreeArgs a) {
         const uint32_t ns_of_rank = (lane + 1 < cnt) ? succ : kNil;
         const uint32_t ns = (uint32_t)__shfl((int)ns_of_rank, (int)(on ? rank : 0));
         if (on) {
-            a.up[c] = make_uint2(ns, p);
-            if (rank == 0) a.dn[p].x = c;
+            set_up(a, c, ns, p);
+            if (rank == 0) set_fc(a, p, c);
         }
     }
 }
@@ -750,9 +758,9 @@ __global__ __launch_bounds__(kBigThreads) void k_sortbig(TreeArgs a) {
         }
         for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) {
             const uint32_t c = seg[i];
-            a.up[c] = make_uint2(i + 1 < cnt ? seg[i + 1] : kNil, p);
+            set_up(a, c, i + 1 < cnt ? seg[i + 1] : kNil, p);
         }
-        if (threadIdx.x == 0) a.dn[p].x = seg[0];
+        if (threadIdx.x == 0) set_fc(a, p, seg[0]);
         __syncthreads();
     }
 }
@@ -784,18 +792,23 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
     uint32_t sum = 0, steps = 0, nxt = kNil;
     if (splitter_arc(a, s, v, up)) {
         for (;;) {
+            const uint4 r = a.rec[v];
             uint32_t nv;
             bool nup;
             if (!up) {
-                const uint2 r = a.dn[v];
                 sum += r.y;
-                if (r.x != kNil) { nv = r.x; nup = false; } else { nv = v; nup = true; }
-            } else {
-                const uint2 r = a.up[v];
-                if (r.x != kNil) { nv = r.x; nup = false; }
-                else if (r.y != kNil) { nv = r.y; nup = true; }
-                else break;  // up arc of a document start: end of that document's tour
+                if (r.x != kNil) {
+                    nv = r.x;
+                    nup = false;
+                    goto next1;
+                }
+                // a leaf: its up arc follows, from the same record
+                if ((v & mask) == 0) { nxt = ((v >> m) << 1) | 1u; break; }
             }
+            if (r.z != kNil) { nv = r.z; nup = false; }
+            else if (r.w != kNil) { nv = r.w; nup = true; }
+            else break;  // up arc of a document start: end of that document's tour
+        next1:
             if ((nv & mask) == 0) { nxt = ((nv >> m) << 1) | (nup ? 1u : 0u); break; }
             v = nv;
             up = nup;
@@ -895,20 +908,24 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
     uint32_t off = live ? spref[s] : 0u;
     uint32_t steps = 0, runs = 0;
     for (; live;) {
+        const uint4 r = a.rec[v];
         uint32_t nv;
         bool nup;
         if (!up) {
-            const uint2 r = a.dn[v];
-            a.roff[v] = off;
+            if (r.y) a.roff[v] = off;  // runs without visible bytes are never expanded
             off += r.y;
             ++runs;
-            if (r.x != kNil) { nv = r.x; nup = false; } else { nv = v; nup = true; }
-        } else {
-            const uint2 r = a.up[v];
-            if (r.x != kNil) { nv = r.x; nup = false; }
-            else if (r.y != kNil) { nv = r.y; nup = true; }
-            else break;
+            if (r.x != kNil) {
+                nv = r.x;
+                nup = false;
+                goto next2;
+            }
+            if ((v & mask) == 0) break;  // a leaf whose up arc is a splitter
         }
+        if (r.z != kNil) { nv = r.z; nup = false; }
+        else if (r.w != kNil) { nv = r.w; nup = true; }
+        else break;
+    next2:
         if ((nv & mask) == 0) break;
         v = nv;
         up = nup;
@@ -1083,11 +1100,12 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(ticket_); dfree(tile_exw_);
+    dfree(jbits_); dfree(seqb_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(ticket_);
+    dfree(tile_exw_);
     dfree(doc_root_); dfree(doc_p0_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
-    dfree(ctl_); dfree(dn_); dfree(up_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
+    dfree(ctl_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
     dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
     dfree(dig_); dfree(leafh_); dfree(text_);
     if (host_ctl_) (void)hipHostFree(host_ctl_);
@@ -1242,9 +1260,10 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jump_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(tile_exw_);
+        dfree(jbits_); dfree(seqb_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(tile_exw_);
         const uint64_t tiles = slots / kTile + 2;
-        HIPCHK(dalloc(&jump_, slots + 64), "hipMalloc jump");
+        HIPCHK(dalloc(&jbits_, slots / 32 + 4), "hipMalloc jump bits");
+        HIPCHK(dalloc(&seqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&hbits_, slots / 64 + 2), "hipMalloc hbits");
         HIPCHK(dalloc(&hrank_, slots / 64 + 2), "hipMalloc hrank");
         HIPCHK(dalloc(&look_, 4 * tiles), "hipMalloc look-back");
@@ -1291,7 +1310,7 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
     if (R > cap_runs_) {
         dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
         dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_);
-        dfree(scan_sums_); dfree(dn_); dfree(up_);
+        dfree(scan_sums_); dfree(rec_);
         const uint64_t r = R + (R >> 3) + 4096;  // headroom against regrowth
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
         HIPCHK(dalloc(&r_w_, r), "hipMalloc r_w");
@@ -1304,8 +1323,7 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
         HIPCHK(dalloc(&defer_, r / 3 + 64), "hipMalloc defer");
         HIPCHK(dalloc(&bigl_, r / 65 + 64), "hipMalloc bigl");
         HIPCHK(dalloc(&scan_sums_, r / kScanTile + 2), "hipMalloc scan sums");
-        HIPCHK(dalloc(&dn_, r), "hipMalloc dn");
-        HIPCHK(dalloc(&up_, r), "hipMalloc up");
+        HIPCHK(dalloc(&rec_, r), "hipMalloc run records");
         cap_runs_ = r;
     }
     if (S > cap_splitters_) {
@@ -1344,7 +1362,8 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.in_agent = L.agent + w.slot0;
     a0.in_deleted = L.deleted + w.slot0;
     a0.in_cp = L.cp + w.slot0;
-    a0.jump = jump_;
+    a0.jbits = jbits_;
+    a0.seqb = seqb_;
     a0.hbits = hbits_;
     a0.hrank = hrank_;
     a0.ntiles = ntiles;
@@ -1370,7 +1389,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     // ---- level 0: runs -------------------------------------------------------------------
     HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
     HIPCHK(hipMemsetAsync(ticket_, 0, 16, s), "memset ticket");
-    HIPCHK(hipMemsetAsync(jump_, 0, w.nslots + 64ull, s), "memset jump");
+    HIPCHK(hipMemsetAsync(jbits_, 0, (w.nslots / 32 + 4) * 4ull, s), "memset jump bits");
     BEGIN(S_JUMP);
     k_jump<<<njump, kBlock, 0, s>>>(a0);
     END(S_JUMP);
@@ -1415,7 +1434,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a.doc_root = doc_root_;
     a.doc_p0 = doc_p0_;
     a.wtotal = wtotal;
-    a.deg = deg_; a.cstart = cstart_; a.child = child_; a.dn = dn_; a.up = up_;
+    a.deg = deg_; a.cstart = cstart_; a.child = child_; a.rec = rec_;
     a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;
     a.roff = roff_;
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.dig = dig_;

@@ -87,7 +87,8 @@ public:
 private:
     // level-0 scratch (per slot / per tile), grown on demand
     uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
-    uint8_t* jump_ = nullptr;
+    uint32_t* jbits_ = nullptr;
+    uint16_t* seqb_ = nullptr;
     uint64_t *hbits_ = nullptr, *look_ = nullptr;
     uint32_t *hrank_ = nullptr, *ticket_ = nullptr, *tile_exw_ = nullptr;
     uint32_t epoch_ = 0;  // look-back epoch, unique per tile-scan launch
@@ -102,7 +103,7 @@ private:
     uint64_t* r_key_ = nullptr;
     uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
              *bigl_ = nullptr, *scan_sums_ = nullptr, *ctl_ = nullptr;
-    uint2 *dn_ = nullptr, *up_ = nullptr;
+    uint4* rec_ = nullptr;
     uint32_t *sw_ = nullptr, *snext_ = nullptr, *pred_ = nullptr, *v0_ = nullptr, *v1_ = nullptr,
              *p0_ = nullptr, *p1_ = nullptr;
     uint32_t* host_ctl_ = nullptr;       // pinned
