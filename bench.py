@@ -40,24 +40,23 @@ METRIC = "merged CRDT ops/sec (whole node) + achieved HBM GB/s, batched trace me
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # SURVEY.md §8(d) algorithmic-bytes contract: 117 B per op-log item + survivor bytes
 PIPE_B_PER_ITEM = 117.0
-# Per-kernel algorithmic bytes (declared before tuning): each kernel's
-# declared inputs read once + outputs written once, as (bytes per item slot, bytes per run);
-# "s" = survivor (visible UTF-8) bytes per slot is added where the kernel touches the text.
+# Per-kernel algorithmic bytes: each kernel's declared inputs read once +
+# outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
-    "jump": (4.125, 0.0),        # parent; sequential-parent bits
-    "tile_scan": (5.34, 8.0),    # cp, deleted, seq/jump bits; head bits/ranks; run records
-    "run_parent": (0.0, 28.0),   # run head/prefix, parent lookup (+ rank word); weight, parent
-    "count": (0.0, 8.0),
-    "scan": (0.0, 8.0),
-    "place": (0.0, 12.0),
-    "link": (0.0, 28.0),
-    "walk1": (0.0, 16.0),
-    "rank": (0.0, 0.5),
-    "walk2": (0.0, 20.0),
-    "expand": (5.19, 8.0),       # cp, deleted, head bits; run offset/prefix; + text (s)
-    "digest": (0.0, 0.0),        # + text (s)
+    "classify": (9.625, 0.0, 1.0),   # parent, cp, deleted; seq bits, weight nibbles; tile UTF-8
+    "runs": (1.0, 8.0, 2.0),         # seq/jump/head bits, nibbles, rank words; run records; text move
+    "run_parent": (0.0, 28.0, 0.0),  # run head/prefix, parent lookup (+ rank word); weight, parent
+    "count": (0.0, 8.0, 0.0),
+    "scan": (0.0, 8.0, 0.0),
+    "place": (0.0, 12.0, 0.0),
+    "link": (0.0, 28.0, 0.0),
+    "walk1": (0.0, 16.0, 0.0),
+    "rank": (0.0, 0.5, 0.0),
+    "walk2": (0.0, 20.0, 0.0),
+    "expand": (0.0, 16.0, 2.0),      # run prefix/weight/head/offset; slot-order text -> document
+    "digest": (0.0, 0.0, 1.0),
 }
-TEXT_KERNELS = ("expand", "digest")
+
 
 def expected_digests(golden_dig, docs: int) -> np.ndarray:
     """Document r of a replica batch is a copy of trace r % 4."""
@@ -214,11 +213,8 @@ def main() -> int:
     text_bytes = stats[0]["text_bytes"]
 
     def alg_bytes(k):
-        per_slot, per_run = KERNEL_BYTES[k]
-        b = per_slot * slots + per_run * runs
-        if k in TEXT_KERNELS:
-            b += text_bytes
-        return b
+        per_slot, per_run, per_text = KERNEL_BYTES[k]
+        return per_slot * slots + per_run * runs + per_text * text_bytes
 
     per_kernel = {k: {"ms": stage_ns[k] / 1e6, "launches": launches[k],
                       "alg_gbps": alg_bytes(k) / stage_ns[k] if stage_ns[k] else 0.0}

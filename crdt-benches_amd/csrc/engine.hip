@@ -12,11 +12,11 @@
 //  the document; on the josephg traces they hold 93-98 % of all items.  Run heads are recorded
 //  in a rank bitvector (1 bit/slot + a u32 rank per 64 slots) and every run gets its parent run,
 //  its key (lamport, agent of the head) and its weight (visible UTF-8 bytes).
-//    k_jump        flag slots that have a non-consecutive child
-//    k_tile_reduce per-tile head count + weight sum, per-document run counts
-//    k_tile_top    tile bases; per-document run bases (each document padded to M runs)
-//    k_tile_apply  head bitvector + rank words; run records (head slot, key, weight prefix)
-//    k_run_parent  parent run (rank lookup) and weight of every run
+//    k_classify    seq/jump bits, weight nibbles, each tile's UTF-8 compacted in slot order
+//    k_heads       head bitvector words, per-tile head counts
+//    k_tiles_*     exclusive scan of the per-tile (heads, weight) pairs
+//    k_runs        rank words, run records (head slot, weight prefix), slot-order UTF-8
+//    k_run_parent  parent run (rank lookup), key and weight of every run
 //  Level 1 merges the tree of runs:
 //    k_count / k_scan_* / k_place        children grouped by parent run
 //    k_link / k_sortmid / k_sortbig      sibling order -> first-child / next-sibling
@@ -25,7 +25,7 @@
 //                                        run id % M == 0, pointer jumping over the splitter
 //                                        lists); weighted so the rank is each run's byte offset
 //  Expansion and digest:
-//    k_expand      every visible item's UTF-8 lands at run offset + in-run prefix (coalesced)
+//    k_expand      runs copy their slot-order UTF-8 to run offset in the document
 //    k_leafhash / k_docdigest  xxh64 tree digest per document
 // The Euler tour is never materialised: succ(down v) = down(first_child v) or up v;
 // succ(up v) = down(next_sibling v) or up(parent v).
@@ -46,9 +46,8 @@ constexpr int kBlock = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kBlock * kScanItems;
 constexpr uint32_t kDocAlignLog2 = 6;  // slot-level document alignment (chunk table: 1/64)
-constexpr int kTileThreads = 1024;                       // level-0 tile: 1024 threads x 16 slots
-constexpr int kTile = kTileThreads * kScanItems;
 constexpr uint32_t kLeaf = 4096;
+constexpr uint64_t kMaxWaveText = (1ull << 32) - (1ull << 20);  // weight prefixes are u32
 constexpr int kMidGrid = 16384;
 constexpr int kBigGrid = 256;
 constexpr int kBigThreads = 1024;
@@ -59,7 +58,7 @@ enum Ctl {
     C_NDEFER = 0,   // deferred sibling segments (9..64 children)
     C_NBIG = 1,     // sibling segments with > 64 children
     C_ERR = 2,      // error bits: 1 bad parent, 2 walk overrun, 4 text overflow, 8 write out
-                    //   of range, 16 unreachable runs (cycle), 32 look-back timeout
+                    //   of range, 16 unreachable runs (cycle)
     C_RTOTAL = 3,   // runs of the wave
     C_WTOTAL = 4,   // weight total of the wave
     C_RMAX = 5,     // most runs in one document
@@ -67,7 +66,7 @@ enum Ctl {
 };
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
-enum Stage { S_JUMP, S_TSCAN, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
+enum Stage { S_CLASSIFY, S_RUNS, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
              S_WALK2, S_EXPAND, S_DIGEST, S_N };
 
 // ---------------------------------------------------------------------------------------------
@@ -118,245 +117,315 @@ __device__ __forceinline__ uint32_t utf8_len(uint32_t c) {
 // ---------------------------------------------------------------------------------------------
 // Level 0: runs
 // ---------------------------------------------------------------------------------------------
-// Runs are numbered by global head rank within the wave (run rho = number of heads before its
-// head slot), so a run's weight is pstart[rho+1] - pstart[rho] and no per-document padding is
-// needed: documents are contiguous ranges of runs starting at doc_root[d].
+// Level 0 streams over 4096-slot tiles (one workgroup, 16 consecutive slots per thread; a
+// thread's slots are always inside one document because documents start on 64-slot
+// boundaries).  Runs are numbered by global head rank within the wave (run rho = number of
+// heads before its head slot), so a run's weight is pstart[rho+1] - pstart[rho] and no
+// per-document padding is needed: documents are contiguous ranges of runs from doc_root[d].
+// There is no single-pass look-back: the three passes read 9.6, 0.2 and 0.7 bytes per slot.
 struct L0Args {
     uint32_t nslots, log2m, ndocs, mode;  // mode: 0 text, 1 order
-    const uint32_t* chunk_doc;  // per M slots: wave-local document
+    uint32_t ntiles;
+    const uint32_t* chunk_doc;  // per 64 slots: wave-local document
     const uint2* docs;          // per document {wave-relative base slot, n items}
     const uint32_t* in_parent;
     const uint32_t* in_lamport;
     const uint16_t* in_agent;
     const uint8_t* in_deleted;
     const uint32_t* in_cp;
-    uint32_t* jbits;            // per slot bit: has a non-consecutive ("jump") child
-    uint16_t* seqb;             // per slot bit (16 per thread): parent is the previous slot
+    uint32_t* jbits;            // per slot bit: has a non-consecutive child in a later tile
+    uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
+    uint16_t* seqb;             // per slot bit, 16 per thread: parent is the previous slot
+    uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
+    uint8_t* stile;             // per tile: its visible UTF-8 in slot order (kTileBytes each)
+    uint8_t* sbytes;            // the wave's visible UTF-8 in slot order (= weight order)
+    uint64_t sbytes_cap;
+    uint2* tile_hw;             // per tile {heads, weight}: totals, then exclusive prefixes
+    uint2* tile_sums;           // per 4096 tiles: scan carries
     uint64_t* hbits;            // per 64 slots: run-head bits
     uint32_t* hrank;            // per 64 slots: heads before the word (wave-relative)
-    uint32_t ntiles;
-    uint64_t* look;             // per tile: 4 look-back granules {epoch, value}
-    uint32_t* ticket;           // tile ticket counter (zeroed per launch)
-    uint32_t* tile_exw;         // per 4096-slot sub-tile: exclusive weight prefix (k_expand)
-    uint32_t epoch;             // nonzero, unique per launch
+    uint32_t* r_head;           // per run: head slot
+    uint32_t* r_pstart;         // per run: weight prefix at its head
+    uint32_t* r_parent;         // per run: parent run (kNil for a document start)
+    uint32_t* r_w;              // per run: weight
+    uint64_t* r_key;            // per run: (lamport << 16 | agent) of the head
     uint32_t* doc_root;         // per document: its document-start run
     uint32_t* doc_p0;           // per document: weight prefix at its start
-    uint32_t* r_head;           // per run: head slot
-    uint32_t* r_pstart;         // per run: weight prefix at the head
-    uint32_t* r_parent;         // per run: parent run (kNil for a document-start run)
-    uint32_t* r_w;              // per run: weight
-    uint64_t* r_key;            // per run: sibling key (lamport, agent) of its head
-    const uint32_t* roff;       // per run: offset of the run inside its document (level 1)
-    const uint64_t* toff;       // per document: output offset
-    uint8_t* text;
     uint32_t* ctl;
 };
 
-// The 16 slots [gs, gs+16) of one thread (always inside one document: 16 | M).
-struct Slots16 {
-    uint32_t hmask;   // run-head bits
-    uint32_t w[16];   // weights
-    uint32_t d;       // document (kNil when gs is past the wave)
-    uint2 doc;
-};
+constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 
-__device__ __forceinline__ void load_slots16(const L0Args& a, uint32_t gs, bool need_heads,
-                                             Slots16& o) {
-    o.hmask = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) o.w[k] = 0;
-    o.d = kNil;
-    o.doc = make_uint2(0, 0);
-    if (gs >= a.nslots) return;
-    o.d = a.chunk_doc[gs >> a.log2m];
-    o.doc = a.docs[o.d];
-    const uint32_t base = o.doc.x, n = o.doc.y;
-    const uint32_t l0 = gs - base;  // local id of slot gs
-    if (l0 > n) return;             // all padding
-    if (a.mode == 0) {
-        const uint4 dl = *reinterpret_cast<const uint4*>(a.in_deleted + gs);
-        const uint32_t dw[4] = {dl.x, dl.y, dl.z, dl.w};
-        const uint4* cpv = reinterpret_cast<const uint4*>(a.in_cp + gs);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 c = cpv[q];
-            const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int k = 4 * q + j;
-                const uint32_t local = l0 + k;
-                const bool item = (local - 1u) < n;
-                const bool del = (dw[q] >> (8 * j)) & 0xFFu;
-                o.w[k] = (item && !del) ? utf8_len(cc[j] & kCpMask) : 0u;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) o.w[k] = ((l0 + k - 1u) < n) ? 1u : 0u;
-    }
-    if (!need_heads) return;
-    // head(g) = document start, or an item that does not continue g-1's run:
-    //   continue(g) = seq(g) && !jump(g-1)   (both bitvectors written by k_jump)
-    const uint32_t seq = a.seqb[gs >> 4];
-    const uint32_t wj = (a.jbits[gs >> 5] >> (gs & 31u)) & 0xFFFFu;
-    const uint32_t pj = l0 > 0 ? (a.jbits[(gs - 1) >> 5] >> ((gs - 1) & 31u)) & 1u : 0u;
-    const uint32_t prevj = ((wj << 1) | pj) & 0xFFFFu;  // bit k = jump(gs + k - 1)
-    uint32_t item = 0, root = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        item |= (((l0 + k - 1u) < n) ? 1u : 0u) << k;
-        root |= ((l0 + k == 0u) ? 1u : 0u) << k;
-    }
-    o.hmask = root | (item & ~(seq & ~prevj));
-}
-
-// 16 slots per thread (one document: 16 | 64), 4 x 16-byte parent loads.  Writes the
-// "parent is the previous slot" bits (16 per thread, one u16 store) and sets the jump bit of
-// every parent that has a non-consecutive child; a parent out of range is an error.
-__global__ __launch_bounds__(kBlock) void k_jump(L0Args a) {
-    const uint32_t gs = (blockIdx.x * kBlock + threadIdx.x) * kScanItems;
-    if (gs >= a.nslots) return;
-    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-    const uint32_t l0 = gs - doc.x;
+// k_classify: parents and characters of 16 slots per thread (4 + 4 x 16-byte loads + 16 B of
+// deleted flags).
+//  * "parent is the previous slot" bits (one u16 store per thread);
+//  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
+//    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
+//  * per-slot weights as nibbles, the tile's weight total, and the tile's visible UTF-8
+//    compacted in slot order: assembled in LDS, stored to its stile segment in 16-byte pieces.
+// A parent out of range (or an item that is its own parent) is flagged; such an item becomes a
+// run head under the document start, and the merge reports CRDT_HIP_EBADLOG.
+__global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
+    __shared__ uint32_t lds[kBlock / 64];
+    __shared__ uint32_t jl[kScanTile / 32];
+    __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
+    if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
+    __syncthreads();
     uint32_t seq = 0, bad = 0;
-    if (l0 <= doc.y) {
-        const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+    uint32_t cc[16], w[16];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 pp = pv[q];
-            const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
+    for (int k = 0; k < 16; ++k) cc[k] = 0, w[k] = 0;
+    if (gs < a.nslots) {
+        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        const uint32_t l0 = gs - doc.x;
+        if (l0 <= doc.y) {
+            const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+            const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + gs);
+            const uint4 dl = a.mode == 0 ? *reinterpret_cast<const uint4*>(a.in_deleted + gs)
+                                         : make_uint4(0, 0, 0, 0);
+            const uint32_t dw[4] = {dl.x, dl.y, dl.z, dl.w};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = 4 * q + j, local = l0 + k, p = pa[j];
-                if ((local - 1u) >= doc.y) continue;  // document start or padding
-                if (p > doc.y || p == local) {
-                    bad = 1;  // becomes a run head under the document start (flagged)
-                } else if (p == local - 1u) {
-                    seq |= 1u << k;
-                } else {
-                    const uint32_t ps = doc.x + p;
-                    atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+            for (int q = 0; q < 4; ++q) {
+                const uint4 pp = pv[q];
+                const uint4 c4 = cv[q];
+                const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
+                const uint32_t ca[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t k = 4 * q + j, local = l0 + k, p = pa[j];
+                    if ((local - 1u) >= doc.y) continue;  // document start or padding
+                    const uint32_t c = ca[j] & kCpMask;
+                    cc[k] = c;
+                    const bool del = (dw[q] >> (8 * j)) & 0xFFu;
+                    w[k] = a.mode ? 1u : (del ? 0u : utf8_len(c));
+                    if (p > doc.y || p == local) {
+                        bad = 1;
+                    } else if (p == local - 1u) {
+                        seq |= 1u << k;
+                    } else {
+                        const uint32_t ps = doc.x + p;
+                        if ((ps / kScanTile) == tile)
+                            atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
+                        else
+                            atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+                    }
                 }
             }
         }
+        uint64_t nib = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) nib |= (uint64_t)w[k] << (4 * k);
+        a.seqb[gs >> 4] = (uint16_t)seq;
+        a.wnib[gs >> 4] = nib;
     }
-    a.seqb[gs >> 4] = (uint16_t)seq;
-    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
-}
-
-// Look-back granules (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms R2): every shared
-// word is an 8-byte {epoch, value} granule written by ONE relaxed agent-scope atomic store and
-// read by relaxed agent-scope atomic loads, so the value is its own flag and no fence is needed.
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-__device__ __forceinline__ void granule_store(uint64_t* p, uint32_t epoch, uint32_t v) {
-    __hip_atomic_store((gu64*)p, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t granule_load(const uint64_t* p) {
-    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr uint32_t kSpinLimit = 1u << 22;
-
-// Single-pass tile scan with decoupled look-back (tiles ordered by an atomic ticket, so every
-// predecessor a tile waits on is already running and publishes its aggregate without waiting).
-// Per tile: run-head bits + weights of 4096 slots, then the tile's exclusive (heads, weight)
-// prefix, then the rank bitvector words and one record per run head.
-__global__ __launch_bounds__(kTileThreads) void k_tile_scan(L0Args a) {
-    __shared__ uint32_t lds[kTileThreads / 64];
-    __shared__ uint32_t s_tile, s_exh, s_exw;
-    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint32_t gs = tile * kTile + threadIdx.x * kScanItems;
-    Slots16 s;
-    load_slots16(a, gs, true, s);
     uint32_t W = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) W += s.w[k];
-    const uint32_t H = __popc(s.hmask);
-    uint32_t th, tw;
-    const uint32_t exh_t = block_excl_scan<kTileThreads / 64>(H, lds, th);
-    const uint32_t exw_t = block_excl_scan<kTileThreads / 64>(W, lds, tw);
-    uint64_t* look = a.look + 4ull * tile;
-    if (threadIdx.x == 0) {  // aggregate first: never waits on anything
-        granule_store(look + 0, a.epoch, th);
-        granule_store(look + 1, a.epoch, tw);
-    }
-    if (threadIdx.x < 64) {  // wave 0: parallel look-back, 64 predecessors per round
-        const uint32_t lane = threadIdx.x;
-        uint32_t exh = 0, exw = 0, spins = 0;
-        bool fail = false;
-        for (int base = (int)tile - 1; base >= 0; base -= 64) {
-            const int j = base - (int)lane;
-            uint32_t vh = 0, vw = 0;
-            bool inc = true;  // j < 0: the virtual inclusive prefix 0
-            if (j >= 0) {
-                const uint64_t* lj = a.look + 4ull * (uint32_t)j;
-                uint64_t gh = granule_load(lj + 0), gw = granule_load(lj + 1);
-                while (((gh >> 32) != a.epoch || (gw >> 32) != a.epoch) && !fail) {
-                    __builtin_amdgcn_s_sleep(1);
-                    gh = granule_load(lj + 0);
-                    gw = granule_load(lj + 1);
-                    if (++spins > kSpinLimit) fail = true;
-                }
-                const uint64_t ih = granule_load(lj + 2), iw = granule_load(lj + 3);
-                inc = (ih >> 32) == a.epoch && (iw >> 32) == a.epoch;
-                vh = (uint32_t)(inc ? ih : gh);
-                vw = (uint32_t)(inc ? iw : gw);
-            }
-            const uint64_t incm = __ballot(inc);
-            if (incm) {
-                const uint32_t f = (uint32_t)(__ffsll((unsigned long long)incm) - 1);
-                exh += wave_sum(lane <= f ? vh : 0u);
-                exw += wave_sum(lane <= f ? vw : 0u);
+    for (int k = 0; k < 16; ++k) W += w[k];
+    uint32_t tw;
+    const uint32_t ex = block_excl_scan<kBlock / 64>(W, lds, tw);
+    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
+    if (a.mode == 0 && W) {
+        uint8_t* o = sb + ex;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t c = cc[k];
+            switch (w[k]) {
+            case 1:
+                o[0] = (uint8_t)c;
+                break;
+            case 2:
+                o[0] = (uint8_t)(0xC0u | (c >> 6));
+                o[1] = (uint8_t)(0x80u | (c & 63u));
+                break;
+            case 3:
+                o[0] = (uint8_t)(0xE0u | (c >> 12));
+                o[1] = (uint8_t)(0x80u | ((c >> 6) & 63u));
+                o[2] = (uint8_t)(0x80u | (c & 63u));
+                break;
+            case 4:
+                o[0] = (uint8_t)(0xF0u | (c >> 18));
+                o[1] = (uint8_t)(0x80u | ((c >> 12) & 63u));
+                o[2] = (uint8_t)(0x80u | ((c >> 6) & 63u));
+                o[3] = (uint8_t)(0x80u | (c & 63u));
+                break;
+            default:
                 break;
             }
-            exh += wave_sum(vh);
-            exw += wave_sum(vw);
-        }
-        if (__ballot(fail)) {
-            if (lane == 0) atomicOr(&a.ctl[C_ERR], 32u);
-        }
-        if (lane == 0) {
-            granule_store(look + 2, a.epoch, exh + th);
-            granule_store(look + 3, a.epoch, exw + tw);
-            s_exh = exh;
-            s_exw = exw;
+            o += w[k];
         }
     }
     __syncthreads();
-    const uint32_t rank = s_exh + exh_t;
-    uint32_t P = s_exw + exw_t;
-    if ((threadIdx.x & (kBlock - 1)) == 0) a.tile_exw[tile * (kTile / kScanTile) + threadIdx.x / kBlock] = P;
-    if (tile == a.ntiles - 1 && threadIdx.x == 0) {
-        a.ctl[C_RTOTAL] = s_exh + th;
-        a.ctl[C_WTOTAL] = s_exw + tw;
+    if (threadIdx.x == 0) a.tile_hw[tile].y = tw;
+    if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
+    if (a.mode == 0) {
+        uint4* dst = reinterpret_cast<uint4*>(a.stile + (uint64_t)tile * kTileBytes);
+        const uint4* src = reinterpret_cast<const uint4*>(sb);
+        for (uint32_t i = threadIdx.x; i < (tw + 15u) / 16u; i += kBlock) dst[i] = src[i];
     }
-    // 64-bit head word from 4 consecutive lanes
-    const uint32_t q = threadIdx.x & 3u;
-    uint64_t word = (uint64_t)s.hmask << (16 * q);
-    word |= (uint64_t)__shfl_xor((long long)word, 1);
-    word |= (uint64_t)__shfl_xor((long long)word, 2);
+}
+
+__device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
+    return b >= 64u ? ~0ull : ((1ull << b) - 1ull);
+}
+
+// k_heads: one thread per 64-slot word of the rank bitvector (a word is inside one document),
+// one wave per tile.  head(g) = document start, or an item that does not continue the run of
+// the slot before it: continue(g) = seq(g) && !jump(g-1).
+__global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
+    const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t gs = wi * 64u;
+    uint64_t hw = 0;
+    if (gs < a.nslots) {
+        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        const uint32_t l0 = gs - doc.x, n = doc.y;
+        if (l0 <= n) {
+            const uint64_t seq = *reinterpret_cast<const uint64_t*>(a.seqb + (gs >> 4));
+            const uint2 jr = *reinterpret_cast<const uint2*>(a.jbits + (gs >> 5));
+            const uint2 jq = *reinterpret_cast<const uint2*>(a.jloc + (gs >> 5));
+            const uint64_t jw = ((uint64_t)(jr.y | jq.y) << 32) | (uint64_t)(jr.x | jq.x);
+            uint64_t pj = 0;
+            if (l0 > 0) pj = ((a.jbits[(gs >> 5) - 1] | a.jloc[(gs >> 5) - 1]) >> 31) & 1u;
+            const uint64_t prevj = (jw << 1) | pj;  // bit k = jump(gs + k - 1)
+            const uint64_t item = low_mask64(n + 1u - l0) & ~low_mask64(l0 == 0 ? 1u : 0u);
+            const uint64_t root = l0 == 0 ? 1ull : 0ull;
+            hw = root | (item & ~(seq & ~prevj));
+        }
+        a.hbits[wi] = hw;
+    }
+    const uint32_t th = wave_sum((uint32_t)__popcll(hw));
+    const uint32_t tile = wi >> 6;  // 64 words per tile: one wave
+    if ((threadIdx.x & 63u) == 0 && tile < a.ntiles) a.tile_hw[tile].x = th;
+}
+
+// Exclusive scan of the tile {heads, weight} pairs: per-4096-tile sums, one workgroup over the
+// sums (also the wave totals), then the in-place apply.
+__global__ __launch_bounds__(kBlock) void k_tiles_reduce(L0Args a) {
+    __shared__ uint32_t lh[kBlock / 64], lw[kBlock / 64];
+    uint32_t h = 0, w = 0;
+    const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+#pragma unroll 4
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < a.ntiles) {
+            const uint2 v = a.tile_hw[base + k];
+            h += v.x;
+            w += v.y;
+        }
+    uint32_t th, tw;
+    (void)block_excl_scan<kBlock / 64>(h, lh, th);
+    (void)block_excl_scan<kBlock / 64>(w, lw, tw);
+    if (threadIdx.x == 0) a.tile_sums[blockIdx.x] = make_uint2(th, tw);
+}
+__global__ __launch_bounds__(1024) void k_tiles_top(L0Args a, uint32_t nb) {
+    __shared__ uint32_t lh[16], lw[16];
+    uint32_t ch = 0, cw = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint2 v = b < nb ? a.tile_sums[b] : make_uint2(0, 0);
+        uint32_t th, tw;
+        const uint32_t eh = block_excl_scan<16>(v.x, lh, th);
+        const uint32_t ew = block_excl_scan<16>(v.y, lw, tw);
+        if (b < nb) a.tile_sums[b] = make_uint2(ch + eh, cw + ew);
+        ch += th;
+        cw += tw;
+    }
+    if (threadIdx.x == 0) {
+        a.ctl[C_RTOTAL] = ch;
+        a.ctl[C_WTOTAL] = cw;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
+    __shared__ uint32_t lh[kBlock / 64], lw[kBlock / 64];
+    const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    uint2 v[kScanItems];
+    uint32_t h = 0, w = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = base + k < a.ntiles ? a.tile_hw[base + k] : make_uint2(0, 0);
+        h += v[k].x;
+        w += v[k].y;
+    }
+    uint32_t th, tw;
+    const uint2 c = a.tile_sums[blockIdx.x];
+    uint32_t eh = c.x + block_excl_scan<kBlock / 64>(h, lh, th);
+    uint32_t ew = c.y + block_excl_scan<kBlock / 64>(w, lw, tw);
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < a.ntiles) {
+            a.tile_hw[base + k] = make_uint2(eh, ew);
+            eh += v[k].x;
+            ew += v[k].y;
+        }
+}
+
+// Moves a tile's UTF-8 (bytes [0, n) of its 16-byte-aligned stile segment) to sbytes + D.  The
+// dwords of sbytes wholly inside [D, D + n) belong to this tile alone and are written as
+// dwords (funnel-shifted from two source dwords); the partial dwords at either end are
+// shared with the neighbouring tiles and written bytewise.
+__device__ __forceinline__ void move_tile_text(const uint8_t* __restrict__ src, uint8_t* sbytes,
+                                               uint32_t D, uint32_t n) {
+    const uint32_t lo = (D + 3u) & ~3u, hi = (D + n) & ~3u;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(sbytes);
+    const uint32_t sh = (lo - D) & 3u;  // source offset of an aligned destination dword, mod 4
+    for (uint32_t m = lo + 4u * threadIdx.x; m < hi; m += 4u * kBlock) {
+        const uint32_t o = m - D;  // source byte offset, o % 4 == sh
+        const uint32_t w0 = s32[o >> 2];
+        const uint32_t w1 = sh ? s32[(o >> 2) + 1] : 0u;
+        d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
+    }
+    if (threadIdx.x == 0)
+        for (uint32_t g = D; g < min(D + n, lo); ++g) sbytes[g] = src[g - D];
+    if (threadIdx.x == 1)
+        for (uint32_t g = max(hi, lo); g < D + n; ++g) sbytes[g] = src[g - D];
+}
+
+// k_runs: rank words, one record per run head (head slot, weight prefix), document starts, and
+// the tile's UTF-8 moved from its stile segment to its place in sbytes.
+__global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
+    __shared__ uint32_t lh[kBlock / 64], lw[kBlock / 64];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
+    uint32_t hm = 0;
+    uint64_t nib = 0;
+    const uint2 pre = a.tile_hw[tile];
+    if (gs < a.nslots) {
+        hm = (uint32_t)(a.hbits[gs >> 6] >> (gs & 63u)) & 0xFFFFu;
+        nib = a.wnib[gs >> 4];
+    }
+    uint32_t W = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) W += (uint32_t)(nib >> (4 * k)) & 15u;
+    uint32_t th, tw;
+    const uint32_t rank = pre.x + block_excl_scan<kBlock / 64>((uint32_t)__popc(hm), lh, th);
+    uint32_t P = pre.y + block_excl_scan<kBlock / 64>(W, lw, tw);
+    if (a.mode == 0 && tw) {
+        if ((uint64_t)pre.y + tw > a.sbytes_cap) {  // more text than the host bound
+            if (threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 4u);
+        } else {
+            move_tile_text(a.stile + (uint64_t)tile * kTileBytes, a.sbytes, pre.y, tw);
+        }
+    }
     if (gs >= a.nslots) return;
-    if (q == 0) {
-        a.hbits[gs >> 6] = word;
-        a.hrank[gs >> 6] = rank;
-    }
-    if (!s.hmask) return;
+    if ((threadIdx.x & 3u) == 0) a.hrank[gs >> 6] = rank;
+    if (!hm) return;
     uint32_t r = rank;
+    if ((hm & 1u) && (gs & 63u) == 0) {  // document starts are 64-aligned
+        const uint32_t d = a.chunk_doc[gs >> a.log2m];
+        if (a.docs[d].x == gs) {
+            a.doc_root[d] = r;
+            a.doc_p0[d] = P;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        if (s.hmask & (1u << k)) {
-            const uint32_t g = gs + k;
-            a.r_head[r] = g;
+        if (hm & (1u << k)) {
+            a.r_head[r] = gs + k;
             a.r_pstart[r] = P;
-            if (g == s.doc.x) {
-                a.doc_root[s.d] = r;
-                a.doc_p0[s.d] = P;
-            }
             ++r;
         }
-        P += s.w[k];
+        P += (uint32_t)(nib >> (4 * k)) & 15u;
     }
 }
 
@@ -398,69 +467,79 @@ __global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uin
     if (h != doc.x) {
         uint32_t p = a.in_parent[h];
         key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
-        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_jump
+        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_classify
         pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u;
     }
     a.r_parent[rho] = pr;
     a.r_key[rho] = key;
 }
 
-// Expansion: item slot -> its run -> output position; TEXT writes UTF-8, ORDER writes ids.
-__global__ __launch_bounds__(kBlock) void k_expand(L0Args a) {
-    __shared__ uint32_t lds[kBlock / 64];
-    const uint32_t gs = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
-    Slots16 s;
-    load_slots16(a, gs, false, s);
-    uint32_t W = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) W += s.w[k];
-    uint32_t tw;
-    uint32_t P = a.tile_exw[blockIdx.x] + block_excl_scan<kBlock / 64>(W, lds, tw);
-    if (!W) return;
-    const uint32_t wi = gs >> 6, sh = gs & 63u;
-    const uint64_t hw = a.hbits[wi];
-    const uint32_t hm = (uint32_t)(hw >> sh) & 0xFFFFu;
-    // run of slot gs-1: heads strictly before gs, minus one
-    uint32_t rho = a.hrank[wi] + (uint32_t)__popcll(sh ? (hw & ((1ull << sh) - 1ull)) : 0ull) - 1u;
-    const uint64_t obase = a.toff[s.d];
-    const uint64_t olim = a.toff[s.d + 1];
-    uint32_t cur = kNil, roff = 0, pst = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        rho += (hm >> k) & 1u;
-        const uint32_t w = s.w[k];
+// Expansion, one wave per 64 consecutive runs.  Their bytes are contiguous in sbytes (runs are
+// numbered in slot order), so the wave streams them with unit-stride loads and each byte goes
+// to its run's place in the document: text[toff[d] + roff[run] + i].  ORDER mode writes the
+// run's item ids instead (consecutive: a run is a chain of consecutive ids).
+struct ExpandArgs {
+    uint32_t R, mode, log2m;
+    const uint32_t* chunk_doc;
+    const uint2* docs;
+    const uint32_t* r_head;
+    const uint32_t* r_pstart;
+    const uint32_t* r_w;
+    const uint32_t* roff;
+    const uint32_t* tlen;
+    const uint64_t* toff;
+    const uint8_t* sbytes;
+    uint8_t* text;
+    uint32_t* ctl;
+};
+
+__global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t rho = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t w = 0, src = 0, idb = 0;
+    uint64_t dst = 0;
+    if (rho < a.R) {
+        src = a.r_pstart[rho];
+        w = a.r_w[rho];
         if (w) {
-            if (rho != cur) {
-                cur = rho;
-                roff = a.roff[rho];
-                pst = a.r_pstart[rho];
-            }
-            const uint64_t o = obase + roff + (P - pst);
-            if (a.mode == 0) {
-                if (o + w > olim) { atomicOr(&a.ctl[C_ERR], 8u); return; }
-                const uint32_t c = a.in_cp[gs + k] & kCpMask;
-                uint8_t* p = a.text + o;
-                if (c < 0x80u) {
-                    p[0] = (uint8_t)c;
-                } else if (c < 0x800u) {
-                    p[0] = (uint8_t)(0xC0u | (c >> 6));
-                    p[1] = (uint8_t)(0x80u | (c & 63u));
-                } else if (c < 0x10000u) {
-                    p[0] = (uint8_t)(0xE0u | (c >> 12));
-                    p[1] = (uint8_t)(0x80u | ((c >> 6) & 63u));
-                    p[2] = (uint8_t)(0x80u | (c & 63u));
-                } else {
-                    p[0] = (uint8_t)(0xF0u | (c >> 18));
-                    p[1] = (uint8_t)(0x80u | ((c >> 12) & 63u));
-                    p[2] = (uint8_t)(0x80u | ((c >> 6) & 63u));
-                    p[3] = (uint8_t)(0x80u | (c & 63u));
-                }
+            const uint32_t h = a.r_head[rho];
+            const uint32_t d = a.chunk_doc[h >> a.log2m];
+            const uint32_t base = a.docs[d].x;
+            const uint32_t ro = a.roff[rho];
+            if ((uint64_t)ro + w > a.tlen[d]) {
+                atomicOr(&a.ctl[C_ERR], 8u);
+                dst = ~0ull;  // skipped below
             } else {
-                if (o >= olim) { atomicOr(&a.ctl[C_ERR], 8u); return; }
-                reinterpret_cast<uint32_t*>(a.text)[o] = gs + k - s.doc.x;
+                dst = a.toff[d] + ro;
             }
+            idb = h - base + (h == base ? 1u : 0u);
         }
-        P += w;
+    }
+    const uint32_t inc = wave_incl_scan(w);
+    const uint32_t ex = inc - w;
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)src);
+    for (uint32_t b = 0; b < T; b += 64) {
+        const uint32_t x = b + lane;
+        // the last lane whose run starts at or before byte x owns it
+        uint32_t j = 0;
+#pragma unroll
+        for (uint32_t st = 32; st; st >>= 1) {
+            const uint32_t e = (uint32_t)__shfl((int)ex, (int)(j + st));
+            if (e <= x) j += st;
+        }
+        const uint32_t off = x - (uint32_t)__shfl((int)ex, (int)j);
+        const uint64_t dj = ((uint64_t)(uint32_t)__shfl((int)(dst >> 32), (int)j) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)dst, (int)j);
+        // (every shuffle above runs with the whole wave active: a ds_bpermute from an inactive
+        // lane reads 0)
+        const uint32_t ib = a.mode ? (uint32_t)__shfl((int)idb, (int)j) : 0u;
+        if (x < T && dj != ~0ull) {
+            if (a.mode == 0)
+                a.text[dj + off] = a.sbytes[s0 + x];
+            else
+                reinterpret_cast<uint32_t*>(a.text)[dj + off] = ib + off;
+        }
     }
 }
 
@@ -1100,8 +1179,8 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(seqb_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(ticket_);
-    dfree(tile_exw_);
+    dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hrank_); dfree(stile_);
+    dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
@@ -1160,7 +1239,9 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
             err = "document text of 4 GiB or more is not supported";
             return CRDT_HIP_ERANGE;
         }
-        if (L.waves.empty() || (uint64_t)L.waves.back().nslots + ds > max_wave_slots) {
+        const uint64_t dt = (docs[d].text_cap + 15) & ~15ull;
+        if (L.waves.empty() || (uint64_t)L.waves.back().nslots + ds > max_wave_slots ||
+            L.waves.back().text_cap + dt > kMaxWaveText) {
             Wave w{};
             w.first_doc = d;
             w.slot0 = slot;
@@ -1171,7 +1252,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         w.ndocs++;
         w.nslots += (uint32_t)ds;
         w.max_splitters_per_doc = std::max<uint32_t>(w.max_splitters_per_doc, (uint32_t)(2 * ds / M));
-        w.text_cap += (docs[d].text_cap + 15) & ~15ull;
+        w.text_cap += dt;
         w.leaf_cap += (docs[d].text_cap + kLeaf - 1) / kLeaf;
         w.order_cap += docs[d].n;
         L.items += docs[d].n;
@@ -1260,19 +1341,26 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(seqb_); dfree(hbits_); dfree(hrank_); dfree(look_); dfree(tile_exw_);
-        const uint64_t tiles = slots / kTile + 2;
+        dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hrank_); dfree(stile_);
+        dfree(tile_hw_); dfree(tile_sums_);
+        const uint64_t tiles = slots / kScanTile + 2;
         HIPCHK(dalloc(&jbits_, slots / 32 + 4), "hipMalloc jump bits");
+        HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
         HIPCHK(dalloc(&seqb_, slots / 16 + 4), "hipMalloc seq bits");
+        HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
         HIPCHK(dalloc(&hbits_, slots / 64 + 2), "hipMalloc hbits");
         HIPCHK(dalloc(&hrank_, slots / 64 + 2), "hipMalloc hrank");
-        HIPCHK(dalloc(&look_, 4 * tiles), "hipMalloc look-back");
-        HIPCHK(hipMemset(look_, 0, 4 * tiles * 8), "memset look-back");  // no stale epoch
-        HIPCHK(dalloc(&tile_exw_, tiles * (kTile / kScanTile)), "hipMalloc tile prefixes");
+        HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
+        HIPCHK(dalloc(&tile_hw_, tiles), "hipMalloc tile totals");
+        HIPCHK(dalloc(&tile_sums_, tiles / kScanTile + 2), "hipMalloc tile sums");
         cap_slots0_ = slots;
     }
+    if (w.text_cap + 64 > cap_sbytes_) {
+        dfree(sbytes_);
+        HIPCHK(dalloc(&sbytes_, w.text_cap + 64), "hipMalloc slot-order text");
+        cap_sbytes_ = w.text_cap + 64;
+    }
     if (!ctl_) HIPCHK(dalloc(&ctl_, 16), "hipMalloc ctl");
-    if (!ticket_) HIPCHK(dalloc(&ticket_, 16), "hipMalloc ticket");
     if (w.ndocs + 1 > cap_docs_) {
         dfree(tlen_); dfree(loff_); dfree(toff_); dfree(dig_); dfree(doc_root_); dfree(doc_p0_);
         const uint64_t nd = w.ndocs + 1;
@@ -1305,7 +1393,7 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     return CRDT_HIP_OK;
 }
 
-// Level-1 scratch, sized by the runs of the wave (known after k_tile_scan).
+// Level-1 scratch, sized by the runs of the wave (known after level 0).
 int Engine::ensure_runs(uint64_t R, uint64_t S) {
     if (R > cap_runs_) {
         dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
@@ -1345,8 +1433,8 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
                      std::vector<uint32_t>& stage_launches) {
     hipStream_t s = stream;
     const bool ord = mode == ORDER;
-    const uint32_t ntiles = (uint32_t)((w.nslots + kTile - 1) / kTile);
-    const uint32_t njump = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
+    const uint32_t ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
+    const uint32_t nsums = (ntiles + kScanTile - 1) / kScanTile;
 #define BEGIN(st) HIPCHK(hipEventRecord(ev_[2 * (st)], s), "event record")
 #define END(st) HIPCHK(hipEventRecord(ev_[2 * (st) + 1], s), "event record")
 
@@ -1355,6 +1443,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.log2m = L.log2m;
     a0.ndocs = w.ndocs;
     a0.mode = ord ? 1u : 0u;
+    a0.ntiles = ntiles;
     a0.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);
     a0.docs = L.docs_rel + w.first_doc;
     a0.in_parent = L.parent + w.slot0;
@@ -1363,20 +1452,20 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.in_deleted = L.deleted + w.slot0;
     a0.in_cp = L.cp + w.slot0;
     a0.jbits = jbits_;
+    a0.jloc = jloc_;
     a0.seqb = seqb_;
+    a0.wnib = wnib_;
+    a0.stile = stile_;
+    a0.sbytes = sbytes_;
+    a0.sbytes_cap = cap_sbytes_ - 64;
+    a0.tile_hw = tile_hw_;
+    a0.tile_sums = tile_sums_;
     a0.hbits = hbits_;
     a0.hrank = hrank_;
-    a0.ntiles = ntiles;
-    a0.look = look_;
-    a0.ticket = ticket_;
-    a0.tile_exw = tile_exw_;
-    a0.epoch = ++epoch_;
     a0.doc_root = doc_root_;
     a0.doc_p0 = doc_p0_;
-    a0.toff = toff_;
-    a0.text = text_;
     a0.ctl = ctl_;
-    // run records are written by the tile scan before the run count is known: runs <= slots
+    // run records are written before the run count is known: runs <= slots
     if (w.nslots > cap_heads_) {
         dfree(r_head_); dfree(r_pstart_);
         HIPCHK(dalloc(&r_head_, w.nslots + 64ull), "hipMalloc r_head");
@@ -1388,22 +1477,25 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
 
     // ---- level 0: runs -------------------------------------------------------------------
     HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
-    HIPCHK(hipMemsetAsync(ticket_, 0, 16, s), "memset ticket");
     HIPCHK(hipMemsetAsync(jbits_, 0, (w.nslots / 32 + 4) * 4ull, s), "memset jump bits");
-    BEGIN(S_JUMP);
-    k_jump<<<njump, kBlock, 0, s>>>(a0);
-    END(S_JUMP);
-    BEGIN(S_TSCAN);
-    k_tile_scan<<<ntiles, kTileThreads, 0, s>>>(a0);
+    BEGIN(S_CLASSIFY);
+    k_classify<<<ntiles, kBlock, 0, s>>>(a0);
+    END(S_CLASSIFY);
+    BEGIN(S_RUNS);
+    k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
+    k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
+    k_tiles_top<<<1, 1024, 0, s>>>(a0, nsums);
+    k_tiles_apply<<<nsums, kBlock, 0, s>>>(a0);
+    k_runs<<<ntiles, kBlock, 0, s>>>(a0);
     k_docmax<<<1, 1024, 0, s>>>(a0);
-    END(S_TSCAN);
+    END(S_RUNS);
     HIPCHK(hipGetLastError(), "level-0 launch");
     HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "level-0 sync");
     if (host_ctl_[C_ERR]) {
-        err = host_ctl_[C_ERR] & 32u ? "tile look-back timed out"
-                                     : "malformed op log: parent id out of range";
-        return host_ctl_[C_ERR] & 32u ? CRDT_HIP_EDEVICE : CRDT_HIP_EBADLOG;
+        err = host_ctl_[C_ERR] & 4u ? "op log holds more text than planned"
+                                    : "malformed op log: parent id out of range";
+        return CRDT_HIP_EBADLOG;
     }
     const uint32_t R = host_ctl_[C_RTOTAL];
     const uint32_t wtotal = host_ctl_[C_WTOTAL];
@@ -1415,7 +1507,6 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.r_parent = r_parent_;
     a0.r_w = r_w_;
     a0.r_key = r_key_;
-    a0.roff = roff_;
     BEGIN(S_RPARENT);
     k_run_parent<<<grid_for(R), kBlock, 0, s>>>(a0, R, wtotal);
     END(S_RPARENT);
@@ -1483,8 +1574,23 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     END(S_WALK2);
 
     // ---- expansion + digest --------------------------------------------------------------
+    ExpandArgs ea{};
+    ea.R = R;
+    ea.mode = a0.mode;
+    ea.log2m = L.log2m;
+    ea.chunk_doc = a0.chunk_doc;
+    ea.docs = a0.docs;
+    ea.r_head = r_head_;
+    ea.r_pstart = r_pstart_;
+    ea.r_w = r_w_;
+    ea.roff = roff_;
+    ea.tlen = tlen_;
+    ea.toff = toff_;
+    ea.sbytes = sbytes_;
+    ea.text = text_;
+    ea.ctl = ctl_;
     BEGIN(S_EXPAND);
-    k_expand<<<njump, kBlock, 0, s>>>(a0);
+    k_expand<<<gR, kBlock, 0, s>>>(ea);
     END(S_EXPAND);
     BEGIN(S_DIGEST);
     if (!ord) {
@@ -1500,7 +1606,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
                "copy digests");
     HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "merge wave");
-    const uint32_t launches[S_N] = {1, 2, 1, 1, 3, 1, 3, 1, 2 + rounds, 2, 1, ord ? 0u : 2u};
+    const uint32_t launches[S_N] = {1, 6, 1, 1, 3, 1, 3, 1, 2 + rounds, 2, 1, ord ? 0u : 2u};
     for (int i = 0; i < S_N; ++i) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");

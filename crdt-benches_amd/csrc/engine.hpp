@@ -87,11 +87,13 @@ public:
 private:
     // level-0 scratch (per slot / per tile), grown on demand
     uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
-    uint32_t* jbits_ = nullptr;
+    uint32_t *jbits_ = nullptr, *jloc_ = nullptr;
     uint16_t* seqb_ = nullptr;
-    uint64_t *hbits_ = nullptr, *look_ = nullptr;
-    uint32_t *hrank_ = nullptr, *ticket_ = nullptr, *tile_exw_ = nullptr;
-    uint32_t epoch_ = 0;  // look-back epoch, unique per tile-scan launch
+    uint64_t *hbits_ = nullptr, *wnib_ = nullptr;
+    uint32_t* hrank_ = nullptr;
+    uint8_t *stile_ = nullptr, *sbytes_ = nullptr;
+    uint2 *tile_hw_ = nullptr, *tile_sums_ = nullptr;
+    uint64_t cap_sbytes_ = 0;
     // per document
     uint32_t *doc_root_ = nullptr, *doc_p0_ = nullptr, *tlen_ = nullptr, *loff_ = nullptr;
     uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;

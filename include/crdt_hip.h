@@ -85,9 +85,8 @@ typedef struct {
 
 /* Stage indices of crdt_hip_stats.stage_ns (one HIP-event interval per kernel group). */
 enum {
-    CRDT_HIP_STAGE_JUMP = 0,     /* level 0: flag items with a non-consecutive child          */
-    CRDT_HIP_STAGE_TSCAN = 1,    /* level 0: one-pass tile scan (look-back): run heads, rank
-                                    bitvector, run records                                    */
+    CRDT_HIP_STAGE_CLASSIFY = 0, /* level 0: seq/jump bits, weights, per-tile UTF-8           */
+    CRDT_HIP_STAGE_RUNS = 1,     /* level 0: head bitvector, tile scan, run records, text     */
     CRDT_HIP_STAGE_RPARENT = 2,  /* level 0: parent run and weight of every run               */
     CRDT_HIP_STAGE_COUNT = 3,    /* level 1: child count per parent run                       */
     CRDT_HIP_STAGE_SCAN = 4,     /* level 1: exclusive scan of child counts                   */
@@ -96,7 +95,7 @@ enum {
     CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums                          */
     CRDT_HIP_STAGE_RANK = 8,     /* level 1: ranking of the splitter lists                    */
     CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets                  */
-    CRDT_HIP_STAGE_EXPAND = 10,  /* items -> UTF-8 at run offset + in-run prefix              */
+    CRDT_HIP_STAGE_EXPAND = 10,  /* runs copy their UTF-8 to their document offset            */
     CRDT_HIP_STAGE_DIGEST = 11,  /* per-document tree digest                                  */
     CRDT_HIP_NSTAGES = 12
 };
