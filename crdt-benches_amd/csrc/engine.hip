@@ -172,88 +172,81 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     const uint32_t tile = blockIdx.x;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
     if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t seq = 0, bad = 0;
-    uint32_t cc[16], w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) cc[k] = 0, w[k] = 0;
-    if (gs < a.nslots) {
+    const bool live = gs < a.nslots;
+    // every load first (9 x 16 B per thread); padding slots hold junk and are masked below
+    uint4 pq[4], cq[4], dl = make_uint4(0, 0, 0, 0);
+    uint32_t base = 0, n = 0, l0 = 0;
+    if (live) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        const uint32_t l0 = gs - doc.x;
-        if (l0 <= doc.y) {
-            const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
-            const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + gs);
-            const uint4 dl = a.mode == 0 ? *reinterpret_cast<const uint4*>(a.in_deleted + gs)
-                                         : make_uint4(0, 0, 0, 0);
-            const uint32_t dw[4] = {dl.x, dl.y, dl.z, dl.w};
+        base = doc.x;
+        n = doc.y;
+        l0 = gs - base;
+        const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + gs);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint4 pp = pv[q];
-                const uint4 c4 = cv[q];
-                const uint32_t pa[4] = {pp.x, pp.y, pp.z, pp.w};
-                const uint32_t ca[4] = {c4.x, c4.y, c4.z, c4.w};
+        for (int q = 0; q < 4; ++q) pq[q] = pv[q];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t k = 4 * q + j, local = l0 + k, p = pa[j];
-                    if ((local - 1u) >= doc.y) continue;  // document start or padding
-                    const uint32_t c = ca[j] & kCpMask;
-                    cc[k] = c;
-                    const bool del = (dw[q] >> (8 * j)) & 0xFFu;
-                    w[k] = a.mode ? 1u : (del ? 0u : utf8_len(c));
-                    if (p > doc.y || p == local) {
-                        bad = 1;
-                    } else if (p == local - 1u) {
-                        seq |= 1u << k;
-                    } else {
-                        const uint32_t ps = doc.x + p;
-                        if ((ps / kScanTile) == tile)
-                            atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
-                        else
-                            atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
-                    }
-                }
-            }
+        for (int q = 0; q < 4; ++q) cq[q] = cv[q];
+        if (a.mode == 0) dl = *reinterpret_cast<const uint4*>(a.in_deleted + gs);
+    }
+    const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
+                            pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
+    const uint32_t C[16] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z, cq[1].w,
+                            cq[2].x, cq[2].y, cq[2].z, cq[2].w, cq[3].x, cq[3].y, cq[3].z, cq[3].w};
+    const uint32_t D[4] = {dl.x, dl.y, dl.z, dl.w};
+    // branch-free classification of the 16 slots
+    uint32_t seq = 0, jmp = 0, bad = 0, W = 0;
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t local = l0 + k, p = P[k];
+        const bool it = live && (local - 1u) < n;  // an item (not the document start / padding)
+        const bool del = (D[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const bool b = p > n || p == local;
+        const bool sq = p == local - 1u;
+        w[k] = it ? (a.mode ? 1u : (del ? 0u : utf8_len(C[k] & kCpMask))) : 0u;
+        W += w[k];
+        bad |= (it && b) ? 1u : 0u;
+        seq |= (it && !b && sq ? 1u : 0u) << k;
+        jmp |= (it && !b && !sq ? 1u : 0u) << k;
+    }
+    __syncthreads();  // jl cleared
+    // jump bits: parents in this tile in LDS; parents in earlier tiles by global atomics, issued
+    // last so that no wait in this kernel ever has to cover them
+    uint32_t remote = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (jmp & (1u << k)) {
+            const uint32_t ps = base + P[k];
+            if (ps / kScanTile == tile)
+                atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
+            else
+                remote |= 1u << k;
         }
+    }
+    if (live) {
         uint64_t nib = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) nib |= (uint64_t)w[k] << (4 * k);
         a.seqb[gs >> 4] = (uint16_t)seq;
         a.wnib[gs >> 4] = nib;
     }
-    uint32_t W = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) W += w[k];
     uint32_t tw;
     const uint32_t ex = block_excl_scan<kBlock / 64>(W, lds, tw);
-    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
     if (a.mode == 0 && W) {
         uint8_t* o = sb + ex;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const uint32_t c = cc[k];
-            switch (w[k]) {
-            case 1:
-                o[0] = (uint8_t)c;
-                break;
-            case 2:
-                o[0] = (uint8_t)(0xC0u | (c >> 6));
-                o[1] = (uint8_t)(0x80u | (c & 63u));
-                break;
-            case 3:
-                o[0] = (uint8_t)(0xE0u | (c >> 12));
-                o[1] = (uint8_t)(0x80u | ((c >> 6) & 63u));
-                o[2] = (uint8_t)(0x80u | (c & 63u));
-                break;
-            case 4:
-                o[0] = (uint8_t)(0xF0u | (c >> 18));
-                o[1] = (uint8_t)(0x80u | ((c >> 12) & 63u));
-                o[2] = (uint8_t)(0x80u | ((c >> 6) & 63u));
-                o[3] = (uint8_t)(0x80u | (c & 63u));
-                break;
-            default:
-                break;
+            const uint32_t L = w[k], c = C[k] & kCpMask;
+            if (L) {
+                // UTF-8: lead byte = length prefix | top bits, then 6-bit continuation bytes
+                const uint32_t s0 = 6u * (L - 1u);
+                o[0] = (uint8_t)(L == 1u ? c : (((0xFF00u >> L) & 0xFFu) | (c >> s0)));
+                if (L > 1u) o[1] = (uint8_t)(0x80u | ((c >> (s0 - 6u)) & 63u));
+                if (L > 2u) o[2] = (uint8_t)(0x80u | ((c >> (s0 - 12u)) & 63u));
+                if (L > 3u) o[3] = (uint8_t)(0x80u | (c & 63u));
             }
-            o += w[k];
+            o += L;
         }
     }
     __syncthreads();
@@ -264,6 +257,14 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         const uint4* src = reinterpret_cast<const uint4*>(sb);
         for (uint32_t i = threadIdx.x; i < (tw + 15u) / 16u; i += kBlock) dst[i] = src[i];
     }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (remote & (1u << k)) {
+            const uint32_t ps = base + P[k];
+            atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+        }
+    }
+    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
 __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {

@@ -63,10 +63,43 @@ __global__ __launch_bounds__(256) void k_atom(const uint32_t* __restrict__ in, u
     }
 }
 
+// two u32 arrays + one u8 array, classify-like: per-lane contiguous 16 slots
+__global__ __launch_bounds__(256) void k_contig3(const uint32_t* __restrict__ in, const uint32_t* __restrict__ in2,
+                                                 const uint8_t* __restrict__ in3, uint32_t* out, uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t * 16 >= n) return;
+    const uint4* p = reinterpret_cast<const uint4*>(in + t * 16);
+    const uint4* p2 = reinterpret_cast<const uint4*>(in2 + t * 16);
+    const uint4 d = *reinterpret_cast<const uint4*>(in3 + t * 16);
+    uint32_t s = d.x ^ d.y ^ d.z ^ d.w;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { uint4 v = p[q]; uint4 w = p2[q]; s += v.x ^ v.y ^ v.z ^ v.w ^ w.x ^ w.y ^ w.z ^ w.w; }
+    out[t] = s;
+}
+// same, lane-interleaved u32 loads
+__global__ __launch_bounds__(256) void k_inter3(const uint32_t* __restrict__ in, const uint32_t* __restrict__ in2,
+                                                const uint8_t* __restrict__ in3, uint32_t* out, uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t wbase = (t >> 6) * 1024, lane = t & 63;
+    if (wbase >= n) return;
+    const uint4 d = *reinterpret_cast<const uint4*>(in3 + t * 16);
+    uint32_t s = d.x ^ d.y ^ d.z ^ d.w;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint4 v = *reinterpret_cast<const uint4*>(in + wbase + q * 256 + lane * 4);
+        uint4 w = *reinterpret_cast<const uint4*>(in2 + wbase + q * 256 + lane * 4);
+        s += v.x ^ v.y ^ v.z ^ v.w ^ w.x ^ w.y ^ w.z ^ w.w;
+    }
+    out[t] = s;
+}
+
 int main() {
     const uint64_t n = 512ull << 20;  // 512 Mi u32 = 2 GiB
-    uint32_t *in, *out, *bits;
+    uint32_t *in, *out, *bits, *in2;
+    uint8_t* in3;
     hipMalloc(&in, n * 4); hipMalloc(&out, n / 16 * 4); hipMalloc(&bits, n / 8 + 64);
+    hipMalloc(&in2, n * 4); hipMalloc(&in3, n);
+    hipMemset(in2, 1, n * 4); hipMemset(in3, 0, n);
     // fill with pseudo-random words
     {
         uint32_t* h = (uint32_t*)malloc(64 << 20);
@@ -78,8 +111,10 @@ int main() {
     hipMemset(bits, 0, n / 8 + 64);
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     const uint32_t grid = (uint32_t)(n / 16 / 256);
-    const char* names[] = {"contig64B", "interleaved16B", "lds_transpose", "atomicOr_5pct_span256K"};
-    for (int k = 0; k < 4; ++k) {
+    const char* names[] = {"contig64B", "interleaved16B", "lds_transpose", "atomicOr_5pct_span256K",
+                           "contig3 (9 B/slot)", "inter3 (9 B/slot)"};
+    const double bytes[] = {4, 4, 4, 4, 9, 9};
+    for (int k = 0; k < 6; ++k) {
         float best = 1e9;
         for (int it = 0; it < 6; ++it) {
             hipEventRecord(e0);
@@ -87,11 +122,13 @@ int main() {
             if (k == 1) k_inter<<<grid, 256>>>(in, out, n);
             if (k == 2) k_lds<<<grid, 256>>>(in, out, n);
             if (k == 3) k_atom<<<grid, 256>>>(in, bits, n, 1u << 18);
+            if (k == 4) k_contig3<<<grid, 256>>>(in, in2, in3, out, n);
+            if (k == 5) k_inter3<<<grid, 256>>>(in, in2, in3, out, n);
             hipEventRecord(e1); hipEventSynchronize(e1);
             float ms; hipEventElapsedTime(&ms, e0, e1);
             if (it) best = ms < best ? ms : best;
         }
-        printf("%-24s %8.3f ms  %7.1f GB/s\n", names[k], best, n * 4.0 / best / 1e6);
+        printf("%-24s %8.3f ms  %7.1f GB/s\n", names[k], best, n * bytes[k] / best / 1e6);
     }
     return 0;
 }
