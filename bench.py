@@ -55,6 +55,7 @@ KERNEL_BYTES = {
     "walk2": (0.0, 20.0, 0.0),
     "expand": (0.0, 16.0, 2.0),      # run prefix/weight/head/offset; slot-order text -> document
     "digest": (0.0, 0.0, 1.0),
+    "doctree": (0.0, 20.0, 0.0),     # parent run, weight, key in; run offset out (LDS level 1)
 }
 
 
@@ -127,6 +128,8 @@ def main() -> int:
     ap.add_argument("--replicas", type=int, default=4096, help="replicas of each trace per GPU")
     ap.add_argument("--relabel", default="rotate", choices=["none", "rotate", "shuffle"])
     ap.add_argument("--splitter-stride", type=int, default=0)
+    ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
+                    help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -160,6 +163,7 @@ def main() -> int:
     ctx = crdt_hip.Context(local)
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
+    ctx.set_param("level1", args.level1)
     batch = ctx.batch(bases, replicas=args.replicas, relabel=args.relabel,
                       seed=0x5EED0003 + 7919 * rank)
     if rank == 0:

@@ -148,6 +148,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.max_wave_slots = value;
         return 0;
     }
+    if (k == "level1") {
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "level1 must be 0 (auto) or 1 (global)");
+        ctx->eng.level1_global = value == 1;
+        return 0;
+    }
     return set_err(ctx, CRDT_HIP_EINVAL, "unknown parameter " + k);
 }
 

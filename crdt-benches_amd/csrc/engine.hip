@@ -67,7 +67,7 @@ enum Ctl {
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
 enum Stage { S_CLASSIFY, S_RUNS, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
-             S_WALK2, S_EXPAND, S_DIGEST, S_N };
+             S_WALK2, S_EXPAND, S_DIGEST, S_DOCTREE, S_N };
 
 // ---------------------------------------------------------------------------------------------
 // wave / block primitives
@@ -1015,7 +1015,495 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
     const uint32_t tot = wave_sum(runs);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
 }
+// ---------------------------------------------------------------------------------------------
+// Level 1 in LDS: the whole run tree of one document per workgroup (k_doctree)
+// ---------------------------------------------------------------------------------------------
+// Documents of the batched configs have at most ~17 k runs, so a document's run tree fits a
+// workgroup's 160 KiB of LDS as four u16 arrays (8 B/run).  The count / scan / place / sort /
+// Euler-tour ranking sequence of the global level-1 path then runs on LDS atomics and LDS
+// gathers inside one 1024-thread workgroup, with barriers between phases, instead of 7+
+// grid-wide kernels of HBM atomics and dependent HBM gathers.  From global memory it reads
+// r_parent and r_w (coalesced) and r_key (sibling groups of two or more only); it writes the
+// run offsets roff exactly as the global path's k_walk2 does.
+//
+// LDS image (u16 arrays indexed by the local run v in [0, R); run 0 is the document start):
+//   D[v]   child count -> segment start (exclusive scan) -> segment end (after placement)
+//          -> first child (kNil16: a leaf) once the siblings are sorted
+//   nx[v]  parent until placement, then the tour successor of v's up arc: the next sibling's
+//          down arc, (parent | kUp16) = the parent's up arc, or kNil16 for the root
+//   ch[]   children grouped by parent (segment of v = [D[v-1], D[v])), sorted by key desc;
+//          reused for the splitter lists (u32 sums + u16 links) once the first children are known
+//   w[v]   the deferred sort list during the sort, then the weight (0xFFFF: look it up in
+//          r_w), then, once walk 1 has passed v, the splitter whose sublist holds v (kNil16 for
+//          weightless runs)
+// Splitters are both arcs of every run v with v % 8 == 0 (splitter 2(v/8) + up).  Each thread
+// walks up to kDocK sublists in lockstep so that their LDS latencies overlap; a walker that
+// passes v's down arc stores v's offset inside its sublist to roff, and after the splitter
+// lists are ranked one coalesced pass adds the sublist offsets.
+constexpr int kDocThreads = 1024;
+constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
+constexpr int kDocK = 5;           // splitters per thread: 2 * ceil(20480 / 8) = 5 * 1024
+constexpr uint32_t kDocLog2S = 3;  // splitter stride 8
+constexpr uint32_t kDocLds = 163840 - 512;  // dynamic LDS budget (static arrays use the rest)
+constexpr uint16_t kNil16 = 0xFFFFu;
+constexpr uint16_t kUp16 = 0x8000u;
+constexpr uint16_t kDead16 = 0xFFFEu;  // nx of a pruned run
+constexpr uint32_t kDocBig = 32;       // runs of >= 0xFFFF bytes per document (LDS side table)
 
+struct DocArgs {
+    uint32_t ndocs, rtotal, rcap, scap, chbytes;
+    uint32_t probe;  // 1 + document whose phase times are printed (0: none)
+    const uint32_t* doc_root;
+    const uint32_t* r_parent;
+    const uint32_t* r_w;
+    const uint64_t* r_key;
+    uint32_t* roff;
+    uint32_t* ctl;
+};
+
+// LDS bytes of a document with up to rcap - 2 runs: D, nx, w (2 B/run each) and the ch region,
+// which must also hold the splitter lists (6 B per splitter).
+__host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t scap) {
+    return ((2u * rcap > 6u * scap ? 2u * rcap : 6u * scap) + 15u) & ~15u;
+}
+__host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap) {
+    return 6ull * rcap + doctree_ch_bytes(rcap, scap);
+}
+
+// Sort key: (lamport, agent) of the run's head (48 bits) and the local run index (15 bits), so
+// that equal timestamps still order deterministically (greater run first, as the oracle does).
+__device__ __forceinline__ uint64_t doc_key(const DocArgs& a, uint32_t base, uint32_t v) {
+    return (a.r_key[base + v] << 15) | v;
+}
+
+__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    __shared__ uint32_t scan_lds[kDocThreads / 64];
+    __shared__ uint32_t ndefer, flags, visited_lds, pruned_any, qhead, probe_max, probe_sum, nbig;
+    __shared__ uint32_t bigv[kDocBig], bigw[kDocBig];
+    const uint32_t d = blockIdx.x;
+    const uint32_t t = threadIdx.x;
+    const uint32_t base = a.doc_root[d];
+    const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.rtotal) - base;
+    const uint32_t S = 2u * ((R + 7u) >> kDocLog2S);
+    uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
+    uint16_t* nx = D + a.rcap;
+    uint16_t* ch = nx + a.rcap;
+    uint32_t* sval = reinterpret_cast<uint32_t*>(ch);
+    uint16_t* sptr = reinterpret_cast<uint16_t*>(sval + a.scap);
+    uint16_t* w = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(ch) + a.chbytes);
+    uint16_t* defer = w;
+    uint32_t* D32 = dyn;
+    // phase timestamps of one document (CRDT_HIP_PROBE=<doc>, off by default)
+    const bool probe = a.probe && d == a.probe - 1u && t == 0;
+    uint64_t tp[10];
+    tp[0] = wall_clock64();
+#define PROBE(i) if (probe) tp[i] = wall_clock64()
+    if (t == 0) {
+        ndefer = 0;
+        flags = 0;
+        visited_lds = 0;
+        pruned_any = 0;
+        qhead = kDocThreads;
+        probe_max = probe_sum = 0;
+        nbig = 0;
+    }
+    if (R + 2u > a.rcap || S > a.scap || R > (uint32_t)(kDocJ * kDocThreads)) {
+        if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);  // host sized rcap/scap from the largest document
+        return;
+    }
+    // ---- parents and weightless flags (all loads first), cleared counts --------------------
+    uint32_t zw = 0, pruned = 0;  // bit j: run t + 1024 j has no visible bytes / was pruned
+    {
+        uint32_t gp[kDocJ], gw[kDocJ];
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            gp[j] = v < R ? a.r_parent[base + v] : 0u;
+            gw[j] = v < R ? a.r_w[base + v] : 1u;
+        }
+        for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
+        uint32_t bad = 0;
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            if (v < R) {
+                uint16_t p = kNil16;
+                if (v) {
+                    const uint32_t lp = gp[j] - base;
+                    if (lp >= R || lp == v) bad = 1;
+                    else p = (uint16_t)lp;
+                }
+                nx[v] = p;
+            }
+            zw |= (gw[j] == 0u && v != 0u ? 1u : 0u) << j;
+        }
+        if (bad) atomicOr(&flags, 1u);
+    }
+    __syncthreads();
+    PROBE(1);
+    // ---- child counts (u16 counters, two per LDS dword) ------------------------------------
+#pragma unroll
+    for (int j = 0; j < kDocJ; ++j) {
+        const uint32_t v = t + (uint32_t)j * kDocThreads;
+        if (v < R) {
+            const uint16_t p = nx[v];
+            if (p != kNil16) atomicAdd(&D32[p >> 1], 1u << (16u * (p & 1u)));
+        }
+    }
+    __syncthreads();
+    // ---- pruning: a weightless leaf adds nothing to the document and is dropped from its
+    // parent's children; a parent that loses its last child may go in the same pass (the
+    // outcome depends on timing, never the text).  Repeated while it finds anything.
+    for (int round = 0; round < 8; ++round) {
+        uint32_t found = 0;
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            const uint32_t bit = 1u << j;
+            if ((zw & ~pruned & bit) && D[v] == 0) {
+                const uint16_t p = nx[v];
+                pruned |= bit;
+                found = 1;
+                if (p != kNil16) atomicSub(&D32[p >> 1], 1u << (16u * (p & 1u)));
+            }
+        }
+        if (found) atomicOr(&pruned_any, 1u << round);
+        __syncthreads();
+        if (!((pruned_any >> round) & 1u)) break;
+    }
+    PROBE(2);
+    // ---- exclusive scan of the counts -> segment starts ------------------------------------
+    {
+        const uint32_t K = (R + kDocThreads - 1) / kDocThreads;
+        const uint32_t lo = min(R, t * K), hi = min(R, lo + K);
+        uint32_t s = 0;
+        for (uint32_t v = lo; v < hi; ++v) s += D[v];
+        uint32_t total;
+        uint32_t ex = block_excl_scan<kDocThreads / 64>(s, scan_lds, total);
+        for (uint32_t v = lo; v < hi; ++v) {
+            const uint32_t c = D[v];
+            D[v] = (uint16_t)ex;
+            ex += c;
+        }
+    }
+    __syncthreads();
+    PROBE(3);
+    // ---- placement: D[p] walks from the segment start to the segment end -------------------
+#pragma unroll
+    for (int j = 0; j < kDocJ; ++j) {
+        const uint32_t v = t + (uint32_t)j * kDocThreads;
+        if (v < R) {
+            const uint16_t p = nx[v];
+            if (pruned & (1u << j)) {
+                nx[v] = kDead16;  // never reached by the tour; its splitters are empty
+            } else if (p != kNil16) {
+                const uint32_t sh = 16u * (p & 1u);
+                const uint32_t old = atomicAdd(&D32[p >> 1], 1u << sh);
+                ch[(old >> sh) & 0xFFFFu] = (uint16_t)v;
+            }
+        }
+    }
+    __syncthreads();
+    PROBE(4);
+    // ---- sibling order + up-arc successors -------------------------------------------------
+    // nx[] is rewritten here: a child's entry is written only by the thread owning its parent.
+    // Groups of two (the common case) first, with every key load of the thread issued at once.
+    if (t == 0) nx[0] = kNil16;
+    {
+        constexpr int H = kDocJ / 2;
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {
+            uint32_t s0[H], cn[H], cc[H];
+            uint64_t k0[H], k1[H];
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const uint32_t p = t + (uint32_t)(h * H + j) * kDocThreads;
+                s0[j] = (p && p < R) ? D[p - 1] : 0u;
+                cn[j] = p < R ? D[p] - s0[j] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const uint32_t c0 = cn[j] ? ch[s0[j]] : 0u;
+                const uint32_t c1 = cn[j] == 2u ? ch[s0[j] + 1u] : 0u;
+                cc[j] = c0 | (c1 << 16);
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const bool two = cn[j] == 2u;
+                k0[j] = a.r_key[base + (two ? (cc[j] & 0xFFFFu) : 0u)];
+                k1[j] = a.r_key[base + (two ? (cc[j] >> 16) : 0u)];
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const uint32_t p = t + (uint32_t)(h * H + j) * kDocThreads;
+                const uint16_t up = (uint16_t)(p | kUp16);
+                const uint32_t c0 = cc[j] & 0xFFFFu, c1 = cc[j] >> 16;
+                if (cn[j] == 1u) {
+                    nx[c0] = up;
+                } else if (cn[j] == 2u) {
+                    const bool sw = ((k0[j] << 15) | c0) < ((k1[j] << 15) | c1);
+                    const uint32_t a0 = sw ? c1 : c0, a1 = sw ? c0 : c1;
+                    ch[s0[j]] = (uint16_t)a0;
+                    ch[s0[j] + 1u] = (uint16_t)a1;
+                    nx[a0] = (uint16_t)a1;
+                    nx[a1] = up;
+                }
+            }
+        }
+        // 3..8 children: Batcher's 19-comparator network (padding key 0 sorts last)
+#pragma unroll 1
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t p = t + (uint32_t)j * kDocThreads;
+            if (p >= R) break;
+            const uint32_t b = p ? D[p - 1] : 0u, cnt = D[p] - b;
+            if (cnt <= 2u) continue;
+            if (cnt > 64u) {
+                atomicOr(&flags, 2u);  // wider sibling groups: the global path handles this wave
+                continue;
+            }
+            if (cnt > 8u) {
+                defer[atomicAdd(&ndefer, 1u)] = (uint16_t)p;
+                continue;
+            }
+            uint64_t k[8];
+            uint32_t c[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = (uint32_t)i < cnt ? ch[b + i] : 0u;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) k[i] = (uint32_t)i < cnt ? doc_key(a, base, c[i]) : 0ull;
+            cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
+            cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
+            cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
+            cx(k[4], c[4], k[6], c[6]); cx(k[5], c[5], k[7], c[7]);
+            cx(k[1], c[1], k[2], c[2]); cx(k[5], c[5], k[6], c[6]);
+            cx(k[0], c[0], k[4], c[4]); cx(k[1], c[1], k[5], c[5]);
+            cx(k[2], c[2], k[6], c[6]); cx(k[3], c[3], k[7], c[7]);
+            cx(k[2], c[2], k[4], c[4]); cx(k[3], c[3], k[5], c[5]);
+            cx(k[1], c[1], k[2], c[2]); cx(k[3], c[3], k[4], c[4]); cx(k[5], c[5], k[6], c[6]);
+            const uint16_t up = (uint16_t)(p | kUp16);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if ((uint32_t)i < cnt) {
+                    ch[b + i] = (uint16_t)c[i];
+                    nx[c[i]] = (uint32_t)i + 1 < cnt ? (uint16_t)c[i + 1 < 8 ? i + 1 : 7] : up;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    PROBE(5);
+    // 9..64 siblings: one wave per group, rank = #siblings with a greater key
+    {
+        const uint32_t lane = t & 63u, wv = t >> 6;
+        const uint32_t nd = ndefer;
+        for (uint32_t i = wv; i < nd; i += kDocThreads / 64) {
+            const uint32_t p = defer[i];
+            const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
+            const bool on = lane < cnt;
+            const uint32_t c = on ? ch[s0 + lane] : 0u;
+            const uint64_t k = on ? doc_key(a, base, c) : 0ull;
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const uint64_t kj = ((uint64_t)(uint32_t)__shfl((int)(k >> 32), (int)j) << 32) |
+                                    (uint32_t)__shfl((int)(uint32_t)k, (int)j);
+                rank += kj > k;
+            }
+            const uint32_t sorted =
+                (uint32_t)__builtin_amdgcn_ds_permute((int)((on ? rank : lane) << 2), (int)c);
+            const uint32_t succ = (uint32_t)__shfl((int)sorted, (int)((lane + 1) & 63u));
+            if (on) {
+                ch[s0 + lane] = (uint16_t)sorted;  // lane r < cnt holds the rank-r child
+                nx[sorted] = lane + 1 < cnt ? (uint16_t)succ : (uint16_t)(p | kUp16);
+            }
+        }
+    }
+    __syncthreads();
+    if (flags) {
+        if (t == 0) atomicOr(&a.ctl[C_ERR], (flags & 1u) ? 1u : 32u);
+        return;
+    }
+    // ---- first children (into D) and weights (into w) --------------------------------------
+    {
+        uint32_t wr[kDocJ], fc[kDocJ];
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            wr[j] = v < R ? a.r_w[base + v] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            uint32_t f = kNil16;
+            if (v < R) {
+                const uint32_t s0 = v ? D[v - 1] : 0u;
+                if (s0 < D[v]) f = ch[s0];
+            }
+            fc[j] = f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            if (v < R) {
+                D[v] = (uint16_t)fc[j];
+                w[v] = (uint16_t)min(wr[j], 0xFFFFu);
+                if (wr[j] >= 0xFFFFu) {
+                    const uint32_t i = atomicAdd(&nbig, 1u);
+                    if (i < kDocBig) {
+                        bigv[i] = v;
+                        bigw[i] = wr[j];
+                    } else {
+                        atomicOr(&flags, 2u);  // that much text: the global path
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (flags) {
+        if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);
+        return;
+    }
+    PROBE(6);
+    // ---- walk 1: one walker per lane, splitters handed out by an LDS queue ----------------
+    // A step at arc (v, up) reads fc, nx and w of v together.  Down arc: v's weight is added,
+    // v's offset inside the sublist goes to roff and v records its sublist in w; the walk goes
+    // to the first child, or, for a leaf, straight through v's up arc to its successor (unless
+    // that up arc is itself a splitter).  A lane whose sublist ends takes the next splitter, so
+    // the lanes stay busy until the queue runs dry.  The sublist results (sum, next splitter)
+    // go to the ch region, which no walker reads.
+    uint32_t runs = 0;
+    uint32_t lane_steps = 0;
+    {
+        uint32_t s = t;
+        uint32_t V = (s >> 1) << kDocLog2S, U = s & 1u, SUM = 0;
+        uint32_t steps = 0;
+        const uint32_t step_limit = 2u * R + S + 4u;
+        while (s < S) {
+            const uint32_t f = D[V], n = nx[V], ww = w[V];
+            uint32_t nxt = kNil16;
+            bool fin = false;
+            if (n == kDead16) {
+                fin = true;
+            } else {
+                uint32_t go = n;  // successor arc, encoded like nx
+                if (!U) {
+                    uint32_t wt = ww;
+                    if (ww == 0xFFFFu)  // a run of 64 KiB or more: the LDS side table
+                        for (uint32_t i = 0; i < nbig; ++i)
+                            if (bigv[i] == V) wt = bigw[i];
+                    if (wt) a.roff[base + V] = SUM;
+                    w[V] = wt ? (uint16_t)s : kNil16;
+                    SUM += wt;
+                    ++runs;
+                    if (f != kNil16) go = f;
+                    else if ((V & ((1u << kDocLog2S) - 1u)) == 0) go = V | kUp16;
+                }
+                if (go == kNil16) {  // past the root's up arc: the end of the tour
+                    fin = true;
+                } else {
+                    const uint32_t nv = go & 0x7FFFu;
+                    if ((nv & ((1u << kDocLog2S) - 1u)) == 0) {
+                        nxt = 2u * (nv >> kDocLog2S) + (go >> 15);
+                        fin = true;
+                    } else {
+                        V = nv;
+                        U = go >> 15;
+                    }
+                }
+            }
+            if (fin) {
+                sval[s] = SUM;
+                sptr[s] = (uint16_t)nxt;
+                s = atomicAdd(&qhead, 1u);
+                V = (s >> 1) << kDocLog2S;
+                U = s & 1u;
+                SUM = 0;
+            }
+            if (++steps > step_limit) {
+                atomicOr(&flags, 4u);
+                break;
+            }
+        }
+        lane_steps = steps;
+    }
+    if (a.probe && d == a.probe - 1u) {
+        atomicMax(&probe_max, lane_steps);
+        atomicAdd(&probe_sum, lane_steps);
+    }
+    __syncthreads();
+    PROBE(7);
+    // ---- pointer jumping: sval = sum from the splitter to the end of the tour --------------
+    for (uint32_t r = 1; r < S; r <<= 1) {
+        uint32_t nv[kDocK], np[kDocK];
+#pragma unroll
+        for (int k = 0; k < kDocK; ++k) {
+            const uint32_t s = t + (uint32_t)k * kDocThreads;
+            uint32_t v = 0, q = kNil16;
+            if (s < S) {
+                const uint32_t p = sptr[s];
+                v = sval[s];
+                if (p != kNil16) {
+                    v += sval[p];
+                    q = sptr[p];
+                }
+            }
+            nv[k] = v;
+            np[k] = q;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kDocK; ++k) {
+            const uint32_t s = t + (uint32_t)k * kDocThreads;
+            if (s < S) {
+                sval[s] = nv[k];
+                sptr[s] = (uint16_t)np[k];
+            }
+        }
+        __syncthreads();
+    }
+    PROBE(8);
+    // ---- run offsets: sublist offset (total - suffix of its splitter) + offset inside ------
+    {
+        const uint32_t total = sval[0];
+        uint32_t sid[kDocJ], lo[kDocJ];
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            sid[j] = v < R ? w[v] : kNil16;
+            if (sid[j] >= S) sid[j] = kNil16;  // weightless (or never reached: flagged below)
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            lo[j] = sid[j] != kNil16 ? a.roff[base + v] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            if (sid[j] != kNil16) a.roff[base + v] = lo[j] + total - sval[sid[j]];
+        }
+    }
+    const uint32_t wr = wave_sum(runs + (uint32_t)__popc(pruned));  // pruned runs count as reached
+    if ((t & 63u) == 0 && wr) atomicAdd(&visited_lds, wr);
+    __syncthreads();
+    PROBE(9);
+    if (probe) {
+        printf("[doctree] doc %u R %u S %u us: load %.1f count %.1f scan %.1f place %.1f "
+               "sort %.1f defer+fc %.1f walk1 %.1f jump %.1f offsets %.1f | visited %u steps max %u "
+               "sum %u\n", d, R, S,
+               (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
+               (tp[4] - tp[3]) / 100.0, (tp[5] - tp[4]) / 100.0, (tp[6] - tp[5]) / 100.0,
+               (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0, (tp[9] - tp[8]) / 100.0,
+               visited_lds, probe_max, probe_sum);
+    }
+#undef PROBE
+    if (t == 0) {
+        if (visited_lds) atomicAdd(&a.ctl[C_VISITED], visited_lds);
+        if (flags & 4u) atomicOr(&a.ctl[C_ERR], 2u);
+    }
+}
 // ---------------------------------------------------------------------------------------------
 // digest: xxh64 of 4 KiB leaves, then xxh64 of the leaf digests seeded with the length
 // ---------------------------------------------------------------------------------------------
@@ -1221,6 +1709,10 @@ std::string Engine::init(int dev) {
         if ((e = hipEventCreate(&x)) != hipSuccess) return hipGetErrorString(e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&host_ctl_), 64)) != hipSuccess)
         return hipGetErrorString(e);
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
+        hipSuccess)
+        return std::string("k_doctree LDS: ") + hipGetErrorString(e);
     return "";
 }
 
@@ -1431,7 +1923,7 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
 }
 
 int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
-                     std::vector<uint32_t>& stage_launches) {
+                     std::vector<uint32_t>& stage_launches, bool force_global) {
     hipStream_t s = stream;
     const bool ord = mode == ORDER;
     const uint32_t ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
@@ -1536,6 +2028,38 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     const uint32_t gR = grid_for(R), gS = grid_for(S);
     const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
 
+    // Per-document LDS path when the largest document's run tree fits one workgroup.
+    const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
+    const uint32_t scap = (2u * ((rmax + 7u) >> kDocLog2S) + 7u) & ~7u;
+    const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
+    const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
+                      dbytes <= kDocLds;
+    uint32_t rounds = 0;
+    if (lds1) {
+        for (int st = S_COUNT; st <= S_WALK2; ++st) {
+            BEGIN(st);
+            END(st);
+        }
+        DocArgs da{};
+        da.ndocs = w.ndocs;
+        da.rtotal = R;
+        da.rcap = rcap;
+        da.scap = scap;
+        da.chbytes = doctree_ch_bytes(rcap, scap);
+        da.doc_root = doc_root_;
+        da.r_parent = r_parent_;
+        da.r_w = r_w_;
+        da.r_key = r_key_;
+        da.roff = roff_;
+        da.ctl = ctl_;
+        if (const char* pe = getenv("CRDT_HIP_PROBE")) da.probe = 1u + (uint32_t)atoi(pe);
+        BEGIN(S_DOCTREE);
+        k_doctotals<<<1, 1024, 0, s>>>(a);
+        k_doctree<<<w.ndocs, kDocThreads, (uint32_t)dbytes, s>>>(da);
+        END(S_DOCTREE);
+    } else {
+    BEGIN(S_DOCTREE);
+    END(S_DOCTREE);
     BEGIN(S_COUNT);
     k_count<<<gR, kBlock, 0, s>>>(a);
     END(S_COUNT);
@@ -1560,7 +2084,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     k_pred<<<gS, kBlock, 0, s>>>(snext_, S, pred_);
     k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, S, v0_, p0_);
     // a document's list holds at most 2 * (ceil(runs / M) + 1) + 1 splitters
-    const uint32_t rounds = ceil_log2(2ull * ((rmax + (1u << log2m) - 1) >> log2m) + 4);
+    rounds = ceil_log2(2ull * ((rmax + (1u << log2m) - 1) >> log2m) + 4);
     uint32_t *vi = v0_, *pi = p0_, *vo = v1_, *po = p1_;
     for (uint32_t r = 0; r < rounds; ++r) {
         k_wstep<<<gS, kBlock, 0, s>>>(vi, pi, S, vo, po);
@@ -1573,6 +2097,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
     END(S_WALK2);
+    }  // global level 1
 
     // ---- expansion + digest --------------------------------------------------------------
     ExpandArgs ea{};
@@ -1607,7 +2132,9 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
                "copy digests");
     HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "merge wave");
-    const uint32_t launches[S_N] = {1, 6, 1, 1, 3, 1, 3, 1, 2 + rounds, 2, 1, ord ? 0u : 2u};
+    const uint32_t g1 = lds1 ? 0u : 1u;
+    const uint32_t launches[S_N] = {1, 6, 1, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
+                                    1, ord ? 0u : 2u, lds1 ? 2u : 0u};
     for (int i = 0; i < S_N; ++i) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");
@@ -1616,8 +2143,12 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     }
 #undef BEGIN
 #undef END
-    runs_ += R;
     uint32_t errs = host_ctl_[C_ERR];
+    if (lds1 && (errs & 32u)) {
+        // a sibling group wider than the LDS path sorts: redo the wave on the global path
+        return run_wave(L, w, mode, stage_ms, stage_launches, true);
+    }
+    runs_ += R;
     if (!errs && host_ctl_[C_VISITED] != R) errs |= 16u;  // unreachable runs: a cycle
     if (errs) {
         (void)hipMemset(deg_, 0, (cap_runs_ + 16) * 4);  // restore the all-zero invariant

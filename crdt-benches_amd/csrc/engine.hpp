@@ -63,6 +63,7 @@ public:
     hipStream_t stream = nullptr;
     uint32_t log2m = 4;                    // level-1 splitter stride M = 2^log2m
     uint64_t max_wave_slots = 1ull << 30;
+    bool level1_global = false;            // never use the per-document LDS level 1
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -118,7 +119,7 @@ private:
     int ensure_runs(uint64_t runs, uint64_t splitters);
     int ensure_scratch(const Wave& w, uint32_t ndocs_total);
     int run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
-                 std::vector<uint32_t>& stage_launches);
+                 std::vector<uint32_t>& stage_launches, bool force_global = false);
     int fail(const char* what, hipError_t e);
 };
 

@@ -97,7 +97,9 @@ enum {
     CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets                  */
     CRDT_HIP_STAGE_EXPAND = 10,  /* runs copy their UTF-8 to their document offset            */
     CRDT_HIP_STAGE_DIGEST = 11,  /* per-document tree digest                                  */
-    CRDT_HIP_NSTAGES = 12
+    CRDT_HIP_STAGE_DOCTREE = 12, /* level 1 in LDS: whole run tree of a document per workgroup
+                                    (replaces stages 3-9 when every document fits)           */
+    CRDT_HIP_NSTAGES = 13
 };
 
 /* ---- library / context ----------------------------------------------------------------- */
@@ -106,8 +108,10 @@ int crdt_hip_device_count(int* out);
 int crdt_hip_init(int device, crdt_hip_ctx** out);
 int crdt_hip_destroy(crdt_hip_ctx* ctx);
 const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
-/* Tuning: splitter stride of the list ranking (power of two, 16..4096; default 16) and the
- * maximum slots per device wave (default 2^30). */
+/* Tuning: "splitter_stride" of the global list ranking (power of two, 16..4096; default 16),
+ * "max_wave_slots" per device wave (default 2^30), and "level1": 0 = per-document LDS merge of
+ * the run tree whenever every document of a wave fits a workgroup's LDS (default), 1 = always
+ * the global (multi-kernel) level-1 path. Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 
 /* ---- op log: host-side resolver (positional patch -> anchor op) ---------------------------- */

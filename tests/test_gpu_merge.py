@@ -191,6 +191,59 @@ def test_replica_batch_relabel_invariance(ctx, oracle, golden, relabel):
     assert st["items"] == 3 * sum(golden[n]["items"] for n in TRACES)
 
 
+def _level1_cases():
+    rng = np.random.default_rng(11)
+    logs = [resolved(n) for n in TRACES]
+    logs.append(crdt_hip.OpLog.synth_agents(20000, 64, 0x5EED0005).arrays())
+    logs.append(crdt_hip.OpLog.synth_agents(4000, 3, 0x5EED0006).arrays())
+    for k in (2, 5, 9, 40, 64, 65):
+        logs.append(fanout_log(k, depth_extra=30))
+    wide = crdt_hip.OpLog.synth_agents(3000, 8, 5).arrays()
+    wide.cp[:] = rng.choice([0x41, 0xE9, 0x2019, 0x4E2D, 0x1F600], wide.n)
+    logs.append(wide)
+    big = crdt_hip.LogArrays(np.arange(70000, dtype=np.uint32), np.arange(1, 70001, dtype=np.uint32),
+                             np.zeros(70000, np.uint16), np.zeros(70000, np.uint8),
+                             np.full(70000, 0x4E2D, np.uint32))  # one run of 210,000 bytes
+    logs.append(big)
+    n = 40 * 22000  # 40 sibling runs of 66,000 bytes each: more heavy runs than the LDS table
+    par = np.arange(n, dtype=np.uint32)
+    par[::22000] = 0
+    logs.append(crdt_hip.LogArrays(par, np.arange(1, n + 1, dtype=np.uint32), np.zeros(n, np.uint16),
+                                   np.zeros(n, np.uint8), np.full(n, 0x4E2D, np.uint32)))
+    logs.append(crdt_hip.LogArrays([], [], [], [], []))
+    return logs
+
+
+@pytest.mark.parametrize("level1", [0, 1])
+def test_level1_paths_match_oracle(oracle, level1):
+    """Per-document LDS level 1 (k_doctree, default) and the global level-1 kernels must give
+    the oracle's bytes and digests, including sibling groups of every sort width (> 64 makes
+    the LDS path hand the wave to the global path) and a run heavier than 0xFFFF bytes."""
+    c = crdt_hip.Context(0)
+    c.set_param("level1", level1)
+    logs = _level1_cases()
+    dig, lens, st = c.merge_batch(logs, stats=True)
+    for i, lg in enumerate(logs):
+        ref = oracle.merge(to_anchor(lg)) if lg.n else b""
+        assert lens[i] == len(ref), i
+        assert dig[i] == oracle.tree_digest(ref), i
+    for i in (0, 4, 6, 11, 12, 13, 14):  # one document per merge: the LDS path where it fits
+        text, d1 = c.merge(logs[i])
+        assert text == (oracle.merge(to_anchor(logs[i])) if logs[i].n else b""), i
+        order = c.merge_order(logs[i])
+        if logs[i].n:
+            _, ref = oracle.merge(to_anchor(logs[i]), want_order=True)
+            assert np.array_equal(order, ref), i
+    c.close()
+
+
+def test_level1_lds_path_is_taken_for_trace_batches(ctx):
+    bases = [resolved(n) for n in TRACES]
+    b = ctx.batch(bases, replicas=2, relabel="rotate", seed=5)
+    _, _, st = b.merge()
+    assert st["stage_launches"]["doctree"] == 2 and st["stage_launches"]["walk1"] == 0
+
+
 def test_malformed_logs_are_rejected(ctx):
     bad_parent = crdt_hip.LogArrays([0, 5], [1, 2], [0, 0], [0, 0], [97, 98])
     with pytest.raises(crdt_hip.CrdtHipError) as e:
