@@ -218,6 +218,8 @@ def main() -> int:
 
     def alg_bytes(k):
         per_slot, per_run, per_text = KERNEL_BYTES[k]
+        if k == "doctree" and launches.get("expand", 1) == 0:
+            per_text = 2.0  # expansion fused: slot-order UTF-8 in, document UTF-8 out
         return per_slot * slots + per_run * runs + per_text * text_bytes
 
     per_kernel = {k: {"ms": stage_ns[k] / 1e6, "launches": launches[k],

@@ -16,7 +16,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libcrdt_hip.so")
+# CRDT_HIP_LIB selects another in-tree build (e.g. libcrdt_hip_probe.so: `make probe`)
+LIB_PATH = os.path.join(PKG_DIR, os.environ.get("CRDT_HIP_LIB", "libcrdt_hip.so"))
 
 OK = 0
 ERRORS = {

@@ -63,6 +63,7 @@ enum Ctl {
     C_WTOTAL = 4,   // weight total of the wave
     C_RMAX = 5,     // most runs in one document
     C_VISITED = 6,  // runs visited by k_walk2
+    C_UNFUSED = 7,  // documents whose text k_doctree left to k_expand
 };
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
@@ -492,6 +493,7 @@ struct ExpandArgs {
     const uint8_t* sbytes;
     uint8_t* text;
     uint32_t* ctl;
+    const uint8_t* fused;  // per document: text already written by k_doctree (or null)
 };
 
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a) {
@@ -507,7 +509,9 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a) {
             const uint32_t d = a.chunk_doc[h >> a.log2m];
             const uint32_t base = a.docs[d].x;
             const uint32_t ro = a.roff[rho];
-            if ((uint64_t)ro + w > a.tlen[d]) {
+            if (a.fused && a.fused[d]) {
+                dst = ~0ull;  // k_doctree wrote this document (w still counts: bytes stay aligned)
+            } else if ((uint64_t)ro + w > a.tlen[d]) {
                 atomicOr(&a.ctl[C_ERR], 8u);
                 dst = ~0ull;  // skipped below
             } else {
@@ -1015,6 +1019,8 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
     const uint32_t tot = wave_sum(runs);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
 }
+__device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, uint64_t seed);
+
 // ---------------------------------------------------------------------------------------------
 // Level 1 in LDS: the whole run tree of one document per workgroup (k_doctree)
 // ---------------------------------------------------------------------------------------------
@@ -1059,6 +1065,15 @@ struct DocArgs {
     const uint64_t* r_key;
     uint32_t* roff;
     uint32_t* ctl;
+    // fused text (phase C): text == nullptr leaves the run offsets in roff for k_expand
+    const uint32_t* r_pstart;
+    const uint32_t* doc_p0;
+    const uint32_t* tlen;
+    const uint64_t* toff;
+    const uint8_t* sbytes;
+    uint8_t* text;
+    uint8_t* fused;       // per document: 1 = text written by k_doctree
+    uint32_t lds_bytes;   // dynamic LDS of the launch
 };
 
 // LDS bytes of a document with up to rcap - 2 runs: D, nx, w (2 B/run each) and the ch region,
@@ -1076,10 +1091,106 @@ __device__ __forceinline__ uint64_t doc_key(const DocArgs& a, uint32_t base, uin
     return (a.r_key[base + v] << 15) | v;
 }
 
+// Phase C of k_doctree: expansion fused, when the document's text and its run-start index fit
+// LDS.  1) The document's visible UTF-8 in slot order (one contiguous range of sbytes: runs are
+// numbered in slot order) is staged in LDS with 16-byte loads.  2) Every run with visible bytes
+// sets the bit of its document offset in a bitvector over the document; with u16 prefix counts
+// per 32-bit word this gives the run its rank in document order, and it stores
+// delta[rank] = staging offset - document offset.  3) The document is written in order, 4 bytes
+// per lane (256-byte coalesced stores per wave): byte y belongs to the run of the last set bit
+// at or before y.  Returns false (nothing written) when the document does not fit.
+constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
+__device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t base, uint32_t R,
+                                         const uint32_t (&ro)[kDocJ], uint8_t* st,
+                                         uint32_t* scan_lds) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t tl = a.tlen[d], p0 = a.doc_p0[d];
+    const uint32_t sh = p0 & 15u;
+    const uint32_t nq = (sh + tl + 15u) >> 4;  // staged 16-byte pieces
+    const uint32_t nw = (tl + 31u) >> 5;       // bitvector words
+    const uint32_t o_bits = 16u * nq + 16u, o_pref = o_bits + 4u * nw;
+    const uint32_t o_delta = (o_pref + 2u * nw + 15u) & ~15u;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < kDocJ; ++j) mine += ro[j] != kNil ? 1u : 0u;
+    uint32_t Rw;
+    (void)block_excl_scan<kDocThreads / 64>(mine, scan_lds, Rw);
+    if (o_delta + 4u * Rw > a.lds_bytes || nq > (uint32_t)(kDocQ * kDocThreads)) return false;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(st + o_bits);
+    uint16_t* pref = reinterpret_cast<uint16_t*>(st + o_pref);
+    uint32_t* delta = reinterpret_cast<uint32_t*>(st + o_delta);
+    // 1) staging (every load first; clamped indices keep the arrays in registers)
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.sbytes + (p0 - sh));
+        uint4 q[kDocQ];
+#pragma unroll
+        for (int k = 0; k < kDocQ; ++k)
+            q[k] = src[min(t + (uint32_t)k * kDocThreads, nq ? nq - 1u : 0u)];
+        uint32_t ps[kDocJ];
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j)
+            ps[j] = a.r_pstart[base + min(t + (uint32_t)j * kDocThreads, R - 1u)];
+        for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
+        uint4* stq = reinterpret_cast<uint4*>(st);
+#pragma unroll
+        for (int k = 0; k < kDocQ; ++k) {
+            const uint32_t i = t + (uint32_t)k * kDocThreads;
+            if (i < nq) stq[i] = q[k];
+        }
+        __syncthreads();
+        // 2) run starts -> ranks in document order -> staging offset minus document offset
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j)
+            if (ro[j] != kNil) atomicOr(&bits[ro[j] >> 5], 1u << (ro[j] & 31u));
+        __syncthreads();
+        {
+            const uint32_t K = (nw + kDocThreads - 1) / kDocThreads;
+            const uint32_t lo = min(nw, t * K), hi = min(nw, lo + K);
+            uint32_t c = 0;
+            for (uint32_t i = lo; i < hi; ++i) c += (uint32_t)__popc(bits[i]);
+            uint32_t tot;
+            uint32_t ex = block_excl_scan<kDocThreads / 64>(c, scan_lds, tot);
+            for (uint32_t i = lo; i < hi; ++i) {
+                pref[i] = (uint16_t)ex;
+                ex += (uint32_t)__popc(bits[i]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            if (ro[j] == kNil) continue;
+            const uint32_t wd = ro[j] >> 5;
+            const uint32_t rank = pref[wd] + (uint32_t)__popc(bits[wd] & ((1u << (ro[j] & 31u)) - 1u));
+            delta[rank] = (ps[j] - p0 + sh) - ro[j];
+        }
+    }
+    __syncthreads();
+    // 3) the document in order, one dword per lane per step
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.text + a.toff[d]);  // 16-aligned
+    for (uint32_t i = t; i < (tl + 3u) >> 2; i += kDocThreads) {
+        uint32_t word = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t y = 4u * i + b;
+            if (y < tl) {
+                const uint32_t wd = y >> 5;
+                const uint32_t mask = (2u << (y & 31u)) - 1u;  // bits at or before y (y&31 = 31: all)
+                const uint32_t r = pref[wd] + (uint32_t)__popc(bits[wd] & mask) - 1u;
+                word |= (uint32_t)st[y + delta[r]] << (8u * b);
+            }
+        }
+        out[i] = word;
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
-    __shared__ uint32_t ndefer, flags, visited_lds, pruned_any, qhead, probe_max, probe_sum, nbig;
+    __shared__ uint32_t ndefer, flags, visited_lds, pruned_any, nbig;
+#ifdef CRDT_HIP_PROBE
+    __shared__ uint32_t probe_max, probe_sum;
+#endif
     __shared__ uint32_t bigv[kDocBig], bigw[kDocBig];
     const uint32_t d = blockIdx.x;
     const uint32_t t = threadIdx.x;
@@ -1094,18 +1205,23 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     uint16_t* w = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(ch) + a.chbytes);
     uint16_t* defer = w;
     uint32_t* D32 = dyn;
-    // phase timestamps of one document (CRDT_HIP_PROBE=<doc>, off by default)
+#ifdef CRDT_HIP_PROBE
+    // phase timestamps of one document (probe build, CRDT_HIP_PROBE=<doc>)
     const bool probe = a.probe && d == a.probe - 1u && t == 0;
-    uint64_t tp[10];
+    uint64_t tp[11];
     tp[0] = wall_clock64();
 #define PROBE(i) if (probe) tp[i] = wall_clock64()
+#else
+#define PROBE(i) (void)0
+#endif
     if (t == 0) {
         ndefer = 0;
         flags = 0;
         visited_lds = 0;
         pruned_any = 0;
-        qhead = kDocThreads;
+#ifdef CRDT_HIP_PROBE
         probe_max = probe_sum = 0;
+#endif
         nbig = 0;
     }
     if (R + 2u > a.rcap || S > a.scap || R > (uint32_t)(kDocJ * kDocThreads)) {
@@ -1155,7 +1271,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // ---- pruning: a weightless leaf adds nothing to the document and is dropped from its
     // parent's children; a parent that loses its last child may go in the same pass (the
     // outcome depends on timing, never the text).  Repeated while it finds anything.
-    for (int round = 0; round < 8; ++round) {
+    for (int round = 0; round < 3; ++round) {
         uint32_t found = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
@@ -1377,49 +1493,40 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     uint32_t lane_steps = 0;
     {
         uint32_t s = t;
-        uint32_t V = (s >> 1) << kDocLog2S, U = s & 1u, SUM = 0;
-        uint32_t steps = 0;
+        uint32_t V = (s >> 1) << kDocLog2S, U = s & 1u, SUM = 0, steps = 0;
         const uint32_t step_limit = 2u * R + S + 4u;
         while (s < S) {
             const uint32_t f = D[V], n = nx[V], ww = w[V];
-            uint32_t nxt = kNil16;
-            bool fin = false;
-            if (n == kDead16) {
-                fin = true;
-            } else {
-                uint32_t go = n;  // successor arc, encoded like nx
-                if (!U) {
-                    uint32_t wt = ww;
-                    if (ww == 0xFFFFu)  // a run of 64 KiB or more: the LDS side table
-                        for (uint32_t i = 0; i < nbig; ++i)
-                            if (bigv[i] == V) wt = bigw[i];
-                    if (wt) a.roff[base + V] = SUM;
-                    w[V] = wt ? (uint16_t)s : kNil16;
-                    SUM += wt;
-                    ++runs;
-                    if (f != kNil16) go = f;
-                    else if ((V & ((1u << kDocLog2S) - 1u)) == 0) go = V | kUp16;
-                }
-                if (go == kNil16) {  // past the root's up arc: the end of the tour
-                    fin = true;
-                } else {
-                    const uint32_t nv = go & 0x7FFFu;
-                    if ((nv & ((1u << kDocLog2S) - 1u)) == 0) {
-                        nxt = 2u * (nv >> kDocLog2S) + (go >> 15);
-                        fin = true;
-                    } else {
-                        V = nv;
-                        U = go >> 15;
-                    }
-                }
+            const bool dead = n == kDead16;
+            const bool dn = !U && !dead;
+            uint32_t wt = ww;
+            if (dn && ww == 0xFFFFu)  // a run of 64 KiB or more: the LDS side table
+                for (uint32_t i = 0; i < nbig; ++i)
+                    if (bigv[i] == V) wt = bigw[i];
+            wt = dn ? wt : 0u;
+            if (dn) {
+                // v's down arc is the last use of D[v] (first child) and w[v] (weight): they now
+                // hold v's offset inside this sublist (19 bits) and the sublist (13 bits)
+                const uint32_t pk = wt ? (SUM | (s << 19)) : 0xFFFFFFFFu;
+                D[V] = (uint16_t)pk;
+                w[V] = (uint16_t)(pk >> 16);
             }
-            if (fin) {
+            SUM += wt;
+            runs += dn ? 1u : 0u;
+            uint32_t go = n;  // successor arc, encoded like nx
+            if (dn) go = f != kNil16 ? f : ((V & 7u) == 0 ? (V | kUp16) : n);
+            const bool end = dead || go == kNil16;
+            const bool split = !end && (go & 7u) == 0;
+            if (end || split) {
                 sval[s] = SUM;
-                sptr[s] = (uint16_t)nxt;
-                s = atomicAdd(&qhead, 1u);
+                sptr[s] = split ? (uint16_t)(2u * ((go & 0x7FFFu) >> kDocLog2S) + (go >> 15)) : kNil16;
+                s += kDocThreads;
                 V = (s >> 1) << kDocLog2S;
                 U = s & 1u;
                 SUM = 0;
+            } else {
+                V = go & 0x7FFFu;
+                U = go >> 15;
             }
             if (++steps > step_limit) {
                 atomicOr(&flags, 4u);
@@ -1428,10 +1535,13 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         }
         lane_steps = steps;
     }
+    (void)lane_steps;
+#ifdef CRDT_HIP_PROBE
     if (a.probe && d == a.probe - 1u) {
         atomicMax(&probe_max, lane_steps);
         atomicAdd(&probe_sum, lane_steps);
     }
+#endif
     __syncthreads();
     PROBE(7);
     // ---- pointer jumping: sval = sum from the splitter to the end of the tour --------------
@@ -1465,39 +1575,50 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     }
     PROBE(8);
     // ---- run offsets: sublist offset (total - suffix of its splitter) + offset inside ------
+    uint32_t ro[kDocJ];  // document offset of every owned run with visible bytes, else kNil
     {
         const uint32_t total = sval[0];
-        uint32_t sid[kDocJ], lo[kDocJ];
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            sid[j] = v < R ? w[v] : kNil16;
-            if (sid[j] >= S) sid[j] = kNil16;  // weightless (or never reached: flagged below)
+            uint32_t pk = 0xFFFFFFFFu;
+            if (v < R && !(pruned & (1u << j))) pk = (uint32_t)D[v] | ((uint32_t)w[v] << 16);
+            const uint32_t sid = pk >> 19;
+            // weightless, pruned (or never reached: flagged below)
+            ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x7FFFFu) + total - sval[sid] : kNil;
         }
+        if (!a.text) {  // offsets for k_expand
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t v = t + (uint32_t)j * kDocThreads;
-            lo[j] = sid[j] != kNil16 ? a.roff[base + v] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t v = t + (uint32_t)j * kDocThreads;
-            if (sid[j] != kNil16) a.roff[base + v] = lo[j] + total - sval[sid[j]];
+            for (int j = 0; j < kDocJ; ++j)
+                if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ro[j];
         }
     }
     const uint32_t wr = wave_sum(runs + (uint32_t)__popc(pruned));  // pruned runs count as reached
     if ((t & 63u) == 0 && wr) atomicAdd(&visited_lds, wr);
     __syncthreads();
     PROBE(9);
+    if (a.text) {
+        const bool fused = doc_text(a, d, base, R, ro, reinterpret_cast<uint8_t*>(dyn), scan_lds);
+        if (!fused) {  // k_expand writes this document
+#pragma unroll
+            for (int j = 0; j < kDocJ; ++j)
+                if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ro[j];
+            if (t == 0) atomicAdd(&a.ctl[C_UNFUSED], 1u);
+        }
+        if (t == 0) a.fused[d] = fused ? 1u : 0u;
+    }
+    PROBE(10);
+#ifdef CRDT_HIP_PROBE
     if (probe) {
         printf("[doctree] doc %u R %u S %u us: load %.1f count %.1f scan %.1f place %.1f "
-               "sort %.1f defer+fc %.1f walk1 %.1f jump %.1f offsets %.1f | visited %u steps max %u "
+               "sort %.1f defer+fc %.1f walk1 %.1f jump %.1f offsets %.1f text %.1f | visited %u steps max %u "
                "sum %u\n", d, R, S,
                (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
                (tp[4] - tp[3]) / 100.0, (tp[5] - tp[4]) / 100.0, (tp[6] - tp[5]) / 100.0,
                (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0, (tp[9] - tp[8]) / 100.0,
-               visited_lds, probe_max, probe_sum);
+               (tp[10] - tp[9]) / 100.0, visited_lds, probe_max, probe_sum);
     }
+#endif
 #undef PROBE
     if (t == 0) {
         if (visited_lds) atomicAdd(&a.ctl[C_VISITED], visited_lds);
@@ -1670,7 +1791,7 @@ Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
     dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hrank_); dfree(stile_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
-    dfree(doc_root_); dfree(doc_p0_);
+    dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(ctl_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
@@ -1746,6 +1867,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         w.nslots += (uint32_t)ds;
         w.max_splitters_per_doc = std::max<uint32_t>(w.max_splitters_per_doc, (uint32_t)(2 * ds / M));
         w.text_cap += dt;
+        w.max_doc_text = std::max<uint64_t>(w.max_doc_text, docs[d].text_cap);
         w.leaf_cap += (docs[d].text_cap + kLeaf - 1) / kLeaf;
         w.order_cap += docs[d].n;
         L.items += docs[d].n;
@@ -1856,6 +1978,7 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     if (!ctl_) HIPCHK(dalloc(&ctl_, 16), "hipMalloc ctl");
     if (w.ndocs + 1 > cap_docs_) {
         dfree(tlen_); dfree(loff_); dfree(toff_); dfree(dig_); dfree(doc_root_); dfree(doc_p0_);
+        dfree(doc_fused_);
         const uint64_t nd = w.ndocs + 1;
         HIPCHK(dalloc(&tlen_, nd), "hipMalloc tlen");
         HIPCHK(dalloc(&loff_, nd), "hipMalloc loff");
@@ -1863,6 +1986,7 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
         HIPCHK(dalloc(&dig_, nd), "hipMalloc dig");
         HIPCHK(dalloc(&doc_root_, nd), "hipMalloc doc_root");
         HIPCHK(dalloc(&doc_p0_, nd), "hipMalloc doc_p0");
+        HIPCHK(dalloc(&doc_fused_, nd), "hipMalloc doc_fused");
         cap_docs_ = nd;
     }
     const uint64_t tb = std::max<uint64_t>(w.text_cap, w.order_cap * 4) + 64;
@@ -2032,8 +2156,16 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
     const uint32_t scap = (2u * ((rmax + 7u) >> kDocLog2S) + 7u) & ~7u;
     const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
+    // (sublist offsets are packed in 19 bits inside the walk: documents below 512 KiB of text)
     const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
-                      dbytes <= kDocLds;
+                      dbytes <= kDocLds && w.max_doc_text < (1ull << 19);
+    // expansion + digest fused into k_doctree when every document's text fits LDS
+    const bool fuse = lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
+    // text staging + run-start bitvector (tl/8 + tl/16) + one u32 per run
+    const uint64_t dyn_bytes =
+        fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
+                   dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
+             : dbytes;
     uint32_t rounds = 0;
     if (lds1) {
         for (int st = S_COUNT; st <= S_WALK2; ++st) {
@@ -2052,10 +2184,18 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
         da.r_key = r_key_;
         da.roff = roff_;
         da.ctl = ctl_;
+        da.r_pstart = r_pstart_;
+        da.doc_p0 = doc_p0_;
+        da.tlen = tlen_;
+        da.toff = toff_;
+        da.sbytes = sbytes_;
+        da.text = fuse ? text_ : nullptr;
+        da.fused = doc_fused_;
+        da.lds_bytes = (uint32_t)dyn_bytes;
         if (const char* pe = getenv("CRDT_HIP_PROBE")) da.probe = 1u + (uint32_t)atoi(pe);
         BEGIN(S_DOCTREE);
         k_doctotals<<<1, 1024, 0, s>>>(a);
-        k_doctree<<<w.ndocs, kDocThreads, (uint32_t)dbytes, s>>>(da);
+        k_doctree<<<w.ndocs, kDocThreads, (uint32_t)dyn_bytes, s>>>(da);
         END(S_DOCTREE);
     } else {
     BEGIN(S_DOCTREE);
@@ -2116,7 +2256,14 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     ea.text = text_;
     ea.ctl = ctl_;
     BEGIN(S_EXPAND);
-    k_expand<<<gR, kBlock, 0, s>>>(ea);
+    bool expand_run = true;
+    if (fuse) {  // only documents whose text did not fit k_doctree's LDS are left
+        HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
+        HIPCHK(hipStreamSynchronize(s), "doctree sync");
+        expand_run = host_ctl_[C_UNFUSED] != 0;
+        ea.fused = doc_fused_;
+    }
+    if (expand_run) k_expand<<<gR, kBlock, 0, s>>>(ea);
     END(S_EXPAND);
     BEGIN(S_DIGEST);
     if (!ord) {
@@ -2134,7 +2281,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     HIPCHK(hipStreamSynchronize(s), "merge wave");
     const uint32_t g1 = lds1 ? 0u : 1u;
     const uint32_t launches[S_N] = {1, 6, 1, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
-                                    1, ord ? 0u : 2u, lds1 ? 2u : 0u};
+                                    expand_run ? 1u : 0u, ord ? 0u : 2u, lds1 ? 2u : 0u};
     for (int i = 0; i < S_N; ++i) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");

@@ -29,6 +29,7 @@ struct Wave {
     uint64_t text_cap;   // bytes (docs aligned to 16)
     uint64_t leaf_cap;   // 4 KiB leaves
     uint64_t order_cap;  // u32 entries for ORDER mode
+    uint64_t max_doc_text;  // largest document text bound of the wave
 };
 
 // Device-resident op logs in slot layout, planned into waves.
@@ -99,6 +100,7 @@ private:
     uint32_t *doc_root_ = nullptr, *doc_p0_ = nullptr, *tlen_ = nullptr, *loff_ = nullptr;
     uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;
     uint8_t* text_ = nullptr;
+    uint8_t* doc_fused_ = nullptr;
     // level-1 scratch (per run / per splitter), grown on demand
     uint64_t cap_heads_ = 0, cap_runs_ = 0, cap_splitters_ = 0;
     uint32_t *r_head_ = nullptr, *r_pstart_ = nullptr, *r_parent_ = nullptr, *r_w_ = nullptr,

@@ -242,6 +242,8 @@ def test_level1_lds_path_is_taken_for_trace_batches(ctx):
     b = ctx.batch(bases, replicas=2, relabel="rotate", seed=5)
     _, _, st = b.merge()
     assert st["stage_launches"]["doctree"] == 2 and st["stage_launches"]["walk1"] == 0
+    # the expansion runs inside k_doctree (the texts fit LDS)
+    assert st["stage_launches"]["expand"] == 0
 
 
 def test_malformed_logs_are_rejected(ctx):
