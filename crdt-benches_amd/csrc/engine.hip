@@ -463,14 +463,20 @@ __global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uin
     const uint32_t ps = a.r_pstart[rho];
     const uint32_t next = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
     a.r_w[rho] = next - ps;
-    const uint2 doc = a.docs[a.chunk_doc[h >> a.log2m]];
     uint32_t pr = kNil;
     uint64_t key = 0;
-    if (h != doc.x) {
-        uint32_t p = a.in_parent[h];
+    if ((a.seqb[h >> 4] >> (h & 15u)) & 1u) {
+        // the head's parent is the slot before it, the last slot of the previous run
+        pr = rho - 1u;
         key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
-        if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_classify
-        pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u;
+    } else {
+        const uint2 doc = a.docs[a.chunk_doc[h >> a.log2m]];
+        if (h != doc.x) {
+            uint32_t p = a.in_parent[h];
+            key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
+            if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_classify
+            pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u;
+        }
     }
     a.r_parent[rho] = pr;
     a.r_key[rho] = key;
@@ -1042,18 +1048,19 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 //   w[v]   the deferred sort list during the sort, then the weight (0xFFFF: look it up in
 //          r_w), then, once walk 1 has passed v, the splitter whose sublist holds v (kNil16 for
 //          weightless runs)
-// Splitters are both arcs of every run v with v % 8 == 0 (splitter 2(v/8) + up).  Each thread
-// walks up to kDocK sublists in lockstep so that their LDS latencies overlap; a walker that
-// passes v's down arc stores v's offset inside its sublist to roff, and after the splitter
-// lists are ranked one coalesced pass adds the sublist offsets.
+// Splitters are both arcs of the runs v with v % 4 == 0 (splitter 2(v/4) + up; a leaf's down
+// and up arcs are one step unless the up arc is a splitter).  A walker that passes v's down arc leaves
+// v's offset inside its sublist and the sublist's id in v's LDS entries, and once the splitter
+// list is ranked (pointer jumping) one pass turns them into document offsets.
 constexpr int kDocThreads = 1024;
 constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
-constexpr int kDocK = 5;           // splitters per thread: 2 * ceil(20480 / 8) = 5 * 1024
-constexpr uint32_t kDocLog2S = 3;  // splitter stride 8
+constexpr int kDocK = 10;          // splitters per thread: 2 * ceil(20480 / 4) = 10 * 1024
+constexpr uint32_t kDocLog2S = 2;  // splitters: both arcs of the runs v % 4 == 0
 constexpr uint32_t kDocLds = 163840 - 512;  // dynamic LDS budget (static arrays use the rest)
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
 constexpr uint16_t kDead16 = 0xFFFEu;  // nx of a pruned run
+constexpr uint32_t kNil14 = 0x3FFFu;   // no next splitter (splitter records: sum << 14 | next)
 constexpr uint32_t kDocBig = 32;       // runs of >= 0xFFFF bytes per document (LDS side table)
 
 struct DocArgs {
@@ -1076,13 +1083,15 @@ struct DocArgs {
     uint32_t lds_bytes;   // dynamic LDS of the launch
 };
 
-// LDS bytes of a document with up to rcap - 2 runs: D, nx, w (2 B/run each) and the ch region,
-// which must also hold the splitter lists (6 B per splitter).
+// LDS bytes of a document with up to rcap - 2 runs: D, nx, w (2 B/run each), the ch region,
+// which later holds the splitter records (4 B per splitter: sublist sum << 14 | next splitter),
+// and the list of sibling groups of 9..64 (at most one per 9 runs).
 __host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t scap) {
-    return ((2u * rcap > 6u * scap ? 2u * rcap : 6u * scap) + 15u) & ~15u;
+    return ((2u * rcap > 4u * scap ? 2u * rcap : 4u * scap) + 15u) & ~15u;
 }
+__host__ __device__ constexpr uint32_t doctree_defer_cap(uint32_t rcap) { return rcap / 8u + 8u; }
 __host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap) {
-    return 6ull * rcap + doctree_ch_bytes(rcap, scap);
+    return 6ull * rcap + doctree_ch_bytes(rcap, scap) + 2ull * doctree_defer_cap(rcap);
 }
 
 // Sort key: (lamport, agent) of the run's head (48 bits) and the local run index (15 bits), so
@@ -1165,21 +1174,21 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
         }
     }
     __syncthreads();
-    // 3) the document in order, one dword per lane per step
-    uint32_t* out = reinterpret_cast<uint32_t*>(a.text + a.toff[d]);  // 16-aligned
-    for (uint32_t i = t; i < (tl + 3u) >> 2; i += kDocThreads) {
-        uint32_t word = 0;
+    // 3) the document in order, 16 bytes per lane per step (one bitvector word covers them)
+    uint4* out = reinterpret_cast<uint4*>(a.text + a.toff[d]);  // 16-aligned
+    for (uint32_t i = t; i < (tl + 15u) >> 4; i += kDocThreads) {
+        const uint32_t y0 = 16u * i, wd = y0 >> 5, b0 = y0 & 31u;
+        const uint32_t bw = bits[wd], pr = pref[wd];
+        uint32_t q[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t y = 4u * i + b;
-            if (y < tl) {
-                const uint32_t wd = y >> 5;
-                const uint32_t mask = (2u << (y & 31u)) - 1u;  // bits at or before y (y&31 = 31: all)
-                const uint32_t r = pref[wd] + (uint32_t)__popc(bits[wd] & mask) - 1u;
-                word |= (uint32_t)st[y + delta[r]] << (8u * b);
+        for (uint32_t b = 0; b < 16; ++b) {
+            if (y0 + b < tl) {
+                // the run of the last start at or before y (b0 + b = 31: the whole word)
+                const uint32_t r = pr + (uint32_t)__popc(bw & ((2u << (b0 + b)) - 1u)) - 1u;
+                q[b >> 2] |= (uint32_t)st[y0 + b + delta[r]] << (8u * (b & 3u));
             }
         }
-        out[i] = word;
+        out[i] = make_uint4(q[0], q[1], q[2], q[3]);
     }
     return true;
 }
@@ -1187,7 +1196,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
 __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
-    __shared__ uint32_t ndefer, flags, visited_lds, pruned_any, nbig;
+    __shared__ uint32_t ndefer, flags, visited_lds, pruned_any, nbig, qhead;
 #ifdef CRDT_HIP_PROBE
     __shared__ uint32_t probe_max, probe_sum;
 #endif
@@ -1196,19 +1205,18 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     const uint32_t t = threadIdx.x;
     const uint32_t base = a.doc_root[d];
     const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.rtotal) - base;
-    const uint32_t S = 2u * ((R + 7u) >> kDocLog2S);
+    const uint32_t S = 2u * ((R + 3u) >> kDocLog2S);
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
     uint16_t* ch = nx + a.rcap;
-    uint32_t* sval = reinterpret_cast<uint32_t*>(ch);
-    uint16_t* sptr = reinterpret_cast<uint16_t*>(sval + a.scap);
+    uint32_t* srec = reinterpret_cast<uint32_t*>(ch);  // splitter records, once ch is dead
     uint16_t* w = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(ch) + a.chbytes);
-    uint16_t* defer = w;
+    uint16_t* defer = w + a.rcap;
     uint32_t* D32 = dyn;
 #ifdef CRDT_HIP_PROBE
     // phase timestamps of one document (probe build, CRDT_HIP_PROBE=<doc>)
     const bool probe = a.probe && d == a.probe - 1u && t == 0;
-    uint64_t tp[11];
+    uint64_t tp[12];
     tp[0] = wall_clock64();
 #define PROBE(i) if (probe) tp[i] = wall_clock64()
 #else
@@ -1219,6 +1227,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         flags = 0;
         visited_lds = 0;
         pruned_any = 0;
+        qhead = kDocThreads;
 #ifdef CRDT_HIP_PROBE
         probe_max = probe_sum = 0;
 #endif
@@ -1251,6 +1260,16 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
                     else p = (uint16_t)lp;
                 }
                 nx[v] = p;
+                w[v] = (uint16_t)min(gw[j], 0xFFFFu);
+                if (gw[j] >= 0xFFFFu) {  // a run of 64 KiB or more: the LDS side table
+                    const uint32_t i = atomicAdd(&nbig, 1u);
+                    if (i < kDocBig) {
+                        bigv[i] = v;
+                        bigw[i] = gw[j];
+                    } else {
+                        atomicOr(&flags, 2u);  // that much text: the global path
+                    }
+                }
             }
             zw |= (gw[j] == 0u && v != 0u ? 1u : 0u) << j;
         }
@@ -1271,7 +1290,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // ---- pruning: a weightless leaf adds nothing to the document and is dropped from its
     // parent's children; a parent that loses its last child may go in the same pass (the
     // outcome depends on timing, never the text).  Repeated while it finds anything.
-    for (int round = 0; round < 3; ++round) {
+    for (int round = 0; round < 2; ++round) {
         uint32_t found = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
@@ -1367,6 +1386,10 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
                 }
             }
         }
+#ifdef CRDT_HIP_PROBE
+        __syncthreads();
+        PROBE(11);
+#endif
         // 3..8 children: Batcher's 19-comparator network (padding key 0 sorts last)
 #pragma unroll 1
         for (int j = 0; j < kDocJ; ++j) {
@@ -1439,14 +1462,9 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         if (t == 0) atomicOr(&a.ctl[C_ERR], (flags & 1u) ? 1u : 32u);
         return;
     }
-    // ---- first children (into D) and weights (into w) --------------------------------------
+    // ---- first children (into D) --------------------------------------------------------------
     {
-        uint32_t wr[kDocJ], fc[kDocJ];
-#pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t v = t + (uint32_t)j * kDocThreads;
-            wr[j] = v < R ? a.r_w[base + v] : 0u;
-        }
+        uint32_t fc[kDocJ];
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
@@ -1461,26 +1479,10 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            if (v < R) {
-                D[v] = (uint16_t)fc[j];
-                w[v] = (uint16_t)min(wr[j], 0xFFFFu);
-                if (wr[j] >= 0xFFFFu) {
-                    const uint32_t i = atomicAdd(&nbig, 1u);
-                    if (i < kDocBig) {
-                        bigv[i] = v;
-                        bigw[i] = wr[j];
-                    } else {
-                        atomicOr(&flags, 2u);  // that much text: the global path
-                    }
-                }
-            }
+            if (v < R) D[v] = (uint16_t)fc[j];
         }
     }
     __syncthreads();
-    if (flags) {
-        if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);
-        return;
-    }
     PROBE(6);
     // ---- walk 1: one walker per lane, splitters handed out by an LDS queue ----------------
     // A step at arc (v, up) reads fc, nx and w of v together.  Down arc: v's weight is added,
@@ -1493,6 +1495,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     uint32_t lane_steps = 0;
     {
         uint32_t s = t;
+        uint32_t s_next = atomicAdd(&qhead, 1u);  // the lane's next splitter, fetched ahead
         uint32_t V = (s >> 1) << kDocLog2S, U = s & 1u, SUM = 0, steps = 0;
         const uint32_t step_limit = 2u * R + S + 4u;
         while (s < S) {
@@ -1506,21 +1509,25 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             wt = dn ? wt : 0u;
             if (dn) {
                 // v's down arc is the last use of D[v] (first child) and w[v] (weight): they now
-                // hold v's offset inside this sublist (19 bits) and the sublist (13 bits)
-                const uint32_t pk = wt ? (SUM | (s << 19)) : 0xFFFFFFFFu;
+                // hold v's offset inside this sublist (18 bits) and the sublist (14 bits)
+                const uint32_t pk = wt ? (SUM | (s << 18)) : 0xFFFFFFFFu;
                 D[V] = (uint16_t)pk;
                 w[V] = (uint16_t)(pk >> 16);
             }
             SUM += wt;
             runs += dn ? 1u : 0u;
             uint32_t go = n;  // successor arc, encoded like nx
-            if (dn) go = f != kNil16 ? f : ((V & 7u) == 0 ? (V | kUp16) : n);
+            constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
+            // a leaf goes straight through its up arc to the successor, unless that up arc is
+            // itself a splitter
+            if (dn) go = f != kNil16 ? f : ((V & mm) == 0 ? (V | kUp16) : n);
             const bool end = dead || go == kNil16;
-            const bool split = !end && (go & 7u) == 0;
+            const bool split = !end && (go & mm) == 0;
             if (end || split) {
-                sval[s] = SUM;
-                sptr[s] = split ? (uint16_t)(2u * ((go & 0x7FFFu) >> kDocLog2S) + (go >> 15)) : kNil16;
-                s += kDocThreads;
+                srec[s] = (SUM << 14) |
+                          (split ? 2u * ((go & 0x7FFFu) >> kDocLog2S) + (go >> 15) : kNil14);
+                s = s_next;
+                s_next = atomicAdd(&qhead, 1u);
                 V = (s >> 1) << kDocLog2S;
                 U = s & 1u;
                 SUM = 0;
@@ -1544,32 +1551,25 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #endif
     __syncthreads();
     PROBE(7);
-    // ---- pointer jumping: sval = sum from the splitter to the end of the tour --------------
+    // ---- pointer jumping: record = (sum from the splitter to the end of the tour) << 14 | next
     for (uint32_t r = 1; r < S; r <<= 1) {
-        uint32_t nv[kDocK], np[kDocK];
+        uint32_t nr[kDocK];
 #pragma unroll
         for (int k = 0; k < kDocK; ++k) {
             const uint32_t s = t + (uint32_t)k * kDocThreads;
-            uint32_t v = 0, q = kNil16;
+            uint32_t x = 0;
             if (s < S) {
-                const uint32_t p = sptr[s];
-                v = sval[s];
-                if (p != kNil16) {
-                    v += sval[p];
-                    q = sptr[p];
-                }
+                x = srec[s];
+                const uint32_t p = x & kNil14;
+                if (p != kNil14) x = (x & ~kNil14) + srec[p];  // sums add, the link jumps
             }
-            nv[k] = v;
-            np[k] = q;
+            nr[k] = x;
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kDocK; ++k) {
             const uint32_t s = t + (uint32_t)k * kDocThreads;
-            if (s < S) {
-                sval[s] = nv[k];
-                sptr[s] = (uint16_t)np[k];
-            }
+            if (s < S) srec[s] = nr[k];
         }
         __syncthreads();
     }
@@ -1577,15 +1577,15 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // ---- run offsets: sublist offset (total - suffix of its splitter) + offset inside ------
     uint32_t ro[kDocJ];  // document offset of every owned run with visible bytes, else kNil
     {
-        const uint32_t total = sval[0];
+        const uint32_t total = srec[0] >> 14;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t pk = 0xFFFFFFFFu;
             if (v < R && !(pruned & (1u << j))) pk = (uint32_t)D[v] | ((uint32_t)w[v] << 16);
-            const uint32_t sid = pk >> 19;
+            const uint32_t sid = pk >> 18;
             // weightless, pruned (or never reached: flagged below)
-            ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x7FFFFu) + total - sval[sid] : kNil;
+            ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (srec[sid] >> 14) : kNil;
         }
         if (!a.text) {  // offsets for k_expand
 #pragma unroll
@@ -1611,10 +1611,11 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #ifdef CRDT_HIP_PROBE
     if (probe) {
         printf("[doctree] doc %u R %u S %u us: load %.1f count %.1f scan %.1f place %.1f "
-               "sort %.1f defer+fc %.1f walk1 %.1f jump %.1f offsets %.1f text %.1f | visited %u steps max %u "
+               "sort %.1f (pairs %.1f) defer+fc %.1f walk1 %.1f jump %.1f offsets %.1f text %.1f | visited %u steps max %u "
                "sum %u\n", d, R, S,
                (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
-               (tp[4] - tp[3]) / 100.0, (tp[5] - tp[4]) / 100.0, (tp[6] - tp[5]) / 100.0,
+               (tp[4] - tp[3]) / 100.0, (tp[5] - tp[4]) / 100.0, (tp[11] - tp[4]) / 100.0,
+               (tp[6] - tp[5]) / 100.0,
                (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0, (tp[9] - tp[8]) / 100.0,
                (tp[10] - tp[9]) / 100.0, visited_lds, probe_max, probe_sum);
     }
@@ -2154,11 +2155,11 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
 
     // Per-document LDS path when the largest document's run tree fits one workgroup.
     const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
-    const uint32_t scap = (2u * ((rmax + 7u) >> kDocLog2S) + 7u) & ~7u;
+    const uint32_t scap = ((2u * ((rmax + 3u) >> kDocLog2S)) + 7u) & ~7u;
     const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
-    // (sublist offsets are packed in 19 bits inside the walk: documents below 512 KiB of text)
+    // (sublist offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
     const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
-                      dbytes <= kDocLds && w.max_doc_text < (1ull << 19);
+                      dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
     // expansion + digest fused into k_doctree when every document's text fits LDS
     const bool fuse = lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
     // text staging + run-start bitvector (tl/8 + tl/16) + one u32 per run
