@@ -455,31 +455,69 @@ __device__ __forceinline__ uint32_t rank_incl(const uint64_t* hbits, const uint3
 }
 
 // Per run: weight (next run's prefix - own prefix) and parent run (rank lookup of the head's
-// parent item; the parent item is always the last item of its run).
+// parent item; the parent item is always the last item of its run; a head whose parent is the
+// slot before it has the previous run as parent).  kRunsPerThread runs per thread, every load of
+// a stage issued before any is used, so that enough gathers are in flight to cover HBM latency.
+constexpr int kRunsPerThread = 4;
 __global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uint32_t wtotal) {
-    const uint32_t rho = blockIdx.x * kBlock + threadIdx.x;
-    if (rho >= R) return;
-    const uint32_t h = a.r_head[rho];
-    const uint32_t ps = a.r_pstart[rho];
-    const uint32_t next = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
-    a.r_w[rho] = next - ps;
-    uint32_t pr = kNil;
-    uint64_t key = 0;
-    if ((a.seqb[h >> 4] >> (h & 15u)) & 1u) {
-        // the head's parent is the slot before it, the last slot of the previous run
-        pr = rho - 1u;
-        key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
-    } else {
-        const uint2 doc = a.docs[a.chunk_doc[h >> a.log2m]];
-        if (h != doc.x) {
-            uint32_t p = a.in_parent[h];
-            key = ((uint64_t)a.in_lamport[h] << 16) | (uint64_t)a.in_agent[h];
-            if (p > doc.y || p == h - doc.x) p = 0;  // flagged by k_classify
-            pr = rank_incl(a.hbits, a.hrank, doc.x + p) - 1u;
-        }
+    constexpr int K = kRunsPerThread;
+    const uint32_t r0 = blockIdx.x * (kBlock * K) + threadIdx.x;
+    uint32_t h[K], ps[K], nx[K], sq[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t rho = min(r0 + (uint32_t)k * kBlock, R - 1u);
+        h[k] = a.r_head[rho];
+        ps[k] = a.r_pstart[rho];
+        nx[k] = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
     }
-    a.r_parent[rho] = pr;
-    a.r_key[rho] = key;
+    uint32_t dx[K], dy[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        sq[k] = a.seqb[h[k] >> 4];
+        const uint2 doc = a.docs[a.chunk_doc[h[k] >> a.log2m]];
+        dx[k] = doc.x;
+        dy[k] = doc.y;
+    }
+    uint32_t lam[K], ag[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        lam[k] = a.in_lamport[h[k]];
+        ag[k] = a.in_agent[h[k]];
+    }
+    uint32_t ps_slot[K];  // parent slot of a non-seq head (0: none)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        sq[k] = (sq[k] >> (h[k] & 15u)) & 1u;
+        uint32_t p = (!sq[k] && h[k] != dx[k]) ? a.in_parent[h[k]] : 0u;
+        if (p > dy[k] || p == h[k] - dx[k]) p = 0;  // flagged by k_classify
+        ps_slot[k] = dx[k] + p;
+    }
+    uint64_t hb[K];
+    uint32_t hr[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {  // rank lookups (only non-seq heads use them)
+        hb[k] = a.hbits[ps_slot[k] >> 6];
+        hr[k] = a.hrank[ps_slot[k] >> 6];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t rho = r0 + (uint32_t)k * kBlock;
+        if (rho >= R) break;
+        uint32_t pr = kNil;
+        uint64_t key = 0;
+        if (sq[k]) {
+            pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
+            key = ((uint64_t)lam[k] << 16) | ag[k];
+        } else if (h[k] != dx[k]) {
+            const uint32_t b = ps_slot[k] & 63u;
+            const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
+            pr = hr[k] + (uint32_t)__popcll(hb[k] & mask) - 1u;
+            key = ((uint64_t)lam[k] << 16) | ag[k];
+        }
+        a.r_w[rho] = nx[k] - ps[k];
+        a.r_parent[rho] = pr;
+        a.r_key[rho] = key;
+    }
 }
 
 // Expansion, one wave per 64 consecutive runs.  Their bytes are contiguous in sbytes (runs are
@@ -2125,8 +2163,15 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.r_parent = r_parent_;
     a0.r_w = r_w_;
     a0.r_key = r_key_;
+    // Per-document LDS path when the largest document's run tree fits one workgroup.
+    const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
+    const uint32_t scap = ((2u * ((rmax + 3u) >> kDocLog2S)) + 7u) & ~7u;
+    const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
+    // (sublist offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
+    const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
+                      dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
     BEGIN(S_RPARENT);
-    k_run_parent<<<grid_for(R), kBlock, 0, s>>>(a0, R, wtotal);
+    k_run_parent<<<grid_for(R, kBlock * kRunsPerThread), kBlock, 0, s>>>(a0, R, wtotal);
     END(S_RPARENT);
 
     // ---- level 1: the tree of runs -------------------------------------------------------
@@ -2153,13 +2198,6 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     const uint32_t gR = grid_for(R), gS = grid_for(S);
     const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
 
-    // Per-document LDS path when the largest document's run tree fits one workgroup.
-    const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
-    const uint32_t scap = ((2u * ((rmax + 3u) >> kDocLog2S)) + 7u) & ~7u;
-    const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
-    // (sublist offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
-    const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
-                      dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
     // expansion + digest fused into k_doctree when every document's text fits LDS
     const bool fuse = lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
     // text staging + run-start bitvector (tl/8 + tl/16) + one u32 per run
