@@ -59,6 +59,23 @@ KERNEL_BYTES = {
 }
 
 
+# HBM bytes per item of each kernel from rocprofv3 PMC passes of this build (FETCH_SIZE x2 for
+# gfx950 wide reads + WRITE_SIZE, one pass each: tools/profile.sh + tools/pmc_summary.py).
+PMC_FILE = "profiles/pmc_per_item.json"
+STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs", "run_parent": "k_run_parent",
+                "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
+
+
+def measured_traffic(stage: str, items_per_launch: float):
+    """PMC-measured HBM bytes of one launch of the stage's main kernel, or None."""
+    try:
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            k = json.load(f)["kernels"][STAGE_KERNEL[stage]]
+        return (k["fetch_x2_per_item"] + k["write_per_item"]) * items_per_launch
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def expected_digests(golden_dig, docs: int) -> np.ndarray:
     """Document r of a replica batch is a copy of trace r % 4."""
     return np.array([golden_dig[d % len(golden_dig)] for d in range(docs)], np.uint64)
@@ -223,16 +240,17 @@ def main() -> int:
         return per_slot * slots + per_run * runs + per_text * text_bytes
 
     per_kernel = {k: {"ms": stage_ns[k] / 1e6, "launches": launches[k],
-                      "alg_gbps": alg_bytes(k) / stage_ns[k] if stage_ns[k] else 0.0}
+                      "alg_gbps": alg_bytes(k) / stage_ns[k] if stage_ns[k] and launches[k] else 0.0}
                   for k in stage_ns}
     dom = max(stage_ns, key=lambda k: stage_ns[k])
     dom_launch_ns = stage_ns[dom] / max(1, launches[dom])
     dom_bytes_per_launch = alg_bytes(dom) / max(1, launches[dom])
     achieved = dom_bytes_per_launch / dom_launch_ns  # bytes/ns == GB/s
+    traffic = measured_traffic(dom, items_per_gpu / max(1, launches[dom]))
     surv_per_item = sum(survivors) / sum(items)
     pipe_bytes = (PIPE_B_PER_ITEM + surv_per_item) * items_per_gpu
     pipe_gbps = pipe_bytes / kern_ns
-    real_bytes = sum(alg_bytes(k) for k in stage_ns)
+    real_bytes = sum(alg_bytes(k) for k in stage_ns if launches[k])
 
     if rank == 0:
         out = {
@@ -270,7 +288,8 @@ def main() -> int:
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": PMC_FILE if traffic is not None else None,
                 "alg_bytes_per_launch": dom_bytes_per_launch,
                 "launch_us": dom_launch_ns / 1e3,
             },
