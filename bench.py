@@ -137,6 +137,87 @@ def cpu_baseline(bases, patches, seconds: float, threads: int) -> dict:
                       "document per thread"}
 
 
+def side_workload(args) -> int:
+    """one document per GPU, resident in HBM, merged `steps`
+    times.  value = op-log items merged per second (every item is one insert op; config 2 also
+    reports patches/s).  Multi-GPU: replicas only (each rank merges its own copy)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    ctx = crdt_hip.Context(local)
+    ctx.set_param("level1", args.level1)
+    if args.splitter_stride:
+        ctx.set_param("splitter_stride", args.splitter_stride)
+    t_setup = time.perf_counter()
+    patches = None
+    if args.workload == "seph":
+        t = crdt_hip.Trace(os.path.join(ROOT, "traces", "seph-blog1.json.gz"))
+        lg = t.resolve().arrays()
+        patches = len(t)
+        with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
+            g = json.load(f)["seph-blog1"]
+        expect = (int(g["tree_digest"], 16), g["end_bytes"])
+        batch = ctx.batch([lg], replicas=1, relabel="none")
+        desc = "config 2: seph-blog1 anchor log, one document"
+    elif args.workload == "agents64":
+        n = args.items or 10_000_000
+        lg = crdt_hip.OpLog.synth_agents(n, 64, 0x5EED0001).arrays()
+        ref_text, ref_dig = ctx.merge(lg)  # host-view merge (PCIe incl.): the resident batch must agree
+        expect = (ref_dig, len(ref_text))
+        batch = ctx.batch([lg], replicas=1, relabel="none")
+        desc = f"config 4: 64-agent concurrent log, {n} items, seed 0x5EED0001"
+    else:
+        n = args.items or 1_000_000_000
+        batch = crdt_hip.Batch.synth_tree(ctx, n, 90, 50, 0x5EED0002)
+        expect = (None, crdt_hip.synth_tree_visible(n, 50, 0x5EED0002))
+        desc = f"config 5: one document of {n} items (p_chain 0.9, 50% tombstones), generated on device"
+    if rank == 0:
+        log(f"[bench] {desc}: {batch.items} items, setup {time.perf_counter() - t_setup:.1f} s")
+    for _ in range(args.warmup):
+        batch.merge()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        dig, lens, st = batch.merge()
+        stats.append(st)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ok = int(lens[0]) == expect[1] and (expect[0] is None or int(dig[0]) == expect[0])
+    stage_ns = {k: float(np.mean([x["stage_ns"][k] for x in stats])) for k in stats[0]["stage_ns"]}
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": batch.items * world / (el / args.steps), "unit": "items/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic" if patches is None else "trace",
+            "config": {"workload": desc, "items_per_gpu": batch.items, "runs": stats[0]["runs"],
+                       "parallelism": f"replicas x{world} (no data-path collective)"},
+            "kernels_ms": {k: v / 1e6 for k, v in stage_ns.items() if v > 2e4},
+            "device_ms_per_step": float(np.mean([x["total_ns"] for x in stats])) / 1e6,
+            "text_bytes": int(lens[0]), "digest": "%016x" % int(dig[0]), "digests_ok": ok,
+        }
+        if patches is not None:
+            out["patches_per_s"] = patches * world / (el / args.steps)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,7 +231,13 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="traces", choices=["traces", "seph", "agents64", "big1b"],
+                    help="traces: config 3 (headline); seph: config 2; agents64: config 4; "
+                         "big1b: config 5 (SURVEY.md §8(d))")
+    ap.add_argument("--items", type=int, default=0, help="items of the synthetic workloads")
     args = ap.parse_args()
+    if args.workload != "traces":
+        return side_workload(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

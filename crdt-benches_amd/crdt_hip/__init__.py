@@ -37,8 +37,8 @@ EXPORTS = [
     "crdt_hip_trace_load", "crdt_hip_trace_free", "crdt_hip_trace_len", "crdt_hip_trace_txns",
     "crdt_hip_trace_patch", "crdt_hip_trace_start_content", "crdt_hip_trace_end_content",
     "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_synth_agents",
-    "crdt_hip_synth_tree", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
-    "crdt_hip_batch_create", "crdt_hip_batch_free", "crdt_hip_batch_info",
+    "crdt_hip_synth_tree", "crdt_hip_synth_tree_visible", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
+    "crdt_hip_batch_create", "crdt_hip_batch_synth_tree", "crdt_hip_batch_free", "crdt_hip_batch_info",
     "crdt_hip_batch_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
     "crdt_hip_allgather_u64", "crdt_hip_comm_destroy", "crdt_hip_xxh64",
     "crdt_hip_tree_digest",
@@ -128,10 +128,12 @@ def lib() -> C.CDLL:
         "crdt_hip_trace_resolve": (i32, [vp, P(vp)]),
         "crdt_hip_synth_agents": (i32, [u32, u32, u64, P(vp)]),
         "crdt_hip_synth_tree": (i32, [u32, u32, u32, u64, P(vp)]),
+        "crdt_hip_synth_tree_visible": (i32, [u32, u32, u64, P(u64)]),
         "crdt_hip_merge": (i32, [vp, P(View), vp, sz, P(sz), P(u64)]),
         "crdt_hip_merge_batch": (i32, [vp, P(View), u32, vp, vp, P(Stats)]),
         "crdt_hip_merge_order": (i32, [vp, P(View), vp]),
         "crdt_hip_batch_create": (i32, [vp, P(View), u32, u32, u32, u64, P(vp)]),
+        "crdt_hip_batch_synth_tree": (i32, [vp, u32, u32, u32, u64, P(vp)]),
         "crdt_hip_batch_free": (i32, [vp]),
         "crdt_hip_batch_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_batch_merge": (i32, [vp, vp, vp, vp, P(Stats)]),
@@ -422,29 +424,49 @@ class Context:
         return out
 
 
+def synth_tree_visible(n_items: int, del_pct: int, seed: int) -> int:
+    """Visible items (= merged bytes) of OpLog.synth_tree(n_items, *, del_pct, seed)."""
+    out = C.c_uint64()
+    _check(lib().crdt_hip_synth_tree_visible(n_items, del_pct, seed, C.byref(out)))
+    return int(out.value)
+
+
 class Batch:
     """Device-resident replica batch (crdt_hip_batch_*)."""
 
     RELABEL = {"none": 0, "rotate": 1, "shuffle": 2}
 
-    def __init__(self, ctx: Context, bases: list, replicas: int, relabel=0, seed: int = 0):
-        if isinstance(relabel, str):
-            relabel = self.RELABEL[relabel]
-        views = []
-        keep = []
-        for b in bases:
-            v, k = _as_view(b)
-            views.append(v)
-            keep.append(k)
-        arr = (View * len(views))(*views)
-        h = C.c_void_p()
-        _check(lib().crdt_hip_batch_create(ctx._h, arr, len(views), replicas, relabel, seed,
-                                           C.byref(h)), ctx._h)
+    def __init__(self, ctx: Context, bases: list, replicas: int, relabel=0, seed: int = 0,
+                 _handle=None):
+        if _handle is not None:
+            h = _handle
+        else:
+            if isinstance(relabel, str):
+                relabel = self.RELABEL[relabel]
+            views = []
+            keep = []
+            for b in bases:
+                v, k = _as_view(b)
+                views.append(v)
+                keep.append(k)
+            arr = (View * len(views))(*views)
+            h = C.c_void_p()
+            _check(lib().crdt_hip_batch_create(ctx._h, arr, len(views), replicas, relabel, seed,
+                                               C.byref(h)), ctx._h)
         self._h = h
         self.ctx = ctx
         docs, items, dev = C.c_uint64(), C.c_uint64(), C.c_uint64()
         _check(lib().crdt_hip_batch_info(h, C.byref(docs), C.byref(items), C.byref(dev)))
         self.docs, self.items, self.device_bytes = int(docs.value), int(items.value), int(dev.value)
+
+    @classmethod
+    def synth_tree(cls, ctx: Context, n_items: int, p_chain_pct: int, del_pct: int,
+                   seed: int) -> "Batch":
+        """One config-5 document generated on the device (= OpLog.synth_tree, no host copy)."""
+        h = C.c_void_p()
+        _check(lib().crdt_hip_batch_synth_tree(ctx._h, n_items, p_chain_pct, del_pct, seed,
+                                               C.byref(h)), ctx._h)
+        return cls(ctx, [], 0, _handle=h)
 
     def close(self) -> None:
         if getattr(self, "_h", None) and _LIB is not None:

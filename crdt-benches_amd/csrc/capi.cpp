@@ -140,6 +140,7 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         uint32_t l = 0;
         while ((1ull << l) < value) ++l;
         ctx->eng.log2m = l;
+        ctx->eng.log2m_set = true;
         return 0;
     }
     if (k == "max_wave_slots") {
@@ -311,6 +312,10 @@ int crdt_hip_synth_agents(uint32_t n_items, uint32_t agents, uint64_t seed, crdt
         return 0;
     });
 }
+int crdt_hip_synth_tree_visible(uint32_t n_items, uint32_t del_pct, uint64_t seed, uint64_t* out) {
+    if (!out || del_pct > 100) return set_err(nullptr, CRDT_HIP_EINVAL, "bad arguments");
+    return guard(nullptr, [&] { *out = crdt::synth_tree_visible(n_items, del_pct, seed); return 0; });
+}
 int crdt_hip_synth_tree(uint32_t n_items, uint32_t p_chain_pct, uint32_t del_pct, uint64_t seed,
                         crdt_hip_oplog** out) {
     if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
@@ -388,6 +393,24 @@ int crdt_hip_batch_create(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* bases, u
         crdt_hip_batch* b = new crdt_hip_batch();
         b->ctx = ctx;
         rc = ctx->eng.replicate(ctx->staging, b->logs, replicas, relabel, seed);
+        if (rc) {
+            delete b;
+            return from_engine(ctx, rc);
+        }
+        b->device_bytes = b->logs.total_slots * 15 + (b->logs.total_slots >> b->logs.log2m) * 4;
+        *out = b;
+        return 0;
+    });
+}
+int crdt_hip_batch_synth_tree(crdt_hip_ctx* ctx, uint32_t n_items, uint32_t p_chain_pct,
+                              uint32_t del_pct, uint64_t seed, crdt_hip_batch** out) {
+    if (!ctx || !out || p_chain_pct > 100 || del_pct > 100)
+        return set_err(ctx, CRDT_HIP_EINVAL, "bad synth arguments");
+    *out = nullptr;
+    return guard(ctx, [&] {
+        crdt_hip_batch* b = new crdt_hip_batch();
+        b->ctx = ctx;
+        int rc = ctx->eng.synth_tree(b->logs, n_items, p_chain_pct, del_pct, seed);
         if (rc) {
             delete b;
             return from_engine(ctx, rc);

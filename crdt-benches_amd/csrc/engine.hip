@@ -618,6 +618,7 @@ struct TreeArgs {
     uint64_t* toff;
     uint32_t* loff;
     uint64_t* leafh;
+    uint64_t* ghash;  // group digests of documents above 16 MiB (indexed like leafh)
     uint64_t* dig;
     uint8_t* text;
     uint64_t text_cap;
@@ -1728,12 +1729,30 @@ __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_c
     a.leafh[L] = xxh64_aligned(a.text + a.toff[d] + (uint64_t)j * kLeaf, len, 0);
 }
 
+// Documents of more than kGroup leaves (16 MiB): leaf digests hashed in groups of kGroup (seed =
+// group index) by one thread per group, into ghash[loff[d] + k].
+constexpr uint32_t kGroup = 4096;
+__global__ __launch_bounds__(kBlock) void k_grouphash(TreeArgs a, uint32_t leaf_cap) {
+    const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
+    if (L >= leaf_cap || L >= a.loff[a.ndocs]) return;
+    uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.loff[mid] <= L) lo = mid; else hi = mid;
+    }
+    const uint32_t l0 = a.loff[lo], nl = a.loff[lo + 1] - l0, j = L - l0;
+    if (nl <= kGroup || j % kGroup) return;
+    a.ghash[l0 + j / kGroup] = xxh64_aligned(reinterpret_cast<const uint8_t*>(a.leafh + L),
+                                             min(kGroup, nl - j) * 8u, j / kGroup);
+}
+
 __global__ __launch_bounds__(kBlock) void k_docdigest(TreeArgs a) {
     const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
     if (d >= a.ndocs) return;
-    const uint32_t l0 = a.loff[d], l1 = a.loff[d + 1];
-    a.dig[d] = xxh64_aligned(reinterpret_cast<const uint8_t*>(a.leafh + l0), (l1 - l0) * 8u,
-                             a.tlen[d]);
+    const uint32_t l0 = a.loff[d], nl = a.loff[d + 1] - l0;
+    const uint64_t* h = nl > kGroup ? a.ghash + l0 : a.leafh + l0;
+    const uint32_t nh = nl > kGroup ? (nl + kGroup - 1) / kGroup : nl;
+    a.dig[d] = xxh64_aligned(reinterpret_cast<const uint8_t*>(h), nh * 8u, a.tlen[d]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1795,6 +1814,39 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
     rc[o] = bc[src + k];
 }
 
+// Config 5 generator, item by item on the device: exactly synth.cpp's synth_tree_item (the same
+// counter-based hashes), so a device batch equals the host log of the same seed.  Slot 0 is the
+// document start; padding slots are deleted, parentless.
+__global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ par,
+                                                        uint32_t* __restrict__ lam,
+                                                        uint16_t* __restrict__ ag,
+                                                        uint8_t* __restrict__ del,
+                                                        uint32_t* __restrict__ cp, uint32_t n,
+                                                        uint64_t nslots, uint32_t p_chain_pct,
+                                                        uint32_t del_pct, uint64_t seed) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= nslots) return;
+    const uint32_t i = (uint32_t)g;
+    uint32_t p = 0, l = 0, c = 0;
+    uint16_t a = 0;
+    uint8_t d = 1;
+    if (i >= 1 && i <= n) {
+        const uint64_t h0 = mix64(seed, i);
+        const uint64_t h1 = mix64(seed ^ 0xA5A5A5A5A5A5A5A5ULL, i);
+        const uint64_t h2 = mix64(seed ^ 0x5A5A5A5A5A5A5A5AULL, i);
+        p = (h0 % 100 < p_chain_pct) ? i - 1 : (uint32_t)(h1 % i);
+        d = (uint8_t)((h2 % 100) < del_pct);
+        c = 'a' + (uint32_t)((h2 >> 32) % 26);
+        l = i;
+        a = (uint16_t)(i % 64);
+    }
+    par[g] = p;
+    lam[g] = l;
+    ag[g] = a;
+    del[g] = d;
+    cp[g] = c;
+}
+
 template <class T>
 hipError_t dalloc(T** p, uint64_t count) {
     *p = nullptr;
@@ -1835,7 +1887,7 @@ Engine::~Engine() {
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(ctl_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
     dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
-    dfree(dig_); dfree(leafh_); dfree(text_);
+    dfree(dig_); dfree(leafh_); dfree(ghash_); dfree(text_);
     if (host_ctl_) (void)hipHostFree(host_ctl_);
     if (host_dig_) (void)hipHostFree(host_dig_);
     if (host_len_) (void)hipHostFree(host_len_);
@@ -2036,7 +2088,9 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     }
     if (w.leaf_cap + 1 > cap_leaves_) {
         dfree(leafh_);
+        dfree(ghash_);
         HIPCHK(dalloc(&leafh_, w.leaf_cap + 1), "hipMalloc leaf hashes");
+        HIPCHK(dalloc(&ghash_, w.leaf_cap + 1), "hipMalloc group hashes");
         cap_leaves_ = w.leaf_cap + 1;
     }
     if (ndocs_total > cap_host_docs_) {
@@ -2156,6 +2210,9 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     const uint32_t R = host_ctl_[C_RTOTAL];
     const uint32_t wtotal = host_ctl_[C_WTOTAL];
     const uint32_t rmax = host_ctl_[C_RMAX];
+    // global path splitter stride: longer sublists once the pointer jumping over the splitter
+    // lists dominates (measured on config 5: 182 M runs, stride 16 -> 64 took 72 -> 59 ms)
+    const uint32_t log2m = log2m_set ? this->log2m : (R > (1u << 24) ? 6u : 4u);
     const uint32_t Sreg = 2 * ((R + (1u << log2m) - 1) >> log2m);
     const uint32_t S = Sreg + w.ndocs;
     const int rc = ensure_runs(R, S);
@@ -2191,7 +2248,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a.deg = deg_; a.cstart = cstart_; a.child = child_; a.rec = rec_;
     a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;
     a.roff = roff_;
-    a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.dig = dig_;
+    a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; a.dig = dig_;
     a.text = text_;
     a.text_cap = ord ? w.order_cap : cap_text_ - 64;
     a.align = ord ? 1u : 16u;
@@ -2307,6 +2364,8 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     BEGIN(S_DIGEST);
     if (!ord) {
         k_leafhash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
+        if (w.max_doc_text > (uint64_t)kLeaf * kGroup)
+            k_grouphash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
         k_docdigest<<<grid_for(w.ndocs), kBlock, 0, s>>>(a);
     }
     END(S_DIGEST);
@@ -2320,7 +2379,9 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     HIPCHK(hipStreamSynchronize(s), "merge wave");
     const uint32_t g1 = lds1 ? 0u : 1u;
     const uint32_t launches[S_N] = {1, 6, 1, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
-                                    expand_run ? 1u : 0u, ord ? 0u : 2u, lds1 ? 2u : 0u};
+                                    expand_run ? 1u : 0u,
+                                    ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
+                                    lds1 ? 2u : 0u};
     for (int i = 0; i < S_N; ++i) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");
@@ -2396,6 +2457,20 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N + 1], ev_[2 * S_N + 2]), "event time");
         st->total_ns = (uint64_t)((double)tot * 1e6);
     }
+    return CRDT_HIP_OK;
+}
+
+int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t del_pct,
+                       uint64_t seed) {
+    std::vector<DocInfo> docs(1);
+    docs[0].n = n;
+    docs[0].text_cap = n;  // one byte per visible item at most ('a'..'z')
+    int rc = plan(R, docs);
+    if (rc) return rc;
+    k_synth_tree<<<grid_for(R.total_slots), kBlock, 0, stream>>>(
+        R.parent, R.lamport, R.agent, R.deleted, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
+    HIPCHK(hipGetLastError(), "synth launch");
+    HIPCHK(hipStreamSynchronize(stream), "synth");
     return CRDT_HIP_OK;
 }
 

@@ -63,6 +63,7 @@ public:
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t log2m = 4;                    // level-1 splitter stride M = 2^log2m
+    bool log2m_set = false;                // set by the caller; else chosen per wave from R
     uint64_t max_wave_slots = 1ull << 30;
     bool level1_global = false;            // never use the per-document LDS level 1
     std::string err;
@@ -82,6 +83,10 @@ public:
               std::vector<uint8_t>* text_out = nullptr,
               std::vector<uint64_t>* text_offsets = nullptr);
 
+    // One config-5 document generated on the device (synth.cpp synth_tree_item, item by item).
+    int synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t del_pct,
+                   uint64_t seed);
+
     // Materialise `replicas` relabelled copies of `bases` (already uploaded in B) into R.
     int replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,
                   uint64_t seed);
@@ -98,7 +103,7 @@ private:
     uint64_t cap_sbytes_ = 0;
     // per document
     uint32_t *doc_root_ = nullptr, *doc_p0_ = nullptr, *tlen_ = nullptr, *loff_ = nullptr;
-    uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr;
+    uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr, *ghash_ = nullptr;
     uint8_t* text_ = nullptr;
     uint8_t* doc_fused_ = nullptr;
     // level-1 scratch (per run / per splitter), grown on demand

@@ -1,6 +1,7 @@
 // synth.cpp — synthetic anchor op logs, splitmix64-seeded.
 #include <algorithm>
 #include <cmath>
+#include <thread>
 #include <vector>
 
 #include "oplog.hpp"
@@ -29,6 +30,23 @@ void synth_tree_item(uint64_t seed, uint32_t i, uint32_t p_chain_pct, uint32_t d
     par = (h0 % 100 < p_chain_pct) ? i - 1 : (uint32_t)(h1 % i);
     del = (uint8_t)((h2 % 100) < del_pct);
     c = 'a' + (uint32_t)((h2 >> 32) % 26);
+}
+
+uint64_t synth_tree_visible(uint32_t n, uint32_t del_pct, uint64_t seed) {
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<uint64_t> part(nt, 0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            uint64_t c = 0;
+            for (uint64_t i = 1 + t; i <= n; i += nt)
+                c += (mix64(seed ^ 0x5A5A5A5A5A5A5A5AULL, i) % 100) >= del_pct;
+            part[t] = c;
+        });
+    for (auto& x : th) x.join();
+    uint64_t v = 0;
+    for (uint64_t c : part) v += c;
+    return v;
 }
 
 OpLog* synth_tree(uint32_t n, uint32_t p_chain_pct, uint32_t del_pct, uint64_t seed) {

@@ -45,6 +45,13 @@ uint64_t tree_digest(const uint8_t* text, size_t len) {
         const size_t n = std::min(leaf, len - i * leaf);
         hs[i] = xxh64(text + i * leaf, n, 0);
     }
+    const size_t group = 4096;  // > 16 MiB: leaf digests hashed in groups of 4096 (seed = index)
+    if (hs.size() > group) {
+        std::vector<uint64_t> gs((hs.size() + group - 1) / group);
+        for (size_t k = 0; k < gs.size(); ++k)
+            gs[k] = xxh64(hs.data() + k * group, std::min(group, hs.size() - k * group) * 8, k);
+        hs.swap(gs);
+    }
     return xxh64(hs.data(), hs.size() * 8, (uint64_t)len);
 }
 

@@ -1,5 +1,6 @@
 // util.hpp — small host helpers shared by the engine's host code: UTF-8, xxh64, splitmix64.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
@@ -54,14 +55,14 @@ inline size_t utf8_count(const char* s, size_t n) {
     return c;
 }
 
-inline uint64_t splitmix64(uint64_t& state) {
+__host__ __device__ inline uint64_t splitmix64(uint64_t& state) {
     uint64_t z = (state += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
 // Counter-based variant (identical on host and device): hash of (seed, i).
-inline uint64_t mix64(uint64_t seed, uint64_t i) {
+__host__ __device__ inline uint64_t mix64(uint64_t seed, uint64_t i) {
     uint64_t s = seed ^ (i * 0xD1B54A32D192ED03ULL);
     return splitmix64(s);
 }

@@ -161,6 +161,8 @@ int crdt_hip_synth_agents(uint32_t n_items, uint32_t agents, uint64_t seed, crdt
  * [0, i-1]; deleted ~ Bernoulli(del_pct/100); cp = 'a' + h % 26; lamport = i; agent = i % 64. */
 int crdt_hip_synth_tree(uint32_t n_items, uint32_t p_chain_pct, uint32_t del_pct, uint64_t seed,
                         crdt_hip_oplog** out);
+/* Visible items (= merged bytes) of that log, counted without building it. */
+int crdt_hip_synth_tree_visible(uint32_t n_items, uint32_t del_pct, uint64_t seed, uint64_t* out);
 
 /* ---- merge (device) --------------------------------------------------------------------- */
 /* Merge one op log to its document: UTF-8 into out[0..cap), byte length in *out_len, tree
@@ -183,6 +185,10 @@ int crdt_hip_merge_order(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint
 int crdt_hip_batch_create(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* bases, uint32_t nbases,
                           uint32_t replicas, uint32_t relabel, uint64_t seed,
                           crdt_hip_batch** out);
+/* A one-document batch generated on the device: crdt_hip_synth_tree's log (same parameters,
+ * same items) without a host copy, for the 1 G-item config. */
+int crdt_hip_batch_synth_tree(crdt_hip_ctx* ctx, uint32_t n_items, uint32_t p_chain_pct,
+                              uint32_t del_pct, uint64_t seed, crdt_hip_batch** out);
 int crdt_hip_batch_free(crdt_hip_batch* b);
 int crdt_hip_batch_info(const crdt_hip_batch* b, uint64_t* docs, uint64_t* items,
                         uint64_t* device_bytes);

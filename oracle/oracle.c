@@ -92,7 +92,20 @@ uint64_t orc_tree_digest(const uint8_t* text, size_t len) {
         uint64_t h = orc_xxh64(text + i * LEAF, n, 0);
         for (int b = 0; b < 8; ++b) buf[i * 8 + b] = (uint8_t)(h >> (8 * b));
     }
-    uint64_t d = orc_xxh64(buf, nleaf * 8, (uint64_t)len);
+    /* more than 4096 leaves (16 MiB): the leaf digests are hashed in groups of 4096 (seed =
+     * group index) and the document digest is taken over the group digests */
+    const size_t GROUP = 4096;
+    size_t nd = nleaf;
+    if (nleaf > GROUP) {
+        size_t ngroup = (nleaf + GROUP - 1) / GROUP;
+        for (size_t k = 0; k < ngroup; ++k) {
+            size_t n = nleaf - k * GROUP < GROUP ? nleaf - k * GROUP : GROUP;
+            uint64_t h = orc_xxh64(buf + k * GROUP * 8, n * 8, (uint64_t)k);
+            for (int b = 0; b < 8; ++b) buf[k * 8 + b] = (uint8_t)(h >> (8 * b));
+        }
+        nd = ngroup;
+    }
+    uint64_t d = orc_xxh64(buf, nd * 8, (uint64_t)len);
     free(buf);
     return d;
 }

@@ -34,9 +34,15 @@ TRACES = ["automerge-paper", "rustcode", "sveltecomponent", "seph-blog1"]
 LEAF = 4096
 
 
+GROUP = 4096  # leaf digests per group (documents above 16 MiB hash their leaves in groups)
+
+
 def tree_digest(b: bytes) -> int:
     leaves = b"".join(xxhash.xxh64(b[i:i + LEAF]).intdigest().to_bytes(8, "little")
                       for i in range(0, len(b), LEAF))
+    if len(leaves) > 8 * GROUP:
+        leaves = b"".join(xxhash.xxh64(leaves[o:o + 8 * GROUP], seed=k).intdigest().to_bytes(8, "little")
+                          for k, o in enumerate(range(0, len(leaves), 8 * GROUP)))
     return xxhash.xxh64(leaves, seed=len(b)).intdigest()
 
 

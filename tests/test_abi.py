@@ -1,5 +1,6 @@
 """The C-ABI library loads and exports every symbol include/crdt_hip.h declares (CPU only)."""
 import ctypes as C
+import sys
 import os
 import re
 
@@ -59,3 +60,16 @@ def test_host_digest_helpers_match_oracle(oracle):
     assert crdt_hip.xxh64(data, 7) == oracle.xxh64(data, 7)
     assert crdt_hip.tree_digest(data) == oracle.tree_digest(data)
     assert crdt_hip.tree_digest(b"") == oracle.tree_digest(b"")
+
+
+def test_tree_digest_groups_above_16mib(oracle):
+    """Documents of more than 4096 leaves hash their leaf digests in groups of 4096: the host
+    library, the oracle and the pure-Python restatement (make_golden.py) agree."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import tree_digest as py_tree_digest
+    rng = np.random.default_rng(3)
+    for n in (4096 * 4096, 4096 * 4096 + 1, 20_000_003):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        d = crdt_hip.tree_digest(data)
+        assert d == oracle.tree_digest(data) == py_tree_digest(data), n

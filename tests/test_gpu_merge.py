@@ -264,3 +264,31 @@ def test_repeated_merges_are_deterministic(ctx):
     d0 = ctx.merge_digest(log)
     for _ in range(3):
         assert ctx.merge_digest(log) == d0
+
+
+@pytest.mark.parametrize("p_chain", [90, 0])
+def test_device_generated_config5_matches_host_log(ctx, oracle, p_chain):
+    """crdt_hip_batch_synth_tree generates on the device exactly OpLog.synth_tree's log: its
+    merge equals the oracle's merge of the host-generated log (same seed)."""
+    n = 1_000_000
+    b = crdt_hip.Batch.synth_tree(ctx, n, p_chain, 50, 0x5EED0002)
+    assert b.docs == 1 and b.items == n
+    dig, lens, _ = b.merge()
+    host = crdt_hip.OpLog.synth_tree(n, p_chain, 50, 0x5EED0002).arrays()
+    ref = oracle.merge(to_anchor(host))
+    assert int(lens[0]) == len(ref) == int(np.count_nonzero(host.deleted == 0))
+    assert int(dig[0]) == oracle.tree_digest(ref)
+
+
+def test_document_above_16mib_digest(ctx, oracle):
+    """20 MB of text (4,883 leaves > 4,096): the device hashes the leaf digests in groups."""
+    n = 20_000_000
+    par = np.arange(n, dtype=np.uint32)
+    par[::1000] = np.arange(0, n, 1000, dtype=np.uint32) // 2  # some branching
+    rng = np.random.default_rng(5)
+    log = crdt_hip.LogArrays(par, np.arange(1, n + 1, dtype=np.uint32), np.zeros(n, np.uint16),
+                             np.zeros(n, np.uint8), rng.integers(0x61, 0x7B, n).astype(np.uint32))
+    dig, lens = ctx.merge_batch([log])
+    ref = oracle.merge(to_anchor(log))
+    assert int(lens[0]) == len(ref) == n
+    assert int(dig[0]) == oracle.tree_digest(ref)
