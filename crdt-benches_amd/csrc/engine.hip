@@ -1124,11 +1124,12 @@ struct DocArgs {
 
 // LDS bytes of a document with up to rcap - 2 runs: D, nx, w (2 B/run each), the ch region,
 // which later holds the splitter records (4 B per splitter: sublist sum << 14 | next splitter),
-// and the list of sibling groups of 9..64 (at most one per 9 runs).
+// and the work list of sibling groups of two or more (at most one per two runs).
 __host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t scap) {
     return ((2u * rcap > 4u * scap ? 2u * rcap : 4u * scap) + 15u) & ~15u;
 }
-__host__ __device__ constexpr uint32_t doctree_defer_cap(uint32_t rcap) { return rcap / 8u + 8u; }
+// sibling groups of two or more: at most one per two runs
+__host__ __device__ constexpr uint32_t doctree_defer_cap(uint32_t rcap) { return rcap / 2u + 8u; }
 __host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap) {
     return 6ull * rcap + doctree_ch_bytes(rcap, scap) + 2ull * doctree_defer_cap(rcap);
 }
@@ -1235,7 +1236,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
 __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
-    __shared__ uint32_t ndefer, flags, visited_lds, pruned_any, nbig, qhead;
+    __shared__ uint32_t npair, nwide, flags, visited_lds, pruned_any, nbig, qhead;
 #ifdef CRDT_HIP_PROBE
     __shared__ uint32_t probe_max, probe_sum;
 #endif
@@ -1250,7 +1251,8 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     uint16_t* ch = nx + a.rcap;
     uint32_t* srec = reinterpret_cast<uint32_t*>(ch);  // splitter records, once ch is dead
     uint16_t* w = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(ch) + a.chbytes);
-    uint16_t* defer = w + a.rcap;
+    uint16_t* glist = w + a.rcap;  // sibling-group work list (pairs front, 3..64 back)
+    const uint32_t gcap = doctree_defer_cap(a.rcap);
     uint32_t* D32 = dyn;
 #ifdef CRDT_HIP_PROBE
     // phase timestamps of one document (probe build, CRDT_HIP_PROBE=<doc>)
@@ -1262,7 +1264,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #define PROBE(i) (void)0
 #endif
     if (t == 0) {
-        ndefer = 0;
+        npair = nwide = 0;
         flags = 0;
         visited_lds = 0;
         pruned_any = 0;
@@ -1381,103 +1383,101 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     __syncthreads();
     PROBE(4);
     // ---- sibling order + up-arc successors -------------------------------------------------
-    // nx[] is rewritten here: a child's entry is written only by the thread owning its parent.
-    // Groups of two (the common case) first, with every key load of the thread issued at once.
+    // nx[] is rewritten here: a child's entry is written only by whoever sorts its group.
+    // Single children are linked by their parent's owner; groups of 2 go to the front of an LDS
+    // work list and groups of 3..64 to its back, and the list is sorted in passes whose key
+    // loads are issued together: pairs (kPairs per thread at once), 3..8 (one register network
+    // per thread), 9..64 (one wave per group).  Wider groups hand the wave to the global path.
     if (t == 0) nx[0] = kNil16;
-    {
-        constexpr int H = kDocJ / 2;
-#pragma unroll 1
-        for (int h = 0; h < 2; ++h) {
-            uint32_t s0[H], cn[H], cc[H];
-            uint64_t k0[H], k1[H];
 #pragma unroll
-            for (int j = 0; j < H; ++j) {
-                const uint32_t p = t + (uint32_t)(h * H + j) * kDocThreads;
-                s0[j] = (p && p < R) ? D[p - 1] : 0u;
-                cn[j] = p < R ? D[p] - s0[j] : 0u;
-            }
-#pragma unroll
-            for (int j = 0; j < H; ++j) {
-                const uint32_t c0 = cn[j] ? ch[s0[j]] : 0u;
-                const uint32_t c1 = cn[j] == 2u ? ch[s0[j] + 1u] : 0u;
-                cc[j] = c0 | (c1 << 16);
-            }
-#pragma unroll
-            for (int j = 0; j < H; ++j) {
-                const bool two = cn[j] == 2u;
-                k0[j] = a.r_key[base + (two ? (cc[j] & 0xFFFFu) : 0u)];
-                k1[j] = a.r_key[base + (two ? (cc[j] >> 16) : 0u)];
-            }
-#pragma unroll
-            for (int j = 0; j < H; ++j) {
-                const uint32_t p = t + (uint32_t)(h * H + j) * kDocThreads;
-                const uint16_t up = (uint16_t)(p | kUp16);
-                const uint32_t c0 = cc[j] & 0xFFFFu, c1 = cc[j] >> 16;
-                if (cn[j] == 1u) {
-                    nx[c0] = up;
-                } else if (cn[j] == 2u) {
-                    const bool sw = ((k0[j] << 15) | c0) < ((k1[j] << 15) | c1);
-                    const uint32_t a0 = sw ? c1 : c0, a1 = sw ? c0 : c1;
-                    ch[s0[j]] = (uint16_t)a0;
-                    ch[s0[j] + 1u] = (uint16_t)a1;
-                    nx[a0] = (uint16_t)a1;
-                    nx[a1] = up;
-                }
-            }
-        }
-#ifdef CRDT_HIP_PROBE
-        __syncthreads();
-        PROBE(11);
-#endif
-        // 3..8 children: Batcher's 19-comparator network (padding key 0 sorts last)
-#pragma unroll 1
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t p = t + (uint32_t)j * kDocThreads;
-            if (p >= R) break;
-            const uint32_t b = p ? D[p - 1] : 0u, cnt = D[p] - b;
-            if (cnt <= 2u) continue;
-            if (cnt > 64u) {
-                atomicOr(&flags, 2u);  // wider sibling groups: the global path handles this wave
-                continue;
-            }
-            if (cnt > 8u) {
-                defer[atomicAdd(&ndefer, 1u)] = (uint16_t)p;
-                continue;
-            }
-            uint64_t k[8];
-            uint32_t c[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) c[i] = (uint32_t)i < cnt ? ch[b + i] : 0u;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) k[i] = (uint32_t)i < cnt ? doc_key(a, base, c[i]) : 0ull;
-            cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
-            cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
-            cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
-            cx(k[4], c[4], k[6], c[6]); cx(k[5], c[5], k[7], c[7]);
-            cx(k[1], c[1], k[2], c[2]); cx(k[5], c[5], k[6], c[6]);
-            cx(k[0], c[0], k[4], c[4]); cx(k[1], c[1], k[5], c[5]);
-            cx(k[2], c[2], k[6], c[6]); cx(k[3], c[3], k[7], c[7]);
-            cx(k[2], c[2], k[4], c[4]); cx(k[3], c[3], k[5], c[5]);
-            cx(k[1], c[1], k[2], c[2]); cx(k[3], c[3], k[4], c[4]); cx(k[5], c[5], k[6], c[6]);
-            const uint16_t up = (uint16_t)(p | kUp16);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                if ((uint32_t)i < cnt) {
-                    ch[b + i] = (uint16_t)c[i];
-                    nx[c[i]] = (uint32_t)i + 1 < cnt ? (uint16_t)c[i + 1 < 8 ? i + 1 : 7] : up;
-                }
-            }
+    for (int j = 0; j < kDocJ; ++j) {
+        const uint32_t p = t + (uint32_t)j * kDocThreads;
+        if (p < R) {
+            const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
+            if (cnt == 1u) nx[ch[s0]] = (uint16_t)(p | kUp16);
+            else if (cnt == 2u) glist[atomicAdd(&npair, 1u)] = (uint16_t)p;
+            else if (cnt > 64u) atomicOr(&flags, 2u);
+            else if (cnt > 2u) glist[gcap - 1u - atomicAdd(&nwide, 1u)] = (uint16_t)p;
         }
     }
     __syncthreads();
+    {
+        constexpr int kPairs = 8;
+        const uint32_t np = npair;
+        for (uint32_t i0 = 0; i0 < np; i0 += kPairs * kDocThreads) {
+            uint32_t s0[kPairs], cc[kPairs], pp[kPairs];
+            uint64_t k0[kPairs], k1[kPairs];
+#pragma unroll
+            for (int e = 0; e < kPairs; ++e) {
+                const uint32_t i = i0 + t + (uint32_t)e * kDocThreads;
+                const uint32_t p = i < np ? glist[i] : 0u;
+                pp[e] = i < np ? p : kNil;
+                s0[e] = p ? D[p - 1] : 0u;
+            }
+#pragma unroll
+            for (int e = 0; e < kPairs; ++e)
+                cc[e] = pp[e] != kNil ? ((uint32_t)ch[s0[e]] | ((uint32_t)ch[s0[e] + 1u] << 16)) : 0u;
+#pragma unroll
+            for (int e = 0; e < kPairs; ++e) {
+                k0[e] = a.r_key[base + (cc[e] & 0xFFFFu)];
+                k1[e] = a.r_key[base + (cc[e] >> 16)];
+            }
+#pragma unroll
+            for (int e = 0; e < kPairs; ++e) {
+                if (pp[e] == kNil) continue;
+                const uint32_t c0 = cc[e] & 0xFFFFu, c1 = cc[e] >> 16;
+                const bool sw = ((k0[e] << 15) | c0) < ((k1[e] << 15) | c1);
+                const uint32_t a0 = sw ? c1 : c0, a1 = sw ? c0 : c1;
+                ch[s0[e]] = (uint16_t)a0;
+                ch[s0[e] + 1u] = (uint16_t)a1;
+                nx[a0] = (uint16_t)a1;
+                nx[a1] = (uint16_t)(pp[e] | kUp16);
+            }
+        }
+    }
+#ifdef CRDT_HIP_PROBE
+    __syncthreads();
+    PROBE(11);
+#endif
+    // 3..8 children: Batcher's 19-comparator network (padding key 0 sorts last)
+    const uint32_t nw = nwide;
+    for (uint32_t i0 = 0; i0 < nw; i0 += kDocThreads) {
+        const uint32_t i = i0 + t;
+        const uint32_t p = i < nw ? glist[gcap - 1u - i] : 0u;
+        const uint32_t b = p ? D[p - 1] : 0u, cnt = i < nw ? D[p] - b : 0u;
+        if (cnt < 3u || cnt > 8u) continue;
+        uint64_t k[8];
+        uint32_t c[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) c[q] = (uint32_t)q < cnt ? ch[b + q] : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k[q] = (uint32_t)q < cnt ? doc_key(a, base, c[q]) : 0ull;
+        cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
+        cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
+        cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
+        cx(k[4], c[4], k[6], c[6]); cx(k[5], c[5], k[7], c[7]);
+        cx(k[1], c[1], k[2], c[2]); cx(k[5], c[5], k[6], c[6]);
+        cx(k[0], c[0], k[4], c[4]); cx(k[1], c[1], k[5], c[5]);
+        cx(k[2], c[2], k[6], c[6]); cx(k[3], c[3], k[7], c[7]);
+        cx(k[2], c[2], k[4], c[4]); cx(k[3], c[3], k[5], c[5]);
+        cx(k[1], c[1], k[2], c[2]); cx(k[3], c[3], k[4], c[4]); cx(k[5], c[5], k[6], c[6]);
+        const uint16_t up = (uint16_t)(p | kUp16);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if ((uint32_t)q < cnt) {
+                ch[b + q] = (uint16_t)c[q];
+                nx[c[q]] = (uint32_t)q + 1 < cnt ? (uint16_t)c[q + 1 < 8 ? q + 1 : 7] : up;
+            }
+        }
+    }
     PROBE(5);
     // 9..64 siblings: one wave per group, rank = #siblings with a greater key
     {
         const uint32_t lane = t & 63u, wv = t >> 6;
-        const uint32_t nd = ndefer;
-        for (uint32_t i = wv; i < nd; i += kDocThreads / 64) {
-            const uint32_t p = defer[i];
+        for (uint32_t i = wv; i < nw; i += kDocThreads / 64) {
+            const uint32_t p = glist[gcap - 1u - i];
             const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
+            if (cnt <= 8u) continue;  // wave-uniform
             const bool on = lane < cnt;
             const uint32_t c = on ? ch[s0 + lane] : 0u;
             const uint64_t k = on ? doc_key(a, base, c) : 0ull;
