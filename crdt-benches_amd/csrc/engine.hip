@@ -1087,14 +1087,16 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 //   w[v]   the deferred sort list during the sort, then the weight (0xFFFF: look it up in
 //          r_w), then, once walk 1 has passed v, the splitter whose sublist holds v (kNil16 for
 //          weightless runs)
-// Splitters are both arcs of the runs v with v % 4 == 0 (splitter 2(v/4) + up; a leaf's down
-// and up arcs are one step unless the up arc is a splitter).  A walker that passes v's down arc leaves
-// v's offset inside its sublist and the sublist's id in v's LDS entries, and once the splitter
-// list is ranked (pointer jumping) one pass turns them into document offsets.
+// Splitters are the down arcs of the runs v with v % 4 == 0 (splitter v / 4).  Up arcs carry no
+// weight and never split, so a leaf's down and up arcs are one step, and the climb out of a
+// finished subtree follows up links shortened by pointer jumping.  A walker that passes v's down
+// arc leaves v's offset inside its sublist and the sublist's id in v's LDS entries, and once the
+// splitter list is ranked (pointer jumping) one pass turns them into document offsets.
 constexpr int kDocThreads = 1024;
 constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
-constexpr int kDocK = 10;          // splitters per thread: 2 * ceil(20480 / 4) = 10 * 1024
-constexpr uint32_t kDocLog2S = 2;  // splitters: both arcs of the runs v % 4 == 0
+constexpr int kDocK = 5;           // splitters per thread: ceil(20480 / 4) = 5 * 1024
+constexpr int kUpJumps = 4;        // pointer-jumping rounds over last-child up links
+constexpr uint32_t kDocLog2S = 2;  // splitters: the down arcs of the runs v % 4 == 0
 constexpr uint32_t kDocLds = 163840 - 512;  // dynamic LDS budget (static arrays use the rest)
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
@@ -1245,7 +1247,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     const uint32_t t = threadIdx.x;
     const uint32_t base = a.doc_root[d];
     const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.rtotal) - base;
-    const uint32_t S = 2u * ((R + 3u) >> kDocLog2S);
+    const uint32_t S = (R + 3u) >> kDocLog2S;
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
     uint16_t* ch = nx + a.rcap;
@@ -1522,6 +1524,21 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         }
     }
     __syncthreads();
+    // ---- up links: a last child's up arc is followed by its parent's up arc (no weight, never a
+    // splitter), so nx[v] = UP(p) may be replaced by nx[p]; kUpJumps in-place pointer-jumping
+    // rounds shorten every climb out of a finished subtree 2^kUpJumps-fold (a concurrent reader
+    // sees an old or a new link: both are correct successors).
+    for (int r = 0; r < kUpJumps; ++r) {
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            if (v < R) {
+                const uint32_t x = nx[v];
+                if ((x & kUp16) && x < kDead16) nx[v] = nx[x & 0x7FFFu];
+            }
+        }
+        __syncthreads();
+    }
     PROBE(6);
     // ---- walk 1: one walker per lane, splitters handed out by an LDS queue ----------------
     // A step at arc (v, up) reads fc, nx and w of v together.  Down arc: v's weight is added,
@@ -1535,7 +1552,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     {
         uint32_t s = t;
         uint32_t s_next = atomicAdd(&qhead, 1u);  // the lane's next splitter, fetched ahead
-        uint32_t V = (s >> 1) << kDocLog2S, U = s & 1u, SUM = 0, steps = 0;
+        uint32_t V = s << kDocLog2S, U = 0, SUM = 0, steps = 0;
         const uint32_t step_limit = 2u * R + S + 4u;
         while (s < S) {
             const uint32_t f = D[V], n = nx[V], ww = w[V];
@@ -1555,20 +1572,17 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             }
             SUM += wt;
             runs += dn ? 1u : 0u;
-            uint32_t go = n;  // successor arc, encoded like nx
+            // successor arc, encoded like nx: a leaf goes straight on through its up arc
+            const uint32_t go = (dn && f != kNil16) ? f : n;
             constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
-            // a leaf goes straight through its up arc to the successor, unless that up arc is
-            // itself a splitter
-            if (dn) go = f != kNil16 ? f : ((V & mm) == 0 ? (V | kUp16) : n);
             const bool end = dead || go == kNil16;
-            const bool split = !end && (go & mm) == 0;
+            const bool split = !end && (go & (kUp16 | mm)) == 0;  // a splitter's down arc
             if (end || split) {
-                srec[s] = (SUM << 14) |
-                          (split ? 2u * ((go & 0x7FFFu) >> kDocLog2S) + (go >> 15) : kNil14);
+                srec[s] = (SUM << 14) | (split ? go >> kDocLog2S : kNil14);
                 s = s_next;
                 s_next = atomicAdd(&qhead, 1u);
-                V = (s >> 1) << kDocLog2S;
-                U = s & 1u;
+                V = s << kDocLog2S;
+                U = 0;
                 SUM = 0;
             } else {
                 V = go & 0x7FFFu;
@@ -2222,7 +2236,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.r_key = r_key_;
     // Per-document LDS path when the largest document's run tree fits one workgroup.
     const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
-    const uint32_t scap = ((2u * ((rmax + 3u) >> kDocLog2S)) + 7u) & ~7u;
+    const uint32_t scap = (((rmax + 3u) >> kDocLog2S) + 8u) & ~7u;
     const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
     // (sublist offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
     const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
