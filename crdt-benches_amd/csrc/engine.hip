@@ -361,33 +361,19 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
         }
 }
 
-// Moves a tile's UTF-8 (bytes [0, n) of its 16-byte-aligned stile segment) to sbytes + D.  The
-// dwords of sbytes wholly inside [D, D + n) belong to this tile alone and are written as
-// dwords (funnel-shifted from two source dwords); the partial dwords at either end are
-// shared with the neighbouring tiles and written bytewise.
-__device__ __forceinline__ void move_tile_text(const uint8_t* __restrict__ src, uint8_t* sbytes,
-                                               uint32_t D, uint32_t n) {
-    const uint32_t lo = (D + 3u) & ~3u, hi = (D + n) & ~3u;
-    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(sbytes);
-    const uint32_t sh = (lo - D) & 3u;  // source offset of an aligned destination dword, mod 4
-    for (uint32_t m = lo + 4u * threadIdx.x; m < hi; m += 4u * kBlock) {
-        const uint32_t o = m - D;  // source byte offset, o % 4 == sh
-        const uint32_t w0 = s32[o >> 2];
-        const uint32_t w1 = sh ? s32[(o >> 2) + 1] : 0u;
-        d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
-    }
-    if (threadIdx.x == 0)
-        for (uint32_t g = D; g < min(D + n, lo); ++g) sbytes[g] = src[g - D];
-    if (threadIdx.x == 1)
-        for (uint32_t g = max(hi, lo); g < D + n; ++g) sbytes[g] = src[g - D];
-}
-
 // k_runs: rank words, one record per run head (head slot, weight prefix), document starts, and
-// the tile's UTF-8 moved from its stile segment to its place in sbytes.
+// the tile's UTF-8 moved from its stile segment to its place in sbytes.  One packed scan,
+// heads << 16 | weight (a tile holds at most 4096 heads and 16,384 bytes).  The run records
+// are assembled in LDS (tile-local slot << 16 | tile-local weight prefix) and stored as
+// contiguous dword rows: storing them from the thread that found them costs one vector store
+// instruction per head position with lanes scattered over many lines, and the address unit,
+// not HBM, bounded the kernel.
 __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
-    __shared__ uint32_t lh[kBlock / 64], lw[kBlock / 64];
+    constexpr int NW = kBlock / 64;
+    __shared__ uint32_t lsum[NW];
+    __shared__ uint32_t rec[kScanTile];
     const uint32_t tile = blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
     uint32_t hm = 0;
     uint64_t nib = 0;
@@ -398,36 +384,71 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     }
     uint32_t W = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) W += (uint32_t)(nib >> (4 * k)) & 15u;
-    uint32_t th, tw;
-    const uint32_t rank = pre.x + block_excl_scan<kBlock / 64>((uint32_t)__popc(hm), lh, th);
-    uint32_t P = pre.y + block_excl_scan<kBlock / 64>(W, lw, tw);
-    if (a.mode == 0 && tw) {
-        if ((uint64_t)pre.y + tw > a.sbytes_cap) {  // more text than the host bound
-            if (threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 4u);
-        } else {
-            move_tile_text(a.stile + (uint64_t)tile * kTileBytes, a.sbytes, pre.y, tw);
+    for (int j = 0; j < 16; ++j) W += (uint32_t)(nib >> (4 * j)) & 15u;
+    const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane == 63u) lsum[wv] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const uint32_t v = lsum[i];
+        off += (i < (int)wv) ? v : 0u;
+        tot += v;
+    }
+    const uint32_t ex = off + inc - x;
+    const uint32_t nh = tot >> 16;
+    uint32_t tw = tot & 0xFFFFu;
+    if (a.mode == 0 && tw && (uint64_t)pre.y + tw > a.sbytes_cap) {  // more text than the host bound
+        if (threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 4u);
+        tw = 0;
+    }
+    // text: the dwords of sbytes wholly inside [D, D + tw) are this tile's alone (funnel-shifted
+    // from two source dwords); the partial dwords at either end are shared with the neighbouring
+    // tiles and written bytewise.  Loads first, records to LDS while they are in flight.
+    const uint32_t D = pre.y, lo = (D + 3u) & ~3u, hi = (D + tw) & ~3u, sh = (lo - D) & 3u;
+    const uint8_t* src = a.stile + (uint64_t)tile * kTileBytes;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t m = lo + 4u * threadIdx.x, w0 = 0, w1 = 0;
+    if (a.mode == 0 && m < hi) {
+        w0 = s32[(m - D) >> 2];
+        if (sh) w1 = s32[((m - D) >> 2) + 1];
+    }
+    {
+        uint32_t r = ex >> 16, p = ex & 0xFFFFu;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (hm & (1u << j)) rec[r++] = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p;
+            p += (uint32_t)(nib >> (4 * j)) & 15u;
         }
     }
-    if (gs >= a.nslots) return;
-    if ((threadIdx.x & 3u) == 0) a.hrank[gs >> 6] = rank;
-    if (!hm) return;
-    uint32_t r = rank;
+    if (gs < a.nslots && (threadIdx.x & 3u) == 0) a.hrank[gs >> 6] = pre.x + (ex >> 16);
     if ((hm & 1u) && (gs & 63u) == 0) {  // document starts are 64-aligned
         const uint32_t d = a.chunk_doc[gs >> a.log2m];
         if (a.docs[d].x == gs) {
-            a.doc_root[d] = r;
-            a.doc_p0[d] = P;
+            a.doc_root[d] = pre.x + (ex >> 16);
+            a.doc_p0[d] = pre.y + (ex & 0xFFFFu);
         }
     }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (hm & (1u << k)) {
-            a.r_head[r] = gs + k;
-            a.r_pstart[r] = P;
-            ++r;
+    if (a.mode == 0) {
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(a.sbytes);
+        if (m < hi) d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
+        for (m += 4u * kBlock; m < hi; m += 4u * kBlock) {
+            const uint32_t o = m - D;
+            const uint32_t v0 = s32[o >> 2], v1 = sh ? s32[(o >> 2) + 1] : 0u;
+            d32[m >> 2] = sh ? (uint32_t)((((uint64_t)v1 << 32) | v0) >> (8 * sh)) : v0;
         }
-        P += (uint32_t)(nib >> (4 * k)) & 15u;
+        if (tw && threadIdx.x == 0)
+            for (uint32_t g = D; g < min(D + tw, lo); ++g) a.sbytes[g] = src[g - D];
+        if (tw && threadIdx.x == 1)
+            for (uint32_t g = max(hi, lo); g < D + tw; ++g) a.sbytes[g] = src[g - D];
+    }
+    __syncthreads();
+    const uint32_t tbase = tile * kScanTile;
+    for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
+        const uint32_t v = rec[i];
+        a.r_head[pre.x + i] = tbase + (v >> 16);
+        a.r_pstart[pre.x + i] = pre.y + (v & 0xFFFFu);
     }
 }
 
@@ -1088,16 +1109,16 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 //          r_w), then, once walk 1 has passed v, the splitter whose sublist holds v (kNil16 for
 //          weightless runs)
 // Splitters are the down arcs of the runs v with v % 4 == 0 (splitter v / 4).  Up arcs carry no
-// weight and never split, so a leaf's down and up arcs are one step, and the climb out of a
-// finished subtree follows up links shortened by pointer jumping.  A walker that passes v's down
-// arc leaves v's offset inside its sublist and the sublist's id in v's LDS entries, and once the
-// splitter list is ranked (pointer jumping) one pass turns them into document offsets.
+// weight and never split: pointer jumping over the last-child up links until none is left makes
+// the tour a list of down arcs only (a leaf goes straight to the next sibling of its nearest
+// ancestor-or-self that has one).  A walker that passes v's down arc leaves v's offset inside its
+// sublist and the sublist's id in v's LDS entries, and once the splitter list is ranked (pointer
+// jumping) one pass turns them into document offsets.
 constexpr int kDocThreads = 1024;
 constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
 constexpr int kDocK = 5;           // splitters per thread: ceil(20480 / 4) = 5 * 1024
-constexpr int kUpJumps = 4;        // pointer-jumping rounds over last-child up links
 constexpr uint32_t kDocLog2S = 2;  // splitters: the down arcs of the runs v % 4 == 0
-constexpr uint32_t kDocLds = 163840 - 512;  // dynamic LDS budget (static arrays use the rest)
+constexpr uint32_t kDocLds = 163840 - 1024;  // dynamic LDS budget (static arrays use the rest)
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
 constexpr uint16_t kDead16 = 0xFFFEu;  // nx of a pruned run
@@ -1525,39 +1546,51 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     }
     __syncthreads();
     // ---- up links: a last child's up arc is followed by its parent's up arc (no weight, never a
-    // splitter), so nx[v] = UP(p) may be replaced by nx[p]; kUpJumps in-place pointer-jumping
-    // rounds shorten every climb out of a finished subtree 2^kUpJumps-fold (a concurrent reader
-    // sees an old or a new link: both are correct successors).
-    for (int r = 0; r < kUpJumps; ++r) {
+    // splitter), so nx[v] = UP(p) may be replaced by nx[p].  In-place pointer jumping until no up
+    // link is left: each thread keeps a bit per owned run still holding one and works only on
+    // those; a concurrent reader sees an old or a new link, both correct successors, so a round
+    // needs no barrier between its reads and writes, only the block-wide "anything left" test.
+    {
+        uint32_t act = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             if (v < R) {
                 const uint32_t x = nx[v];
-                if ((x & kUp16) && x < kDead16) nx[v] = nx[x & 0x7FFFu];
+                if ((x & kUp16) && x < kDead16) act |= 1u << j;
             }
         }
-        __syncthreads();
+        volatile uint16_t* vnx = nx;
+        while (__syncthreads_or(act != 0u)) {
+            for (uint32_t m = act; m; m &= m - 1u) {
+                const uint32_t j = (uint32_t)__ffs(m) - 1u;
+                const uint32_t v = t + j * kDocThreads;
+                const uint32_t y = vnx[vnx[v] & 0x7FFFu];  // an internal run: never dead
+                vnx[v] = (uint16_t)y;
+                if (!((y & kUp16) && y < kDead16)) act &= ~(1u << j);
+            }
+        }
     }
     PROBE(6);
     // ---- walk 1: one walker per lane, splitters handed out by an LDS queue ----------------
-    // A step at arc (v, up) reads fc, nx and w of v together.  Down arc: v's weight is added,
-    // v's offset inside the sublist goes to roff and v records its sublist in w; the walk goes
-    // to the first child, or, for a leaf, straight through v's up arc to its successor (unless
-    // that up arc is itself a splitter).  A lane whose sublist ends takes the next splitter, so
-    // the lanes stay busy until the queue runs dry.  The sublist results (sum, next splitter)
-    // go to the ch region, which no walker reads.
+    // A step at v's down arc reads fc, nx and w of v together: v's weight is added, v's offset
+    // inside the sublist and the sublist go to v's D and w entries, and the walk goes to the
+    // first child, or for a leaf to nx (a down arc, or the end of the tour).  A lane whose
+    // sublist ends takes the next splitter, so the lanes stay busy until the queue runs dry.
+    // The sublist results (sum, next splitter) go to the ch region, which no walker reads.
     uint32_t runs = 0;
     uint32_t lane_steps = 0;
+#ifdef CRDT_HIP_PROBE
+    const uint64_t wc0 = clock64();
+#endif
     {
         uint32_t s = t;
         uint32_t s_next = atomicAdd(&qhead, 1u);  // the lane's next splitter, fetched ahead
-        uint32_t V = s << kDocLog2S, U = 0, SUM = 0, steps = 0;
-        const uint32_t step_limit = 2u * R + S + 4u;
+        uint32_t V = s << kDocLog2S, SUM = 0, steps = 0;
+        const uint32_t step_limit = R + S + 4u;
         while (s < S) {
             const uint32_t f = D[V], n = nx[V], ww = w[V];
-            const bool dead = n == kDead16;
-            const bool dn = !U && !dead;
+            const bool dn = n != kDead16;  // a pruned run (only ever a splitter's own) ends it
             uint32_t wt = ww;
             if (dn && ww == 0xFFFFu)  // a run of 64 KiB or more: the LDS side table
                 for (uint32_t i = 0; i < nbig; ++i)
@@ -1572,21 +1605,19 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             }
             SUM += wt;
             runs += dn ? 1u : 0u;
-            // successor arc, encoded like nx: a leaf goes straight on through its up arc
-            const uint32_t go = (dn && f != kNil16) ? f : n;
+            // the next down arc: the first child, or for a leaf nx (kNil16 at the tour's end)
+            const uint32_t go = !dn ? kNil16 : (f != kNil16 ? f : n);
             constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
-            const bool end = dead || go == kNil16;
-            const bool split = !end && (go & (kUp16 | mm)) == 0;  // a splitter's down arc
+            const bool end = go == kNil16;
+            const bool split = !end && (go & mm) == 0;  // a splitter's down arc
             if (end || split) {
                 srec[s] = (SUM << 14) | (split ? go >> kDocLog2S : kNil14);
                 s = s_next;
                 s_next = atomicAdd(&qhead, 1u);
                 V = s << kDocLog2S;
-                U = 0;
                 SUM = 0;
             } else {
-                V = go & 0x7FFFu;
-                U = go >> 15;
+                V = go;
             }
             if (++steps > step_limit) {
                 atomicOr(&flags, 4u);
@@ -1598,6 +1629,11 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     (void)lane_steps;
 #ifdef CRDT_HIP_PROBE
     if (a.probe && d == a.probe - 1u) {
+        const uint64_t wc1 = clock64();
+        uint32_t wm = lane_steps;
+        for (int o = 32; o; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, o));
+        if ((t & 63u) == 0) printf("[walkwave] %u iters %u cycles %llu\n", t >> 6, wm,
+                                   (unsigned long long)(wc1 - wc0));
         atomicMax(&probe_max, lane_steps);
         atomicAdd(&probe_sum, lane_steps);
     }
