@@ -39,7 +39,9 @@ EXPORTS = [
     "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_synth_agents",
     "crdt_hip_synth_tree", "crdt_hip_synth_tree_visible", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
     "crdt_hip_batch_create", "crdt_hip_batch_synth_tree", "crdt_hip_batch_free", "crdt_hip_batch_info",
-    "crdt_hip_batch_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
+    "crdt_hip_batch_merge", "crdt_hip_replica_new", "crdt_hip_replica_clone",
+    "crdt_hip_replica_free", "crdt_hip_replica_apply_updates", "crdt_hip_replica_info",
+    "crdt_hip_replica_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
     "crdt_hip_allgather_u64", "crdt_hip_comm_destroy", "crdt_hip_xxh64",
     "crdt_hip_tree_digest",
 ]
@@ -137,6 +139,12 @@ def lib() -> C.CDLL:
         "crdt_hip_batch_free": (i32, [vp]),
         "crdt_hip_batch_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_batch_merge": (i32, [vp, vp, vp, vp, P(Stats)]),
+        "crdt_hip_replica_new": (i32, [vp, P(View), P(vp)]),
+        "crdt_hip_replica_clone": (i32, [vp, vp, P(vp)]),
+        "crdt_hip_replica_free": (i32, [vp]),
+        "crdt_hip_replica_apply_updates": (i32, [vp, vp, vp, sz, vp, u32]),
+        "crdt_hip_replica_info": (i32, [vp, P(u64), P(u64), P(u64)]),
+        "crdt_hip_replica_merge": (i32, [vp, vp, vp, sz, P(sz), P(u64)]),
         "crdt_hip_comm_unique_id": (i32, [vp]),
         "crdt_hip_comm_init": (i32, [vp, i32, i32, vp]),
         "crdt_hip_allgather_u64": (i32, [vp, vp, sz, vp]),
@@ -484,6 +492,82 @@ class Batch:
         return dig, lens, st.as_dict()
 
 
+def pack_updates(updates) -> tuple:
+    """Concatenate encoded updates: (bytes as np.uint8, n + 1 byte offsets as np.uint64)."""
+    lens = np.fromiter((len(u) for u in updates), np.uint64, count=len(updates))
+    offsets = np.zeros(len(updates) + 1, np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    buf = np.frombuffer(b"".join(updates), np.uint8) if updates else np.zeros(0, np.uint8)
+    return buf, offsets
+
+
+class Replica:
+    """Device-resident replica (crdt_hip_replica_*): Downstream on the device.
+
+    Updates (OpLog.encode_from's wire format) are decoded by the HIP kernels straight into the
+    replica's HBM slot arrays, a whole batch per call, and the replica is merged where it lies.
+    """
+
+    def __init__(self, ctx: Context, init=None, _handle=None):
+        if _handle is None:
+            h = C.c_void_p()
+            if init is None:
+                rc = lib().crdt_hip_replica_new(ctx._h, None, C.byref(h))
+            else:
+                v, keep = _as_view(init)
+                rc = lib().crdt_hip_replica_new(ctx._h, C.byref(v), C.byref(h))
+            _check(rc, ctx._h)
+            _handle = h
+        self._h = _handle
+        self.ctx = ctx
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_replica_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def clone(self) -> "Replica":
+        h = C.c_void_p()
+        _check(lib().crdt_hip_replica_clone(self.ctx._h, self._h, C.byref(h)), self.ctx._h)
+        return Replica(self.ctx, _handle=h)
+
+    def apply_packed(self, buf: np.ndarray, offsets: np.ndarray) -> None:
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        if n <= 0:
+            return
+        _check(lib().crdt_hip_replica_apply_updates(
+            self.ctx._h, self._h, buf.ctypes.data if buf.size else None, buf.size,
+            offsets.ctypes.data, n), self.ctx._h)
+
+    def apply_updates(self, updates) -> None:
+        self.apply_packed(*pack_updates(list(updates)))
+
+    def info(self) -> tuple:
+        """(items, visible codepoints, visible UTF-8 bytes)."""
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().crdt_hip_replica_info(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return int(a.value), int(b.value), int(c.value)
+
+    def merge(self) -> tuple:
+        """Merged document: (utf8 bytes, tree digest)."""
+        cap = self.info()[2] + 16
+        buf = C.create_string_buffer(cap)
+        n, dig = C.c_size_t(), C.c_uint64()
+        _check(lib().crdt_hip_replica_merge(self.ctx._h, self._h, buf, cap, C.byref(n),
+                                            C.byref(dig)), self.ctx._h)
+        return buf.raw[: n.value], int(dig.value)
+
+    def merge_digest(self) -> tuple:
+        n, dig = C.c_size_t(), C.c_uint64()
+        _check(lib().crdt_hip_replica_merge(self.ctx._h, self._h, None, 0, C.byref(n),
+                                            C.byref(dig)), self.ctx._h)
+        return int(n.value), int(dig.value)
+
+
 class HipMerge:
     """Mirror of the reference's per-CRDT adapter for the GPU engine.
 
@@ -546,3 +630,48 @@ class HipMerge:
 
     def apply_update(self, update: bytes) -> None:
         self.log.apply_update(update)
+
+
+class HipDownstream:
+    """`Downstream` (/root/reference/src/rope.rs:185-191) with the replica on the device.
+
+    apply_update() queues the encoded update on the host; len() decodes every queued update on
+    the device in one batch (crdt_hip_replica_apply_updates), merges the replica there and
+    returns its visible codepoints.  clone() copies the replica device to device.  This is the
+    shape of the Rust adapter in INTEGRATION.md.
+    """
+
+    NAME = "mi355x-device"
+    EDITS_USE_BYTE_OFFSETS = False
+
+    def __init__(self, replica: Replica):
+        self.replica = replica
+        self.pending: list = []
+
+    @classmethod
+    def upstream_updates(cls, start_content: str, patches) -> tuple:
+        up, updates = HipMerge.upstream_updates(start_content, patches)
+        ctx = HipMerge.context()
+        return cls(Replica(ctx, up.log if up.log.view().n else None)), updates
+
+    def clone(self) -> "HipDownstream":
+        c = HipDownstream(self.replica.clone())
+        c.pending = list(self.pending)
+        return c
+
+    def apply_update(self, update: bytes) -> None:
+        self.pending.append(update)
+
+    def flush(self) -> None:
+        if self.pending:
+            self.replica.apply_updates(self.pending)
+            self.pending = []
+
+    def text(self) -> str:
+        self.flush()
+        return self.replica.merge()[0].decode("utf-8")
+
+    def len(self) -> int:
+        self.flush()
+        self.replica.merge_digest()
+        return self.replica.info()[1]

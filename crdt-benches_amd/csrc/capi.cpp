@@ -12,6 +12,7 @@
 #include "crdt_hip.h"
 #include "engine.hpp"
 #include "oplog.hpp"
+#include "replica.hpp"
 #include "synth.hpp"
 #include "trace.hpp"
 #include "util.hpp"
@@ -33,6 +34,10 @@ struct crdt_hip_batch {
     crdt_hip_ctx* ctx = nullptr;
     crdt::DeviceLogs logs;
     uint64_t device_bytes = 0;
+};
+struct crdt_hip_replica {
+    crdt_hip_ctx* ctx = nullptr;
+    crdt::Replica r;
 };
 
 namespace {
@@ -438,6 +443,83 @@ int crdt_hip_batch_merge(crdt_hip_ctx* ctx, crdt_hip_batch* b, uint64_t* digests
     if (b->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "batch belongs to another context");
     return guard(ctx, [&] {
         return from_engine(ctx, ctx->eng.merge(b->logs, crdt::Engine::TEXT, digests, lens, stats));
+    });
+}
+
+// ---- device-resident replicas ----------------------------------------------------------------
+int crdt_hip_replica_new(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* init,
+                         crdt_hip_replica** out) {
+    if (!ctx || !out) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    *out = nullptr;
+    if (init) {
+        int rc = check_view(ctx, init);
+        if (rc) return rc;
+    }
+    return guard(ctx, [&] {
+        crdt_hip_replica* r = new crdt_hip_replica();
+        r->ctx = ctx;
+        int rc = crdt::replica_upload(ctx->eng, r->r, init);
+        if (rc) {
+            delete r;
+            return from_engine(ctx, rc);
+        }
+        *out = r;
+        return 0;
+    });
+}
+int crdt_hip_replica_clone(crdt_hip_ctx* ctx, const crdt_hip_replica* src,
+                           crdt_hip_replica** out) {
+    if (!ctx || !src || !out) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (src->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "replica belongs to another context");
+    *out = nullptr;
+    return guard(ctx, [&] {
+        crdt_hip_replica* r = new crdt_hip_replica();
+        r->ctx = ctx;
+        int rc = crdt::replica_copy(ctx->eng, src->r, r->r);
+        if (rc) {
+            delete r;
+            return from_engine(ctx, rc);
+        }
+        *out = r;
+        return 0;
+    });
+}
+int crdt_hip_replica_free(crdt_hip_replica* r) {
+    delete r;
+    return 0;
+}
+int crdt_hip_replica_apply_updates(crdt_hip_ctx* ctx, crdt_hip_replica* r, const uint8_t* buf,
+                                   size_t len, const uint64_t* offsets, uint32_t n) {
+    if (!ctx || !r) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (r->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "replica belongs to another context");
+    return guard(ctx, [&] {
+        return from_engine(ctx, crdt::replica_apply(ctx->eng, r->r, buf, len, offsets, n));
+    });
+}
+int crdt_hip_replica_info(const crdt_hip_replica* r, uint64_t* items,
+                          uint64_t* visible_codepoints, uint64_t* visible_bytes) {
+    if (!r) return set_err(nullptr, CRDT_HIP_EINVAL, "null replica");
+    if (items) *items = r->r.n;
+    if (visible_codepoints) *visible_codepoints = r->r.vis_cp;
+    if (visible_bytes) *visible_bytes = r->r.vis_bytes;
+    return 0;
+}
+int crdt_hip_replica_merge(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out, size_t cap,
+                           size_t* out_len, uint64_t* digest) {
+    if (!ctx || !r) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (r->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "replica belongs to another context");
+    return guard(ctx, [&] {
+        std::vector<uint8_t> text;
+        uint64_t len = 0, dig = 0;
+        int rc = crdt::replica_merge(ctx->eng, r->r, out ? &text : nullptr, &len, &dig, nullptr);
+        if (rc) return from_engine(ctx, rc);
+        if (out_len) *out_len = (size_t)len;
+        if (digest) *digest = dig;
+        if (out) {
+            if (cap < len) return set_err(ctx, CRDT_HIP_ESPACE, "output buffer too small");
+            if (len) std::memcpy(out, text.data(), (size_t)len);
+        }
+        return 0;
     });
 }
 

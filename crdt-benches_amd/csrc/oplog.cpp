@@ -11,8 +11,8 @@ namespace crdt {
 
 namespace {
 constexpr size_t kChunkMax = 512;
-constexpr uint32_t kMagic = 0x55445243u;  // "CRDU"
-constexpr uint32_t kWireVersion = 1;
+constexpr uint32_t kMagic = kUpdateMagic;
+constexpr uint32_t kWireVersion = kUpdateVersion;
 
 void put32(std::vector<uint8_t>& b, uint32_t v) {
     for (int i = 0; i < 4; ++i) b.push_back((uint8_t)(v >> (8 * i)));

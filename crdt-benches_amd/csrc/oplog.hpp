@@ -16,6 +16,10 @@
 
 namespace crdt {
 
+// Update wire format (OpLog::encode_from / apply_update, decoded on the device by replica.hip).
+constexpr uint32_t kUpdateMagic = 0x55445243u;  // "CRDU"
+constexpr uint32_t kUpdateVersion = 1;
+
 class OpLog {
 public:
     // ---- SoA (index k holds item id k+1) ----

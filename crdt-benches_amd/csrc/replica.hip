@@ -1,0 +1,509 @@
+// replica.hip — device-side decode of Downstream updates into a resident replica (replica.hpp).
+//
+// Replaces diamond-types' decode_and_add (/root/reference/src/rope.rs:222-224) with the
+// semantics of OpLog::apply_update (oplog.cpp), for a whole batch of updates per call:
+//   k_upd_parse  one thread per update: header checks -> {first id, items, deletes, data
+//                word offset}; per-256-update aggregates (items, deletes, largest last id)
+//   k_upd_top    one workgroup: exclusive scan of the aggregates, seeded with the replica's
+//                size (ids known before the batch)
+//   k_upd_scan   per update: item and delete offsets in the flattened batch, ids known before
+//                and after it (prefix max of last ids), causal readiness (first <= known + 1)
+//   k_upd_items  per flattened item, 4 per thread: parent check; in the write pass the item's
+//                fields go to slot id.  Ids known before the update are skipped, so the first
+//                update carrying an id wins, exactly as in the sequential decoder
+//   k_upd_dels   per flattened delete: target check; in the write pass the tombstone byte is
+//                set by a word atomicOr, so a target deleted twice is counted once
+// The check passes run before the write passes on the same stream and the write passes do
+// nothing once any check failed: a rejected batch leaves the replica unchanged, and the host
+// waits once per batch.  Visible codepoints / bytes are kept incrementally from the items
+// written and the tombstones newly set.
+#include "replica.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "oplog.hpp"
+#include "util.hpp"
+#include "wave.hpp"
+
+namespace crdt {
+namespace {
+
+constexpr int kUB = 256;            // threads per block (updates per block in parse / scan)
+constexpr int kItemsPerThread = 4;
+constexpr uint32_t kCpMaskR = 0x001FFFFFu;
+constexpr uint32_t kMaxGrid = 4096;
+
+// device counters (u64)
+enum UCtl { U_ERR = 0, U_ITEMS, U_DELS, U_MAXID, U_ADD_CP, U_ADD_B, U_DEL_CP, U_DEL_B, U_N };
+// U_ERR bits
+constexpr uint64_t E_HEADER = 1, E_NOT_READY = 2, E_PARENT = 4, E_DELETE = 8, E_BOUNDS = 16;
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= (uint32_t)o) x = max(x, y);
+    }
+    return x;
+}
+// Exclusive max-scan over the block (identity 0); `total` = block max.
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_max(uint32_t x, uint32_t* lds, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_max(x);
+    if (lane == 63u) lds[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const uint32_t t = lds[i];
+        off = (i < (int)w) ? max(off, t) : off;
+        tot = max(tot, t);
+    }
+    __syncthreads();
+    total = tot;
+    const uint32_t prev = (uint32_t)__shfl_up((int)inc, 1);
+    return max(off, lane ? prev : 0u);
+}
+
+struct UpdArgs {
+    const uint32_t* buf;  // the batch, as words (every update starts 4-aligned)
+    const uint64_t* off;  // n + 1 byte offsets
+    uint32_t n;
+    uint64_t len;
+    uint4* hdr;
+    uint4* scan;
+    uint4* blk;
+    uint32_t nblk;
+    uint32_t known0;  // items of the replica before the batch
+    uint64_t* ctl;
+    // replica slot arrays (slot = id)
+    uint32_t* parent;
+    uint32_t* lamport;
+    uint16_t* agent;
+    uint8_t* deleted;
+    uint32_t* cp;
+    uint64_t cap_slots;
+};
+
+__global__ __launch_bounds__(kUB) void k_upd_parse(UpdArgs a) {
+    __shared__ uint32_t l0[kUB / 64], l1[kUB / 64], l2[kUB / 64];
+    const uint32_t u = blockIdx.x * kUB + threadIdx.x;
+    uint32_t first = 1, nit = 0, m = 0, wo = 0;
+    if (u < a.n) {
+        const uint64_t o0 = a.off[u], o1 = a.off[u + 1];
+        bool bad = o0 > o1 || o1 > a.len || (o0 & 3u) || o1 - o0 < 24;
+        if (!bad) {
+            const uint32_t* h = a.buf + (o0 >> 2);
+            const uint32_t h0 = h[0], h1 = h[1], f = h[2], ni = h[3], mm = h[5];
+            const uint64_t need =
+                24ull + 16ull * ni + ((2ull * ni + 3ull) / 4ull) * 4ull + 4ull * mm;
+            bad = h0 != kUpdateMagic || h1 != kUpdateVersion || need > o1 - o0;
+            if (!bad) {
+                first = f;
+                nit = ni;
+                m = mm;
+                wo = (uint32_t)(o0 >> 2) + 6u;
+            }
+        }
+        if (bad) atomicOr((unsigned long long*)&a.ctl[U_ERR], (unsigned long long)E_HEADER);
+        a.hdr[u] = make_uint4(first, nit, m, wo);
+    }
+    // per-block aggregates: items, deletes, largest last id (first + items - 1)
+    const uint32_t last = nit ? first + nit - 1u : 0u;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t s0 = wave_sum(nit), s1 = wave_sum(m), s2 = wave_max(last);
+    if (lane == 0) {
+        l0[w] = s0;
+        l1[w] = s1;
+        l2[w] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t0 = 0, t1 = 0, t2 = 0;
+        for (int i = 0; i < kUB / 64; ++i) {
+            t0 += l0[i];
+            t1 += l1[i];
+            t2 = max(t2, l2[i]);
+        }
+        a.blk[blockIdx.x] = make_uint4(t0, t1, t2, 0u);
+    }
+}
+
+// One workgroup: block aggregates -> exclusive prefixes (max seeded with known0), totals.
+__global__ __launch_bounds__(1024) void k_upd_top(UpdArgs a) {
+    __shared__ uint32_t l0[16], l1[16], l2[16];
+    uint32_t c0 = 0, c1 = 0, c2 = a.known0;
+    for (uint32_t base = 0; base < a.nblk; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint4 v = i < a.nblk ? a.blk[i] : make_uint4(0, 0, 0, 0);
+        uint32_t t0, t1, t2;
+        const uint32_t e0 = block_excl_scan<16>(v.x, l0, t0);
+        const uint32_t e1 = block_excl_scan<16>(v.y, l1, t1);
+        const uint32_t e2 = block_excl_max<16>(v.z, l2, t2);
+        if (i < a.nblk) a.blk[i] = make_uint4(c0 + e0, c1 + e1, max(c2, e2), 0u);
+        c0 += t0;
+        c1 += t1;
+        c2 = max(c2, t2);
+    }
+    if (threadIdx.x == 0) {
+        a.ctl[U_ITEMS] = c0;
+        a.ctl[U_DELS] = c1;
+        a.ctl[U_MAXID] = c2;
+    }
+}
+
+__global__ __launch_bounds__(kUB) void k_upd_scan(UpdArgs a) {
+    __shared__ uint32_t l0[kUB / 64], l1[kUB / 64], l2[kUB / 64];
+    const uint32_t u = blockIdx.x * kUB + threadIdx.x;
+    const uint4 h = u < a.n ? a.hdr[u] : make_uint4(1, 0, 0, 0);
+    const uint32_t last = h.y ? h.x + h.y - 1u : 0u;
+    uint32_t t;
+    const uint32_t e0 = block_excl_scan<kUB / 64>(h.y, l0, t);
+    const uint32_t e1 = block_excl_scan<kUB / 64>(h.z, l1, t);
+    const uint32_t e2 = block_excl_max<kUB / 64>(last, l2, t);
+    if (u >= a.n) return;
+    const uint4 b = a.blk[blockIdx.x];
+    const uint32_t kb = max(b.z, e2);  // ids known before update u
+    const uint32_t ka = max(kb, last);
+    if (h.x == 0 || (uint64_t)h.x > (uint64_t)kb + 1u)
+        atomicOr((unsigned long long*)&a.ctl[U_ERR], (unsigned long long)E_NOT_READY);
+    a.scan[u] = make_uint4(b.x + e0, b.y + e1, kb, ka);
+}
+
+// last update u with scan[u].<field> <= j (scan[0].<field> == 0 <= j)
+template <int F>
+__device__ __forceinline__ uint32_t find_update(const uint4* __restrict__ scan, uint32_t n,
+                                                uint32_t j) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint4 s = scan[mid];
+        if ((F == 0 ? s.x : s.y) <= j) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
+    if (WRITE && a.ctl[U_ERR]) return;
+    const uint32_t T = (uint32_t)a.ctl[U_ITEMS];
+    uint32_t add_cp = 0, add_b = 0;
+    uint64_t err = 0;
+    const uint32_t stride = gridDim.x * kUB * kItemsPerThread;
+    for (uint32_t j0 = (blockIdx.x * kUB + threadIdx.x) * kItemsPerThread; j0 < T; j0 += stride) {
+        uint32_t u = find_update<0>(a.scan, a.n, j0);
+        uint4 h = a.hdr[u], s = a.scan[u];
+#pragma unroll
+        for (int q = 0; q < kItemsPerThread; ++q) {
+            const uint32_t j = j0 + (uint32_t)q;
+            if (j >= T) break;
+            while (j >= s.x + h.y) {  // next update holding items
+                ++u;
+                h = a.hdr[u];
+                s = a.scan[u];
+            }
+            const uint32_t k = j - s.x, id = h.x + k;
+            if (id <= s.z) continue;  // already known (decode_and_add is idempotent)
+            const uint32_t par = a.buf[h.w + k];
+            if (par != 0u && par >= id) {
+                err |= E_PARENT;
+                continue;
+            }
+            if (WRITE) {
+                if ((uint64_t)id >= a.cap_slots) {
+                    err |= E_BOUNDS;
+                    continue;
+                }
+                const uint32_t c = a.buf[h.w + 3u * h.y + k];
+                a.parent[id] = par;
+                a.lamport[id] = a.buf[h.w + 2u * h.y + k];
+                a.cp[id] = c;
+                a.agent[id] = reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
+                a.deleted[id] = 0;
+                add_cp += 1u;
+                add_b += utf8_len(c & kCpMaskR);
+            }
+        }
+    }
+    if (err) atomicOr((unsigned long long*)&a.ctl[U_ERR], (unsigned long long)err);
+    if (WRITE) {
+        const uint32_t s0 = wave_sum(add_cp), s1 = wave_sum(add_b);
+        if ((threadIdx.x & 63u) == 0 && s0) {
+            atomicAdd((unsigned long long*)&a.ctl[U_ADD_CP], (unsigned long long)s0);
+            atomicAdd((unsigned long long*)&a.ctl[U_ADD_B], (unsigned long long)s1);
+        }
+    }
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
+    if (WRITE && a.ctl[U_ERR]) return;
+    const uint32_t Dm = (uint32_t)a.ctl[U_DELS];
+    uint32_t del_cp = 0, del_b = 0;
+    uint64_t err = 0;
+    for (uint32_t j = blockIdx.x * kUB + threadIdx.x; j < Dm; j += gridDim.x * kUB) {
+        const uint32_t u = find_update<1>(a.scan, a.n, j);
+        const uint4 h = a.hdr[u], s = a.scan[u];
+        const uint32_t dw = h.w + 4u * h.y + (2u * h.y + 3u) / 4u;
+        const uint32_t id = a.buf[dw + (j - s.y)];
+        if (id == 0u || id > s.w) {  // unknown item (s.w = ids known after update u)
+            err |= E_DELETE;
+            continue;
+        }
+        if (WRITE) {
+            const uint32_t sh = 8u * (id & 3u);
+            const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(a.deleted) + (id >> 2), 1u << sh);
+            if (((old >> sh) & 0xFFu) == 0u) {  // newly tombstoned
+                del_cp += 1u;
+                del_b += utf8_len(a.cp[id] & kCpMaskR);
+            }
+        }
+    }
+    if (err) atomicOr((unsigned long long*)&a.ctl[U_ERR], (unsigned long long)err);
+    if (WRITE) {
+        const uint32_t s0 = wave_sum(del_cp), s1 = wave_sum(del_b);
+        if ((threadIdx.x & 63u) == 0 && s0) {
+            atomicAdd((unsigned long long*)&a.ctl[U_DEL_CP], (unsigned long long)s0);
+            atomicAdd((unsigned long long*)&a.ctl[U_DEL_B], (unsigned long long)s1);
+        }
+    }
+}
+
+// padding / unused slots: a tombstoned child of the document start with key 0 (never visible,
+// pruned by the merge)
+__global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint32_t* lamport,
+                                                 uint16_t* agent, uint8_t* deleted, uint32_t* cp,
+                                                 uint64_t s0, uint64_t s1) {
+    const uint64_t g = s0 + (uint64_t)blockIdx.x * kUB + threadIdx.x;
+    if (g >= s1) return;
+    parent[g] = 0;
+    lamport[g] = 0;
+    agent[g] = 0;
+    deleted[g] = 1;
+    cp[g] = 0;
+}
+
+int hip_fail(Engine& E, const char* what, hipError_t e) {
+    E.err = std::string(what) + ": " + hipGetErrorString(e);
+    (void)hipGetLastError();
+    return CRDT_HIP_EDEVICE;
+}
+
+#define RCHK(expr, what)                                \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(E, what, _e); \
+    } while (0)
+
+template <class T>
+hipError_t grow(T** p, uint64_t& cap, uint64_t need) {
+    if (need <= cap) return hipSuccess;
+    dfree(*p);
+    cap = 0;
+    hipError_t e = dalloc(p, need);
+    if (e == hipSuccess) cap = need;
+    return e;
+}
+
+}  // namespace
+
+Replica::~Replica() {
+    dfree(ubuf);
+    dfree(uoff);
+    dfree(uhdr);
+    dfree(uscan);
+    dfree(ublk);
+    dfree(uctl);
+    if (hctl) (void)hipHostFree(hctl);
+}
+
+int replica_reserve(Engine& E, Replica& r, uint64_t items) {
+    DeviceLogs& L = r.logs;
+    const uint64_t need = (items + 1 + 63) / 64 * 64;
+    if (need > (1ull << 31) - 64) {
+        E.err = "replica too large (ids are u32 slots of one wave)";
+        return CRDT_HIP_ERANGE;
+    }
+    if (need <= L.cap_slots) return CRDT_HIP_OK;
+    const uint64_t cap = std::min<uint64_t>((1ull << 31) - 64,
+                                            std::max<uint64_t>({need, 2 * L.cap_slots, 4096}));
+    uint32_t *par = nullptr, *lam = nullptr, *c = nullptr;
+    uint16_t* ag = nullptr;
+    uint8_t* del = nullptr;
+    hipError_t e = dalloc(&par, cap);
+    if (e == hipSuccess) e = dalloc(&lam, cap);
+    if (e == hipSuccess) e = dalloc(&ag, cap);
+    if (e == hipSuccess) e = dalloc(&del, cap);
+    if (e == hipSuccess) e = dalloc(&c, cap);
+    const uint64_t old = L.cap_slots;
+    hipStream_t s = E.stream;
+    if (e == hipSuccess && old) {
+        e = hipMemcpyAsync(par, L.parent, old * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(lam, L.lamport, old * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(ag, L.agent, old * 2, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(del, L.deleted, old, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(c, L.cp, old * 4, hipMemcpyDeviceToDevice, s);
+    }
+    if (e == hipSuccess) {
+        k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, lam, ag, del, c, old, cap);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        dfree(par); dfree(lam); dfree(ag); dfree(del); dfree(c);
+        return hip_fail(E, "replica reserve", e);
+    }
+    dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.deleted); dfree(L.cp);
+    L.parent = par;
+    L.lamport = lam;
+    L.agent = ag;
+    L.deleted = del;
+    L.cp = c;
+    L.cap_slots = cap;
+    return CRDT_HIP_OK;
+}
+
+int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
+    RCHK(hipSetDevice(E.device), "hipSetDevice");
+    const uint32_t n = v ? v->n : 0u;
+    int rc = replica_reserve(E, r, n);
+    if (rc) return rc;
+    r.n = n;
+    r.vis_cp = r.vis_bytes = 0;
+    if (!n) return CRDT_HIP_OK;
+    DeviceLogs& L = r.logs;
+    RCHK(hipMemcpy(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice), "upload parent");
+    RCHK(hipMemcpy(L.lamport + 1, v->lamport, n * 4ull, hipMemcpyHostToDevice), "upload lamport");
+    RCHK(hipMemcpy(L.agent + 1, v->agent, n * 2ull, hipMemcpyHostToDevice), "upload agent");
+    RCHK(hipMemcpy(L.deleted + 1, v->deleted, n, hipMemcpyHostToDevice), "upload deleted");
+    RCHK(hipMemcpy(L.cp + 1, v->cp, n * 4ull, hipMemcpyHostToDevice), "upload cp");
+    for (uint32_t i = 0; i < n; ++i)
+        if (!v->deleted[i]) {
+            r.vis_cp += 1;
+            r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
+        }
+    return CRDT_HIP_OK;
+}
+
+int replica_copy(Engine& E, const Replica& src, Replica& dst) {
+    RCHK(hipSetDevice(E.device), "hipSetDevice");
+    const uint64_t cap = src.logs.cap_slots;
+    int rc = replica_reserve(E, dst, cap ? cap - 1 : 0);
+    if (rc) return rc;
+    const DeviceLogs& S = src.logs;
+    DeviceLogs& D = dst.logs;
+    hipStream_t s = E.stream;
+    if (cap) {
+        RCHK(hipMemcpyAsync(D.parent, S.parent, cap * 4, hipMemcpyDeviceToDevice, s), "copy parent");
+        RCHK(hipMemcpyAsync(D.lamport, S.lamport, cap * 4, hipMemcpyDeviceToDevice, s), "copy lamport");
+        RCHK(hipMemcpyAsync(D.agent, S.agent, cap * 2, hipMemcpyDeviceToDevice, s), "copy agent");
+        RCHK(hipMemcpyAsync(D.deleted, S.deleted, cap, hipMemcpyDeviceToDevice, s), "copy deleted");
+        RCHK(hipMemcpyAsync(D.cp, S.cp, cap * 4, hipMemcpyDeviceToDevice, s), "copy cp");
+        RCHK(hipStreamSynchronize(s), "copy sync");
+    }
+    dst.n = src.n;
+    dst.vis_cp = src.vis_cp;
+    dst.vis_bytes = src.vis_bytes;
+    return CRDT_HIP_OK;
+}
+
+int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                  const uint64_t* offsets, uint32_t n) {
+    if (n == 0) return CRDT_HIP_OK;
+    if (!buf || !offsets) {
+        E.err = "null update buffer or offsets";
+        return CRDT_HIP_EINVAL;
+    }
+    if (len >= (1ull << 32) - 16) {
+        E.err = "update batch of 4 GiB or more";
+        return CRDT_HIP_ERANGE;
+    }
+    RCHK(hipSetDevice(E.device), "hipSetDevice");
+    hipStream_t s = E.stream;
+    // ids a batch can add: every item takes at least 16 bytes of it
+    int rc = replica_reserve(E, r, (uint64_t)r.n + len / 16 + 1);
+    if (rc) return rc;
+    const uint32_t nblk = (n + kUB - 1) / kUB;
+    RCHK(grow(&r.ubuf, r.ubuf_cap, (len + 4) & ~3ull), "hipMalloc update buffer");
+    if (n + 1ull > r.ucap) {
+        dfree(r.uoff); dfree(r.uhdr); dfree(r.uscan);
+        r.ucap = 0;
+        const uint64_t c = std::max<uint64_t>(n + 1ull, 1024);
+        RCHK(dalloc(&r.uoff, c), "hipMalloc update offsets");
+        RCHK(dalloc(&r.uhdr, c), "hipMalloc update headers");
+        RCHK(dalloc(&r.uscan, c), "hipMalloc update scan");
+        r.ucap = c;
+    }
+    RCHK(grow(&r.ublk, r.ublk_cap, (uint64_t)nblk), "hipMalloc update blocks");
+    if (!r.uctl) RCHK(dalloc(&r.uctl, (uint64_t)U_N), "hipMalloc update counters");
+    if (!r.hctl) RCHK(hipHostMalloc(reinterpret_cast<void**>(&r.hctl), U_N * 8), "hipHostMalloc");
+    RCHK(hipMemcpyAsync(r.ubuf, buf, len, hipMemcpyHostToDevice, s), "upload updates");
+    RCHK(hipMemcpyAsync(r.uoff, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice, s),
+         "upload update offsets");
+    RCHK(hipMemsetAsync(r.uctl, 0, U_N * 8, s), "memset update counters");
+    DeviceLogs& L = r.logs;
+    UpdArgs a{};
+    a.buf = reinterpret_cast<const uint32_t*>(r.ubuf);
+    a.off = r.uoff;
+    a.n = n;
+    a.len = len;
+    a.hdr = r.uhdr;
+    a.scan = r.uscan;
+    a.blk = r.ublk;
+    a.nblk = nblk;
+    a.known0 = r.n;
+    a.ctl = r.uctl;
+    a.parent = L.parent;
+    a.lamport = L.lamport;
+    a.agent = L.agent;
+    a.deleted = L.deleted;
+    a.cp = L.cp;
+    a.cap_slots = L.cap_slots;
+    const uint32_t gi = std::min<uint64_t>(kMaxGrid, grid_for(len / 16 / kItemsPerThread + 1, kUB));
+    const uint32_t gd = std::min<uint64_t>(kMaxGrid, grid_for(len / 4 + 1, kUB));
+    k_upd_parse<<<nblk, kUB, 0, s>>>(a);
+    k_upd_top<<<1, 1024, 0, s>>>(a);
+    k_upd_scan<<<nblk, kUB, 0, s>>>(a);
+    k_upd_items<false><<<gi, kUB, 0, s>>>(a);
+    k_upd_dels<false><<<gd, kUB, 0, s>>>(a);
+    k_upd_items<true><<<gi, kUB, 0, s>>>(a);
+    k_upd_dels<true><<<gd, kUB, 0, s>>>(a);
+    RCHK(hipGetLastError(), "update kernels");
+    RCHK(hipMemcpyAsync(r.hctl, r.uctl, U_N * 8, hipMemcpyDeviceToHost, s), "copy update counters");
+    RCHK(hipStreamSynchronize(s), "update sync");
+    const uint64_t* c = r.hctl;
+    if (c[U_ERR]) {
+        const uint64_t e = c[U_ERR];
+        E.err = e & E_HEADER      ? "not an update, unsupported version or truncated update"
+                : e & E_NOT_READY ? "update is not causally ready (missing items)"
+                : e & E_PARENT    ? "update item references an unknown parent"
+                : e & E_DELETE    ? "update deletes an unknown item"
+                                  : "update writes outside the replica";
+        return CRDT_HIP_EBADLOG;
+    }
+    r.n = (uint32_t)std::max<uint64_t>(r.n, c[U_MAXID]);
+    r.vis_cp = r.vis_cp + c[U_ADD_CP] - c[U_DEL_CP];
+    r.vis_bytes = r.vis_bytes + c[U_ADD_B] - c[U_DEL_B];
+    return CRDT_HIP_OK;
+}
+
+int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* len,
+                  uint64_t* digest, crdt_hip_stats* st) {
+    int rc = replica_reserve(E, r, r.n);
+    if (rc) return rc;
+    std::vector<DocInfo> docs{DocInfo{r.n, r.vis_bytes}};
+    rc = E.plan(r.logs, docs);
+    if (rc) return rc;
+    return E.merge(r.logs, Engine::TEXT, digest, len, st, text, nullptr);
+}
+
+}  // namespace crdt

@@ -13,7 +13,8 @@
  *   remove(a..b)         -> crdt_hip_oplog_remove                               (rope.rs:129-131)
  *   len()                -> crdt_hip_merge  (replaces OpLog::checkout_tip().len(), rope.rs:134-136)
  *   upstream_updates     -> crdt_hip_oplog_version + crdt_hip_oplog_encode_from (rope.rs:196-220)
- *   apply_update(u)      -> crdt_hip_oplog_apply_update (replaces decode_and_add, rope.rs:222-224)
+ *   apply_update(u)      -> crdt_hip_oplog_apply_update (replaces decode_and_add, rope.rs:222-224),
+ *                           or on the device: crdt_hip_replica_apply_updates (batched)
  *   clone()              -> crdt_hip_oplog_clone (the device context is shared, never copied)
  *
  * Conventions
@@ -55,6 +56,7 @@ typedef struct crdt_hip_ctx crdt_hip_ctx;
 typedef struct crdt_hip_oplog crdt_hip_oplog;
 typedef struct crdt_hip_trace crdt_hip_trace;
 typedef struct crdt_hip_batch crdt_hip_batch;
+typedef struct crdt_hip_replica crdt_hip_replica;
 
 /* Anchor op log, structure of arrays (borrowed view).  Item k (0-based) has id k+1.
  * parent = origin_left id (0 = document start).  Document order (RGA): pre-order of the tree
@@ -196,6 +198,33 @@ int crdt_hip_batch_info(const crdt_hip_batch* b, uint64_t* docs, uint64_t* items
  * NULL). */
 int crdt_hip_batch_merge(crdt_hip_ctx* ctx, crdt_hip_batch* b, uint64_t* digests,
                          uint64_t* lens, crdt_hip_stats* stats);
+
+/* ---- device-resident replicas: Downstream on the device ------------------------------------
+ * A replica is an op log resident in HBM that receives encoded updates and is merged where it
+ * lies.  Replaces diamond-types' decode_and_add (Dt Downstream, rope.rs:222-224) for the
+ * downstream bench group (main.rs:63-69: clone the initial CRDT, apply every update, len()).
+ * Updates are in the wire format of crdt_hip_oplog_encode_from; they are decoded on the device,
+ * a whole batch per call, with crdt_hip_oplog_apply_update's semantics (ids already known are
+ * skipped; an update must be causally ready: its first id <= known ids + 1).  Unlike the
+ * host decoder, a batch that fails validation changes nothing.  A replica belongs to the
+ * context that created it. */
+/* New replica holding `init` (NULL: empty, = Downstream's from_str("")). */
+int crdt_hip_replica_new(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* init,
+                         crdt_hip_replica** out);
+/* Device-to-device copy (Downstream: Clone, main.rs:64). */
+int crdt_hip_replica_clone(crdt_hip_ctx* ctx, const crdt_hip_replica* src,
+                           crdt_hip_replica** out);
+int crdt_hip_replica_free(crdt_hip_replica* r);
+/* Apply updates i = 0..n-1, update i = buf[offsets[i], offsets[i+1]) (n + 1 offsets, each a
+ * multiple of 4, offsets[n] <= len < 4 GiB), in order (apply_update, rope.rs:222-224). */
+int crdt_hip_replica_apply_updates(crdt_hip_ctx* ctx, crdt_hip_replica* r, const uint8_t* buf,
+                                   size_t len, const uint64_t* offsets, uint32_t n);
+/* Items held, visible codepoints (Upstream::len, rope.rs:16-19) and visible UTF-8 bytes. */
+int crdt_hip_replica_info(const crdt_hip_replica* r, uint64_t* items,
+                          uint64_t* visible_codepoints, uint64_t* visible_bytes);
+/* Merge the replica to its document (as crdt_hip_merge: out may be NULL). */
+int crdt_hip_replica_merge(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out, size_t cap,
+                           size_t* out_len, uint64_t* digest);
 
 /* ---- multi-GPU (RCCL over xGMI): digest/counter exchange only ----------------------------- */
 int crdt_hip_comm_unique_id(uint8_t id[128]);
