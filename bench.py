@@ -218,6 +218,90 @@ def side_workload(args) -> int:
     return 0 if ok else 1
 
 
+def downstream_workload(args) -> int:
+    """The reference's downstream group (main.rs:50-81) on the device: per trace, a step clones
+    the initial replica (main.rs:64), applies every per-patch update (:65-67) and merges (:68).
+    Updates are encoded on the host beforehand, as upstream_updates does (rope.rs:196-220), and
+    packed into one buffer + offsets; the timed region includes their PCIe upload, the device
+    decode (replica.hip) and the merge.  value = patches/s over the 4 traces."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    ctx = crdt_hip.Context(local)
+    with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
+        golden = json.load(f)
+    t_setup = time.perf_counter()
+    work = []
+    for name in TRACES:
+        t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
+        patches = [t.patch(i) for i in range(len(t))]
+        up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
+        init = crdt_hip.Replica(ctx, up.log if up.log.view().n else None)
+        buf, offs = crdt_hip.pack_updates(updates)
+        work.append((name, len(t), init, buf, offs, int(golden[name]["tree_digest"], 16),
+                     golden[name]["end_bytes"]))
+    if rank == 0:
+        log(f"[bench] downstream: {sum(w[1] for w in work)} updates, "
+            f"{sum(w[3].size for w in work) / 2**20:.1f} MiB encoded, "
+            f"setup {time.perf_counter() - t_setup:.1f} s")
+
+    def step(per):
+        ok = True
+        for name, npatch, init, buf, offs, dig, nbytes in work:
+            t0 = time.perf_counter()
+            r = init.clone()
+            r.apply_packed(buf, offs)
+            n, d = r.merge_digest()
+            per[name] = per.get(name, 0.0) + time.perf_counter() - t0
+            ok &= (n, d) == (nbytes, dig)
+            r.close()
+        return ok
+
+    for _ in range(args.warmup):
+        step({})
+    if dist is not None:
+        dist.barrier()
+    per: dict = {}
+    t0 = time.perf_counter()
+    ok = True
+    for _ in range(args.steps):
+        ok &= step(per)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    total_patches = sum(w[1] for w in work)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": total_patches * world / (el / args.steps),
+            "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "trace",
+            "config": {"workload": "downstream (main.rs:63-69): clone + apply every update + len, "
+                                   "device decode, 4 traces one after the other",
+                       "updates": total_patches,
+                       "encoded_bytes": int(sum(w[3].size for w in work)),
+                       "parallelism": f"replicas x{world} (no data-path collective)"},
+            "per_trace": {w[0]: {"ms": per[w[0]] / args.steps * 1e3,
+                                 "patches_per_s": w[1] / (per[w[0]] / args.steps)} for w in work},
+            "pcie_included": True, "digests_ok": bool(ok),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -231,11 +315,14 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="traces", choices=["traces", "seph", "agents64", "big1b"],
+    ap.add_argument("--workload", default="traces", choices=["traces", "seph", "agents64", "big1b", "downstream"],
                     help="traces: config 3 (headline); seph: config 2; agents64: config 4; "
-                         "big1b: config 5 (SURVEY.md §8(d))")
+                         "big1b: config 5 (SURVEY.md §8(d)); downstream: the reference's "
+                         "downstream group with device-side update decode (§8(f) row 2)")
     ap.add_argument("--items", type=int, default=0, help="items of the synthetic workloads")
     args = ap.parse_args()
+    if args.workload == "downstream":
+        return downstream_workload(args)
     if args.workload != "traces":
         return side_workload(args)
 

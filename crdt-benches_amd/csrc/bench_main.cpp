@@ -163,7 +163,10 @@ int main(int argc, char** argv) {
     if (group == "upstream" || group == "all")
         for (const char* t : TRACES) upstream<HipMerge>(dir, t, iters);
     if (group == "downstream" || group == "all")
-        for (const char* t : TRACES) downstream<HipMerge>(dir, t, iters);
+        for (const char* t : TRACES) {
+            downstream<HipMerge>(dir, t, iters);       // host decode, device merge
+            downstream<hipmerge::HipDownstream>(dir, t, iters);  // device decode + merge
+        }
     if (group == "batched" || group == "all") batched(dir, iters, replicas, relabel);
     return 0;
 }

@@ -424,14 +424,6 @@ __global__ __launch_bounds__(1024) void k_docmax(L0Args a) {
     if (threadIdx.x == 0) a.ctl[C_RMAX] = mx;
 }
 
-// Heads at or before slot g (wave-relative), from the rank bitvector.
-__device__ __forceinline__ uint32_t rank_incl(const uint64_t* hbits, const uint32_t* hrank,
-                                              uint32_t g) {
-    const uint32_t w = g >> 6, b = g & 63u;
-    const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
-    return hrank[w] + (uint32_t)__popcll(hbits[w] & mask);
-}
-
 // Per run: weight (next run's prefix - own prefix) and parent run (rank lookup of the head's
 // parent item; the parent item is always the last item of its run; a head whose parent is the
 // slot before it has the previous run as parent).  kRunsPerThread runs per thread, every load of

@@ -88,6 +88,13 @@ public:
         check(crdt_hip_merge(dev_->ctx, &v, nullptr, 0, &n, &d), dev_->ctx, "crdt_hip_merge");
         return d;
     }
+    // Borrowed SoA view of the host op log (valid until the next mutation).
+    crdt_hip_oplog_view view() const {
+        crdt_hip_oplog_view v;
+        check(crdt_hip_oplog_get_view(log_.get(), &v), nullptr, "view");
+        return v;
+    }
+    const std::shared_ptr<Device>& device() const { return dev_; }
     HipMerge clone() const {
         crdt_hip_oplog* c = nullptr;
         check(crdt_hip_oplog_clone(log_.get(), &c), nullptr, "clone");
@@ -136,6 +143,88 @@ private:
         log_.reset(l);
     }
     HipMerge(crdt_hip_oplog* l, std::shared_ptr<Device> d) : log_(l), dev_(std::move(d)) {}
+};
+
+// Downstream with the replica resident on the device (crdt_hip_replica_*).  apply_update only
+// queues the encoded update in a host buffer; len() decodes every queued update on the device in
+// one batch (the decode_and_add of rope.rs:222-224 for all of them), merges the replica where it
+// lies and returns its visible codepoints.  clone() copies the replica device to device.
+class HipDownstream {
+public:
+    static constexpr const char* NAME = "mi355x-device";
+    static constexpr bool EDITS_USE_BYTE_OFFSETS = false;
+    using Update = HipMerge::Update;
+
+    template <class PatchFn>
+    static std::pair<HipDownstream, std::vector<Update>> upstream_updates(std::string_view start,
+                                                                           size_t npatches,
+                                                                           PatchFn&& patch) {
+        auto pr = HipMerge::upstream_updates(start, npatches, patch);
+        crdt_hip_oplog_view v = pr.first.view();
+        HipDownstream d(pr.first.device());
+        check(crdt_hip_replica_new(d.dev_->ctx, v.n ? &v : nullptr, &d.rep_), d.dev_->ctx,
+              "replica_new");
+        return {std::move(d), std::move(pr.second)};
+    }
+    HipDownstream(HipDownstream&& o) noexcept
+        : dev_(std::move(o.dev_)), rep_(o.rep_), buf_(std::move(o.buf_)), off_(std::move(o.off_)) {
+        o.rep_ = nullptr;
+    }
+    HipDownstream(const HipDownstream&) = delete;
+    ~HipDownstream() {
+        if (rep_) crdt_hip_replica_free(rep_);
+    }
+    HipDownstream clone() const {  // main.rs:64
+        HipDownstream c(dev_);
+        check(crdt_hip_replica_clone(dev_->ctx, rep_, &c.rep_), dev_->ctx, "replica_clone");
+        c.buf_ = buf_;
+        c.off_ = off_;
+        return c;
+    }
+    void apply_update(const Update& u) {  // rope.rs:222-224 (queued)
+        buf_.insert(buf_.end(), u.begin(), u.end());
+        off_.push_back(buf_.size());
+    }
+    size_t len() const {  // Upstream::len (codepoints) after the device merge
+        flush();
+        size_t n = 0;
+        uint64_t d = 0, items = 0, cps = 0, bytes = 0;
+        check(crdt_hip_replica_merge(dev_->ctx, rep_, nullptr, 0, &n, &d), dev_->ctx, "replica_merge");
+        crdt_hip_replica_info(rep_, &items, &cps, &bytes);
+        if (bytes != n) {
+            std::fprintf(stderr, "replica: merged %zu bytes, %llu visible\n", n, (unsigned long long)bytes);
+            std::abort();
+        }
+        return (size_t)cps;
+    }
+    std::string text() const {
+        flush();
+        uint64_t items = 0, cps = 0, bytes = 0;
+        crdt_hip_replica_info(rep_, &items, &cps, &bytes);
+        std::string out((size_t)bytes + 16, '\0');
+        size_t n = 0;
+        check(crdt_hip_replica_merge(dev_->ctx, rep_, reinterpret_cast<uint8_t*>(out.data()),
+                                     out.size(), &n, nullptr),
+              dev_->ctx, "replica_merge");
+        out.resize(n);
+        return out;
+    }
+
+private:
+    std::shared_ptr<Device> dev_;
+    crdt_hip_replica* rep_ = nullptr;
+    mutable std::vector<uint8_t> buf_;
+    mutable std::vector<uint64_t> off_{0};
+
+    explicit HipDownstream(std::shared_ptr<Device> d) : dev_(std::move(d)) {}
+    void flush() const {
+        if (off_.size() < 2) return;
+        check(crdt_hip_replica_apply_updates(dev_->ctx, rep_, buf_.data(), buf_.size(), off_.data(),
+                                             (uint32_t)(off_.size() - 1)),
+              dev_->ctx, "replica_apply_updates");
+        buf_.clear();
+        off_.assign(1, 0);
+    }
 };
 
 }  // namespace hipmerge
