@@ -1,5 +1,6 @@
-// oplog.cpp — order-statistic resolver over a chunked sequence (chunks of item ids + a Fenwick
-// tree of per-chunk visible counts): O(log C + chunk) per positional lookup.
+// oplog.cpp — order-statistic resolver over a chunked span sequence (runs of consecutive ids,
+// chunks of <= 64 spans + a Fenwick tree of per-chunk visible counts): O(log C + 64) per
+// positional lookup, O(1) amortised appends while typing on (the span of the last item grows).
 #include "oplog.hpp"
 
 #include <algorithm>
@@ -10,7 +11,7 @@
 namespace crdt {
 
 namespace {
-constexpr size_t kChunkMax = 512;
+constexpr size_t kSpanMax = 64;
 constexpr uint32_t kMagic = kUpdateMagic;
 constexpr uint32_t kWireVersion = kUpdateVersion;
 
@@ -22,7 +23,16 @@ uint32_t get32(const uint8_t* p) {
 }
 }  // namespace
 
-OpLog::OpLog() { chunks_.emplace_back(); fen_build(); }
+OpLog::OpLog() {
+    chunks_.push_back(new_chunk());
+    fen_build();
+}
+
+OpLog::Chunk OpLog::new_chunk() const {
+    Chunk c;
+    c.s.reserve(kSpanMax + 4);
+    return c;
+}
 
 void OpLog::fen_build() {
     fen_.assign(chunks_.size() + 1, 0);
@@ -52,32 +62,43 @@ size_t OpLog::fen_find(uint64_t& p) const {
     return pos;  // 0-based chunk; p is now the rank inside it
 }
 
-bool OpLog::find_visible(uint64_t p, size_t& c, size_t& i) const {
+bool OpLog::find_visible(uint64_t p, size_t& c, size_t& si, uint32_t& off) const {
     if (p == 0 || p > nvis_) return false;
     uint64_t r = p;
     c = fen_find(r);
     if (c >= chunks_.size()) return false;
-    const std::vector<uint32_t>& ids = chunks_[c].ids;
-    for (i = 0; i < ids.size(); ++i) {
-        if (!deleted[ids[i] - 1] && --r == 0) return true;
+    const std::vector<Span>& v = chunks_[c].s;
+    for (si = 0; si < v.size(); ++si) {
+        if (v[si].del()) continue;
+        uint32_t len = v[si].len();
+        if (r <= len) {
+            off = (uint32_t)r - 1;
+            return true;
+        }
+        r -= len;
     }
     return false;
 }
 
-void OpLog::split_chunk(size_t c) {
-    if (chunks_[c].ids.size() <= kChunkMax) return;
-    std::vector<uint32_t> all;
-    all.swap(chunks_[c].ids);
-    size_t pieces = (all.size() + kChunkMax / 2 - 1) / (kChunkMax / 2);
-    std::vector<Chunk> repl(pieces);
-    for (size_t k = 0; k < pieces; ++k) {
-        size_t a = k * all.size() / pieces, b = (k + 1) * all.size() / pieces;
-        repl[k].ids.assign(all.begin() + a, all.begin() + b);
-        for (uint32_t id : repl[k].ids) repl[k].vis += !deleted[id - 1];
-    }
-    chunks_.erase(chunks_.begin() + c);
-    chunks_.insert(chunks_.begin() + c, repl.begin(), repl.end());
+uint32_t OpLog::first_id_from(size_t c, size_t si) const {
+    for (; c < chunks_.size(); ++c, si = 0)
+        if (si < chunks_[c].s.size()) return chunks_[c].s[si].id;
+    return NIL;
+}
+
+bool OpLog::split_chunk(size_t c) {
+    if (chunks_[c].s.size() <= kSpanMax) return false;
+    Chunk hi = new_chunk();
+    std::vector<Span>& lo = chunks_[c].s;
+    size_t half = lo.size() / 2;
+    hi.s.assign(lo.begin() + half, lo.end());
+    lo.resize(half);
+    for (const Span& x : hi.s)
+        if (!x.del()) hi.vis += x.len();
+    chunks_[c].vis -= hi.vis;
+    chunks_.insert(chunks_.begin() + c + 1, std::move(hi));
     fen_build();
+    return true;
 }
 
 std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
@@ -87,25 +108,30 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
     }
     if (pos > nvis_) return "insert position out of range";
     if (k == 0) return "";
-    if ((uint64_t)size() + k >= 0xFFFFFFF0ull) return "op log too large";
-    size_t c = 0, at = 0;
-    uint32_t left = 0;
-    if (pos > 0) {
-        size_t i;
-        if (!find_visible(pos, c, i)) return "resolver index corrupt";
-        left = chunks_[c].ids[i];
-        at = i + 1;
-    }
-    // origin_right: the item now following `left` (tombstones included)
-    uint32_t right = NIL;
-    if (at < chunks_[c].ids.size()) {
-        right = chunks_[c].ids[at];
+    if ((uint64_t)size() + k >= 0x7FFFFFF0ull) return "op log too large";
+    const uint32_t first = size() + 1;
+    size_t c = 0, at = 0;  // new span goes to chunks_[c].s[at]
+    uint32_t left = 0, right;
+    bool extend = false;
+    if (pos == 0) {
+        right = first_id_from(0, 0);
     } else {
-        for (size_t cc = c + 1; cc < chunks_.size(); ++cc)
-            if (!chunks_[cc].ids.empty()) { right = chunks_[cc].ids[0]; break; }
+        size_t si;
+        uint32_t off;
+        if (!find_visible(pos, c, si, off)) return "resolver index corrupt";
+        std::vector<Span>& v = chunks_[c].s;
+        const Span S = v[si];
+        left = S.id + off;
+        if (off + 1 < S.len()) {  // split S after `left`
+            right = left + 1;
+            v[si].n = off + 1;
+            v.insert(v.begin() + si + 1, Span{left + 1, S.len() - off - 1});
+        } else {
+            right = first_id_from(c, si + 1);
+            extend = (S.id + S.len() == first);  // typing on: left is the last item created
+        }
+        at = si + 1;
     }
-    uint32_t first = size() + 1;
-    std::vector<uint32_t> ids(k);
     for (size_t j = 0; j < k; ++j) {
         uint32_t id = first + (uint32_t)j;
         parent.push_back(j == 0 ? left : id - 1);
@@ -114,10 +140,12 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
         agent.push_back(local_agent);
         deleted.push_back(0);
         cp.push_back(cps[j]);
-        ids[j] = id;
     }
-    std::vector<uint32_t>& v = chunks_[c].ids;
-    v.insert(v.begin() + at, ids.begin(), ids.end());
+    std::vector<Span>& v = chunks_[c].s;
+    if (extend)
+        v[at - 1].n += (uint32_t)k;
+    else
+        v.insert(v.begin() + at, Span{first, (uint32_t)k});
     chunks_[c].vis += (uint32_t)k;
     nvis_ += k;
     fen_add(c, (int64_t)k);
@@ -126,10 +154,40 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
 }
 
 std::string OpLog::insert_utf8(uint64_t pos, const char* s, size_t nbytes) {
-    std::vector<uint32_t> cps;
-    cps.reserve(nbytes);
-    if (!utf8_decode(s, nbytes, cps)) return "invalid UTF-8";
-    return insert(pos, cps.data(), cps.size());
+    cps_.clear();
+    if (!utf8_decode(s, nbytes, cps_)) return "invalid UTF-8";
+    return insert(pos, cps_.data(), cps_.size());
+}
+
+// Tombstone items [off, off+take) of visible span si; merges the tombstone span with deleted
+// neighbours whose ids continue it.  Returns the index of the span after the tombstones.
+size_t OpLog::delete_in_span(Chunk& ch, size_t si, uint32_t off, uint32_t take) {
+    std::vector<Span>& v = ch.s;
+    const Span S = v[si];
+    const uint32_t len = S.len(), did = S.id + off, dend = did + take;
+    for (uint32_t id = did; id < dend; ++id) {
+        deleted[id - 1] = 1;
+        del_ops.push_back(id);
+    }
+    Span rep[3];
+    int nr = 0;
+    if (off) rep[nr++] = Span{S.id, off};
+    size_t mid = si + nr;
+    rep[nr++] = Span{did, take | 0x80000000u};
+    const bool tail = off + take < len;
+    if (tail) rep[nr++] = Span{dend, len - off - take};
+    v[si] = rep[0];
+    if (nr > 1) v.insert(v.begin() + si + 1, rep + 1, rep + nr);
+    if (!tail && mid + 1 < v.size() && v[mid + 1].del() && v[mid + 1].id == dend) {
+        v[mid].n += v[mid + 1].len();
+        v.erase(v.begin() + mid + 1);
+    }
+    if (mid > 0 && v[mid - 1].del() && v[mid - 1].id + v[mid - 1].len() == did) {
+        v[mid - 1].n += v[mid].len();
+        v.erase(v.begin() + mid);
+        --mid;
+    }
+    return mid + 1;
 }
 
 std::string OpLog::remove(uint64_t start, uint64_t end) {
@@ -140,19 +198,33 @@ std::string OpLog::remove(uint64_t start, uint64_t end) {
     if (end < start || end > nvis_) return "remove range out of range";
     uint64_t left = end - start;
     if (!left) return "";
-    size_t c, i;
-    if (!find_visible(start + 1, c, i)) return "resolver index corrupt";
+    size_t c, si;
+    uint32_t off;
+    if (!find_visible(start + 1, c, si, off)) return "resolver index corrupt";
+    const size_t c0 = c;
     while (left) {
-        if (i >= chunks_[c].ids.size()) { ++c; i = 0; continue; }
-        uint32_t id = chunks_[c].ids[i++];
-        if (deleted[id - 1]) continue;
-        deleted[id - 1] = 1;
-        del_ops.push_back(id);
-        chunks_[c].vis--;
-        fen_add(c, -1);
-        --left;
+        Chunk& ch = chunks_[c];
+        if (si >= ch.s.size()) {
+            if (++c >= chunks_.size()) return "resolver index corrupt";
+            si = 0;
+            off = 0;
+            continue;
+        }
+        if (ch.s[si].del()) {
+            ++si;
+            off = 0;
+            continue;
+        }
+        uint32_t take = ch.s[si].len() - off;
+        if (take > left) take = (uint32_t)left;
+        si = delete_in_span(ch, si, off, take);
+        off = 0;
+        ch.vis -= take;
+        fen_add(c, -(int64_t)take);
+        left -= take;
     }
     nvis_ -= end - start;
+    for (size_t cc = c + 1; cc-- > c0;) split_chunk(cc);
     return "";
 }
 
@@ -196,7 +268,7 @@ std::string OpLog::rebuild_index() {
         return agent[a - 1] > agent[b - 1];
     };
     chunks_.clear();
-    chunks_.emplace_back();
+    chunks_.push_back(new_chunk());
     nvis_ = 0;
     std::vector<uint32_t> stack;
     stack.reserve(n + 1);
@@ -207,9 +279,19 @@ std::string OpLog::rebuild_index() {
         stack.pop_back();
         if (v) {
             ++seen;
-            if (chunks_.back().ids.size() >= kChunkMax / 2) chunks_.emplace_back();
-            chunks_.back().ids.push_back(v);
-            if (!deleted[v - 1]) { chunks_.back().vis++; nvis_++; }
+            const bool del = deleted[v - 1] != 0;
+            Chunk* ch = &chunks_.back();
+            Span* last = ch->s.empty() ? nullptr : &ch->s.back();
+            if (last && last->del() == del && last->id + last->len() == v) {
+                last->n++;
+            } else {
+                if (ch->s.size() >= kSpanMax / 2) {
+                    chunks_.push_back(new_chunk());
+                    ch = &chunks_.back();
+                }
+                ch->s.push_back(Span{v, 1u | (del ? 0x80000000u : 0u)});
+            }
+            if (!del) { ch->vis++; nvis_++; }
         }
         uint32_t a = start[v], b = start[v + 1];
         std::sort(kids.begin() + a, kids.begin() + b, [&](uint32_t x, uint32_t y) { return newer(y, x); });

@@ -54,21 +54,35 @@ public:
     void reset_visible(uint64_t v) { nvis_ = v; }
 
 private:
+    // Positional index: the document sequence (tombstones included) as spans of consecutive
+    // item ids that are also consecutive in document order and share one deleted state, packed
+    // into chunks of at most kSpanMax spans with a Fenwick tree over the chunks' visible counts.
+    struct Span {
+        uint32_t id;  // first item id
+        uint32_t n;   // bit 31: deleted; low 31 bits: length
+        uint32_t len() const { return n & 0x7FFFFFFFu; }
+        bool del() const { return (n >> 31) != 0; }
+    };
     struct Chunk {
-        std::vector<uint32_t> ids;
+        std::vector<Span> s;
         uint32_t vis = 0;
     };
     std::vector<Chunk> chunks_;
     std::vector<int64_t> fen_;  // Fenwick tree over chunks_[i].vis
+    std::vector<uint32_t> cps_;  // scratch for insert_utf8
     uint64_t nvis_ = 0;
     bool stale_ = false;  // positional index must be rebuilt (after remote items arrived)
 
     void fen_build();
     void fen_add(size_t i, int64_t d);
     size_t fen_find(uint64_t& p) const;  // chunk holding the p-th visible item (p >= 1)
-    void split_chunk(size_t c);
+    Chunk new_chunk() const;
+    bool split_chunk(size_t c);  // true if chunk c was split in two
     std::string rebuild_index();
-    bool find_visible(uint64_t p, size_t& c, size_t& i) const;
+    // p-th visible item (p >= 1): chunk c, span si, offset off inside the span.
+    bool find_visible(uint64_t p, size_t& c, size_t& si, uint32_t& off) const;
+    uint32_t first_id_from(size_t c, size_t si) const;  // first item at or after (c, si), or NIL
+    size_t delete_in_span(Chunk& ch, size_t si, uint32_t off, uint32_t take);
 };
 
 }  // namespace crdt
