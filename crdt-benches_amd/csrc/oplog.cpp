@@ -28,6 +28,15 @@ OpLog::OpLog() {
     fen_build();
 }
 
+void OpLog::reserve(size_t items) {
+    parent.reserve(items);
+    oright.reserve(items);
+    lamport.reserve(items);
+    cp.reserve(items);
+    agent.reserve(items);
+    deleted.reserve(items);
+}
+
 OpLog::Chunk OpLog::new_chunk() const {
     Chunk c;
     c.s.reserve(kSpanMax + 4);
@@ -65,8 +74,15 @@ size_t OpLog::fen_find(uint64_t& p) const {
 bool OpLog::find_visible(uint64_t p, size_t& c, size_t& si, uint32_t& off) const {
     if (p == 0 || p > nvis_) return false;
     uint64_t r = p;
-    c = fen_find(r);
-    if (c >= chunks_.size()) return false;
+    if (hint_c_ < chunks_.size() && p > hint_base_ && p - hint_base_ <= chunks_[hint_c_].vis) {
+        c = hint_c_;
+        r = p - hint_base_;
+    } else {
+        c = fen_find(r);
+        if (c >= chunks_.size()) return false;
+        hint_c_ = c;
+        hint_base_ = p - r;
+    }
     const std::vector<Span>& v = chunks_[c].s;
     for (si = 0; si < v.size(); ++si) {
         if (v[si].del()) continue;
@@ -115,6 +131,8 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
     bool extend = false;
     if (pos == 0) {
         right = first_id_from(0, 0);
+        hint_c_ = 0;  // chunk 0 changes: keep the hint on it
+        hint_base_ = 0;
     } else {
         size_t si;
         uint32_t off;
@@ -270,6 +288,7 @@ std::string OpLog::rebuild_index() {
     chunks_.clear();
     chunks_.push_back(new_chunk());
     nvis_ = 0;
+    hint_c_ = SIZE_MAX;
     std::vector<uint32_t> stack;
     stack.reserve(n + 1);
     stack.push_back(0);

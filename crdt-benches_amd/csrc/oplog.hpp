@@ -52,6 +52,7 @@ public:
     // For bulk builders that fill the SoA directly.
     void mark_stale() { stale_ = true; }
     void reset_visible(uint64_t v) { nvis_ = v; }
+    void reserve(size_t items);
 
 private:
     // Positional index: the document sequence (tombstones included) as spans of consecutive
@@ -71,6 +72,10 @@ private:
     std::vector<int64_t> fen_;  // Fenwick tree over chunks_[i].vis
     std::vector<uint32_t> cps_;  // scratch for insert_utf8
     uint64_t nvis_ = 0;
+    // Chunk of the last lookup and the visible items before it.  Edits only change counts at or
+    // after the chunk they start in and splits append after it, so the hint stays exact.
+    mutable size_t hint_c_ = SIZE_MAX;
+    mutable uint64_t hint_base_ = 0;
     bool stale_ = false;  // positional index must be rebuilt (after remote items arrived)
 
     void fen_build();
