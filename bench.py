@@ -43,7 +43,7 @@ PIPE_B_PER_ITEM = 117.0
 # Per-kernel algorithmic bytes: each kernel's declared inputs read once +
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
-    "classify": (9.625, 0.0, 1.0),   # parent, cp, deleted; seq bits, weight nibbles; tile UTF-8
+    "classify": (8.625, 0.0, 1.0),   # parent, cp|tombstone bit; seq bits, weight nibbles; tile UTF-8
     "runs": (1.0, 8.0, 2.0),         # seq/jump/head bits, nibbles, rank words; run records; text move
     "run_parent": (0.0, 28.0, 0.0),  # run head/prefix, parent lookup (+ rank word); weight, parent
     "count": (0.0, 8.0, 0.0),

@@ -89,7 +89,6 @@ struct L0Args {
     const uint32_t* in_parent;
     const uint32_t* in_lamport;
     const uint16_t* in_agent;
-    const uint8_t* in_deleted;
     const uint32_t* in_cp;
     uint32_t* jbits;            // per slot bit: has a non-consecutive child in a later tile
     uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
@@ -114,8 +113,8 @@ struct L0Args {
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 
-// k_classify: parents and characters of 16 slots per thread (4 + 4 x 16-byte loads + 16 B of
-// deleted flags).
+// k_classify: parents and characters (tombstone in bit 31) of 16 slots per thread (4 + 4 x 16-byte
+// loads).
 //  * "parent is the previous slot" bits (one u16 store per thread);
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
@@ -131,8 +130,8 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
     if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
     const bool live = gs < a.nslots;
-    // every load first (9 x 16 B per thread); padding slots hold junk and are masked below
-    uint4 pq[4], cq[4], dl = make_uint4(0, 0, 0, 0);
+    // every load first (8 x 16 B per thread); padding slots hold junk and are masked below
+    uint4 pq[4], cq[4];
     uint32_t base = 0, n = 0, l0 = 0;
     if (live) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
@@ -145,13 +144,11 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         for (int q = 0; q < 4; ++q) pq[q] = pv[q];
 #pragma unroll
         for (int q = 0; q < 4; ++q) cq[q] = cv[q];
-        if (a.mode == 0) dl = *reinterpret_cast<const uint4*>(a.in_deleted + gs);
     }
     const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
                             pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
     const uint32_t C[16] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z, cq[1].w,
                             cq[2].x, cq[2].y, cq[2].z, cq[2].w, cq[3].x, cq[3].y, cq[3].z, cq[3].w};
-    const uint32_t D[4] = {dl.x, dl.y, dl.z, dl.w};
     // branch-free classification of the 16 slots
     uint32_t seq = 0, jmp = 0, bad = 0, W = 0;
     uint32_t w[16];
@@ -159,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     for (int k = 0; k < 16; ++k) {
         const uint32_t local = l0 + k, p = P[k];
         const bool it = live && (local - 1u) < n;  // an item (not the document start / padding)
-        const bool del = (D[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const bool del = (C[k] & kDelBit) != 0u;
         const bool b = p > n || p == local;
         const bool sq = p == local - 1u;
         w[k] = it ? (a.mode ? 1u : (del ? 0u : utf8_len(C[k] & kCpMask))) : 0u;
@@ -1799,9 +1796,8 @@ __device__ __forceinline__ uint32_t perm_apply(const Perm& P, uint32_t id) {
 
 __global__ __launch_bounds__(kBlock) void k_replicate(
     const uint32_t* __restrict__ bp, const uint32_t* __restrict__ bl,
-    const uint16_t* __restrict__ ba, const uint8_t* __restrict__ bd,
-    const uint32_t* __restrict__ bc, uint64_t src, uint32_t* __restrict__ rp,
-    uint32_t* __restrict__ rl, uint16_t* __restrict__ ra, uint8_t* __restrict__ rd,
+    const uint16_t* __restrict__ ba, const uint32_t* __restrict__ bc, uint64_t src,
+    uint32_t* __restrict__ rp, uint32_t* __restrict__ rl, uint16_t* __restrict__ ra,
     uint32_t* __restrict__ rc, uint64_t dst, Perm P) {
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x + 1;
     if (k > P.n) return;
@@ -1809,7 +1805,6 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
     rp[o] = perm_apply(P, bp[src + k]);
     rl[o] = bl[src + k];
     ra[o] = ba[src + k];
-    rd[o] = bd[src + k];
     rc[o] = bc[src + k];
 }
 
@@ -1819,7 +1814,6 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
 __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ par,
                                                         uint32_t* __restrict__ lam,
                                                         uint16_t* __restrict__ ag,
-                                                        uint8_t* __restrict__ del,
                                                         uint32_t* __restrict__ cp, uint32_t n,
                                                         uint64_t nslots, uint32_t p_chain_pct,
                                                         uint32_t del_pct, uint64_t seed) {
@@ -1842,8 +1836,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ pa
     par[g] = p;
     lam[g] = l;
     ag[g] = a;
-    del[g] = d;
-    cp[g] = c;
+    cp[g] = c | (d ? kDelBit : 0u);
 }
 
 inline uint32_t ceil_log2(uint64_t x) {
@@ -1858,7 +1851,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 // host side
 // =============================================================================================
 void DeviceLogs::release() {
-    dfree(parent); dfree(lamport); dfree(agent); dfree(deleted); dfree(cp);
+    dfree(parent); dfree(lamport); dfree(agent); dfree(cp);
     dfree(docs_rel); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
 }
@@ -1952,11 +1945,10 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     L.total_slots = slot;
     const uint64_t nchunks = slot / M;
     if (slot > L.cap_slots) {
-        dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.deleted); dfree(L.cp);
+        dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.cp);
         HIPCHK(dalloc(&L.parent, slot), "hipMalloc logs.parent");
         HIPCHK(dalloc(&L.lamport, slot), "hipMalloc logs.lamport");
         HIPCHK(dalloc(&L.agent, slot), "hipMalloc logs.agent");
-        HIPCHK(dalloc(&L.deleted, slot), "hipMalloc logs.deleted");
         HIPCHK(dalloc(&L.cp, slot), "hipMalloc logs.cp");
         L.cap_slots = slot;
     }
@@ -2008,9 +2000,8 @@ int Engine::upload_tables(DeviceLogs& L) {
 
 int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) {
     const uint64_t S = L.total_slots;
-    std::vector<uint32_t> par(S, 0), lam(S, 0), c(S, 0);
+    std::vector<uint32_t> par(S, 0), lam(S, 0), c(S, kDelBit);
     std::vector<uint16_t> ag(S, 0);
-    std::vector<uint8_t> del(S, 1);
     for (uint32_t d = 0; d < n; ++d) {
         const crdt_hip_oplog_view& v = views[d];
         const uint64_t b = L.doc_slot[d] + 1;
@@ -2018,13 +2009,12 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
         std::memcpy(&par[b], v.parent, v.n * 4ull);
         std::memcpy(&lam[b], v.lamport, v.n * 4ull);
         std::memcpy(&ag[b], v.agent, v.n * 2ull);
-        std::memcpy(&del[b], v.deleted, v.n);
-        std::memcpy(&c[b], v.cp, v.n * 4ull);
+        for (uint32_t i = 0; i < v.n; ++i)
+            c[b + i] = (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u);
     }
     HIPCHK(hipMemcpy(L.parent, par.data(), S * 4, hipMemcpyHostToDevice), "upload parent");
     HIPCHK(hipMemcpy(L.lamport, lam.data(), S * 4, hipMemcpyHostToDevice), "upload lamport");
     HIPCHK(hipMemcpy(L.agent, ag.data(), S * 2, hipMemcpyHostToDevice), "upload agent");
-    HIPCHK(hipMemcpy(L.deleted, del.data(), S, hipMemcpyHostToDevice), "upload deleted");
     HIPCHK(hipMemcpy(L.cp, c.data(), S * 4, hipMemcpyHostToDevice), "upload cp");
     return CRDT_HIP_OK;
 }
@@ -2144,7 +2134,6 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.in_parent = L.parent + w.slot0;
     a0.in_lamport = L.lamport + w.slot0;
     a0.in_agent = L.agent + w.slot0;
-    a0.in_deleted = L.deleted + w.slot0;
     a0.in_cp = L.cp + w.slot0;
     a0.jbits = jbits_;
     a0.jloc = jloc_;
@@ -2453,7 +2442,7 @@ int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t
     int rc = plan(R, docs);
     if (rc) return rc;
     k_synth_tree<<<grid_for(R.total_slots), kBlock, 0, stream>>>(
-        R.parent, R.lamport, R.agent, R.deleted, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
+        R.parent, R.lamport, R.agent, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
     HIPCHK(hipGetLastError(), "synth launch");
     HIPCHK(hipStreamSynchronize(stream), "synth");
     return CRDT_HIP_OK;
@@ -2485,8 +2474,8 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
             P.add[k] = (uint32_t)mix64(h, 2 * k + 1);
         }
         k_replicate<<<grid_for(n), kBlock, 0, stream>>>(
-            B.parent, B.lamport, B.agent, B.deleted, B.cp, B.doc_slot[b], R.parent, R.lamport,
-            R.agent, R.deleted, R.cp, R.doc_slot[r], P);
+            B.parent, B.lamport, B.agent, B.cp, B.doc_slot[b], R.parent, R.lamport, R.agent, R.cp,
+            R.doc_slot[r], P);
     }
     HIPCHK(hipGetLastError(), "replicate launch");
     HIPCHK(hipStreamSynchronize(stream), "replicate");

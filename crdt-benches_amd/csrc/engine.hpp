@@ -32,6 +32,10 @@ struct Wave {
     uint64_t max_doc_text;  // largest document text bound of the wave
 };
 
+// Tombstone flag of a device slot, folded into its codepoint word (one 4-byte stream instead of
+// a 4-byte and a 1-byte one; codepoints use 21 bits).
+constexpr uint32_t kDelBit = 0x80000000u;
+
 // Device-resident op logs in slot layout, planned into waves.
 struct DeviceLogs {
     uint32_t log2m = 6;
@@ -44,8 +48,7 @@ struct DeviceLogs {
     uint32_t* parent = nullptr;
     uint32_t* lamport = nullptr;
     uint16_t* agent = nullptr;
-    uint8_t* deleted = nullptr;
-    uint32_t* cp = nullptr;
+    uint32_t* cp = nullptr;        // codepoint (bits 0-20) | tombstone (bit 31, kDelBit)
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
     uint64_t cap_docs = 0, cap_chunks = 0;

@@ -11,8 +11,9 @@
 //   k_upd_items  per flattened item, 4 per thread: parent check; in the write pass the item's
 //                fields go to slot id.  Ids known before the update are skipped, so the first
 //                update carrying an id wins, exactly as in the sequential decoder
-//   k_upd_dels   per flattened delete: target check; in the write pass the tombstone byte is
-//                set by a word atomicOr, so a target deleted twice is counted once
+//   k_upd_dels   per flattened delete: target check; in the write pass the tombstone bit of
+//                the target's codepoint word is set by atomicOr, so a target deleted twice is
+//                counted once
 // The check passes run before the write passes on the same stream and the write passes do
 // nothing once any check failed: a rejected batch leaves the replica unchanged, and the host
 // waits once per batch.  Visible codepoints / bytes are kept incrementally from the items
@@ -88,8 +89,7 @@ struct UpdArgs {
     uint32_t* parent;
     uint32_t* lamport;
     uint16_t* agent;
-    uint8_t* deleted;
-    uint32_t* cp;
+    uint32_t* cp;  // codepoint | kDelBit
     uint64_t cap_slots;
 };
 
@@ -226,9 +226,8 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
                 const uint32_t c = a.buf[h.w + 3u * h.y + k];
                 a.parent[id] = par;
                 a.lamport[id] = a.buf[h.w + 2u * h.y + k];
-                a.cp[id] = c;
+                a.cp[id] = c & kCpMaskR;  // live
                 a.agent[id] = reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
-                a.deleted[id] = 0;
                 add_cp += 1u;
                 add_b += utf8_len(c & kCpMaskR);
             }
@@ -260,11 +259,10 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
             continue;
         }
         if (WRITE) {
-            const uint32_t sh = 8u * (id & 3u);
-            const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(a.deleted) + (id >> 2), 1u << sh);
-            if (((old >> sh) & 0xFFu) == 0u) {  // newly tombstoned
+            const uint32_t old = atomicOr(a.cp + id, kDelBit);
+            if (!(old & kDelBit)) {  // newly tombstoned
                 del_cp += 1u;
-                del_b += utf8_len(a.cp[id] & kCpMaskR);
+                del_b += utf8_len(old & kCpMaskR);
             }
         }
     }
@@ -281,15 +279,14 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
 // padding / unused slots: a tombstoned child of the document start with key 0 (never visible,
 // pruned by the merge)
 __global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint32_t* lamport,
-                                                 uint16_t* agent, uint8_t* deleted, uint32_t* cp,
+                                                 uint16_t* agent, uint32_t* cp,
                                                  uint64_t s0, uint64_t s1) {
     const uint64_t g = s0 + (uint64_t)blockIdx.x * kUB + threadIdx.x;
     if (g >= s1) return;
     parent[g] = 0;
     lamport[g] = 0;
     agent[g] = 0;
-    deleted[g] = 1;
-    cp[g] = 0;
+    cp[g] = kDelBit;
 }
 
 int hip_fail(Engine& E, const char* what, hipError_t e) {
@@ -338,11 +335,9 @@ int replica_reserve(Engine& E, Replica& r, uint64_t items) {
                                             std::max<uint64_t>({need, 2 * L.cap_slots, 4096}));
     uint32_t *par = nullptr, *lam = nullptr, *c = nullptr;
     uint16_t* ag = nullptr;
-    uint8_t* del = nullptr;
     hipError_t e = dalloc(&par, cap);
     if (e == hipSuccess) e = dalloc(&lam, cap);
     if (e == hipSuccess) e = dalloc(&ag, cap);
-    if (e == hipSuccess) e = dalloc(&del, cap);
     if (e == hipSuccess) e = dalloc(&c, cap);
     const uint64_t old = L.cap_slots;
     hipStream_t s = E.stream;
@@ -350,23 +345,21 @@ int replica_reserve(Engine& E, Replica& r, uint64_t items) {
         e = hipMemcpyAsync(par, L.parent, old * 4, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(lam, L.lamport, old * 4, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(ag, L.agent, old * 2, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(del, L.deleted, old, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(c, L.cp, old * 4, hipMemcpyDeviceToDevice, s);
     }
     if (e == hipSuccess) {
-        k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, lam, ag, del, c, old, cap);
+        k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, lam, ag, c, old, cap);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
-        dfree(par); dfree(lam); dfree(ag); dfree(del); dfree(c);
+        dfree(par); dfree(lam); dfree(ag); dfree(c);
         return hip_fail(E, "replica reserve", e);
     }
-    dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.deleted); dfree(L.cp);
+    dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.cp);
     L.parent = par;
     L.lamport = lam;
     L.agent = ag;
-    L.deleted = del;
     L.cp = c;
     L.cap_slots = cap;
     return CRDT_HIP_OK;
@@ -384,13 +377,15 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     RCHK(hipMemcpy(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice), "upload parent");
     RCHK(hipMemcpy(L.lamport + 1, v->lamport, n * 4ull, hipMemcpyHostToDevice), "upload lamport");
     RCHK(hipMemcpy(L.agent + 1, v->agent, n * 2ull, hipMemcpyHostToDevice), "upload agent");
-    RCHK(hipMemcpy(L.deleted + 1, v->deleted, n, hipMemcpyHostToDevice), "upload deleted");
-    RCHK(hipMemcpy(L.cp + 1, v->cp, n * 4ull, hipMemcpyHostToDevice), "upload cp");
-    for (uint32_t i = 0; i < n; ++i)
+    std::vector<uint32_t> c(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        c[i] = (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u);
         if (!v->deleted[i]) {
             r.vis_cp += 1;
             r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
         }
+    }
+    RCHK(hipMemcpy(L.cp + 1, c.data(), n * 4ull, hipMemcpyHostToDevice), "upload cp");
     return CRDT_HIP_OK;
 }
 
@@ -406,7 +401,6 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst) {
         RCHK(hipMemcpyAsync(D.parent, S.parent, cap * 4, hipMemcpyDeviceToDevice, s), "copy parent");
         RCHK(hipMemcpyAsync(D.lamport, S.lamport, cap * 4, hipMemcpyDeviceToDevice, s), "copy lamport");
         RCHK(hipMemcpyAsync(D.agent, S.agent, cap * 2, hipMemcpyDeviceToDevice, s), "copy agent");
-        RCHK(hipMemcpyAsync(D.deleted, S.deleted, cap, hipMemcpyDeviceToDevice, s), "copy deleted");
         RCHK(hipMemcpyAsync(D.cp, S.cp, cap * 4, hipMemcpyDeviceToDevice, s), "copy cp");
         RCHK(hipStreamSynchronize(s), "copy sync");
     }
@@ -465,7 +459,6 @@ int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     a.parent = L.parent;
     a.lamport = L.lamport;
     a.agent = L.agent;
-    a.deleted = L.deleted;
     a.cp = L.cp;
     a.cap_slots = L.cap_slots;
     const uint32_t gi = std::min<uint64_t>(kMaxGrid, grid_for(len / 16 / kItemsPerThread + 1, kUB));
