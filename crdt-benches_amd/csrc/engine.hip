@@ -336,6 +336,16 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         hm = (uint32_t)(a.hbits[gs >> 6] >> (gs & 63u)) & 0xFFFFu;
         nib = a.wnib[gs >> 4];
     }
+    // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
+    // offset is known: thread t's destination dword needs source dwords t and t+1 whatever the
+    // offset's alignment (the segment is kTileBytes long, so both are in bounds).
+    const uint8_t* src = a.stile + (uint64_t)tile * kTileBytes;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t w0 = 0, w1 = 0;
+    if (a.mode == 0) {
+        w0 = s32[threadIdx.x];
+        w1 = s32[threadIdx.x + 1];
+    }
     uint32_t W = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) W += (uint32_t)(nib >> (4 * j)) & 15u;
@@ -359,15 +369,9 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     }
     // text: the dwords of sbytes wholly inside [D, D + tw) are this tile's alone (funnel-shifted
     // from two source dwords); the partial dwords at either end are shared with the neighbouring
-    // tiles and written bytewise.  Loads first, records to LDS while they are in flight.
+    // tiles and written bytewise.
     const uint32_t D = pre.y, lo = (D + 3u) & ~3u, hi = (D + tw) & ~3u, sh = (lo - D) & 3u;
-    const uint8_t* src = a.stile + (uint64_t)tile * kTileBytes;
-    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
-    uint32_t m = lo + 4u * threadIdx.x, w0 = 0, w1 = 0;
-    if (a.mode == 0 && m < hi) {
-        w0 = s32[(m - D) >> 2];
-        if (sh) w1 = s32[((m - D) >> 2) + 1];
-    }
+    uint32_t m = lo + 4u * threadIdx.x;
     {
         uint32_t r = ex >> 16, p = ex & 0xFFFFu;
 #pragma unroll
