@@ -36,7 +36,9 @@ EXPORTS = [
     "crdt_hip_oplog_version", "crdt_hip_oplog_encode_from", "crdt_hip_oplog_apply_update",
     "crdt_hip_trace_load", "crdt_hip_trace_free", "crdt_hip_trace_len", "crdt_hip_trace_txns",
     "crdt_hip_trace_patch", "crdt_hip_trace_start_content", "crdt_hip_trace_end_content",
-    "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_synth_agents",
+    "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_trace_save",
+    "crdt_hip_oplog_save", "crdt_hip_oplog_load", "crdt_hip_logfile_open",
+    "crdt_hip_logfile_close", "crdt_hip_synth_agents",
     "crdt_hip_synth_tree", "crdt_hip_synth_tree_visible", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
     "crdt_hip_batch_create", "crdt_hip_batch_synth_tree", "crdt_hip_batch_free", "crdt_hip_batch_info",
     "crdt_hip_batch_merge", "crdt_hip_replica_new", "crdt_hip_replica_clone",
@@ -128,6 +130,11 @@ def lib() -> C.CDLL:
         "crdt_hip_trace_end_content": (i32, [vp, P(vp), P(sz)]),
         "crdt_hip_trace_chars_to_bytes": (i32, [vp]),
         "crdt_hip_trace_resolve": (i32, [vp, P(vp)]),
+        "crdt_hip_trace_save": (i32, [vp, C.c_char_p]),
+        "crdt_hip_oplog_save": (i32, [vp, C.c_char_p]),
+        "crdt_hip_oplog_load": (i32, [C.c_char_p, P(vp)]),
+        "crdt_hip_logfile_open": (i32, [C.c_char_p, P(vp), P(View)]),
+        "crdt_hip_logfile_close": (i32, [vp]),
         "crdt_hip_synth_agents": (i32, [u32, u32, u64, P(vp)]),
         "crdt_hip_synth_tree": (i32, [u32, u32, u32, u64, P(vp)]),
         "crdt_hip_synth_tree_visible": (i32, [u32, u32, u64, P(u64)]),
@@ -281,6 +288,16 @@ class OpLog:
     def apply_update(self, update: bytes) -> None:
         _check(lib().crdt_hip_oplog_apply_update(self._h, update, len(update)))
 
+    def save(self, path: str) -> None:
+        """Op-log file (crdt_hip_oplog_save): 64-byte-aligned SoA arrays."""
+        _check(lib().crdt_hip_oplog_save(self._h, path.encode()))
+
+    @staticmethod
+    def load(path: str) -> "OpLog":
+        h = C.c_void_p()
+        _check(lib().crdt_hip_oplog_load(path.encode(), C.byref(h)))
+        return OpLog(h)
+
     @staticmethod
     def synth_agents(n_items: int, agents: int, seed: int) -> "OpLog":
         h = C.c_void_p()
@@ -343,12 +360,52 @@ class Trace:
         _check(lib().crdt_hip_trace_resolve(self._h, C.byref(h)))
         return OpLog(h)
 
+    def save(self, path: str) -> None:
+        """Trace cache (crdt_hip_trace_save); Trace(path) reads it back without gunzip + JSON."""
+        _check(lib().crdt_hip_trace_save(self._h, path.encode()))
+
+
+class LogFile:
+    """An op-log file mapped read-only (crdt_hip_logfile_open): view() points into the mapping,
+    so it can be merged, batched or uploaded without a host copy."""
+
+    def __init__(self, path: str):
+        h = C.c_void_p()
+        self._v = View()
+        _check(lib().crdt_hip_logfile_open(path.encode(), C.byref(h), C.byref(self._v)))
+        self._h = h
+        self.path = path
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_logfile_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def view(self) -> View:
+        if not self._h:
+            raise ValueError("log file is closed")
+        return self._v
+
+    def arrays(self) -> LogArrays:
+        v, n = self.view(), self._v.n
+
+        def arr(ptr, dt):
+            if n == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
+        return LogArrays(arr(v.parent, np.uint32), arr(v.lamport, np.uint32),
+                         arr(v.agent, np.uint16), arr(v.deleted, np.uint8),
+                         arr(v.cp, np.uint32), arr(v.origin_right, np.uint32))
+
 
 def _as_view(log) -> tuple:
     """(View, keepalive) for an OpLog or LogArrays."""
     if isinstance(log, OpLog):
         return log.view(), log
-    if isinstance(log, LogArrays):
+    if isinstance(log, (LogArrays, LogFile)):
         return log.view(), log
     raise TypeError(type(log))
 

@@ -13,6 +13,7 @@
 #include "engine.hpp"
 #include "oplog.hpp"
 #include "replica.hpp"
+#include "store.hpp"
 #include "synth.hpp"
 #include "trace.hpp"
 #include "util.hpp"
@@ -306,6 +307,65 @@ int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out) {
         *out = L;
         return 0;
     });
+}
+
+// ---- binary files ----------------------------------------------------------------------------
+struct crdt_hip_logfile {
+    crdt::MappedLog m;
+};
+
+int crdt_hip_trace_save(const crdt_hip_trace* t, const char* path) {
+    if (!t || !path) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::string e = crdt::save_trace_bin(t->t, path);
+        return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EIO, e);
+    });
+}
+int crdt_hip_oplog_save(const crdt_hip_oplog* log, const char* path) {
+    if (!log || !path) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    return guard(nullptr, [&] {
+        std::string e = crdt::save_oplog(log->log, path);
+        return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EIO, e);
+    });
+}
+int crdt_hip_oplog_load(const char* path, crdt_hip_oplog** out) {
+    if (!path || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    *out = nullptr;
+    return guard(nullptr, [&] {
+        crdt_hip_oplog* L = new crdt_hip_oplog();
+        std::string e = crdt::load_oplog(path, L->log);
+        if (!e.empty()) {
+            delete L;
+            return set_err(nullptr, CRDT_HIP_EIO, e);
+        }
+        *out = L;
+        return 0;
+    });
+}
+int crdt_hip_logfile_open(const char* path, crdt_hip_logfile** out, crdt_hip_oplog_view* view) {
+    if (!path || !out || !view) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    *out = nullptr;
+    return guard(nullptr, [&] {
+        crdt_hip_logfile* f = new crdt_hip_logfile();
+        std::string e = crdt::map_oplog(path, f->m);
+        if (!e.empty()) {
+            delete f;
+            return set_err(nullptr, CRDT_HIP_EIO, e);
+        }
+        view->n = f->m.n;
+        view->parent = f->m.parent;
+        view->origin_right = f->m.oright;
+        view->lamport = f->m.lamport;
+        view->agent = f->m.agent;
+        view->deleted = f->m.deleted;
+        view->cp = f->m.cp;
+        *out = f;
+        return 0;
+    });
+}
+int crdt_hip_logfile_close(crdt_hip_logfile* f) {
+    delete f;
+    return 0;
 }
 
 // ---- synthetic -------------------------------------------------------------------------------

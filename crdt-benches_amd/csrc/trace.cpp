@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "store.hpp"
 #include "util.hpp"
 
 namespace crdt {
@@ -214,6 +215,7 @@ std::string parse_trace_json(const char* data, size_t n, Trace& t) {
 }
 
 std::string load_trace(const std::string& path, Trace& out) {
+    if (is_trace_bin(path)) return load_trace_bin(path, out);  // trace cache (store.hpp)
     std::string raw;
     std::string e = gunzip_file(path, raw);
     if (!e.empty()) return e;

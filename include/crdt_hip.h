@@ -57,6 +57,7 @@ typedef struct crdt_hip_oplog crdt_hip_oplog;
 typedef struct crdt_hip_trace crdt_hip_trace;
 typedef struct crdt_hip_batch crdt_hip_batch;
 typedef struct crdt_hip_replica crdt_hip_replica;
+typedef struct crdt_hip_logfile crdt_hip_logfile;
 
 /* Anchor op log, structure of arrays (borrowed view).  Item k (0-based) has id k+1.
  * parent = origin_left id (0 = document start).  Document order (RGA): pre-order of the tree
@@ -155,6 +156,21 @@ int crdt_hip_trace_end_content(const crdt_hip_trace* t, const char** s, size_t* 
 int crdt_hip_trace_chars_to_bytes(crdt_hip_trace* t);
 /* Replay every patch into a fresh op log (the upstream loop body of main.rs:29-34). */
 int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out);
+
+/* ---- binary files (skip gunzip + JSON; map resolved logs) ------------
+ * Trace cache: the parsed trace in one flat file; crdt_hip_trace_load reads either format
+ * (recognised by the file's magic), so a cache is a drop-in for the .json.gz path of
+ * load_testing_data (main.rs:19,52).  Op-log file: the resolved anchor log as 64-byte-aligned
+ * SoA arrays.  Files are written to `path`.tmp and renamed. */
+int crdt_hip_trace_save(const crdt_hip_trace* t, const char* path);
+int crdt_hip_oplog_save(const crdt_hip_oplog* log, const char* path);
+/* An editable op log read from a file (positional edits rebuild the resolver index first). */
+int crdt_hip_oplog_load(const char* path, crdt_hip_oplog** out);
+/* Map an op-log file read-only: *view points into the mapping (no copy) and stays valid until
+ * crdt_hip_logfile_close.  The view can be passed to crdt_hip_merge*, crdt_hip_batch_create and
+ * crdt_hip_replica_new. */
+int crdt_hip_logfile_open(const char* path, crdt_hip_logfile** out, crdt_hip_oplog_view* view);
+int crdt_hip_logfile_close(crdt_hip_logfile* f);
 
 /* ---- synthetic op logs -------------------------------- */
 /* 64-agent concurrent interleaved edits; `n_items` inserts, ~20% deletes, splitmix64 seed. */
