@@ -155,6 +155,16 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.max_wave_slots = value;
         return 0;
     }
+    if (k == "lanes") {
+        if (value < 1 || value > 8) return set_err(ctx, CRDT_HIP_EINVAL, "lanes must be in [1, 8]");
+        ctx->eng.lanes = (uint32_t)value;
+        return 0;
+    }
+    if (k == "lane_gate") {
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "lane_gate must be 0 or 1");
+        ctx->eng.l0_gated = value == 1;
+        return 0;
+    }
     if (k == "level1") {
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "level1 must be 0 (auto) or 1 (global)");
         ctx->eng.level1_global = value == 1;

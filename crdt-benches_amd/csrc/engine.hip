@@ -32,7 +32,10 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <mutex>
+#include <thread>
 
 #include "util.hpp"
 #include "wave.hpp"
@@ -2164,6 +2167,10 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     a0.r_pstart = r_pstart_;
 
     // ---- level 0: runs -------------------------------------------------------------------
+    // Lanes take turns at level 0 (an HBM stream): the gate is held from the first level-0 launch
+    // to the level-0 sync, so one lane's level 0 overlaps the others' latency-bound level 1.
+    std::unique_lock<std::mutex> gate;
+    if (l0_gate_) gate = std::unique_lock<std::mutex>(*l0_gate_);
     HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
     HIPCHK(hipMemsetAsync(jbits_, 0, (w.nslots / 32 + 4) * 4ull, s), "memset jump bits");
     BEGIN(S_CLASSIFY);
@@ -2180,6 +2187,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     HIPCHK(hipGetLastError(), "level-0 launch");
     HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "level-0 sync");
+    if (gate.owns_lock()) gate.unlock();
     if (host_ctl_[C_ERR]) {
         err = host_ctl_[C_ERR] & 4u ? "op log holds more text than planned"
                                     : "malformed op log: parent id out of range";
@@ -2390,6 +2398,7 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         err = "text output needs a single-wave merge";
         return CRDT_HIP_EINVAL;
     }
+    if (lanes > 1 && L.waves.size() > 1) return merge_lanes(L, mode, digests, lens, st);
     std::vector<float> stage_ms(S_N, 0.f);
     std::vector<uint32_t> stage_launches(S_N, 0);
     const uint32_t ndocs = (uint32_t)L.docs.size();
@@ -2434,6 +2443,97 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         float tot = 0;
         HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N + 1], ev_[2 * S_N + 2]), "event time");
         st->total_ns = (uint64_t)((double)tot * 1e6);
+    }
+    return CRDT_HIP_OK;
+}
+
+// Multi-wave merge over lanes: wave i runs on lane i % K, every lane in its own host thread on
+// its own stream and scratch (run_wave is synchronous per wave).  Stage times are summed over
+// the lanes (kernel time, which can exceed the wall time); total_ns is the host wall time.
+int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+                        crdt_hip_stats* st) {
+    const uint32_t nw = (uint32_t)L.waves.size();
+    const uint32_t K = std::min<uint32_t>(lanes, nw);
+    while (lane_eng_.size() + 1 < K) {
+        auto e = std::make_unique<Engine>();
+        const std::string m = e->init(device);
+        if (!m.empty()) {
+            err = "lane engine: " + m;
+            return CRDT_HIP_EDEVICE;
+        }
+        lane_eng_.push_back(std::move(e));
+    }
+    std::vector<Engine*> eng(K, this);
+    std::mutex gate;
+    for (uint32_t i = 1; i < K; ++i) {
+        eng[i] = lane_eng_[i - 1].get();
+        eng[i]->log2m = log2m;
+        eng[i]->log2m_set = log2m_set;
+        eng[i]->level1_global = level1_global;
+    }
+    const uint32_t ndocs = (uint32_t)L.docs.size();
+    std::vector<int> rc(K, CRDT_HIP_OK);
+    std::vector<std::vector<float>> ms(K, std::vector<float>(S_N, 0.f));
+    std::vector<std::vector<uint32_t>> nl(K, std::vector<uint32_t>(S_N, 0));
+    auto lane = [&](uint32_t i) {
+        Engine& E = *eng[i];
+        const hipError_t e = hipSetDevice(device);  // the current device is per host thread
+        if (e != hipSuccess) {
+            rc[i] = E.fail("hipSetDevice", e);
+            return;
+        }
+        E.runs_ = 0;
+        E.l0_gate_ = l0_gated ? &gate : nullptr;
+        for (uint32_t wi = i; wi < nw && rc[i] == CRDT_HIP_OK; wi += K) {
+            rc[i] = E.ensure_scratch(L.waves[wi], ndocs);
+            if (rc[i] == CRDT_HIP_OK) rc[i] = E.run_wave(L, L.waves[wi], mode, ms[i], nl[i]);
+        }
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    th.reserve(K - 1);
+    for (uint32_t i = 1; i < K; ++i) th.emplace_back(lane, i);
+    lane(0);
+    for (std::thread& t : th) t.join();
+    for (uint32_t i = 0; i < K; ++i) eng[i]->l0_gate_ = nullptr;
+    const double wall_ns =
+        std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+    for (uint32_t i = 0; i < K; ++i)
+        if (rc[i] != CRDT_HIP_OK) {
+            if (i) err = eng[i]->err;
+            return rc[i];
+        }
+    uint64_t text_bytes = 0, runs = 0;
+    for (uint32_t wi = 0; wi < nw; ++wi) {
+        const Engine& E = *eng[wi % K];
+        const Wave& w = L.waves[wi];
+        for (uint32_t d = w.first_doc; d < w.first_doc + w.ndocs; ++d) {
+            if (lens) lens[d] = E.host_len_[d];
+            if (digests) digests[d] = E.host_dig_[d];
+            text_bytes += E.host_len_[d];
+        }
+    }
+    for (uint32_t i = 0; i < K; ++i) runs += eng[i]->runs_;
+    runs_ = runs;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->items = L.items;
+        st->docs = ndocs;
+        st->text_bytes = text_bytes;
+        st->runs = runs;
+        st->waves = nw;
+        st->nstages = S_N;
+        for (int s = 0; s < S_N; ++s) {
+            double t = 0;
+            uint32_t n = 0;
+            for (uint32_t i = 0; i < K; ++i) {
+                t += ms[i][s];
+                n += nl[i][s];
+            }
+            st->stage_ns[s] = (uint64_t)(t * 1e6);
+            st->stage_launches[s] = n;
+        }
+        st->total_ns = (uint64_t)wall_ns;
     }
     return CRDT_HIP_OK;
 }

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -69,6 +71,11 @@ public:
     bool log2m_set = false;                // set by the caller; else chosen per wave from R
     uint64_t max_wave_slots = 1ull << 30;
     bool level1_global = false;            // never use the per-document LDS level 1
+    // Waves merged at once by a multi-wave merge, each on a lane of its own: a helper engine
+    // (non-blocking stream + scratch) driven by its own host thread.  The latency-bound level 1
+    // of one wave then overlaps the HBM-bound level 0 of another.
+    uint32_t lanes = 2;
+    bool l0_gated = true;  // lanes take turns at level 0 (see run_wave)
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -125,7 +132,11 @@ private:
     uint64_t cap_host_docs_ = 0;
     uint64_t runs_ = 0;
     std::vector<hipEvent_t> ev_;
+    std::vector<std::unique_ptr<Engine>> lane_eng_;  // lanes 1..lanes-1 (lane 0 = this)
+    std::mutex* l0_gate_ = nullptr;                  // set by merge_lanes
 
+    int merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+                    crdt_hip_stats* st);
     int ensure_runs(uint64_t runs, uint64_t splitters);
     int ensure_scratch(const Wave& w, uint32_t ndocs_total);
     int run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,

@@ -114,7 +114,10 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
 /* Tuning: "splitter_stride" of the global list ranking (power of two, 16..4096; default 16),
  * "max_wave_slots" per device wave (default 2^30), and "level1": 0 = per-document LDS merge of
  * the run tree whenever every document of a wave fits a workgroup's LDS (default), 1 = always
- * the global (multi-kernel) level-1 path. Results never depend on these. */
+ * the global (multi-kernel) level-1 path, and "lanes" (1..8, default 2): waves of a multi-wave
+ * merge run concurrently on that many streams, each with its own scratch (1 = one after the
+ * other), "lane_gate" (default 1: lanes take turns at the HBM-bound level 0). Results never
+ * depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 
 /* ---- op log: host-side resolver (positional patch -> anchor op) ---------------------------- */

@@ -177,6 +177,47 @@ def test_splitter_stride_and_waves_do_not_change_results(oracle, stride):
     c.close()
 
 
+@pytest.mark.parametrize("lanes", [2, 3, 8])
+@pytest.mark.parametrize("level1", [0, 1])
+def test_concurrent_wave_lanes_do_not_change_results(golden, lanes, level1):
+    """Waves of one merge run on `lanes` streams at once (Engine::merge_lanes): every replica's
+    digest and length equal the one-lane merge's and the trace's, and every run is counted once."""
+    bases = [resolved(n) for n in TRACES]
+    out = {}
+    for k in (1, lanes):
+        c = crdt_hip.Context(0)
+        c.set_param("lanes", k)
+        c.set_param("level1", level1)
+        c.set_param("max_wave_slots", 1 << 20)  # 3 replicas x 4 traces: several waves
+        b = c.batch(bases, replicas=3, relabel="rotate", seed=77)
+        for _ in range(2):  # the second merge reuses every lane's scratch
+            dig, lens, st = b.merge()
+        assert st["waves"] >= 3
+        out[k] = (dig.copy(), lens.copy(), st["runs"], st["stage_launches"]["classify"])
+        b.close()
+        c.close()
+    assert np.array_equal(out[1][0], out[lanes][0]) and np.array_equal(out[1][1], out[lanes][1])
+    assert out[1][2:] == out[lanes][2:]
+    for r in range(len(out[1][0])):
+        name = TRACES[r % 4]
+        assert "%016x" % out[lanes][0][r] == golden[name]["tree_digest"], r
+        assert out[lanes][1][r] == golden[name]["end_bytes"], r
+
+
+def test_concurrent_wave_lanes_report_a_malformed_wave():
+    c = crdt_hip.Context(0)
+    c.set_param("lanes", 4)
+    c.set_param("max_wave_slots", 1 << 20)
+    good = [resolved(n) for n in TRACES]
+    bad = crdt_hip.LogArrays([0, 5], [1, 2], [0, 0], [0, 0], [97, 98])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        c.merge_batch(good + [bad] + good)
+    assert e.value.code == -5
+    dig, lens = c.merge_batch(good + good)  # every lane recovers
+    assert np.array_equal(dig[:4], dig[4:]) and all(int(x) > 0 for x in lens)
+    c.close()
+
+
 @pytest.mark.parametrize("relabel", ["none", "rotate", "shuffle"])
 def test_replica_batch_relabel_invariance(ctx, oracle, golden, relabel):
     """Config 3 shape at small scale: relabelled HBM replicas merge to the trace documents."""
