@@ -310,6 +310,8 @@ def main() -> int:
     ap.add_argument("--replicas", type=int, default=4096, help="replicas of each trace per GPU")
     ap.add_argument("--relabel", default="rotate", choices=["none", "rotate", "shuffle"])
     ap.add_argument("--splitter-stride", type=int, default=0)
+    ap.add_argument("--wave-slots-log2", type=int, default=30,
+                    help="slots per device wave (2^N; smaller waves pipeline better over lanes)")
     ap.add_argument("--lane-gate", type=int, default=1, choices=[0, 1],
                     help="1: lanes take turns at level 0 (the HBM stream)")
     ap.add_argument("--lanes", type=int, default=2,
@@ -362,6 +364,7 @@ def main() -> int:
     ctx.set_param("level1", args.level1)
     ctx.set_param("lanes", args.lanes)
     ctx.set_param("lane_gate", args.lane_gate)
+    ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     batch = ctx.batch(bases, replicas=args.replicas, relabel=args.relabel,
                       seed=0x5EED0003 + 7919 * rank)
     if rank == 0:

@@ -287,6 +287,31 @@ def test_level1_lds_path_is_taken_for_trace_batches(ctx):
     assert st["stage_launches"]["expand"] == 0
 
 
+@pytest.mark.parametrize("shape", ["typing", "tree"])
+def test_tiles_above_the_lds_text_stage(ctx, oracle, shape):
+    """Tiles holding more than k_classify's 8 KiB LDS text stage (4-byte characters, nearly all
+    visible) take the direct-store path; the document must still equal the oracle's."""
+    rng = np.random.default_rng(7 if shape == "typing" else 8)
+    n = 50_000
+    ids = np.arange(1, n + 1, dtype=np.uint32)
+    if shape == "typing":
+        parent = ids - 1
+        deleted = np.zeros(n, np.uint8)
+    else:
+        parent = np.where(rng.random(n) < 0.8, ids - 1, rng.integers(0, ids, dtype=np.uint32))
+        deleted = (rng.random(n) < 0.05).astype(np.uint8)
+    cp = rng.integers(0x10000, 0x110000, n, dtype=np.uint32)
+    cp[::7] = rng.integers(0x800, 0xD800, len(cp[::7]), dtype=np.uint32)  # some 3-byte ones
+    lg = crdt_hip.LogArrays(parent, ids, np.zeros(n, np.uint16), deleted, cp)
+    text, dig = ctx.merge(lg)
+    ref = oracle.merge(to_anchor(lg))
+    assert len(ref) > 3 * n and text == ref and dig == oracle.tree_digest(ref)
+    b = ctx.batch([lg], replicas=3, relabel="shuffle", seed=3)  # resident, relabelled
+    d3, l3, _ = b.merge()
+    assert all(int(x) == dig for x in d3) and all(int(x) == len(ref) for x in l3)
+    b.close()
+
+
 def test_malformed_logs_are_rejected(ctx):
     bad_parent = crdt_hip.LogArrays([0, 5], [1, 2], [0, 0], [0, 0], [97, 98])
     with pytest.raises(crdt_hip.CrdtHipError) as e:
