@@ -31,9 +31,9 @@ namespace crdt {
 namespace {
 
 constexpr int kUB = 256;            // threads per block (updates per block in parse / scan)
-constexpr int kItemsPerThread = 4;
+constexpr int kItemsPerThread = 1;
 constexpr uint32_t kCpMaskR = 0x001FFFFFu;
-constexpr uint32_t kMaxGrid = 4096;
+constexpr uint32_t kMaxGrid = 1024;  // write passes: one counter atomic per block
 
 // device counters (u64)
 enum UCtl { U_ERR = 0, U_ITEMS, U_DELS, U_MAXID, U_ADD_CP, U_ADD_B, U_DEL_CP, U_DEL_B, U_N };
@@ -72,6 +72,20 @@ __device__ __forceinline__ uint32_t block_excl_max(uint32_t x, uint32_t* lds, ui
     total = tot;
     const uint32_t prev = (uint32_t)__shfl_up((int)inc, 1);
     return max(off, lane ? prev : 0u);
+}
+
+// Sum of x over the block, valid in thread 0 (a device-wide counter then takes one atomic per
+// block: thousands of same-address atomics, one per wave, serialise at the L2 and cost more
+// than the decode itself).
+__device__ __forceinline__ uint32_t block_sum_t0(uint32_t x, uint32_t* lds) {
+    x = wave_sum(x);
+    if ((threadIdx.x & 63u) == 0) lds[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint32_t t = 0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < kUB / 64; ++i) t += lds[i];
+    __syncthreads();
+    return t;
 }
 
 struct UpdArgs {
@@ -235,8 +249,9 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
     }
     if (err) atomicOr((unsigned long long*)&a.ctl[U_ERR], (unsigned long long)err);
     if (WRITE) {
-        const uint32_t s0 = wave_sum(add_cp), s1 = wave_sum(add_b);
-        if ((threadIdx.x & 63u) == 0 && s0) {
+        __shared__ uint32_t red[kUB / 64];
+        const uint32_t s0 = block_sum_t0(add_cp, red), s1 = block_sum_t0(add_b, red);
+        if (threadIdx.x == 0 && s0) {
             atomicAdd((unsigned long long*)&a.ctl[U_ADD_CP], (unsigned long long)s0);
             atomicAdd((unsigned long long*)&a.ctl[U_ADD_B], (unsigned long long)s1);
         }
@@ -268,8 +283,9 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
     }
     if (err) atomicOr((unsigned long long*)&a.ctl[U_ERR], (unsigned long long)err);
     if (WRITE) {
-        const uint32_t s0 = wave_sum(del_cp), s1 = wave_sum(del_b);
-        if ((threadIdx.x & 63u) == 0 && s0) {
+        __shared__ uint32_t red[kUB / 64];
+        const uint32_t s0 = block_sum_t0(del_cp, red), s1 = block_sum_t0(del_b, red);
+        if (threadIdx.x == 0 && s0) {
             atomicAdd((unsigned long long*)&a.ctl[U_DEL_CP], (unsigned long long)s0);
             atomicAdd((unsigned long long*)&a.ctl[U_DEL_B], (unsigned long long)s1);
         }
