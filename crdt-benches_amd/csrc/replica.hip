@@ -336,7 +336,7 @@ Replica::~Replica() {
     dfree(uscan);
     dfree(ublk);
     dfree(uctl);
-    if (hctl) (void)hipHostFree(hctl);
+    pool_free(hctl, true);
 }
 
 int replica_reserve(Engine& E, Replica& r, uint64_t items) {
@@ -455,7 +455,7 @@ int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     }
     RCHK(grow(&r.ublk, r.ublk_cap, (uint64_t)nblk), "hipMalloc update blocks");
     if (!r.uctl) RCHK(dalloc(&r.uctl, (uint64_t)U_N), "hipMalloc update counters");
-    if (!r.hctl) RCHK(hipHostMalloc(reinterpret_cast<void**>(&r.hctl), U_N * 8), "hipHostMalloc");
+    if (!r.hctl) RCHK(pool_alloc(reinterpret_cast<void**>(&r.hctl), U_N * 8, true), "hipHostMalloc");
     RCHK(hipMemcpyAsync(r.ubuf, buf, len, hipMemcpyHostToDevice, s), "upload updates");
     RCHK(hipMemcpyAsync(r.uoff, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice, s),
          "upload update offsets");

@@ -2,6 +2,8 @@
 #include "util.hpp"
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 namespace crdt {
@@ -53,6 +55,110 @@ uint64_t tree_digest(const uint8_t* text, size_t len) {
         hs.swap(gs);
     }
     return xxh64(hs.data(), hs.size() * 8, (uint64_t)len);
+}
+
+namespace {
+constexpr size_t kPoolMaxBlock = 256ull << 20;  // larger blocks go straight to HIP
+constexpr size_t kPoolMaxCached = 4ull << 30;   // bytes kept per pool
+
+struct Pool {
+    std::mutex mu;
+    std::unordered_map<void*, uint64_t> live;                 // pooled block -> key
+    std::unordered_map<uint64_t, std::vector<void*>> cached;  // key -> free blocks
+    size_t cached_bytes = 0;
+};
+
+Pool& pool(bool host) {
+    static Pool dev, hst;
+    return host ? hst : dev;
+}
+
+size_t size_class(size_t bytes) {
+    size_t c = 256;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+hipError_t raw_alloc(void** p, size_t bytes, bool host) {
+    return host ? hipHostMalloc(p, bytes) : hipMalloc(p, bytes);
+}
+void raw_free(void* p, bool host) { (void)(host ? hipHostFree(p) : hipFree(p)); }
+
+// Return every cached block to HIP (on an allocation failure).
+void drain(Pool& P, bool host) {
+    std::vector<void*> blocks;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        for (auto& kv : P.cached)
+            for (void* b : kv.second) blocks.push_back(b);
+        P.cached.clear();
+        P.cached_bytes = 0;
+    }
+    for (void* b : blocks) raw_free(b, host);
+}
+}  // namespace
+
+hipError_t pool_alloc(void** p, size_t bytes, bool host) {
+    *p = nullptr;
+    if (bytes > kPoolMaxBlock) return raw_alloc(p, bytes, host);
+    int dev = 0;
+    if (!host) (void)hipGetDevice(&dev);
+    const size_t c = size_class(bytes);
+    const uint64_t key = ((uint64_t)dev << 48) | c;
+    Pool& P = pool(host);
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto it = P.cached.find(key);
+        if (it != P.cached.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            P.cached_bytes -= c;
+            P.live[*p] = key;
+            return hipSuccess;
+        }
+    }
+    hipError_t e = raw_alloc(p, c, host);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        drain(P, host);
+        e = raw_alloc(p, c, host);
+    }
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
+    std::lock_guard<std::mutex> g(P.mu);
+    P.live[*p] = key;
+    return hipSuccess;
+}
+
+void pool_free(void* p, bool host) {
+    if (!p) return;
+    Pool& P = pool(host);
+    uint64_t key = 0;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto it = P.live.find(p);
+        if (it != P.live.end()) {
+            key = it->second;
+            P.live.erase(it);
+        }
+    }
+    if (!key) {  // not pooled (a large block)
+        raw_free(p, host);
+        return;
+    }
+    (void)hipDeviceSynchronize();  // what hipFree would wait for
+    const size_t c = (size_t)(key & ((1ull << 48) - 1));
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        if (P.cached_bytes + c <= kPoolMaxCached) {
+            P.cached[key].push_back(p);
+            P.cached_bytes += c;
+            return;
+        }
+    }
+    raw_free(p, host);
 }
 
 }  // namespace crdt

@@ -10,6 +10,14 @@ namespace crdt {
 
 constexpr uint32_t NIL = 0xFFFFFFFFu;
 
+// Caching allocator (util.cpp) for device blocks and pinned host blocks up to 256 MiB: freed
+// blocks are kept per device and power-of-two size class and handed out again, so objects made
+// and dropped every step (the downstream loop clones a replica, applies a batch, merges and
+// drops it) do not pay hipMalloc / hipFree each time.  pool_free synchronises the device before
+// caching a block, as hipFree would, so a cached block is never still in use by queued work.
+hipError_t pool_alloc(void** p, size_t bytes, bool host = false);
+void pool_free(void* p, bool host = false);
+
 inline size_t utf8_len_cp(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
 
 inline size_t utf8_put(uint32_t c, char* o) {

@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "util.hpp"
+
 namespace crdt {
 namespace {
 
@@ -55,11 +57,11 @@ template <class T>
 hipError_t dalloc(T** p, uint64_t count) {
     *p = nullptr;
     if (count == 0) count = 1;
-    return hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+    return pool_alloc(reinterpret_cast<void**>(p), count * sizeof(T));
 }
 template <class T>
 void dfree(T*& p) {
-    if (p) (void)hipFree(p);
+    pool_free(p);
     p = nullptr;
 }
 inline uint32_t grid_for(uint64_t n, uint32_t block = 256) {
