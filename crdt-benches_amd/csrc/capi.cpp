@@ -41,6 +41,11 @@ struct crdt_hip_replica {
     crdt::Replica r;
 };
 
+struct crdt_hip_updates {
+    crdt_hip_ctx* ctx = nullptr;
+    crdt::UpdateBatch u;
+};
+
 namespace {
 thread_local std::string g_err;
 
@@ -567,6 +572,34 @@ int crdt_hip_replica_apply_updates(crdt_hip_ctx* ctx, crdt_hip_replica* r, const
     if (r->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "replica belongs to another context");
     return guard(ctx, [&] {
         return from_engine(ctx, crdt::replica_apply(ctx->eng, r->r, buf, len, offsets, n));
+    });
+}
+int crdt_hip_updates_upload(crdt_hip_ctx* ctx, const uint8_t* buf, size_t len,
+                            const uint64_t* offsets, uint32_t n, crdt_hip_updates** out) {
+    if (!ctx || !out) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    return guard(ctx, [&] {
+        crdt_hip_updates* u = new crdt_hip_updates();
+        u->ctx = ctx;
+        int rc = crdt::updates_upload(ctx->eng, u->u, buf, len, offsets, n);
+        if (rc) {
+            delete u;
+            return from_engine(ctx, rc);
+        }
+        *out = u;
+        return 0;
+    });
+}
+int crdt_hip_updates_free(crdt_hip_updates* u) {
+    delete u;
+    return 0;
+}
+int crdt_hip_replica_apply_resident(crdt_hip_ctx* ctx, crdt_hip_replica* r,
+                                    const crdt_hip_updates* u) {
+    if (!ctx || !r || !u) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (r->ctx != ctx || u->ctx != ctx)
+        return set_err(ctx, CRDT_HIP_EINVAL, "replica or updates belong to another context");
+    return guard(ctx, [&] {
+        return from_engine(ctx, crdt::replica_apply_resident(ctx->eng, r->r, u->u));
     });
 }
 int crdt_hip_replica_info(const crdt_hip_replica* r, uint64_t* items,

@@ -426,8 +426,42 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst) {
     return CRDT_HIP_OK;
 }
 
+int updates_upload(Engine& E, UpdateBatch& ub, const uint8_t* buf, uint64_t len,
+                   const uint64_t* offsets, uint32_t n) {
+    if (n && (!buf || !offsets)) {
+        E.err = "null update buffer or offsets";
+        return CRDT_HIP_EINVAL;
+    }
+    if (len >= (1ull << 32) - 16) {
+        E.err = "update batch of 4 GiB or more";
+        return CRDT_HIP_ERANGE;
+    }
+    RCHK(hipSetDevice(E.device), "hipSetDevice");
+    RCHK(dalloc(&ub.buf, (len + 4) & ~3ull), "hipMalloc update buffer");
+    RCHK(dalloc(&ub.off, n + 1ull), "hipMalloc update offsets");
+    if (len) RCHK(hipMemcpy(ub.buf, buf, len, hipMemcpyHostToDevice), "upload updates");
+    if (n) RCHK(hipMemcpy(ub.off, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice), "upload offsets");
+    ub.len = len;
+    ub.n = n;
+    return CRDT_HIP_OK;
+}
+
+UpdateBatch::~UpdateBatch() {
+    dfree(buf);
+    dfree(off);
+}
+
 int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
                   const uint64_t* offsets, uint32_t n) {
+    return replica_decode(E, r, buf, len, offsets, n, false);
+}
+
+int replica_apply_resident(Engine& E, Replica& r, const UpdateBatch& ub) {
+    return replica_decode(E, r, ub.buf, ub.len, ub.off, ub.n, true);
+}
+
+int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                   const uint64_t* offsets, uint32_t n, bool resident) {
     if (n == 0) return CRDT_HIP_OK;
     if (!buf || !offsets) {
         E.err = "null update buffer or offsets";
@@ -443,7 +477,7 @@ int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     int rc = replica_reserve(E, r, (uint64_t)r.n + len / 16 + 1);
     if (rc) return rc;
     const uint32_t nblk = (n + kUB - 1) / kUB;
-    RCHK(grow(&r.ubuf, r.ubuf_cap, (len + 4) & ~3ull), "hipMalloc update buffer");
+    if (!resident) RCHK(grow(&r.ubuf, r.ubuf_cap, (len + 4) & ~3ull), "hipMalloc update buffer");
     if (n + 1ull > r.ucap) {
         dfree(r.uoff); dfree(r.uhdr); dfree(r.uscan);
         r.ucap = 0;
@@ -456,14 +490,16 @@ int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     RCHK(grow(&r.ublk, r.ublk_cap, (uint64_t)nblk), "hipMalloc update blocks");
     if (!r.uctl) RCHK(dalloc(&r.uctl, (uint64_t)U_N), "hipMalloc update counters");
     if (!r.hctl) RCHK(pool_alloc(reinterpret_cast<void**>(&r.hctl), U_N * 8, true), "hipHostMalloc");
-    RCHK(hipMemcpyAsync(r.ubuf, buf, len, hipMemcpyHostToDevice, s), "upload updates");
-    RCHK(hipMemcpyAsync(r.uoff, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice, s),
-         "upload update offsets");
+    if (!resident) {
+        RCHK(hipMemcpyAsync(r.ubuf, buf, len, hipMemcpyHostToDevice, s), "upload updates");
+        RCHK(hipMemcpyAsync(r.uoff, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice, s),
+             "upload update offsets");
+    }
     RCHK(hipMemsetAsync(r.uctl, 0, U_N * 8, s), "memset update counters");
     DeviceLogs& L = r.logs;
     UpdArgs a{};
-    a.buf = reinterpret_cast<const uint32_t*>(r.ubuf);
-    a.off = r.uoff;
+    a.buf = reinterpret_cast<const uint32_t*>(resident ? buf : r.ubuf);
+    a.off = resident ? offsets : r.uoff;
     a.n = n;
     a.len = len;
     a.hdr = r.uhdr;

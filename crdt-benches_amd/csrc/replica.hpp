@@ -37,6 +37,28 @@ struct Replica {
     ~Replica();
 };
 
+// A batch of encoded updates resident in HBM (uploaded once, applied to any replica of the
+// context without a PCIe transfer).
+struct UpdateBatch {
+    uint8_t* buf = nullptr;   // the updates, concatenated (each 4-aligned)
+    uint64_t* off = nullptr;  // n + 1 byte offsets
+    uint64_t len = 0;
+    uint32_t n = 0;
+
+    UpdateBatch() = default;
+    UpdateBatch(const UpdateBatch&) = delete;
+    UpdateBatch& operator=(const UpdateBatch&) = delete;
+    ~UpdateBatch();
+};
+
+int updates_upload(Engine& E, UpdateBatch& ub, const uint8_t* buf, uint64_t len,
+                   const uint64_t* offsets, uint32_t n);
+// As replica_apply, with the batch already in HBM.
+int replica_apply_resident(Engine& E, Replica& r, const UpdateBatch& ub);
+// The decode itself: buf/offsets are host pointers (uploaded first) or, if resident, device ones.
+int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                   const uint64_t* offsets, uint32_t n, bool resident);
+
 // Room for ids 0..items (slot arrays grow by doubling; new slots are padding).
 int replica_reserve(Engine& E, Replica& r, uint64_t items);
 // Initial contents (Downstream's initial CRDT; may be empty).

@@ -57,6 +57,7 @@ typedef struct crdt_hip_oplog crdt_hip_oplog;
 typedef struct crdt_hip_trace crdt_hip_trace;
 typedef struct crdt_hip_batch crdt_hip_batch;
 typedef struct crdt_hip_replica crdt_hip_replica;
+typedef struct crdt_hip_updates crdt_hip_updates;
 typedef struct crdt_hip_logfile crdt_hip_logfile;
 
 /* Anchor op log, structure of arrays (borrowed view).  Item k (0-based) has id k+1.
@@ -238,6 +239,15 @@ int crdt_hip_replica_free(crdt_hip_replica* r);
  * multiple of 4, offsets[n] <= len < 4 GiB), in order (apply_update, rope.rs:222-224). */
 int crdt_hip_replica_apply_updates(crdt_hip_ctx* ctx, crdt_hip_replica* r, const uint8_t* buf,
                                    size_t len, const uint64_t* offsets, uint32_t n);
+/* A batch of encoded updates (layout as crdt_hip_replica_apply_updates) uploaded to HBM once:
+ * Downstream's `updates` vector held on the device (main.rs:58), so that applying it to a fresh
+ * clone every iteration (main.rs:64-67) moves no bytes over PCIe. */
+int crdt_hip_updates_upload(crdt_hip_ctx* ctx, const uint8_t* buf, size_t len,
+                            const uint64_t* offsets, uint32_t n, crdt_hip_updates** out);
+int crdt_hip_updates_free(crdt_hip_updates* u);
+/* crdt_hip_replica_apply_updates with a resident batch (same semantics and validation). */
+int crdt_hip_replica_apply_resident(crdt_hip_ctx* ctx, crdt_hip_replica* r,
+                                    const crdt_hip_updates* u);
 /* Items held, visible codepoints (Upstream::len, rope.rs:16-19) and visible UTF-8 bytes. */
 int crdt_hip_replica_info(const crdt_hip_replica* r, uint64_t* items,
                           uint64_t* visible_codepoints, uint64_t* visible_bytes);

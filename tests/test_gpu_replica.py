@@ -188,3 +188,37 @@ def test_downstream_device_bench_loop(golden):
             crdt.apply_update(u)
         assert crdt.len() == len(t.end_content)         # main.rs:68 (codepoints here)
         assert hashlib.sha256(crdt.text().encode()).hexdigest() == golden[name]["sha256"]
+
+
+@pytest.mark.parametrize("name", TRACES)
+def test_resident_update_batch_matches_host_batch(ctx, golden, name):
+    """crdt_hip_replica_apply_resident: the update vector uploaded once, applied to fresh clones
+    (main.rs:64-67 with the updates in HBM) gives the same replica as the host-buffer path."""
+    t, patches, updates = trace_updates(name)
+    buf, offs = crdt_hip.pack_updates(updates)
+    ub = crdt_hip.UpdateBatch(ctx, buf, offs)
+    init = crdt_hip.Replica(ctx)
+    via_host = init.clone()
+    via_host.apply_packed(buf, offs)
+    for _ in range(2):  # the batch is reusable
+        r = init.clone()
+        r.apply_resident(ub)
+        assert r.info() == via_host.info()
+        n, dig = r.merge_digest()
+        assert (n, "%016x" % dig) == (golden[name]["end_bytes"], golden[name]["tree_digest"])
+        r.close()
+    # applying it again is a no-op (every id already known)
+    via_host.apply_resident(ub)
+    assert via_host.merge_digest()[0] == golden[name]["end_bytes"]
+    ub.close()
+
+
+def test_resident_update_batch_rejects_bad_updates(ctx):
+    t, patches, updates = trace_updates("sveltecomponent")
+    buf, offs = crdt_hip.pack_updates(updates[1:50])  # update 0 missing: not causally ready
+    ub = crdt_hip.UpdateBatch(ctx, buf, offs)
+    r = crdt_hip.Replica(ctx)
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        r.apply_resident(ub)
+    assert e.value.code == -5 and r.info()[0] == 0
+    ub.close()
