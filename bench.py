@@ -7,23 +7,34 @@ host into anchor op logs (untimed, like the reference's load at main.rs:19), mat
 `--replicas` independent relabelled HBM copies each (4 x 4096 = 16,384 documents, 4.14 G items
 per GPU by default), merged by the gfx950 kernels to per-document text + digest.
 
-value = patches merged per second, whole job: sum over ranks of (patches per replica set x
-replicas) / max-over-ranks step time; the reference's accounting unit is criterion's
+value = patches merged per second, whole job: sum over ranks of the patches each rank merged per
+step / max-over-ranks step time; the reference's accounting unit is criterion's
 Throughput::Elements(trace.len()) = patches (/root/reference/src/main.rs:25,58).
 
-Multi-GPU (torchrun, one process per GPU): replicas shard with no data-path collective (weak
-scaling); after timing, the per-document digests are all-gathered over RCCL through the
-engine's C ABI (crdt_hip_allgather_u64) and rank 0 checks every one against the golden digest
-of the trace's endContent.
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) this process is one rank; with
+`--gpus N` and no WORLD_SIZE it starts N rank processes itself (before any GPU call) and exits
+with their status.  Replicas shard with no data-path collective (weak scaling).  After timing,
+every rank's counters (patches, items, runs, text bytes, elapsed and device ns, digest check)
+and its per-document digests are all-gathered over RCCL through the engine's C ABI
+(crdt_hip_allgather_u64); rank 0 takes the max elapsed time and checks every digest against the
+golden digest of the trace's endContent.  torch.distributed (gloo) is the control plane only:
+the barriers around the timed region and the RCCL unique-id broadcast.
 
 cpu_baseline: the oracle's sequential RGA merge (oracle/oracle.c orc_merge_many), one document
-per thread over the box's host cores, on a bounded sample of the same documents.
+per thread over every CPU this process may run on, on a bounded sample of the same documents.
+config1: the oracle's positional replay (orc_replay, one core) of automerge-paper, timed like the
+reference's upstream closure (main.rs:28-36), beside the engine's own upstream path (host
+resolve + device merge of the same trace).
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,14 +44,18 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
 
-import crdt_hip  # noqa: E402
+crdt_hip = None  # the engine binding, imported once this process knows it is a rank
 
 TRACES = ["automerge-paper", "rustcode", "sveltecomponent", "seph-blog1"]
 METRIC = "merged CRDT ops/sec (whole node) + achieved HBM GB/s, batched trace merge"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# SURVEY.md §8(d) algorithmic-bytes contract: 117 B per op-log item + survivor bytes
-PIPE_B_PER_ITEM = 117.0
-# Per-kernel algorithmic bytes (DESIGN.md §Roofline): each kernel's declared inputs read once +
+# Minimum HBM traffic of the design (the §8(d) contract restated once for the
+# run-contraction pipeline): every slot's parent and codepoint word read once, the (lamport,
+# agent) of every run head read once, the merged text written once.
+MIN_B_PER_SLOT = 8.0
+MIN_B_PER_RUN = 6.0
+MIN_B_PER_TEXT = 1.0
+# Per-kernel algorithmic bytes (DESIGN.md §5): each kernel's declared inputs read once +
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
     "classify": (8.625, 0.0, 1.0),   # parent, cp|tombstone bit; seq bits, weight nibbles; tile UTF-8
@@ -55,15 +70,15 @@ KERNEL_BYTES = {
     "walk2": (0.0, 20.0, 0.0),
     "expand": (0.0, 16.0, 2.0),      # run prefix/weight/head/offset; slot-order text -> document
     "digest": (0.0, 0.0, 1.0),
-    "doctree": (0.0, 20.0, 0.0),     # parent run, weight, key in; run offset out (LDS level 1)
+    "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out
 }
-
-
+STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs", "run_parent": "k_run_parent",
+                "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
 # HBM bytes per item of each kernel from rocprofv3 PMC passes of this build (FETCH_SIZE x2 for
 # gfx950 wide reads + WRITE_SIZE, one pass each: tools/profile.sh + tools/pmc_summary.py).
 PMC_FILE = "profiles/pmc_per_item.json"
-STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs", "run_parent": "k_run_parent",
-                "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
+# per-rank counters exchanged after timing (u64 each)
+COUNTERS = ["patches", "items", "runs", "text_bytes", "docs", "elapsed_ns", "device_ns", "ok"]
 
 
 def measured_traffic(stage: str, items_per_launch: float):
@@ -91,22 +106,154 @@ def whole_job_rate(units_per_rank: int, world: int, step_seconds: float) -> floa
     return units_per_rank * world / step_seconds
 
 
+def shard_seed(rank: int) -> int:
+    """Relabel seed of a rank's replica shard: every rank's HBM copies differ."""
+    return 0x5EED0003 + 7919 * rank
+
+
 def log(msg: str) -> None:
     print(msg, file=sys.stderr, flush=True)
 
 
+# ---------------------------------------------------------------------------------------------
+# ranks and communication
+# ---------------------------------------------------------------------------------------------
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list, env_extra: dict | None = None) -> int:
+    """Start n rank processes of `argv` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, rendezvous on
+    127.0.0.1) and wait for them; the first failure stops the others.  Called before this
+    process touches the GPU, so only the children do."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update(env_extra or {})
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            st = p.poll()
+            if st is None:
+                continue
+            live.remove(p)
+            if st != 0 and rc == 0:
+                rc = st
+                for q in live:  # the exact children this call started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+@contextlib.contextmanager
+def native_stdout_to_stderr():
+    """RCCL writes a version banner to stdout at communicator init; the bench's stdout is one
+    JSON line, so native writes go to stderr while the engine's communicator is set up."""
+    sys.stdout.flush()
+    libc = ctypes.CDLL(None)
+    libc.fflush(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+class Comm:
+    """Control plane over torch.distributed (gloo: barriers, the RCCL unique-id broadcast) and
+    the data collective over RCCL through the engine's C ABI (crdt_hip_comm_init /
+    crdt_hip_allgather_u64).  With world 1 every call is local."""
+
+    def __init__(self, world: int, rank: int, ctx=None, data_plane: str = "rccl"):
+        self.world, self.rank, self.ctx, self.dist = world, rank, ctx, None
+        self.data_plane = data_plane
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group("gloo", rank=rank, world_size=world)
+            self.dist = dist
+            if data_plane == "rccl":
+                uid = [crdt_hip.Context.comm_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                with native_stdout_to_stderr():
+                    ctx.comm_init(world, rank, uid[0])
+        elif data_plane == "rccl" and ctx is not None:
+            with native_stdout_to_stderr():
+                ctx.comm_init(1, 0, crdt_hip.Context.comm_unique_id())
+
+    def barrier(self) -> None:
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def allgather_u64(self, values) -> np.ndarray:
+        v = np.ascontiguousarray(values, dtype=np.uint64)
+        if self.data_plane == "rccl":
+            with native_stdout_to_stderr():
+                return self.ctx.allgather_u64(v, self.world)
+        if self.dist is None:
+            return v.copy()
+        import torch
+        t = torch.from_numpy(v.view(np.int64).copy())
+        parts = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return np.concatenate([p.numpy().view(np.uint64) for p in parts])
+
+    def close(self) -> None:
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def rank_env() -> tuple:
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+# ---------------------------------------------------------------------------------------------
+# inputs
+# ---------------------------------------------------------------------------------------------
 def load_bases():
+    """Resolve the four traces on the host (untimed setup, like the reference's load at
+    main.rs:19): anchor logs + per-trace patches, items, end bytes, golden digest, resolve ms."""
     with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
         golden = json.load(f)
-    bases, patches, items, survivors, digests = [], [], [], [], []
+    bases, patches, items, survivors, digests, resolve_ms = [], [], [], [], [], []
     for name in TRACES:
         t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
-        bases.append(t.resolve().arrays())
+        t0 = time.perf_counter()
+        lg = t.resolve()
+        resolve_ms.append((time.perf_counter() - t0) * 1e3)
+        bases.append(lg.arrays())
         patches.append(len(t))
         items.append(bases[-1].n)
         survivors.append(golden[name]["end_bytes"])
         digests.append(int(golden[name]["tree_digest"], 16))
-    return bases, patches, items, survivors, digests
+    return {"bases": bases, "patches": patches, "items": items, "survivors": survivors,
+            "digests": digests, "resolve_ms": resolve_ms}
+
+
+def host_cpus() -> dict:
+    """CPUs this process may run on (hardware_concurrency honouring the affinity mask) and the
+    cgroup CPU quota, if any."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    return {"threads": n, "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(bases, patches, seconds: float, threads: int) -> dict:
@@ -131,26 +278,274 @@ def cpu_baseline(bases, patches, seconds: float, threads: int) -> dict:
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    cpus = host_cpus()
     return {"value": done / el, "unit": "patches/s", "cores": threads, "kind": "port",
+            "cgroup_cpu_quota": cpus["cgroup_cpu_quota"],
             "sample": f"{rounds} rounds x {len(batch)} documents ({threads} copies of the 4 "
                       f"resolved traces), {el:.1f} s, oracle/oracle.c orc_merge_rga, one "
-                      "document per thread"}
+                      "document per thread over every CPU of the affinity mask"}
 
 
+def config1(ctx, seconds: float) -> dict:
+    """automerge-paper replayed from scratch per iteration, the reference's
+    upstream closure (main.rs:28-36).  CPU: the oracle's positional replay (orc_replay, gap
+    buffer, one core).  Engine: the native upstream loop (crdt_hip_trace_resolve: from_str +
+    replace per patch) then len() = the device merge (crdt_hip_merge, PCIe included)."""
+    from oracle_bind import Oracle, load_trace
+
+    name = "automerge-paper"
+    oracle = Oracle()
+    td = load_trace(name)
+    end = td.end_content.encode()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        out = oracle.replay(td)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    assert out == end, "oracle replay differs from endContent"
+    cpu = {"value": len(td) * n / el, "unit": "patches/s", "cores": 1, "kind": "port",
+           "sample": f"{n} replays of {name} ({len(td)} patches), {el:.1f} s, "
+                     "oracle/oracle.c orc_replay"}
+    t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
+    res_s = mer_s = 0.0
+    k = 0
+    ok = True
+    while k < 3 or res_s + mer_s < min(seconds, 3.0):
+        a = time.perf_counter()
+        lg = t.resolve()
+        b = time.perf_counter()
+        text, _ = ctx.merge(lg)
+        c = time.perf_counter()
+        ok &= text == end
+        res_s += b - a
+        mer_s += c - b
+        k += 1
+    eng = {"value": len(t) * k / (res_s + mer_s), "unit": "patches/s", "iterations": k,
+           "resolve_ms": res_s / k * 1e3, "merge_ms": mer_s / k * 1e3, "text_ok": bool(ok),
+           "note": "host resolve (one core) + one-document device merge incl. PCIe"}
+    return {"trace": name, "patches": len(td), "cpu_replay": cpu, "engine_upstream": eng}
+
+
+# ---------------------------------------------------------------------------------------------
+# config 3: the headline
+# ---------------------------------------------------------------------------------------------
+def merge_steps(batch, comm, warmup: int, steps: int, on_warmup=None):
+    for i in range(warmup):
+        st = batch.merge()[2]
+        if on_warmup:
+            on_warmup(i, st)
+    comm.barrier()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(steps):
+        dig, lens, st = batch.merge()  # synchronous: returns after the device finished
+        stats.append(st)
+    comm.barrier()
+    return dig, lens, stats, time.perf_counter() - t0
+
+
+def traces_rank(args, comm, make_batch, inputs) -> dict | None:
+    """One rank of the headline: its replica shard (seeded by rank), the timed merges, the counter
+    and digest exchange, the whole-job figures.  Returns rank 0's result (None elsewhere)."""
+    world, rank = comm.world, comm.rank
+    batch = make_batch(inputs["bases"], args.replicas, args.relabel, shard_seed(rank))
+    if rank == 0:
+        log(f"[bench] rank0: {batch.docs} docs, {batch.items} items, "
+            f"{batch.device_bytes / 1e9:.1f} GB resident")
+
+    def on_warmup(i, st):
+        if rank == 0:
+            log(f"[bench] warmup {i}: device {st['total_ns'] / 1e6:.1f} ms")
+
+    dig, lens, stats, elapsed = merge_steps(batch, comm, args.warmup, args.steps, on_warmup)
+    expect = expected_digests(inputs["digests"], batch.docs)
+    surv = np.array([inputs["survivors"][d % 4] for d in range(batch.docs)], np.uint64)
+    ok_local = bool(np.array_equal(dig, expect)) and bool(np.array_equal(lens, surv))
+    patches_rank = sum(inputs["patches"]) * args.replicas
+    cnt = np.array([patches_rank, batch.items, stats[0]["runs"], stats[0]["text_bytes"],
+                    batch.docs, int(elapsed * 1e9),
+                    int(np.mean([s["total_ns"] for s in stats])), int(ok_local)], np.uint64)
+    allc = comm.allgather_u64(cnt).reshape(world, len(COUNTERS))
+    all_dig = comm.allgather_u64(dig)
+    digests_ok = verify_gathered(all_dig, expect, world) and bool(np.all(allc[:, 7] == 1))
+    el_max = float(allc[:, 5].max()) / 1e9
+    step_s = el_max / args.steps
+    res = {
+        "batch": batch, "stats": stats, "elapsed": el_max, "step_s": step_s,
+        "value": float(allc[:, 0].sum()) / step_s, "digests_ok": digests_ok,
+        "per_rank": [{c: int(allc[r, i]) for i, c in enumerate(COUNTERS)} for r in range(world)],
+        "items_per_s": float(allc[:, 1].sum()) / step_s,
+    }
+    return res if rank == 0 else None
+
+
+def roofline_fields(stats, batch, items_per_gpu, step_s) -> dict:
+    """Per-kernel algorithmic GB/s, the dominant kernel's roofline, the pipeline's fraction."""
+    stage_ns = {k: float(np.mean([s["stage_ns"][k] for s in stats])) for k in stats[0]["stage_ns"]}
+    launches = stats[0]["stage_launches"]
+    slots = items_per_gpu + batch.docs  # items + one document-start slot per document
+    runs = stats[0]["runs"]
+    text_bytes = stats[0]["text_bytes"]
+
+    def alg_bytes(k):
+        per_slot, per_run, per_text = KERNEL_BYTES[k]
+        if k == "doctree" and launches.get("expand", 1):
+            per_text = 0.0  # expansion left to k_expand: no text in or out of k_doctree
+        return per_slot * slots + per_run * runs + per_text * text_bytes
+
+    per_kernel = {k: {"ms": stage_ns[k] / 1e6, "launches": launches[k],
+                      "alg_gbps": alg_bytes(k) / stage_ns[k] if stage_ns[k] and launches[k] else 0.0}
+                  for k in stage_ns}
+
+    def roof(k):
+        ns = stage_ns[k] / max(1, launches[k])
+        b = alg_bytes(k) / max(1, launches[k])
+        return {"bound": "hbm", "kernel": STAGE_KERNEL.get(k, k), "achieved": b / ns,
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": b / ns / HBM_PEAK_GBPS,
+                "traffic": measured_traffic(k, items_per_gpu / max(1, launches[k])),
+                "alg_bytes_per_launch": b, "launch_us": ns / 1e3}
+
+    # the dominant kernel = the stage with the most device time per step (HIP events, summed
+    # over its launches; with lanes a stage's launches can overlap another lane's)
+    timed = [k for k in stage_ns if launches[k]]
+    dom = max(timed, key=lambda k: stage_ns[k])
+    out = roof(dom)
+    out["traffic_source"] = PMC_FILE if out["traffic"] is not None else None
+    min_bytes = MIN_B_PER_SLOT * slots + MIN_B_PER_RUN * runs + MIN_B_PER_TEXT * text_bytes
+    pipeline = {"min_bytes_per_step": min_bytes,
+                "contract_b_per_item": min_bytes / items_per_gpu,
+                "gbps": min_bytes / step_s / 1e9, "frac": min_bytes / step_s / 1e9 / HBM_PEAK_GBPS,
+                "note": "design minimum: 8 B/slot (parent, codepoint word) + 6 B/run head "
+                        "(lamport, agent) + 1 B/merged byte, over the wall time of a step"}
+    return {"kernels": per_kernel, "roofline": out, "pipeline": pipeline,
+            "stream_kernel": roof("classify") if launches.get("classify") else None,
+            "stage_ns": stage_ns, "launches": launches}
+
+
+def traces_workload(args) -> int:
+    world, rank, local = rank_env()
+    ctx = crdt_hip.Context(local)
+    comm = Comm(world, rank, ctx)
+    t_setup = time.perf_counter()
+    inputs = load_bases()
+    if args.splitter_stride:
+        ctx.set_param("splitter_stride", args.splitter_stride)
+    ctx.set_param("level1", args.level1)
+    ctx.set_param("lanes", args.lanes)
+    ctx.set_param("lane_gate", args.lane_gate)
+    ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
+    ctx.set_param("plan_cache", args.plan_cache)
+
+    def make_batch(bases, replicas, relabel, seed):
+        return ctx.batch(bases, replicas=replicas, relabel=relabel, seed=seed)
+
+    if rank == 0:
+        log(f"[bench] setup (load + resolve) {time.perf_counter() - t_setup:.1f} s")
+    res = traces_rank(args, comm, make_batch, inputs)
+    out = None
+    if rank == 0:
+        batch, stats = res["batch"], res["stats"]
+        items_per_gpu = batch.items
+        rf = roofline_fields(stats, batch, items_per_gpu, res["step_s"])
+        # The stream kernel again with one lane (untimed extra merges after the timed region):
+        # its launches then have the GPU to themselves, as in a one-lane rocprofv3 profile.
+        iso = None
+        if args.lanes > 1 and rf["launches"].get("classify"):
+            ctx.set_param("lanes", 1)
+            st1 = [batch.merge()[2] for _ in range(2)][-1]
+            ctx.set_param("lanes", args.lanes)
+            ns1 = st1["stage_ns"]["classify"] / max(1, st1["stage_launches"]["classify"])
+            b = rf["stream_kernel"]["alg_bytes_per_launch"]
+            iso = {"achieved": b / ns1, "frac": b / ns1 / HBM_PEAK_GBPS, "launch_us": ns1 / 1e3,
+                   "ms_per_step_1_lane": st1["total_ns"] / 1e6,
+                   "kernel_ms_sum_1_lane": sum(st1["stage_ns"].values()) / 1e6}
+            rf["stream_kernel"]["isolated_1_lane"] = iso
+        patches_per_gpu = sum(inputs["patches"]) * args.replicas
+        out = {
+            "metric": METRIC,
+            "value": res["value"],
+            "unit": "patches/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": res["step_s"] * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic replicas of the 4 real josephg traces (resolved on host, "
+                    f"relabel={args.relabel}, resident in HBM)",
+            "config": {
+                "workload": "config 3: 4 traces x %d replicas per GPU" % args.replicas,
+                "docs_per_gpu": batch.docs,
+                "items_per_gpu": items_per_gpu,
+                "patches_per_gpu": patches_per_gpu,
+                "relabel": args.relabel,
+                "waves": stats[0]["waves"],
+                "lanes": min(args.lanes, stats[0]["waves"]),
+                "parallelism": f"replicas x{world} (no data-path collective)",
+            },
+            "items_per_s": res["items_per_s"],
+            "device_ms_per_step": float(np.mean([s["total_ns"] for s in stats])) / 1e6,
+            "runs_per_gpu": stats[0]["runs"],
+            "kernels": rf["kernels"],
+            "roofline": rf["roofline"],
+            "stream_kernel": rf["stream_kernel"],
+            "pipeline": rf["pipeline"],
+            "resolve": {"ms_per_trace": dict(zip(TRACES, inputs["resolve_ms"])),
+                        "ms_total_one_core": sum(inputs["resolve_ms"]),
+                        "note": "host resolver (positional patches -> anchor log), untimed "
+                                "setup of the batch; once per trace"},
+            "per_rank": res["per_rank"],
+            "digests_ok": res["digests_ok"],
+        }
+        res["batch"].close()  # free the headline shard before the companion's
+        res = batch = stats = None
+    # companion line: the same shard relabelled by a seeded random permutation per replica
+    # (SURVEY §8(d) config 3's "seed-r permutation": runs no longer contract)
+    if args.companion_replicas and args.relabel != "shuffle":
+        ca = argparse.Namespace(replicas=args.companion_replicas, relabel="shuffle", warmup=1,
+                                steps=2)
+        cres = traces_rank(ca, comm, make_batch, inputs)
+        if rank == 0:
+            cb, cs = cres["batch"], cres["stats"]
+            out["companion_shuffle"] = {
+                "workload": "config 3, relabel=shuffle: 4 traces x %d replicas per GPU"
+                            % ca.replicas,
+                "value": cres["value"], "unit": "patches/s",
+                "ms_per_step": cres["step_s"] * 1e3, "steps": ca.steps,
+                "items_per_s": cres["items_per_s"], "runs_per_gpu": cs[0]["runs"],
+                "waves": cs[0]["waves"], "digests_ok": cres["digests_ok"],
+                "kernels_ms": {k: v / 1e6 for k, v in
+                               {k: float(np.mean([s["stage_ns"][k] for s in cs]))
+                                for k in cs[0]["stage_ns"]}.items() if v > 2e4},
+            }
+            out["digests_ok"] = out["digests_ok"] and cres["digests_ok"]
+            cb.close()
+    if rank == 0:
+        if not args.no_cpu_baseline:
+            threads = args.cpu_threads or host_cpus()["threads"]
+            out["cpu_baseline"] = cpu_baseline(inputs["bases"], inputs["patches"],
+                                               args.cpu_seconds, threads)
+            out["config1"] = config1(ctx, args.config1_seconds)
+        print(json.dumps(out), flush=True)
+    ok = out["digests_ok"] if rank == 0 else True
+    comm.close()
+    return 0 if ok else 1
+
+
+# ---------------------------------------------------------------------------------------------
+# side workloads
+# ---------------------------------------------------------------------------------------------
 def side_workload(args) -> int:
     """one document per GPU, resident in HBM, merged `steps`
     times.  value = op-log items merged per second (every item is one insert op; config 2 also
     reports patches/s).  Multi-GPU: replicas only (each rank merges its own copy)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+    world, rank, local = rank_env()
     ctx = crdt_hip.Context(local)
+    comm = Comm(world, rank, ctx)
     ctx.set_param("level1", args.level1)
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
@@ -168,39 +563,30 @@ def side_workload(args) -> int:
     elif args.workload == "agents64":
         n = args.items or 10_000_000
         lg = crdt_hip.OpLog.synth_agents(n, 64, 0x5EED0001).arrays()
-        ref_text, ref_dig = ctx.merge(lg)  # host-view merge (PCIe incl.): the resident batch must agree
-        expect = (ref_dig, len(ref_text))
+        # expected length = the log's visible items (each item is one 1-byte codepoint here);
+        # the digest itself is checked against the oracle by tests/test_gpu_scale.py
+        expect = (None, int(np.count_nonzero(lg.deleted == 0)))
         batch = ctx.batch([lg], replicas=1, relabel="none")
         desc = f"config 4: 64-agent concurrent log, {n} items, seed 0x5EED0001"
     else:
         n = args.items or 1_000_000_000
-        batch = crdt_hip.Batch.synth_tree(ctx, n, 90, 50, 0x5EED0002)
+        batch = crdt_hip.Batch.synth_tree(ctx, n, args.p_chain, 50, 0x5EED0002)
         expect = (None, crdt_hip.synth_tree_visible(n, 50, 0x5EED0002))
-        desc = f"config 5: one document of {n} items (p_chain 0.9, 50% tombstones), generated on device"
+        desc = (f"config 5: one document of {n} items (p_chain {args.p_chain / 100:.2f}, "
+                "50% tombstones), generated on device")
     if rank == 0:
         log(f"[bench] {desc}: {batch.items} items, setup {time.perf_counter() - t_setup:.1f} s")
-    for _ in range(args.warmup):
-        batch.merge()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(args.steps):
-        dig, lens, st = batch.merge()
-        stats.append(st)
-    if dist is not None:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    dig, lens, stats, el = merge_steps(batch, comm, args.warmup, args.steps)
     ok = int(lens[0]) == expect[1] and (expect[0] is None or int(dig[0]) == expect[0])
+    cnt = np.array([batch.items, int(el * 1e9), int(ok)], np.uint64)
+    allc = comm.allgather_u64(cnt).reshape(world, 3)
+    el = float(allc[:, 1].max()) / 1e9
+    ok = bool(np.all(allc[:, 2] == 1))
     stage_ns = {k: float(np.mean([x["stage_ns"][k] for x in stats])) for k in stats[0]["stage_ns"]}
     if rank == 0:
         out = {
-            "metric": METRIC, "value": batch.items * world / (el / args.steps), "unit": "items/s",
+            "metric": METRIC, "value": float(allc[:, 0].sum()) / (el / args.steps),
+            "unit": "items/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic" if patches is None else "trace",
@@ -213,8 +599,7 @@ def side_workload(args) -> int:
         if patches is not None:
             out["patches_per_s"] = patches * world / (el / args.steps)
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    comm.close()
     return 0 if ok else 1
 
 
@@ -224,17 +609,11 @@ def downstream_workload(args) -> int:
     Updates are encoded on the host beforehand, as upstream_updates does (rope.rs:196-220), and
     packed into one buffer + offsets and uploaded to HBM once (crdt_hip_updates_upload; --pcie
     times the upload too); the timed region holds the clone, the device decode (replica.hip) and
-    the merge.  value = patches/s over the 4 traces."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+    the merge, whose codepoint count is the len() the reference asserts (main.rs:68).
+    value = patches/s over the 4 traces."""
+    world, rank, local = rank_env()
     ctx = crdt_hip.Context(local)
+    comm = Comm(world, rank, ctx)
     with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
         golden = json.load(f)
     t_setup = time.perf_counter()
@@ -247,8 +626,9 @@ def downstream_workload(args) -> int:
         buf, offs = crdt_hip.pack_updates(updates)
         # the update vector (main.rs:58) resident in HBM, unless the PCIe upload is timed too
         src = (buf, offs) if args.pcie else crdt_hip.UpdateBatch(ctx, buf, offs)
+        end = t.end_content
         work.append((name, len(t), init, src, buf.size, int(golden[name]["tree_digest"], 16),
-                     golden[name]["end_bytes"]))
+                     golden[name]["end_bytes"], len(end)))
     if rank == 0:
         log(f"[bench] downstream: {sum(w[1] for w in work)} updates, "
             f"{sum(w[4] for w in work) / 2**20:.1f} MiB encoded, "
@@ -256,40 +636,37 @@ def downstream_workload(args) -> int:
 
     def step(per):
         ok = True
-        for name, npatch, init, src, _, dig, nbytes in work:
+        for name, npatch, init, src, _, dig, nbytes, ncp in work:
             t0 = time.perf_counter()
             r = init.clone()
             if args.pcie:
                 r.apply_packed(*src)
             else:
                 r.apply_resident(src)
-            n, d = r.merge_digest()
+            cps, n, d = r.merge_len()
             per[name] = per.get(name, 0.0) + time.perf_counter() - t0
-            ok &= (n, d) == (nbytes, dig)
+            ok &= (cps, n, d) == (ncp, nbytes, dig)
             r.close()
         return ok
 
     for _ in range(args.warmup):
         step({})
-    if dist is not None:
-        dist.barrier()
+    comm.barrier()
     per: dict = {}
     t0 = time.perf_counter()
     ok = True
     for _ in range(args.steps):
         ok &= step(per)
-    if dist is not None:
-        dist.barrier()
+    comm.barrier()
     el = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
     total_patches = sum(w[1] for w in work)
+    allc = comm.allgather_u64(np.array([total_patches, int(el * 1e9), int(ok)], np.uint64))
+    allc = allc.reshape(world, 3)
+    el = float(allc[:, 1].max()) / 1e9
+    ok = bool(np.all(allc[:, 2] == 1))
     if rank == 0:
         out = {
-            "metric": METRIC, "value": total_patches * world / (el / args.steps),
+            "metric": METRIC, "value": float(allc[:, 0].sum()) / (el / args.steps),
             "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32", "data": "trace",
@@ -303,18 +680,21 @@ def downstream_workload(args) -> int:
             "pcie_included": bool(args.pcie), "digests_ok": bool(ok),
         }
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    comm.close()
     return 0 if ok else 1
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; without WORLD_SIZE in the environment, bench.py "
+                         "starts this many rank processes itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--replicas", type=int, default=4096, help="replicas of each trace per GPU")
     ap.add_argument("--relabel", default="rotate", choices=["none", "rotate", "shuffle"])
+    ap.add_argument("--companion-replicas", type=int, default=0,
+                    help="replicas per trace of the relabel=shuffle companion line (0: none)")
     ap.add_argument("--splitter-stride", type=int, default=0)
     ap.add_argument("--wave-slots-log2", type=int, default=30,
                     help="slots per device wave (2^N; smaller waves pipeline better over lanes)")
@@ -326,199 +706,45 @@ def main() -> int:
     ap.add_argument("--lanes", type=int, default=2,
                     help="waves merged concurrently, each on its own stream and scratch "
                          "(Engine::merge_lanes; 1 = one after the other)")
+    ap.add_argument("--plan-cache", type=int, default=1, choices=[0, 1],
+                    help="1: merges after the first enqueue every wave with its learnt launch "
+                         "plan and wait once (Engine::merge_async); 0: wait after each level 0")
     ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
                     help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--config1-seconds", type=float, default=4.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="traces", choices=["traces", "seph", "agents64", "big1b", "downstream"],
+    ap.add_argument("--workload", default="traces",
+                    choices=["traces", "seph", "agents64", "big1b", "downstream"],
                     help="traces: config 3 (headline); seph: config 2; agents64: config 4; "
                          "big1b: config 5 (SURVEY.md §8(d)); downstream: the reference's "
                          "downstream group with device-side update decode (§8(f) row 2)")
     ap.add_argument("--items", type=int, default=0, help="items of the synthetic workloads")
-    args = ap.parse_args()
+    ap.add_argument("--p-chain", type=int, default=90,
+                    help="config 5: percent of items whose parent is the previous item "
+                         "(0 = uniform random parents, the worst case for gathers)")
+    return ap.parse_args(argv)
+
+
+def main() -> int:
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started before this process touches the GPU
+        return spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if world > 1:
+        log(f"[bench] rank {os.environ.get('RANK', '0')} of {world}")
+    global crdt_hip
+    import crdt_hip as _engine
+    crdt_hip = _engine
     if args.workload == "downstream":
         return downstream_workload(args)
     if args.workload != "traces":
         return side_workload(args)
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def allmax(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    t_setup = time.perf_counter()
-    bases, patches, items, survivors, golden_dig = load_bases()
-    ctx = crdt_hip.Context(local)
-    if args.splitter_stride:
-        ctx.set_param("splitter_stride", args.splitter_stride)
-    ctx.set_param("level1", args.level1)
-    ctx.set_param("lanes", args.lanes)
-    ctx.set_param("lane_gate", args.lane_gate)
-    ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
-    batch = ctx.batch(bases, replicas=args.replicas, relabel=args.relabel,
-                      seed=0x5EED0003 + 7919 * rank)
-    if rank == 0:
-        log(f"[bench] rank0: {batch.docs} docs, {batch.items} items, "
-            f"{batch.device_bytes / 1e9:.1f} GB resident, setup {time.perf_counter() - t_setup:.1f} s")
-
-    for i in range(args.warmup):
-        dig, lens, st = batch.merge()
-        if rank == 0:
-            log(f"[bench] warmup {i}: device {st['total_ns'] / 1e6:.1f} ms")
-    barrier()
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(args.steps):
-        dig, lens, st = batch.merge()  # synchronous: returns after the device finished
-        stats.append(st)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = allmax(elapsed)
-    ms_per_step = elapsed / args.steps * 1e3
-
-    # correctness: every document's digest must equal its trace's endContent digest
-    expect = expected_digests(golden_dig, batch.docs)
-    ok_local = bool(np.array_equal(dig, expect)) and bool(
-        np.array_equal(lens, np.array([survivors[d % 4] for d in range(batch.docs)], np.uint64)))
-    if world > 1:
-        # digest exchange over RCCL/xGMI through the engine's C ABI
-        import torch
-        uid = [crdt_hip.Context.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(world, rank, uid[0])
-        all_dig = ctx.allgather_u64(dig, world)
-        ok = verify_gathered(all_dig, expect, world)
-        flag = torch.tensor([1 if (ok and ok_local) else 0], device=f"cuda:{local}")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        digests_ok = bool(flag.item())
-    else:
-        digests_ok = ok_local
-
-    patches_per_gpu = sum(patches) * args.replicas
-    items_per_gpu = batch.items
-    value = whole_job_rate(patches_per_gpu, world, elapsed / args.steps)
-
-    # per-kernel device times (HIP events on the engine stream), mean over timed steps
-    stage_ns = {k: float(np.mean([s["stage_ns"][k] for s in stats])) for k in stats[0]["stage_ns"]}
-    launches = stats[0]["stage_launches"]
-    dev_ns = float(np.mean([s["total_ns"] for s in stats]))
-    kern_ns = sum(stage_ns.values())
-    slots = items_per_gpu + batch.docs  # items + one document-start slot per document
-    runs = stats[0]["runs"]
-    text_bytes = stats[0]["text_bytes"]
-
-    def alg_bytes(k):
-        per_slot, per_run, per_text = KERNEL_BYTES[k]
-        if k == "doctree" and launches.get("expand", 1) == 0:
-            per_text = 2.0  # expansion fused: slot-order UTF-8 in, document UTF-8 out
-        return per_slot * slots + per_run * runs + per_text * text_bytes
-
-    per_kernel = {k: {"ms": stage_ns[k] / 1e6, "launches": launches[k],
-                      "alg_gbps": alg_bytes(k) / stage_ns[k] if stage_ns[k] and launches[k] else 0.0}
-                  for k in stage_ns}
-    # The roofline kernel is the HBM-bound k_classify (the largest single-lane stage; with lanes
-    # the summed time of the latency-bound k_doctree, which overlaps other lanes, can be larger).
-    dom = "classify" if launches.get("classify") else max(stage_ns, key=lambda k: stage_ns[k])
-    dom_launch_ns = stage_ns[dom] / max(1, launches[dom])
-    dom_bytes_per_launch = alg_bytes(dom) / max(1, launches[dom])
-    achieved = dom_bytes_per_launch / dom_launch_ns  # bytes/ns == GB/s
-    traffic = measured_traffic(dom, items_per_gpu / max(1, launches[dom]))
-    # The same kernel with one lane (untimed extra merges after the timed region): its launches
-    # then have the GPU to themselves, as in the single-lane rocprofv3 profile.
-    iso = None
-    if args.lanes > 1 and launches.get(dom):
-        ctx.set_param("lanes", 1)
-        st1 = [batch.merge()[2] for _ in range(2)][-1]
-        ctx.set_param("lanes", args.lanes)
-        ns1 = st1["stage_ns"][dom] / max(1, st1["stage_launches"][dom])
-        iso = {"achieved": dom_bytes_per_launch / ns1, "frac": dom_bytes_per_launch / ns1 / HBM_PEAK_GBPS,
-               "launch_us": ns1 / 1e3, "ms_per_step_1_lane": st1["total_ns"] / 1e6}
-    surv_per_item = sum(survivors) / sum(items)
-    pipe_bytes = (PIPE_B_PER_ITEM + surv_per_item) * items_per_gpu
-    pipe_gbps = pipe_bytes / kern_ns
-    real_bytes = sum(alg_bytes(k) for k in stage_ns if launches[k])
-
-    if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "patches/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic replicas of the 4 real josephg traces (resolved on host, "
-                    f"relabel={args.relabel}, resident in HBM)",
-            "config": {
-                "workload": "config 3: 4 traces x %d replicas per GPU" % args.replicas,
-                "docs_per_gpu": batch.docs,
-                "items_per_gpu": items_per_gpu,
-                "patches_per_gpu": patches_per_gpu,
-                "relabel": args.relabel,
-                "waves": stats[0]["waves"],
-                "lanes": min(args.lanes, stats[0]["waves"]),
-                "parallelism": f"replicas x{world} (no data-path collective)",
-            },
-            "items_per_s": items_per_gpu * world / (elapsed / args.steps),
-            "hbm_gbps_alg_pipeline": pipe_gbps,
-            "device_ms_per_step": dev_ns / 1e6,
-            "runs_per_gpu": runs,
-            "kernels": per_kernel,
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dom,
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": traffic,
-                "traffic_source": PMC_FILE if traffic is not None else None,
-                "alg_bytes_per_launch": dom_bytes_per_launch,
-                "launch_us": dom_launch_ns / 1e3,
-                "note": "launch time measured while other lanes' level 1 overlaps it",
-                "isolated_1_lane": iso,
-            },
-            # SURVEY.md §8(d) contract: 117 B per item + survivors over the whole pipeline.  It
-            # prices the uncontracted item-level pipeline; run contraction avoids most of that
-            # traffic, so this figure can exceed the HBM peak.
-            "survey_contract": {
-                "alg_bytes_per_item": PIPE_B_PER_ITEM + surv_per_item,
-                "gbps": pipe_gbps, "frac_of_peak": pipe_gbps / HBM_PEAK_GBPS,
-            },
-            # the pipeline's own kernels' algorithmic bytes over its kernel time
-            "pipeline_alg_gbps": real_bytes / kern_ns,
-            "digests_ok": digests_ok,
-        }
-        if not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(bases, patches, args.cpu_seconds, threads)
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
-    return 0 if digests_ok else 1
+    return traces_workload(args)
 
 
 if __name__ == "__main__":

@@ -46,7 +46,7 @@ EXPORTS = [
     "crdt_hip_updates_upload", "crdt_hip_updates_free", "crdt_hip_replica_apply_resident",
     "crdt_hip_replica_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
     "crdt_hip_allgather_u64", "crdt_hip_comm_destroy", "crdt_hip_xxh64",
-    "crdt_hip_tree_digest",
+    "crdt_hip_tree_digest", "crdt_hip_merge_len", "crdt_hip_replica_merge_len",
 ]
 
 
@@ -156,6 +156,8 @@ def lib() -> C.CDLL:
         "crdt_hip_replica_apply_resident": (i32, [vp, vp, vp]),
         "crdt_hip_replica_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_replica_merge": (i32, [vp, vp, vp, sz, P(sz), P(u64)]),
+        "crdt_hip_replica_merge_len": (i32, [vp, vp, P(u64), P(u64), P(u64)]),
+        "crdt_hip_merge_len": (i32, [vp, P(View), P(u64), P(u64), P(u64)]),
         "crdt_hip_comm_unique_id": (i32, [vp]),
         "crdt_hip_comm_init": (i32, [vp, i32, i32, vp]),
         "crdt_hip_allgather_u64": (i32, [vp, vp, sz, vp]),
@@ -451,6 +453,15 @@ class Context:
                self._h)
         return int(n.value), int(dig.value)
 
+    def merge_len(self, log) -> tuple:
+        """Upstream::len on the device: (codepoints, UTF-8 bytes, tree digest) of the merged
+        document, without copying the text back (crdt_hip_merge_len)."""
+        v, keep = _as_view(log)
+        c, n, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().crdt_hip_merge_len(self._h, C.byref(v), C.byref(c), C.byref(n), C.byref(d)),
+               self._h)
+        return int(c.value), int(n.value), int(d.value)
+
     def merge_batch(self, logs: list, stats: bool = False):
         views = []
         keep = []
@@ -655,6 +666,14 @@ class Replica:
                                             C.byref(dig)), self.ctx._h)
         return int(n.value), int(dig.value)
 
+    def merge_len(self) -> tuple:
+        """(codepoints, UTF-8 bytes, tree digest) of the merged document; the codepoints are
+        counted on the device from the merged bytes (crdt_hip_replica_merge_len)."""
+        c, n, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().crdt_hip_replica_merge_len(self.ctx._h, self._h, C.byref(c), C.byref(n),
+                                                C.byref(d)), self.ctx._h)
+        return int(c.value), int(n.value), int(d.value)
+
 
 class HipMerge:
     """Mirror of the reference's per-CRDT adapter for the GPU engine.
@@ -702,8 +721,9 @@ class HipMerge:
         return data.decode("utf-8")
 
     def len(self) -> int:
-        data, _ = self.context().merge(self.log)
-        return len(data.decode("utf-8"))  # codepoints (EDITS_USE_BYTE_OFFSETS = false)
+        # the merge (Dt::len -> checkout_tip, rope.rs:133-136): codepoints of the merged text,
+        # counted on the device (EDITS_USE_BYTE_OFFSETS = false)
+        return self.context().merge_len(self.log)[0]
 
     # Downstream
     @classmethod
@@ -760,6 +780,11 @@ class HipDownstream:
         return self.replica.merge()[0].decode("utf-8")
 
     def len(self) -> int:
+        """Codepoints of the merged document (main.rs:68 asserts them): the merge's own count,
+        cross-checked against the decoder's visible-codepoint counter."""
         self.flush()
-        self.replica.merge_digest()
-        return self.replica.info()[1]
+        cps, _, _ = self.replica.merge_len()
+        counter = self.replica.info()[1]
+        if cps != counter:
+            raise CrdtHipError(-5, f"merged text has {cps} codepoints, the decoder counted {counter}")
+        return cps

@@ -170,6 +170,15 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.l0_gated = value == 1;
         return 0;
     }
+    if (k == "plan_cache") {
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "plan_cache must be 0 or 1");
+        ctx->eng.plan_cache = value == 1;
+        return 0;
+    }
+    if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)
+        ctx->eng.plan_shrink = value != 0;
+        return 0;
+    }
     if (k == "level1") {
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "level1 must be 0 (auto) or 1 (global)");
         ctx->eng.level1_global = value == 1;
@@ -436,6 +445,23 @@ int crdt_hip_merge(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint8_t* o
     });
 }
 
+int crdt_hip_merge_len(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint64_t* codepoints,
+                       uint64_t* bytes, uint64_t* digest) {
+    if (!ctx) return set_err(nullptr, CRDT_HIP_EINVAL, "null context");
+    return guard(ctx, [&] {
+        int rc = stage_views(ctx, log, 1);
+        if (rc) return rc;
+        uint64_t dig = 0, len = 0, cps = 0;
+        rc = ctx->eng.merge(ctx->staging, crdt::Engine::TEXT, &dig, &len, nullptr, nullptr,
+                            nullptr, &cps);
+        if (rc) return from_engine(ctx, rc);
+        if (codepoints) *codepoints = cps;
+        if (bytes) *bytes = len;
+        if (digest) *digest = dig;
+        return 0;
+    });
+}
+
 int crdt_hip_merge_batch(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* logs, uint32_t n,
                          uint64_t* digests, uint64_t* lens, crdt_hip_stats* stats) {
     if (!ctx || (!logs && n)) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
@@ -625,6 +651,21 @@ int crdt_hip_replica_merge(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out,
             if (cap < len) return set_err(ctx, CRDT_HIP_ESPACE, "output buffer too small");
             if (len) std::memcpy(out, text.data(), (size_t)len);
         }
+        return 0;
+    });
+}
+
+int crdt_hip_replica_merge_len(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint64_t* codepoints,
+                               uint64_t* bytes, uint64_t* digest) {
+    if (!ctx || !r) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (r->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "replica belongs to another context");
+    return guard(ctx, [&] {
+        uint64_t len = 0, dig = 0, cps = 0;
+        int rc = crdt::replica_merge(ctx->eng, r->r, nullptr, &len, &dig, nullptr, &cps);
+        if (rc) return from_engine(ctx, rc);
+        if (codepoints) *codepoints = cps;
+        if (bytes) *bytes = len;
+        if (digest) *digest = dig;
         return 0;
     });
 }

@@ -68,7 +68,13 @@ enum Ctl {
     C_RMAX = 5,     // most runs in one document
     C_VISITED = 6,  // runs visited by k_walk2
     C_UNFUSED = 7,  // documents whose text k_doctree left to k_expand
+    C_REPLAN = 8,   // the wave outgrew the launch plan it was enqueued with (runs / largest
+                    //   document above the planned capacity): every later kernel of the wave
+                    //   exits at once and the host merges the wave again with a fresh plan
 };
+
+// Every kernel after level 0 starts with this: a wave whose plan was too small does nothing.
+__device__ __forceinline__ bool replan(const uint32_t* ctl) { return ctl[C_REPLAN] != 0u; }
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
 enum Stage { S_CLASSIFY, S_RUNS, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
@@ -112,6 +118,7 @@ struct L0Args {
     uint32_t* doc_root;         // per document: its document-start run
     uint32_t* doc_p0;           // per document: weight prefix at its start
     uint32_t* ctl;
+    uint32_t cap_runs, cap_rmax;  // capacity of the launch plan (k_docmax flags C_REPLAN above)
 };
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
@@ -425,72 +432,80 @@ __global__ __launch_bounds__(1024) void k_docmax(L0Args a) {
     }
     atomicMax(&mx, m);
     __syncthreads();
-    if (threadIdx.x == 0) a.ctl[C_RMAX] = mx;
+    if (threadIdx.x == 0) {
+        a.ctl[C_RMAX] = mx;
+        if (a.ctl[C_RTOTAL] > a.cap_runs || mx > a.cap_rmax) a.ctl[C_REPLAN] = 1u;
+    }
 }
 
 // Per run: weight (next run's prefix - own prefix) and parent run (rank lookup of the head's
 // parent item; the parent item is always the last item of its run; a head whose parent is the
 // slot before it has the previous run as parent).  kRunsPerThread runs per thread, every load of
 // a stage issued before any is used, so that enough gathers are in flight to cover HBM latency.
+// The run count comes from level 0 on the device (ctl); the grid strides over it.
 constexpr int kRunsPerThread = 4;
-__global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uint32_t wtotal) {
+__global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a) {
     constexpr int K = kRunsPerThread;
-    const uint32_t r0 = blockIdx.x * (kBlock * K) + threadIdx.x;
-    uint32_t h[K], ps[K], nx[K], sq[K];
+    if (replan(a.ctl)) return;
+    const uint32_t R = a.ctl[C_RTOTAL], wtotal = a.ctl[C_WTOTAL];
+    for (uint32_t r0 = blockIdx.x * (kBlock * K) + threadIdx.x; r0 < R;
+         r0 += gridDim.x * (kBlock * K)) {
+        uint32_t h[K], ps[K], nx[K], sq[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t rho = min(r0 + (uint32_t)k * kBlock, R - 1u);
-        h[k] = a.r_head[rho];
-        ps[k] = a.r_pstart[rho];
-        nx[k] = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
-    }
-    uint32_t dx[K], dy[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        sq[k] = a.seqb[h[k] >> 4];
-        const uint2 doc = a.docs[a.chunk_doc[h[k] >> a.log2m]];
-        dx[k] = doc.x;
-        dy[k] = doc.y;
-    }
-    uint32_t lam[K], ag[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        lam[k] = a.in_lamport[h[k]];
-        ag[k] = a.in_agent[h[k]];
-    }
-    uint32_t ps_slot[K];  // parent slot of a non-seq head (0: none)
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        sq[k] = (sq[k] >> (h[k] & 15u)) & 1u;
-        uint32_t p = (!sq[k] && h[k] != dx[k]) ? a.in_parent[h[k]] : 0u;
-        if (p > dy[k] || p == h[k] - dx[k]) p = 0;  // flagged by k_classify
-        ps_slot[k] = dx[k] + p;
-    }
-    uint64_t hb[K];
-    uint32_t hr[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {  // rank lookups (only non-seq heads use them)
-        hb[k] = a.hbits[ps_slot[k] >> 6];
-        hr[k] = a.hrank[ps_slot[k] >> 6];
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t rho = r0 + (uint32_t)k * kBlock;
-        if (rho >= R) break;
-        uint32_t pr = kNil;
-        uint64_t key = 0;
-        if (sq[k]) {
-            pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
-            key = ((uint64_t)lam[k] << 16) | ag[k];
-        } else if (h[k] != dx[k]) {
-            const uint32_t b = ps_slot[k] & 63u;
-            const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
-            pr = hr[k] + (uint32_t)__popcll(hb[k] & mask) - 1u;
-            key = ((uint64_t)lam[k] << 16) | ag[k];
+        for (int k = 0; k < K; ++k) {
+            const uint32_t rho = min(r0 + (uint32_t)k * kBlock, R - 1u);
+            h[k] = a.r_head[rho];
+            ps[k] = a.r_pstart[rho];
+            nx[k] = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
         }
-        a.r_w[rho] = nx[k] - ps[k];
-        a.r_parent[rho] = pr;
-        a.r_key[rho] = key;
+        uint32_t dx[K], dy[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            sq[k] = a.seqb[h[k] >> 4];
+            const uint2 doc = a.docs[a.chunk_doc[h[k] >> a.log2m]];
+            dx[k] = doc.x;
+            dy[k] = doc.y;
+        }
+        uint32_t lam[K], ag[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            lam[k] = a.in_lamport[h[k]];
+            ag[k] = a.in_agent[h[k]];
+        }
+        uint32_t ps_slot[K];  // parent slot of a non-seq head (0: none)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            sq[k] = (sq[k] >> (h[k] & 15u)) & 1u;
+            uint32_t p = (!sq[k] && h[k] != dx[k]) ? a.in_parent[h[k]] : 0u;
+            if (p > dy[k] || p == h[k] - dx[k]) p = 0;  // flagged by k_classify
+            ps_slot[k] = dx[k] + p;
+        }
+        uint64_t hb[K];
+        uint32_t hr[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {  // rank lookups (only non-seq heads use them)
+            hb[k] = a.hbits[ps_slot[k] >> 6];
+            hr[k] = a.hrank[ps_slot[k] >> 6];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t rho = r0 + (uint32_t)k * kBlock;
+            if (rho >= R) break;
+            uint32_t pr = kNil;
+            uint64_t key = 0;
+            if (sq[k]) {
+                pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
+                key = ((uint64_t)lam[k] << 16) | ag[k];
+            } else if (h[k] != dx[k]) {
+                const uint32_t b = ps_slot[k] & 63u;
+                const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
+                pr = hr[k] + (uint32_t)__popcll(hb[k] & mask) - 1u;
+                key = ((uint64_t)lam[k] << 16) | ag[k];
+            }
+            a.r_w[rho] = nx[k] - ps[k];
+            a.r_parent[rho] = pr;
+            a.r_key[rho] = key;
+        }
     }
 }
 
@@ -499,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a, uint32_t R, uin
 // to its run's place in the document: text[toff[d] + roff[run] + i].  ORDER mode writes the
 // run's item ids instead (consecutive: a run is a chain of consecutive ids).
 struct ExpandArgs {
-    uint32_t R, mode, log2m;
+    uint32_t mode, log2m;
     const uint32_t* chunk_doc;
     const uint2* docs;
     const uint32_t* r_head;
@@ -514,54 +529,61 @@ struct ExpandArgs {
     const uint8_t* fused;  // per document: text already written by k_doctree (or null)
 };
 
+// The grid strides over the wave's runs (their count comes from ctl).  After a fused k_doctree
+// it only has work if some document did not fit that kernel's LDS (ctl C_UNFUSED), so it is
+// launched unconditionally and exits at once in the common case.
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a) {
+    if (replan(a.ctl) || (a.fused && a.ctl[C_UNFUSED] == 0u)) return;
+    const uint32_t R = a.ctl[C_RTOTAL];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t rho = blockIdx.x * kBlock + threadIdx.x;
-    uint32_t w = 0, src = 0, idb = 0;
-    uint64_t dst = 0;
-    if (rho < a.R) {
-        src = a.r_pstart[rho];
-        w = a.r_w[rho];
-        if (w) {
-            const uint32_t h = a.r_head[rho];
-            const uint32_t d = a.chunk_doc[h >> a.log2m];
-            const uint32_t base = a.docs[d].x;
-            const uint32_t ro = a.roff[rho];
-            if (a.fused && a.fused[d]) {
-                dst = ~0ull;  // k_doctree wrote this document (w still counts: bytes stay aligned)
-            } else if ((uint64_t)ro + w > a.tlen[d]) {
-                atomicOr(&a.ctl[C_ERR], 8u);
-                dst = ~0ull;  // skipped below
-            } else {
-                dst = a.toff[d] + ro;
+    for (uint32_t r0 = blockIdx.x * kBlock; r0 < R; r0 += gridDim.x * kBlock) {
+        const uint32_t rho = r0 + threadIdx.x;
+        uint32_t w = 0, src = 0, idb = 0;
+        uint64_t dst = 0;
+        if (rho < R) {
+            src = a.r_pstart[rho];
+            w = a.r_w[rho];
+            if (w) {
+                const uint32_t h = a.r_head[rho];
+                const uint32_t d = a.chunk_doc[h >> a.log2m];
+                const uint32_t base = a.docs[d].x;
+                const uint32_t ro = a.roff[rho];
+                if (a.fused && a.fused[d]) {
+                    dst = ~0ull;  // k_doctree wrote this document (w still counts: bytes stay aligned)
+                } else if ((uint64_t)ro + w > a.tlen[d]) {
+                    atomicOr(&a.ctl[C_ERR], 8u);
+                    dst = ~0ull;  // skipped below
+                } else {
+                    dst = a.toff[d] + ro;
+                }
+                idb = h - base + (h == base ? 1u : 0u);
             }
-            idb = h - base + (h == base ? 1u : 0u);
         }
-    }
-    const uint32_t inc = wave_incl_scan(w);
-    const uint32_t ex = inc - w;
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)src);
-    for (uint32_t b = 0; b < T; b += 64) {
-        const uint32_t x = b + lane;
-        // the last lane whose run starts at or before byte x owns it
-        uint32_t j = 0;
+        const uint32_t inc = wave_incl_scan(w);
+        const uint32_t ex = inc - w;
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)src);
+        for (uint32_t b = 0; b < T; b += 64) {
+            const uint32_t x = b + lane;
+            // the last lane whose run starts at or before byte x owns it
+            uint32_t j = 0;
 #pragma unroll
-        for (uint32_t st = 32; st; st >>= 1) {
-            const uint32_t e = (uint32_t)__shfl((int)ex, (int)(j + st));
-            if (e <= x) j += st;
-        }
-        const uint32_t off = x - (uint32_t)__shfl((int)ex, (int)j);
-        const uint64_t dj = ((uint64_t)(uint32_t)__shfl((int)(dst >> 32), (int)j) << 32) |
-                            (uint32_t)__shfl((int)(uint32_t)dst, (int)j);
-        // (every shuffle above runs with the whole wave active: a ds_bpermute from an inactive
-        // lane reads 0)
-        const uint32_t ib = a.mode ? (uint32_t)__shfl((int)idb, (int)j) : 0u;
-        if (x < T && dj != ~0ull) {
-            if (a.mode == 0)
-                a.text[dj + off] = a.sbytes[s0 + x];
-            else
-                reinterpret_cast<uint32_t*>(a.text)[dj + off] = ib + off;
+            for (uint32_t st = 32; st; st >>= 1) {
+                const uint32_t e = (uint32_t)__shfl((int)ex, (int)(j + st));
+                if (e <= x) j += st;
+            }
+            const uint32_t off = x - (uint32_t)__shfl((int)ex, (int)j);
+            const uint64_t dj = ((uint64_t)(uint32_t)__shfl((int)(dst >> 32), (int)j) << 32) |
+                                (uint32_t)__shfl((int)(uint32_t)dst, (int)j);
+            // (every shuffle above runs with the whole wave active: a ds_bpermute from an inactive
+            // lane reads 0)
+            const uint32_t ib = a.mode ? (uint32_t)__shfl((int)idb, (int)j) : 0u;
+            if (x < T && dj != ~0ull) {
+                if (a.mode == 0)
+                    a.text[dj + off] = a.sbytes[s0 + x];
+                else
+                    reinterpret_cast<uint32_t*>(a.text)[dj + off] = ib + off;
+            }
         }
     }
 }
@@ -577,7 +599,6 @@ struct TreeArgs {
     const uint32_t* in_w;        // run weight
     const uint32_t* doc_root;    // per document: its document-start run
     const uint32_t* doc_p0;      // per document: weight prefix at its start
-    uint32_t wtotal;
     uint32_t* deg;
     uint32_t* cstart;
     uint32_t* child;
@@ -594,6 +615,9 @@ struct TreeArgs {
     uint64_t* leafh;
     uint64_t* ghash;  // group digests of documents above 16 MiB (indexed like leafh)
     uint64_t* dig;
+    uint32_t* leafcp;  // per leaf: codepoints (UTF-8 bytes that are not continuation bytes)
+    uint32_t* gcp;     // per group of a document above 16 MiB: codepoints
+    uint32_t* doccp;   // per document: codepoints of the merged text (Upstream::len)
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
@@ -962,6 +986,8 @@ __global__ __launch_bounds__(kBlock) void k_wstep(const uint32_t* __restrict__ v
 __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     __shared__ uint64_t st[1024];
     __shared__ uint32_t sl[1024];
+    if (replan(a.ctl)) return;
+    const uint32_t wtotal = a.ctl[C_WTOTAL];
     uint64_t carry_t = 0;
     uint32_t carry_l = 0;
     const uint64_t am = (uint64_t)a.align - 1u;
@@ -969,7 +995,7 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
         const uint32_t d = d0 + threadIdx.x;
         uint32_t tl = 0;
         if (d < a.ndocs) {
-            const uint32_t end = d + 1 < a.ndocs ? a.doc_p0[d + 1] : a.wtotal;
+            const uint32_t end = d + 1 < a.ndocs ? a.doc_p0[d + 1] : wtotal;
             tl = end - a.doc_p0[d];
             a.tlen[d] = tl;
         }
@@ -1079,7 +1105,7 @@ constexpr uint32_t kNil14 = 0x3FFFu;   // no next splitter (splitter records: su
 constexpr uint32_t kDocBig = 32;       // runs of >= 0xFFFF bytes per document (LDS side table)
 
 struct DocArgs {
-    uint32_t ndocs, rtotal, rcap, scap, chbytes;
+    uint32_t ndocs, rcap, scap, chbytes;
     uint32_t probe;  // 1 + document whose phase times are printed (0: none)
     const uint32_t* doc_root;
     const uint32_t* r_parent;
@@ -1217,10 +1243,11 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     __shared__ uint32_t probe_max, probe_sum;
 #endif
     __shared__ uint32_t bigv[kDocBig], bigw[kDocBig];
+    if (replan(a.ctl)) return;
     const uint32_t d = blockIdx.x;
     const uint32_t t = threadIdx.x;
     const uint32_t base = a.doc_root[d];
-    const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.rtotal) - base;
+    const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL]) - base;
     const uint32_t S = (R + 3u) >> kDocLog2S;
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
@@ -1718,9 +1745,21 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
     return h;
 }
 
+// Codepoints of an 8-byte-aligned UTF-8 range: bytes minus continuation bytes (10xxxxxx).
+__device__ __forceinline__ uint32_t utf8_codepoints(const uint8_t* __restrict__ p, uint32_t len) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
+    uint32_t cont = 0, i = 0;
+    for (; i + 8 <= len; i += 8) {
+        const uint64_t x = w[i / 8];
+        cont += (uint32_t)__popcll(x & ~(x << 1) & 0x8080808080808080ull);
+    }
+    for (; i < len; ++i) cont += (p[i] & 0xC0u) == 0x80u ? 1u : 0u;
+    return len - cont;
+}
+
 __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_cap) {
     const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
-    if (L >= leaf_cap || L >= a.loff[a.ndocs]) return;
+    if (replan(a.ctl) || L >= leaf_cap || L >= a.loff[a.ndocs]) return;
     uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1729,7 +1768,9 @@ __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_c
     const uint32_t d = lo, j = L - a.loff[d];
     const uint32_t tl = a.tlen[d];
     const uint32_t len = min(kLeaf, tl - j * kLeaf);
-    a.leafh[L] = xxh64_aligned(a.text + a.toff[d] + (uint64_t)j * kLeaf, len, 0);
+    const uint8_t* p = a.text + a.toff[d] + (uint64_t)j * kLeaf;
+    a.leafh[L] = xxh64_aligned(p, len, 0);
+    a.leafcp[L] = utf8_codepoints(p, len);
 }
 
 // Documents of more than kGroup leaves (16 MiB): leaf digests hashed in groups of kGroup (seed =
@@ -1737,7 +1778,7 @@ __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_c
 constexpr uint32_t kGroup = 4096;
 __global__ __launch_bounds__(kBlock) void k_grouphash(TreeArgs a, uint32_t leaf_cap) {
     const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
-    if (L >= leaf_cap || L >= a.loff[a.ndocs]) return;
+    if (replan(a.ctl) || L >= leaf_cap || L >= a.loff[a.ndocs]) return;
     uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1745,17 +1786,25 @@ __global__ __launch_bounds__(kBlock) void k_grouphash(TreeArgs a, uint32_t leaf_
     }
     const uint32_t l0 = a.loff[lo], nl = a.loff[lo + 1] - l0, j = L - l0;
     if (nl <= kGroup || j % kGroup) return;
+    const uint32_t ng = min(kGroup, nl - j);
     a.ghash[l0 + j / kGroup] = xxh64_aligned(reinterpret_cast<const uint8_t*>(a.leafh + L),
-                                             min(kGroup, nl - j) * 8u, j / kGroup);
+                                             ng * 8u, j / kGroup);
+    uint32_t cps = 0;
+    for (uint32_t i = 0; i < ng; ++i) cps += a.leafcp[L + i];
+    a.gcp[l0 + j / kGroup] = cps;
 }
 
 __global__ __launch_bounds__(kBlock) void k_docdigest(TreeArgs a) {
     const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
-    if (d >= a.ndocs) return;
+    if (replan(a.ctl) || d >= a.ndocs) return;
     const uint32_t l0 = a.loff[d], nl = a.loff[d + 1] - l0;
     const uint64_t* h = nl > kGroup ? a.ghash + l0 : a.leafh + l0;
+    const uint32_t* c = nl > kGroup ? a.gcp + l0 : a.leafcp + l0;
     const uint32_t nh = nl > kGroup ? (nl + kGroup - 1) / kGroup : nl;
     a.dig[d] = xxh64_aligned(reinterpret_cast<const uint8_t*>(h), nh * 8u, a.tlen[d]);
+    uint32_t cps = 0;
+    for (uint32_t i = 0; i < nh; ++i) cps += c[i];
+    a.doccp[d] = cps;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1801,18 +1850,50 @@ __device__ __forceinline__ uint32_t perm_apply(const Perm& P, uint32_t id) {
     return x + 1;
 }
 
+// The relabelling of replica r (of a base of n items): rotation (kind 1) or a seeded
+// cycle-walking permutation (kind 2), parameters hashed from (seed, r) exactly as the host's
+// mix64 would.
+__device__ __forceinline__ Perm replica_perm(uint32_t kind, uint32_t n, uint64_t seed, uint64_t r) {
+    Perm P{};
+    P.kind = kind;
+    P.n = n;
+    uint32_t bits = 0;
+    while ((1ull << bits) < n) ++bits;
+    P.bits = bits < 2u ? 2u : bits;
+    const uint64_t h = mix64(seed, r);
+    P.shift = n ? (uint32_t)(h % n) : 0u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        P.mul[k] = (uint32_t)mix64(h, 2 * k) | 1u;
+        P.add[k] = (uint32_t)mix64(h, 2 * k + 1);
+    }
+    return P;
+}
+
+// Every replica of a batch in one launch: blockIdx.y strides over the replica documents,
+// blockIdx.x x 256 threads over a document's items.  Replica r is a relabelled copy of base
+// r % nb: item k goes to slot perm(k) and its parent is relabelled the same way.
 __global__ __launch_bounds__(kBlock) void k_replicate(
     const uint32_t* __restrict__ bp, const uint32_t* __restrict__ bl,
-    const uint16_t* __restrict__ ba, const uint32_t* __restrict__ bc, uint64_t src,
+    const uint16_t* __restrict__ ba, const uint32_t* __restrict__ bc,
+    const uint64_t* __restrict__ bslot, const uint32_t* __restrict__ bn, uint32_t nb,
     uint32_t* __restrict__ rp, uint32_t* __restrict__ rl, uint16_t* __restrict__ ra,
-    uint32_t* __restrict__ rc, uint64_t dst, Perm P) {
-    const uint32_t k = blockIdx.x * kBlock + threadIdx.x + 1;
-    if (k > P.n) return;
-    const uint64_t o = dst + perm_apply(P, k);
-    rp[o] = perm_apply(P, bp[src + k]);
-    rl[o] = bl[src + k];
-    ra[o] = ba[src + k];
-    rc[o] = bc[src + k];
+    uint32_t* __restrict__ rc, const uint64_t* __restrict__ rslot, uint64_t ndocs,
+    uint32_t kind, uint64_t seed) {
+    for (uint64_t r = blockIdx.y; r < ndocs; r += gridDim.y) {
+        const uint32_t b = (uint32_t)(r % nb);
+        const uint32_t n = bn[b];
+        if ((uint64_t)blockIdx.x * kBlock >= n) continue;  // block-uniform
+        const Perm P = replica_perm(kind, n, seed, r);
+        const uint64_t src = bslot[b], dst = rslot[r];
+        for (uint32_t k = blockIdx.x * kBlock + threadIdx.x + 1; k <= n; k += gridDim.x * kBlock) {
+            const uint64_t o = dst + perm_apply(P, k);
+            rp[o] = perm_apply(P, bp[src + k]);
+            rl[o] = bl[src + k];
+            ra[o] = ba[src + k];
+            rc[o] = bc[src + k];
+        }
+    }
 }
 
 // Config 5 generator, item by item on the device: exactly synth.cpp's synth_tree_item (the same
@@ -1873,10 +1954,13 @@ Engine::~Engine() {
     dfree(ctl_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
     dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
     dfree(dig_); dfree(leafh_); dfree(ghash_); dfree(text_);
+    dfree(leafcp_); dfree(gcp_); dfree(doccp_);
     if (host_ctl_) (void)hipHostFree(host_ctl_);
     if (host_dig_) (void)hipHostFree(host_dig_);
     if (host_len_) (void)hipHostFree(host_len_);
+    if (host_cp_) (void)hipHostFree(host_cp_);
     for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : wev_) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -1906,6 +1990,7 @@ std::string Engine::init(int dev) {
         if ((e = hipEventCreate(&x)) != hipSuccess) return hipGetErrorString(e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&host_ctl_), 64)) != hipSuccess)
         return hipGetErrorString(e);
+    cap_host_ctl_ = 1;
     if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
         hipSuccess)
@@ -2051,8 +2136,9 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     if (!ctl_) HIPCHK(dalloc(&ctl_, 16), "hipMalloc ctl");
     if (w.ndocs + 1 > cap_docs_) {
         dfree(tlen_); dfree(loff_); dfree(toff_); dfree(dig_); dfree(doc_root_); dfree(doc_p0_);
-        dfree(doc_fused_);
+        dfree(doc_fused_); dfree(doccp_);
         const uint64_t nd = w.ndocs + 1;
+        HIPCHK(dalloc(&doccp_, nd), "hipMalloc doc codepoints");
         HIPCHK(dalloc(&tlen_, nd), "hipMalloc tlen");
         HIPCHK(dalloc(&loff_, nd), "hipMalloc loff");
         HIPCHK(dalloc(&toff_, nd), "hipMalloc toff");
@@ -2071,15 +2157,21 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
     if (w.leaf_cap + 1 > cap_leaves_) {
         dfree(leafh_);
         dfree(ghash_);
+        dfree(leafcp_);
+        dfree(gcp_);
         HIPCHK(dalloc(&leafh_, w.leaf_cap + 1), "hipMalloc leaf hashes");
         HIPCHK(dalloc(&ghash_, w.leaf_cap + 1), "hipMalloc group hashes");
+        HIPCHK(dalloc(&leafcp_, w.leaf_cap + 1), "hipMalloc leaf codepoints");
+        HIPCHK(dalloc(&gcp_, w.leaf_cap + 1), "hipMalloc group codepoints");
         cap_leaves_ = w.leaf_cap + 1;
     }
     if (ndocs_total > cap_host_docs_) {
         if (host_dig_) (void)hipHostFree(host_dig_);
         if (host_len_) (void)hipHostFree(host_len_);
+        if (host_cp_) (void)hipHostFree(host_cp_);
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_dig_), ndocs_total * 8ull), "pinned dig");
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_len_), ndocs_total * 4ull), "pinned len");
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_cp_), ndocs_total * 4ull), "pinned cps");
         cap_host_docs_ = ndocs_total;
     }
     return CRDT_HIP_OK;
@@ -2121,56 +2213,112 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
     return CRDT_HIP_OK;
 }
 
-int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
-                     std::vector<uint32_t>& stage_launches, bool force_global) {
-    hipStream_t s = stream;
-    const bool ord = mode == ORDER;
-    const uint32_t ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
-    const uint32_t nsums = (ntiles + kScanTile - 1) / kScanTile;
-#define BEGIN(st) HIPCHK(hipEventRecord(ev_[2 * (st)], s), "event record")
-#define END(st) HIPCHK(hipEventRecord(ev_[2 * (st) + 1], s), "event record")
+int Engine::ensure_host_ctl(uint32_t waves) {
+    if (waves <= cap_host_ctl_) return CRDT_HIP_OK;
+    if (host_ctl_) (void)hipHostFree(host_ctl_);
+    host_ctl_ = nullptr;
+    cap_host_ctl_ = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_ctl_), waves * 64ull), "pinned ctl");
+    cap_host_ctl_ = waves;
+    return CRDT_HIP_OK;
+}
 
-    L0Args a0{};
-    a0.nslots = w.nslots;
-    a0.log2m = L.log2m;
-    a0.ndocs = w.ndocs;
-    a0.mode = ord ? 1u : 0u;
-    a0.ntiles = ntiles;
-    a0.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);
-    a0.docs = L.docs_rel + w.first_doc;
-    a0.in_parent = L.parent + w.slot0;
-    a0.in_lamport = L.lamport + w.slot0;
-    a0.in_agent = L.agent + w.slot0;
-    a0.in_cp = L.cp + w.slot0;
-    a0.jbits = jbits_;
-    a0.jloc = jloc_;
-    a0.seqb = seqb_;
-    a0.wnib = wnib_;
-    a0.stile = stile_;
-    a0.sbytes = sbytes_;
-    a0.sbytes_cap = cap_sbytes_ - 64;
-    a0.tile_hw = tile_hw_;
-    a0.tile_sums = tile_sums_;
-    a0.hbits = hbits_;
-    a0.hrank = hrank_;
-    a0.doc_root = doc_root_;
-    a0.doc_p0 = doc_p0_;
-    a0.ctl = ctl_;
-    // run records are written before the run count is known: runs <= slots
-    if (w.nslots > cap_heads_) {
-        dfree(r_head_); dfree(r_pstart_);
-        HIPCHK(dalloc(&r_head_, w.nslots + 64ull), "hipMalloc r_head");
-        HIPCHK(dalloc(&r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
-        cap_heads_ = w.nslots;
+int Engine::ensure_events(std::vector<hipEvent_t>& ev, size_t n) {
+    while (ev.size() < n) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e), "event create");
+        ev.push_back(e);
     }
-    a0.r_head = r_head_;
-    a0.r_pstart = r_pstart_;
+    return CRDT_HIP_OK;
+}
 
-    // ---- level 0: runs -------------------------------------------------------------------
-    // Lanes take turns at level 0 (an HBM stream): the gate is held from the first level-0 launch
-    // to the level-0 sync, so one lane's level 0 overlaps the others' latency-bound level 1.
-    std::unique_lock<std::mutex> gate;
-    if (l0_gate_) gate = std::unique_lock<std::mutex>(*l0_gate_);
+// Level-1 path and LDS sizing of a wave with R runs whose largest document has rmax runs.
+L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
+                           bool force_global) const {
+    L1Plan p;
+    p.R = R;
+    p.rmax = rmax;
+    p.rcap = (rmax + 2u + 7u) & ~7u;
+    p.scap = (((rmax + 3u) >> kDocLog2S) + 8u) & ~7u;
+    const uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap);
+    // per-document LDS path when the largest document's run tree fits one workgroup (sublist
+    // offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
+    p.lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
+             dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
+    // expansion + digest fused into k_doctree when every document's text fits LDS: text staging
+    // + run-start bitvector (tl/8 + tl/16) + one u32 per run
+    p.fuse = p.lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
+    p.dyn_bytes = p.fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
+                               dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
+                         : dbytes;
+    return p;
+}
+
+#define BEGIN(st) HIPCHK(hipEventRecord(ev[2 * (st)], s), "event record")
+#define END(st) HIPCHK(hipEventRecord(ev[2 * (st) + 1], s), "event record")
+
+// Level-0 argument block of a wave (device pointers of L and of this engine's scratch).
+#define L0ARGS(a0)                                                  \
+    L0Args a0{};                                                    \
+    a0.nslots = w.nslots;                                           \
+    a0.log2m = L.log2m;                                             \
+    a0.ndocs = w.ndocs;                                             \
+    a0.mode = ord ? 1u : 0u;                                        \
+    a0.ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile); \
+    a0.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);              \
+    a0.docs = L.docs_rel + w.first_doc;                             \
+    a0.in_parent = L.parent + w.slot0;                              \
+    a0.in_lamport = L.lamport + w.slot0;                            \
+    a0.in_agent = L.agent + w.slot0;                                \
+    a0.in_cp = L.cp + w.slot0;                                      \
+    a0.jbits = jbits_;                                              \
+    a0.jloc = jloc_;                                                \
+    a0.seqb = seqb_;                                                \
+    a0.wnib = wnib_;                                                \
+    a0.stile = stile_;                                              \
+    a0.sbytes = sbytes_;                                            \
+    a0.sbytes_cap = cap_sbytes_ - 64;                               \
+    a0.tile_hw = tile_hw_;                                          \
+    a0.tile_sums = tile_sums_;                                      \
+    a0.hbits = hbits_;                                              \
+    a0.hrank = hrank_;                                              \
+    a0.doc_root = doc_root_;                                        \
+    a0.doc_p0 = doc_p0_;                                            \
+    a0.ctl = ctl_;                                                  \
+    a0.r_head = r_head_;                                            \
+    a0.r_pstart = r_pstart_;                                        \
+    a0.r_parent = r_parent_;                                        \
+    a0.r_w = r_w_;                                                  \
+    a0.r_key = r_key_;                                              \
+    a0.cap_runs = 0xFFFFFFFFu;                                      \
+    a0.cap_rmax = 0xFFFFFFFFu
+
+// Tree / digest argument block (run counts come from ctl where the kernels need them).
+#define TREEARGS(a)                                                                   \
+    TreeArgs a{};                                                                     \
+    a.ndocs = w.ndocs;                                                                \
+    a.in_parent = r_parent_;                                                          \
+    a.key = r_key_;                                                                   \
+    a.in_w = r_w_;                                                                    \
+    a.doc_root = doc_root_;                                                           \
+    a.doc_p0 = doc_p0_;                                                               \
+    a.deg = deg_; a.cstart = cstart_; a.child = child_; a.rec = rec_;                 \
+    a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;     \
+    a.roff = roff_;                                                                   \
+    a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
+    a.dig = dig_; a.leafcp = leafcp_; a.gcp = gcp_; a.doccp = doccp_;                 \
+    a.text = text_;                                                                   \
+    a.text_cap = ord ? w.order_cap : cap_text_ - 64;                                  \
+    a.align = ord ? 1u : 16u
+
+int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs,
+                          uint32_t cap_rmax, hipEvent_t* ev) {
+    hipStream_t s = stream;
+    L0ARGS(a0);
+    a0.cap_runs = cap_runs;
+    a0.cap_rmax = cap_rmax;
+    const uint32_t ntiles = a0.ntiles;
+    const uint32_t nsums = (ntiles + kScanTile - 1) / kScanTile;
     HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
     HIPCHK(hipMemsetAsync(jbits_, 0, (w.nslots / 32 + 4) * 4ull, s), "memset jump bits");
     BEGIN(S_CLASSIFY);
@@ -2185,101 +2333,75 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     k_docmax<<<1, 1024, 0, s>>>(a0);
     END(S_RUNS);
     HIPCHK(hipGetLastError(), "level-0 launch");
-    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
-    HIPCHK(hipStreamSynchronize(s), "level-0 sync");
-    if (gate.owns_lock()) gate.unlock();
-    if (host_ctl_[C_ERR]) {
-        err = host_ctl_[C_ERR] & 4u ? "op log holds more text than planned"
-                                    : "malformed op log: parent id out of range";
-        return CRDT_HIP_EBADLOG;
-    }
-    const uint32_t R = host_ctl_[C_RTOTAL];
-    const uint32_t wtotal = host_ctl_[C_WTOTAL];
-    const uint32_t rmax = host_ctl_[C_RMAX];
-    // global path splitter stride: longer sublists once the pointer jumping over the splitter
-    // lists dominates (measured on config 5: 182 M runs, stride 16 -> 64 took 72 -> 59 ms)
-    const uint32_t log2m = log2m_set ? this->log2m : (R > (1u << 24) ? 6u : 4u);
-    const uint32_t Sreg = 2 * ((R + (1u << log2m) - 1) >> log2m);
-    const uint32_t S = Sreg + w.ndocs;
-    const int rc = ensure_runs(R, S);
-    if (rc) return rc;
-    a0.r_parent = r_parent_;
-    a0.r_w = r_w_;
-    a0.r_key = r_key_;
-    // Per-document LDS path when the largest document's run tree fits one workgroup.
-    const uint32_t rcap = (rmax + 2u + 7u) & ~7u;
-    const uint32_t scap = (((rmax + 3u) >> kDocLog2S) + 8u) & ~7u;
-    const uint64_t dbytes = doctree_lds_bytes(rcap, scap);
-    // (sublist offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
-    const bool lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
-                      dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
-    BEGIN(S_RPARENT);
-    k_run_parent<<<grid_for(R, kBlock * kRunsPerThread), kBlock, 0, s>>>(a0, R, wtotal);
-    END(S_RPARENT);
+    return CRDT_HIP_OK;
+}
 
-    // ---- level 1: the tree of runs -------------------------------------------------------
-    TreeArgs a{};
+// k_run_parent, k_doctotals, k_doctree (and k_expand for documents whose text did not fit).
+int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
+                              hipEvent_t* ev) {
+    hipStream_t s = stream;
+    L0ARGS(a0);
+    TREEARGS(a);
+    BEGIN(S_RPARENT);
+    k_run_parent<<<std::min<uint32_t>(grid_for(p.R, kBlock * kRunsPerThread), 8192u) + 1u, kBlock,
+                   0, s>>>(a0);
+    END(S_RPARENT);
+    for (int st = S_COUNT; st <= S_WALK2; ++st) {
+        BEGIN(st);
+        END(st);
+    }
+    DocArgs da{};
+    da.ndocs = w.ndocs;
+    da.rcap = p.rcap;
+    da.scap = p.scap;
+    da.chbytes = doctree_ch_bytes(p.rcap, p.scap);
+    da.doc_root = doc_root_;
+    da.r_parent = r_parent_;
+    da.r_w = r_w_;
+    da.r_key = r_key_;
+    da.roff = roff_;
+    da.ctl = ctl_;
+    da.r_pstart = r_pstart_;
+    da.doc_p0 = doc_p0_;
+    da.tlen = tlen_;
+    da.toff = toff_;
+    da.sbytes = sbytes_;
+    da.text = p.fuse ? text_ : nullptr;
+    da.fused = doc_fused_;
+    da.lds_bytes = (uint32_t)p.dyn_bytes;
+    if (const char* pe = getenv("CRDT_HIP_PROBE")) da.probe = 1u + (uint32_t)atoi(pe);
+    BEGIN(S_DOCTREE);
+    k_doctotals<<<1, 1024, 0, s>>>(a);
+    k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+    END(S_DOCTREE);
+    HIPCHK(hipGetLastError(), "level-1 launch");
+    return CRDT_HIP_OK;
+}
+
+// The global (grid-wide) level 1, for waves whose documents do not fit the LDS path.  Grids are
+// sized by the exact run count (the caller waited for level 0).
+int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
+                                 hipEvent_t* ev, uint32_t& rounds) {
+    hipStream_t s = stream;
+    L0ARGS(a0);
+    TREEARGS(a);
+    const uint32_t R = p.R;
+    // splitter stride: longer sublists once the pointer jumping over the splitter lists
+    // dominates (measured on config 5: 182 M runs, stride 16 -> 64 took 72 -> 59 ms)
+    const uint32_t log2m_w = log2m_set ? this->log2m : (R > (1u << 24) ? 6u : 4u);
+    const uint32_t Sreg = 2 * ((R + (1u << log2m_w) - 1) >> log2m_w);
+    const uint32_t S = Sreg + w.ndocs;
     a.R = R;
-    a.log2m = log2m;
-    a.ndocs = w.ndocs;
+    a.log2m = log2m_w;
     a.Sreg = Sreg;
     a.S = S;
     a.step_limit = 2u * R + 4u;
-    a.in_parent = r_parent_;
-    a.key = r_key_;
-    a.in_w = r_w_;
-    a.doc_root = doc_root_;
-    a.doc_p0 = doc_p0_;
-    a.wtotal = wtotal;
-    a.deg = deg_; a.cstart = cstart_; a.child = child_; a.rec = rec_;
-    a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;
-    a.roff = roff_;
-    a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; a.dig = dig_;
-    a.text = text_;
-    a.text_cap = ord ? w.order_cap : cap_text_ - 64;
-    a.align = ord ? 1u : 16u;
     const uint32_t gR = grid_for(R), gS = grid_for(S);
     const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
-
-    // expansion + digest fused into k_doctree when every document's text fits LDS
-    const bool fuse = lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
-    // text staging + run-start bitvector (tl/8 + tl/16) + one u32 per run
-    const uint64_t dyn_bytes =
-        fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
-                   dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
-             : dbytes;
-    uint32_t rounds = 0;
-    if (lds1) {
-        for (int st = S_COUNT; st <= S_WALK2; ++st) {
-            BEGIN(st);
-            END(st);
-        }
-        DocArgs da{};
-        da.ndocs = w.ndocs;
-        da.rtotal = R;
-        da.rcap = rcap;
-        da.scap = scap;
-        da.chbytes = doctree_ch_bytes(rcap, scap);
-        da.doc_root = doc_root_;
-        da.r_parent = r_parent_;
-        da.r_w = r_w_;
-        da.r_key = r_key_;
-        da.roff = roff_;
-        da.ctl = ctl_;
-        da.r_pstart = r_pstart_;
-        da.doc_p0 = doc_p0_;
-        da.tlen = tlen_;
-        da.toff = toff_;
-        da.sbytes = sbytes_;
-        da.text = fuse ? text_ : nullptr;
-        da.fused = doc_fused_;
-        da.lds_bytes = (uint32_t)dyn_bytes;
-        if (const char* pe = getenv("CRDT_HIP_PROBE")) da.probe = 1u + (uint32_t)atoi(pe);
-        BEGIN(S_DOCTREE);
-        k_doctotals<<<1, 1024, 0, s>>>(a);
-        k_doctree<<<w.ndocs, kDocThreads, (uint32_t)dyn_bytes, s>>>(da);
-        END(S_DOCTREE);
-    } else {
+    BEGIN(S_RPARENT);
+    k_run_parent<<<std::min<uint32_t>(grid_for(R, kBlock * kRunsPerThread), 8192u) + 1u, kBlock,
+                   0, s>>>(a0);
+    END(S_RPARENT);
     BEGIN(S_DOCTREE);
     END(S_DOCTREE);
     BEGIN(S_COUNT);
@@ -2306,7 +2428,7 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     k_pred<<<gS, kBlock, 0, s>>>(snext_, S, pred_);
     k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, S, v0_, p0_);
     // a document's list holds at most 2 * (ceil(runs / M) + 1) + 1 splitters
-    rounds = ceil_log2(2ull * ((rmax + (1u << log2m) - 1) >> log2m) + 4);
+    rounds = ceil_log2(2ull * ((p.rmax + (1u << log2m_w) - 1) >> log2m_w) + 4);
     uint32_t *vi = v0_, *pi = p0_, *vo = v1_, *po = p1_;
     for (uint32_t r = 0; r < rounds; ++r) {
         k_wstep<<<gS, kBlock, 0, s>>>(vi, pi, S, vo, po);
@@ -2319,11 +2441,18 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
     END(S_WALK2);
-    }  // global level 1
+    HIPCHK(hipGetLastError(), "level-1 launch");
+    return CRDT_HIP_OK;
+}
 
-    // ---- expansion + digest --------------------------------------------------------------
+// Expansion (documents k_doctree did not write), digest, and the copies of the wave's results
+// into the pinned host arrays (lengths, digests, codepoints per document; ctl into hctl).
+int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, hipEvent_t* ev,
+                        uint32_t* hctl) {
+    hipStream_t s = stream;
+    L0ARGS(a0);
+    TREEARGS(a);
     ExpandArgs ea{};
-    ea.R = R;
     ea.mode = a0.mode;
     ea.log2m = L.log2m;
     ea.chunk_doc = a0.chunk_doc;
@@ -2337,15 +2466,9 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     ea.sbytes = sbytes_;
     ea.text = text_;
     ea.ctl = ctl_;
+    ea.fused = fused ? doc_fused_ : nullptr;
     BEGIN(S_EXPAND);
-    bool expand_run = true;
-    if (fuse) {  // only documents whose text did not fit k_doctree's LDS are left
-        HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
-        HIPCHK(hipStreamSynchronize(s), "doctree sync");
-        expand_run = host_ctl_[C_UNFUSED] != 0;
-        ea.fused = doc_fused_;
-    }
-    if (expand_run) k_expand<<<gR, kBlock, 0, s>>>(ea);
+    k_expand<<<4096, kBlock, 0, s>>>(ea);
     END(S_EXPAND);
     BEGIN(S_DIGEST);
     if (!ord) {
@@ -2358,57 +2481,135 @@ int Engine::run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>
     HIPCHK(hipGetLastError(), "kernel launch");
     HIPCHK(hipMemcpyAsync(host_len_ + w.first_doc, tlen_, w.ndocs * 4ull, hipMemcpyDeviceToHost, s),
            "copy lens");
-    if (!ord)
+    if (!ord) {
         HIPCHK(hipMemcpyAsync(host_dig_ + w.first_doc, dig_, w.ndocs * 8ull, hipMemcpyDeviceToHost, s),
                "copy digests");
-    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
-    HIPCHK(hipStreamSynchronize(s), "merge wave");
-    const uint32_t g1 = lds1 ? 0u : 1u;
+        HIPCHK(hipMemcpyAsync(host_cp_ + w.first_doc, doccp_, w.ndocs * 4ull, hipMemcpyDeviceToHost, s),
+               "copy codepoints");
+    }
+    HIPCHK(hipMemcpyAsync(hctl, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
+    return CRDT_HIP_OK;
+}
+#undef BEGIN
+#undef END
+#undef L0ARGS
+#undef TREEARGS
+
+int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t rounds,
+                        const hipEvent_t* ev, const uint32_t* hctl, std::vector<float>& stage_ms,
+                        std::vector<uint32_t>& stage_launches) {
+    const uint32_t g1 = p.lds1 ? 0u : 1u;
+    const bool expand_run = !p.fuse || hctl[C_UNFUSED] != 0;
     const uint32_t launches[S_N] = {1, 6, 1, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
-                                    lds1 ? 2u : 0u};
+                                    p.lds1 ? 2u : 0u};
     for (int i = 0; i < S_N; ++i) {
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, ev_[2 * i], ev_[2 * i + 1]), "event time");
+        HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]), "event time");
         stage_ms[i] += ms;
         stage_launches[i] += launches[i];
     }
-#undef BEGIN
-#undef END
+    return CRDT_HIP_OK;
+}
+
+// One wave, waiting for level 0 to learn its run counts (the first merge of a set of logs, the
+// global level-1 path, ORDER mode).  Records the wave's launch plan for later merges.
+int Engine::run_wave(DeviceLogs& L, Wave& w, Mode mode, std::vector<float>& stage_ms,
+                     std::vector<uint32_t>& stage_launches, bool force_global) {
+    hipStream_t s = stream;
+    const bool ord = mode == ORDER;
+    hipEvent_t* ev = ev_.data();
+    // run records are written before the run count is known: runs <= slots
+    if (w.nslots > cap_heads_) {
+        dfree(r_head_); dfree(r_pstart_);
+        HIPCHK(dalloc(&r_head_, w.nslots + 64ull), "hipMalloc r_head");
+        HIPCHK(dalloc(&r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
+        cap_heads_ = w.nslots;
+    }
+    // ---- level 0: runs.  Lanes take turns here (an HBM stream): the gate is held from the first
+    // level-0 launch to the level-0 sync, so one lane's level 0 overlaps the others' latency-bound
+    // level 1.
+    std::unique_lock<std::mutex> gate;
+    if (l0_gate_) gate = std::unique_lock<std::mutex>(*l0_gate_);
+    int rc = launch_level0(L, w, ord, 0xFFFFFFFFu, 0xFFFFFFFFu, ev);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
+    HIPCHK(hipStreamSynchronize(s), "level-0 sync");
+    if (gate.owns_lock()) gate.unlock();
+    if (host_ctl_[C_ERR]) {
+        err = host_ctl_[C_ERR] & 4u ? "op log holds more text than planned"
+                                    : "malformed op log: parent id out of range";
+        return CRDT_HIP_EBADLOG;
+    }
+    const L1Plan p = plan_level1(w, host_ctl_[C_RTOTAL], host_ctl_[C_RMAX], ord, force_global);
+    const uint32_t lg = log2m_set ? log2m : (p.R > (1u << 24) ? 6u : 4u);
+    const uint32_t Sreg = 2 * ((p.R + (1u << lg) - 1) >> lg);
+    rc = ensure_runs(p.R, Sreg + w.ndocs);
+    if (rc) return rc;
+    uint32_t rounds = 0;
+    rc = p.lds1 ? launch_lds_level1(L, w, ord, p, ev) : launch_global_level1(L, w, ord, p, ev, rounds);
+    if (rc) return rc;
+    rc = launch_tail(L, w, ord, p.fuse, ev, host_ctl_);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s), "merge wave");
     uint32_t errs = host_ctl_[C_ERR];
-    if (lds1 && (errs & 32u)) {
+    if (p.lds1 && (errs & 32u)) {
         // a sibling group wider than the LDS path sorts: redo the wave on the global path
         return run_wave(L, w, mode, stage_ms, stage_launches, true);
     }
-    runs_ += R;
-    if (!errs && host_ctl_[C_VISITED] != R) errs |= 16u;  // unreachable runs: a cycle
+    rc = finish_wave(w, ord, p, rounds, ev, host_ctl_, stage_ms, stage_launches);
+    if (rc) return rc;
+    runs_ += p.R;
+    if (!errs && host_ctl_[C_VISITED] != p.R) errs |= 16u;  // unreachable runs: a cycle
     if (errs) {
         (void)hipMemset(deg_, 0, (cap_runs_ + 16) * 4);  // restore the all-zero invariant
         err = "malformed op log detected on device (flags " + std::to_string(errs) + ")";
         return CRDT_HIP_EBADLOG;
     }
+    w.hint_runs = p.R;
+    w.hint_rmax = p.rmax;
+    w.hint_lds = p.lds1 && p.fuse && !ord;
     return CRDT_HIP_OK;
 }
 
+void Engine::collect(const DeviceLogs& L, uint32_t wi, uint64_t* digests, uint64_t* lens,
+                     uint64_t* cps, uint64_t& text_bytes) const {
+    const Wave& w = L.waves[wi];
+    for (uint32_t d = w.first_doc; d < w.first_doc + w.ndocs; ++d) {
+        if (lens) lens[d] = host_len_[d];
+        if (digests) digests[d] = host_dig_[d];
+        if (cps) cps[d] = host_cp_[d];
+        text_bytes += host_len_[d];
+    }
+}
+
 int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, crdt_hip_stats* st,
-                  std::vector<uint8_t>* text_out, std::vector<uint64_t>* text_offsets) {
+                  std::vector<uint8_t>* text_out, std::vector<uint64_t>* text_offsets,
+                  uint64_t* cps) {
     HIPCHK(hipSetDevice(device), "hipSetDevice");
     if ((text_out || text_offsets) && L.waves.size() > 1) {
         err = "text output needs a single-wave merge";
         return CRDT_HIP_EINVAL;
     }
-    if (lanes > 1 && L.waves.size() > 1) return merge_lanes(L, mode, digests, lens, st);
+    bool hinted = plan_cache && mode == TEXT && !text_out && !text_offsets && !L.waves.empty();
+    for (const Wave& w : L.waves) hinted = hinted && w.hint_lds;
+    if (hinted) return merge_async(L, digests, lens, cps, st);
+    if (lanes > 1 && L.waves.size() > 1 && !text_out) return merge_lanes(L, mode, digests, lens, cps, st);
     std::vector<float> stage_ms(S_N, 0.f);
     std::vector<uint32_t> stage_launches(S_N, 0);
     const uint32_t ndocs = (uint32_t)L.docs.size();
     runs_ = 0;
+    if (const int hc = ensure_host_ctl(1)) return hc;
     HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
-    for (const Wave& w : L.waves) {
+    uint64_t text_bytes = 0;
+    for (uint32_t wi = 0; wi < L.waves.size(); ++wi) {
+        Wave& w = L.waves[wi];
         int rc = ensure_scratch(w, ndocs);
         if (rc) return rc;
         rc = run_wave(L, w, mode, stage_ms, stage_launches);
         if (rc) return rc;
+        collect(L, wi, digests, lens, cps, text_bytes);
         if (text_out) {
             std::vector<uint64_t> offs(w.ndocs + 1);
             HIPCHK(hipMemcpy(offs.data(), toff_, (w.ndocs + 1) * 8ull, hipMemcpyDeviceToHost),
@@ -2422,12 +2623,6 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
     }
     HIPCHK(hipEventRecord(ev_[2 * S_N + 2], stream), "event record");
     HIPCHK(hipEventSynchronize(ev_[2 * S_N + 2]), "event sync");
-    uint64_t text_bytes = 0;
-    for (uint32_t d = 0; d < ndocs; ++d) {
-        if (lens) lens[d] = host_len_[d];
-        if (digests) digests[d] = host_dig_[d];
-        text_bytes += host_len_[d];
-    }
     if (st) {
         std::memset(st, 0, sizeof *st);
         st->items = L.items;
@@ -2447,11 +2642,159 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
     return CRDT_HIP_OK;
 }
 
-// Multi-wave merge over lanes: wave i runs on lane i % K, every lane in its own host thread on
-// its own stream and scratch (run_wave is synchronous per wave).  Stage times are summed over
-// the lanes (kernel time, which can exceed the wall time); total_ns is the host wall time.
-int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+// Every wave of a merge whose launch plans are known (an earlier merge of the same logs learnt
+// them), enqueued without waiting: wave i goes to lane i % K (this engine or a helper engine:
+// own stream and scratch), one host thread enqueues them all.  With the level-0 gate, a wave's
+// level 0 waits (hipStreamWaitEvent) for the previous wave's level 0 to end, so level 0 of one
+// wave runs beside the latency-bound level 1 of another, as merge_lanes' mutex does.  The host
+// waits once, at the end; a wave whose device check failed (C_REPLAN, or a sibling group too wide
+// for the LDS path) is merged again on the synchronous path.
+int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64_t* cps,
                         crdt_hip_stats* st) {
+    const uint32_t nw = (uint32_t)L.waves.size();
+    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>(lanes, nw));
+    while (lane_eng_.size() + 1 < K) {
+        auto e = std::make_unique<Engine>();
+        const std::string m = e->init(device);
+        if (!m.empty()) {
+            err = "lane engine: " + m;
+            return CRDT_HIP_EDEVICE;
+        }
+        lane_eng_.push_back(std::move(e));
+    }
+    std::vector<Engine*> eng(K, this);
+    for (uint32_t i = 1; i < K; ++i) {
+        eng[i] = lane_eng_[i - 1].get();
+        eng[i]->log2m = log2m;
+        eng[i]->log2m_set = log2m_set;
+        eng[i]->level1_global = level1_global;
+    }
+    const uint32_t ndocs = (uint32_t)L.docs.size();
+    // every allocation before the first launch (a pool free waits for the device)
+    const uint32_t per_lane = (nw + K - 1) / K;
+    std::vector<L1Plan> plans(nw);
+    for (uint32_t wi = 0; wi < nw; ++wi) {
+        Engine& E = *eng[wi % K];
+        Wave& w = L.waves[wi];
+        // test hook: a plan too small for the wave (the device must flag it, the host redo it)
+        const uint32_t cr = plan_shrink ? w.hint_runs / 2 : w.hint_runs;
+        const uint32_t cm = plan_shrink ? w.hint_rmax / 2 : w.hint_rmax;
+        plans[wi] = E.plan_level1(w, cr, cm, false, false);
+        int rc = E.ensure_scratch(w, ndocs);
+        if (rc) return rc;
+        rc = E.ensure_runs(cr, 0);
+        if (rc) return rc;
+        if (w.nslots > E.cap_heads_) {
+            dfree(E.r_head_); dfree(E.r_pstart_);
+            HIPCHK(dalloc(&E.r_head_, w.nslots + 64ull), "hipMalloc r_head");
+            HIPCHK(dalloc(&E.r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
+            E.cap_heads_ = w.nslots;
+        }
+    }
+    for (uint32_t i = 0; i < K; ++i) {
+        int rc = eng[i]->ensure_host_ctl(per_lane);
+        if (rc) return rc;
+        rc = eng[i]->ensure_events(eng[i]->wev_, per_lane * 2ull * S_N);
+        if (rc) return rc;
+        eng[i]->runs_ = 0;
+    }
+    HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
+    // the other lanes start after the merge's start event
+    for (uint32_t i = 1; i < K; ++i)
+        HIPCHK(hipStreamWaitEvent(eng[i]->stream, ev_[2 * S_N + 1], 0), "stream wait");
+    hipEvent_t prev_l0 = nullptr;
+    for (uint32_t wi = 0; wi < nw; ++wi) {
+        Engine& E = *eng[wi % K];
+        const Wave& w = L.waves[wi];
+        const uint32_t slot = wi / K;
+        hipEvent_t* ev = E.wev_.data() + slot * 2ull * S_N;
+        if (l0_gated && prev_l0 && K > 1)
+            HIPCHK(hipStreamWaitEvent(E.stream, prev_l0, 0), "stream wait");
+        // the plan's capacity: the learnt run counts exactly (the logs have not changed)
+        int rc = E.launch_level0(L, w, false, plans[wi].R, plans[wi].rmax, ev);
+        if (rc) return rc;
+        prev_l0 = ev[2 * S_RUNS + 1];
+        rc = E.launch_lds_level1(L, w, false, plans[wi], ev);
+        if (rc) return rc;
+        rc = E.launch_tail(L, w, false, true, ev, E.host_ctl_ + 16ull * slot);
+        if (rc) return rc;
+    }
+    // join: the merge's end event on this stream after every lane's last launch
+    for (uint32_t i = 1; i < K; ++i) {
+        hipEvent_t done = eng[i]->ev_[2 * S_N + 3];
+        HIPCHK(hipEventRecord(done, eng[i]->stream), "event record");
+        HIPCHK(hipStreamWaitEvent(stream, done, 0), "stream wait");
+    }
+    HIPCHK(hipEventRecord(ev_[2 * S_N + 2], stream), "event record");
+    HIPCHK(hipEventSynchronize(ev_[2 * S_N + 2]), "event sync");
+
+    std::vector<float> stage_ms(S_N, 0.f);
+    std::vector<uint32_t> stage_launches(S_N, 0);
+    uint64_t text_bytes = 0, runs = 0;
+    std::vector<uint32_t> redo;
+    uint32_t bad = 0;
+    for (uint32_t wi = 0; wi < nw; ++wi) {
+        Engine& E = *eng[wi % K];
+        const uint32_t slot = wi / K;
+        const uint32_t* hctl = E.host_ctl_ + 16ull * slot;
+        const Wave& w = L.waves[wi];
+        uint32_t errs = hctl[C_ERR];
+        if (hctl[C_REPLAN] || (errs & 32u)) {
+            redo.push_back(wi);
+            continue;
+        }
+        if (!errs && hctl[C_VISITED] != hctl[C_RTOTAL]) errs |= 16u;
+        if (errs) {
+            bad |= errs;
+            continue;
+        }
+        int rc = E.finish_wave(w, false, plans[wi], 0, E.wev_.data() + slot * 2ull * S_N, hctl,
+                               stage_ms, stage_launches);
+        if (rc) return rc;
+        runs += hctl[C_RTOTAL];
+        E.collect(L, wi, digests, lens, cps, text_bytes);
+    }
+    if (bad) {
+        err = "malformed op log detected on device (flags " + std::to_string(bad) + ")";
+        return CRDT_HIP_EBADLOG;
+    }
+    for (uint32_t wi : redo) {  // the logs changed under the plan: learn it again
+        L.waves[wi].hint_lds = false;
+        if (const int hc = ensure_host_ctl(1)) return hc;
+        runs_ = 0;
+        int rc = ensure_scratch(L.waves[wi], ndocs);
+        if (rc) return rc;
+        rc = run_wave(L, L.waves[wi], TEXT, stage_ms, stage_launches);
+        if (rc) return rc;
+        runs += runs_;
+        collect(L, wi, digests, lens, cps, text_bytes);
+    }
+    runs_ = runs;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->items = L.items;
+        st->docs = ndocs;
+        st->text_bytes = text_bytes;
+        st->runs = runs;
+        st->waves = nw;
+        st->nstages = S_N;
+        for (int i = 0; i < S_N; ++i) {
+            st->stage_ns[i] = (uint64_t)((double)stage_ms[i] * 1e6);
+            st->stage_launches[i] = stage_launches[i];
+        }
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N + 1], ev_[2 * S_N + 2]), "event time");
+        st->total_ns = (uint64_t)((double)tot * 1e6);
+    }
+    return CRDT_HIP_OK;
+}
+
+// Multi-wave merge over lanes, synchronous per wave: wave i runs on lane i % K, every lane in its
+// own host thread on its own stream and scratch (run_wave waits for each wave's level 0).  Stage
+// times are summed over the lanes (kernel time, which can exceed the wall time); total_ns is the
+// host wall time.
+int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+                        uint64_t* cps, crdt_hip_stats* st) {
     const uint32_t nw = (uint32_t)L.waves.size();
     const uint32_t K = std::min<uint32_t>(lanes, nw);
     while (lane_eng_.size() + 1 < K) {
@@ -2504,15 +2847,7 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
             return rc[i];
         }
     uint64_t text_bytes = 0, runs = 0;
-    for (uint32_t wi = 0; wi < nw; ++wi) {
-        const Engine& E = *eng[wi % K];
-        const Wave& w = L.waves[wi];
-        for (uint32_t d = w.first_doc; d < w.first_doc + w.ndocs; ++d) {
-            if (lens) lens[d] = E.host_len_[d];
-            if (digests) digests[d] = E.host_dig_[d];
-            text_bytes += E.host_len_[d];
-        }
-    }
+    for (uint32_t wi = 0; wi < nw; ++wi) eng[wi % K]->collect(L, wi, digests, lens, cps, text_bytes);
     for (uint32_t i = 0; i < K; ++i) runs += eng[i]->runs_;
     runs_ = runs;
     if (st) {
@@ -2560,29 +2895,37 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     const uint64_t total = (uint64_t)nb * replicas;
     if (total > 0xFFFFFFFFull) { err = "too many documents"; return CRDT_HIP_ERANGE; }
     docs.reserve(total);
+    uint32_t nmax = 0;
     for (uint64_t r = 0; r < total; ++r) docs.push_back(B.docs[r % nb]);
+    for (uint32_t b = 0; b < nb; ++b) nmax = std::max(nmax, B.docs[b].n);
     int rc = plan(R, docs);
     if (rc) return rc;
-    for (uint64_t r = 0; r < total; ++r) {
-        const uint32_t b = (uint32_t)(r % nb);
-        const uint32_t n = B.docs[b].n;
-        if (n == 0) continue;
-        Perm P{};
-        P.kind = relabel;
-        P.n = n;
-        P.bits = std::max<uint32_t>(2, ceil_log2(n));
-        const uint64_t h = mix64(seed, r);
-        P.shift = (uint32_t)(h % n);
-        for (int k = 0; k < 3; ++k) {
-            P.mul[k] = (uint32_t)mix64(h, 2 * k) | 1u;
-            P.add[k] = (uint32_t)mix64(h, 2 * k + 1);
-        }
-        k_replicate<<<grid_for(n), kBlock, 0, stream>>>(
-            B.parent, B.lamport, B.agent, B.cp, B.doc_slot[b], R.parent, R.lamport, R.agent, R.cp,
-            R.doc_slot[r], P);
+    std::vector<uint32_t> bn(nb);
+    for (uint32_t b = 0; b < nb; ++b) bn[b] = B.docs[b].n;
+    uint64_t *dbslot = nullptr, *drslot = nullptr;
+    uint32_t* dbn = nullptr;
+    HIPCHK(dalloc(&dbslot, nb), "hipMalloc base slots");
+    HIPCHK(dalloc(&dbn, nb), "hipMalloc base sizes");
+    HIPCHK(dalloc(&drslot, total), "hipMalloc replica slots");
+    hipError_t e = hipMemcpyAsync(dbslot, B.doc_slot.data(), nb * 8ull, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dbn, bn.data(), nb * 4ull, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(drslot, R.doc_slot.data(), total * 8ull, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess && nmax) {
+        // one launch for the whole batch (a launch per replica made setup, and a profiler
+        // serialising every dispatch, slow at 16,384 replicas)
+        const dim3 grid(std::min<uint32_t>(grid_for(nmax), 1024u),
+                        (uint32_t)std::min<uint64_t>(total, 65535u));
+        k_replicate<<<grid, kBlock, 0, stream>>>(B.parent, B.lamport, B.agent, B.cp, dbslot, dbn,
+                                                 nb, R.parent, R.lamport, R.agent, R.cp, drslot,
+                                                 total, relabel, seed);
+        e = hipGetLastError();
     }
-    HIPCHK(hipGetLastError(), "replicate launch");
-    HIPCHK(hipStreamSynchronize(stream), "replicate");
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    dfree(dbslot);
+    dfree(dbn);
+    dfree(drslot);
+    if (e != hipSuccess) return fail("replicate", e);
     return CRDT_HIP_OK;
 }
 

@@ -32,6 +32,20 @@ struct Wave {
     uint64_t leaf_cap;   // 4 KiB leaves
     uint64_t order_cap;  // u32 entries for ORDER mode
     uint64_t max_doc_text;  // largest document text bound of the wave
+    // Launch plan of the wave's level 1, learnt by a merge that waited for level 0 (run count,
+    // runs of the largest document); valid until the logs are planned again.  A merge that
+    // enqueues the wave with it does not wait for level 0: the device checks the plan (k_docmax
+    // flags C_REPLAN if the wave outgrew it) and the host merges such a wave again.
+    uint32_t hint_runs = 0, hint_rmax = 0;
+    bool hint_lds = false;  // the wave took the per-document LDS level 1 with fused text
+};
+
+// Level-1 launch configuration of a wave, from its run count and largest document.
+struct L1Plan {
+    uint32_t R = 0, rmax = 0;
+    bool lds1 = false, fuse = false;
+    uint32_t rcap = 0, scap = 0;
+    uint64_t dyn_bytes = 0;
 };
 
 // Tombstone flag of a device slot, folded into its codepoint word (one 4-byte stream instead of
@@ -76,6 +90,10 @@ public:
     // of one wave then overlaps the HBM-bound level 0 of another.
     uint32_t lanes = 2;
     bool l0_gated = true;  // lanes take turns at level 0 (see run_wave)
+    // Merges of logs merged before enqueue every wave with its learnt plan and wait once at the
+    // end (merge_async) instead of after each wave's level 0.
+    bool plan_cache = true;
+    bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -89,9 +107,10 @@ public:
     // Merge every wave of L.  digests/lens: per doc (host, may be null).  If text_out is set
     // (single-wave only), the merged bytes of the wave are copied back (docs concatenated,
     // each 16-aligned; offsets in text_offsets).
+    // cps: per doc, codepoints of the merged text (counted on the device; may be null).
     int merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, crdt_hip_stats* st,
               std::vector<uint8_t>* text_out = nullptr,
-              std::vector<uint64_t>* text_offsets = nullptr);
+              std::vector<uint64_t>* text_offsets = nullptr, uint64_t* cps = nullptr);
 
     // One config-5 document generated on the device (synth.cpp synth_tree_item, item by item).
     int synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t del_pct,
@@ -114,6 +133,7 @@ private:
     // per document
     uint32_t *doc_root_ = nullptr, *doc_p0_ = nullptr, *tlen_ = nullptr, *loff_ = nullptr;
     uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr, *ghash_ = nullptr;
+    uint32_t *leafcp_ = nullptr, *gcp_ = nullptr, *doccp_ = nullptr;
     uint8_t* text_ = nullptr;
     uint8_t* doc_fused_ = nullptr;
     // level-1 scratch (per run / per splitter), grown on demand
@@ -126,21 +146,43 @@ private:
     uint4* rec_ = nullptr;
     uint32_t *sw_ = nullptr, *snext_ = nullptr, *pred_ = nullptr, *v0_ = nullptr, *v1_ = nullptr,
              *p0_ = nullptr, *p1_ = nullptr;
-    uint32_t* host_ctl_ = nullptr;       // pinned
+    uint32_t* host_ctl_ = nullptr;       // pinned, 16 words per wave slot
+    uint32_t cap_host_ctl_ = 0;          // wave slots
     uint64_t* host_dig_ = nullptr;       // pinned
     uint32_t* host_len_ = nullptr;       // pinned
+    uint32_t* host_cp_ = nullptr;        // pinned
     uint64_t cap_host_docs_ = 0;
     uint64_t runs_ = 0;
-    std::vector<hipEvent_t> ev_;
+    std::vector<hipEvent_t> ev_;         // stage events of a synchronous wave
+    std::vector<hipEvent_t> wev_;        // stage events of every enqueued wave (merge_async)
     std::vector<std::unique_ptr<Engine>> lane_eng_;  // lanes 1..lanes-1 (lane 0 = this)
     std::mutex* l0_gate_ = nullptr;                  // set by merge_lanes
 
-    int merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+    int merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, uint64_t* cps,
+                    crdt_hip_stats* st);
+    int merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64_t* cps,
                     crdt_hip_stats* st);
     int ensure_runs(uint64_t runs, uint64_t splitters);
     int ensure_scratch(const Wave& w, uint32_t ndocs_total);
-    int run_wave(DeviceLogs& L, const Wave& w, Mode mode, std::vector<float>& stage_ms,
+    int ensure_host_ctl(uint32_t waves);
+    int ensure_events(std::vector<hipEvent_t>& ev, size_t n);
+    L1Plan plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord, bool force_global) const;
+    // The launches of one wave, in stream order.  ev: 2 events per stage (begin, end).
+    int launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs, uint32_t cap_rmax,
+                      hipEvent_t* ev);
+    int launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p, hipEvent_t* ev);
+    int launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
+                             hipEvent_t* ev, uint32_t& rounds);
+    int launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, hipEvent_t* ev,
+                    uint32_t* hctl);
+    // After the wave's stream has drained: stage times, launch counts, error flags.
+    int finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t rounds, const hipEvent_t* ev,
+                    const uint32_t* hctl, std::vector<float>& stage_ms,
+                    std::vector<uint32_t>& stage_launches);
+    int run_wave(DeviceLogs& L, Wave& w, Mode mode, std::vector<float>& stage_ms,
                  std::vector<uint32_t>& stage_launches, bool force_global = false);
+    void collect(const DeviceLogs& L, uint32_t wi, uint64_t* digests, uint64_t* lens,
+                 uint64_t* cps, uint64_t& text_bytes) const;
     int fail(const char* what, hipError_t e);
 };
 

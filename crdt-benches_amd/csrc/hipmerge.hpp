@@ -64,10 +64,12 @@ public:
     }
     // Upstream::len: the merge (Dt: checkout_tip().len(), rope.rs:134-136).  Codepoints.
     size_t len() const {
-        std::string t = text();
-        size_t n = 0;
-        for (unsigned char c : t) n += (c & 0xC0) != 0x80;
-        return n;
+        crdt_hip_oplog_view v;
+        check(crdt_hip_oplog_get_view(log_.get(), &v), nullptr, "view");
+        uint64_t cps = 0;
+        check(crdt_hip_merge_len(dev_->ctx, &v, &cps, nullptr, nullptr), dev_->ctx,
+              "crdt_hip_merge_len");
+        return (size_t)cps;
     }
     std::string text() const {
         crdt_hip_oplog_view v;
@@ -185,17 +187,21 @@ public:
         buf_.insert(buf_.end(), u.begin(), u.end());
         off_.push_back(buf_.size());
     }
-    size_t len() const {  // Upstream::len (codepoints) after the device merge
+    // Upstream::len (codepoints) of the merged document: counted on the device from the merged
+    // bytes, cross-checked against the decoder's counters.
+    size_t len() const {
         flush();
-        size_t n = 0;
-        uint64_t d = 0, items = 0, cps = 0, bytes = 0;
-        check(crdt_hip_replica_merge(dev_->ctx, rep_, nullptr, 0, &n, &d), dev_->ctx, "replica_merge");
+        uint64_t mcps = 0, mbytes = 0, items = 0, cps = 0, bytes = 0;
+        check(crdt_hip_replica_merge_len(dev_->ctx, rep_, &mcps, &mbytes, nullptr), dev_->ctx,
+              "replica_merge_len");
         crdt_hip_replica_info(rep_, &items, &cps, &bytes);
-        if (bytes != n) {
-            std::fprintf(stderr, "replica: merged %zu bytes, %llu visible\n", n, (unsigned long long)bytes);
+        if (mcps != cps || mbytes != bytes) {
+            std::fprintf(stderr, "replica: merged %llu codepoints / %llu bytes, decoder %llu / %llu\n",
+                         (unsigned long long)mcps, (unsigned long long)mbytes,
+                         (unsigned long long)cps, (unsigned long long)bytes);
             std::abort();
         }
-        return (size_t)cps;
+        return (size_t)mcps;
     }
     std::string text() const {
         flush();

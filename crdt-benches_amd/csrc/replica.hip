@@ -542,13 +542,13 @@ int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
 }
 
 int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* len,
-                  uint64_t* digest, crdt_hip_stats* st) {
+                  uint64_t* digest, crdt_hip_stats* st, uint64_t* cps) {
     int rc = replica_reserve(E, r, r.n);
     if (rc) return rc;
     std::vector<DocInfo> docs{DocInfo{r.n, r.vis_bytes}};
     rc = E.plan(r.logs, docs);
     if (rc) return rc;
-    return E.merge(r.logs, Engine::TEXT, digest, len, st, text, nullptr);
+    return E.merge(r.logs, Engine::TEXT, digest, len, st, text, nullptr, cps);
 }
 
 }  // namespace crdt

@@ -69,8 +69,9 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst);
 // OpLog::apply_update's semantics.  A batch that fails validation changes nothing.
 int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
                   const uint64_t* offsets, uint32_t n);
-// Merge the replica's document (text may be null: length and digest only).
+// Merge the replica's document (text may be null: length and digest only; cps: codepoints of
+// the merged text, counted on the device).
 int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* len,
-                  uint64_t* digest, crdt_hip_stats* st);
+                  uint64_t* digest, crdt_hip_stats* st, uint64_t* cps = nullptr);
 
 }  // namespace crdt

@@ -117,8 +117,10 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * the run tree whenever every document of a wave fits a workgroup's LDS (default), 1 = always
  * the global (multi-kernel) level-1 path, and "lanes" (1..8, default 2): waves of a multi-wave
  * merge run concurrently on that many streams, each with its own scratch (1 = one after the
- * other), "lane_gate" (default 1: lanes take turns at the HBM-bound level 0). Results never
- * depend on these. */
+ * other), "lane_gate" (default 1: lanes take turns at the HBM-bound level 0), "plan_cache"
+ * (default 1: a merge of logs merged before enqueues every wave with the launch plan the earlier
+ * merge learnt, checked on the device, and waits once instead of after each wave's level 0).
+ * Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 
 /* ---- op log: host-side resolver (positional patch -> anchor op) ---------------------------- */
@@ -191,6 +193,11 @@ int crdt_hip_synth_tree_visible(uint32_t n_items, uint32_t del_pct, uint64_t see
  * digest in *digest (either may be NULL).  If out is NULL only length/digest are produced. */
 int crdt_hip_merge(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint8_t* out, size_t cap,
                    size_t* out_len, uint64_t* digest);
+/* Upstream::len (rope.rs:16-19, 133-136) without copying the document back: merge one op log on
+ * the device and return the merged text's codepoints (counted on the device from the merged
+ * bytes), its UTF-8 length and its tree digest (each may be NULL). */
+int crdt_hip_merge_len(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* log, uint64_t* codepoints,
+                       uint64_t* bytes, uint64_t* digest);
 /* Merge n independent op logs; digests[i], lens[i] per log.  stats may be NULL. */
 int crdt_hip_merge_batch(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* logs, uint32_t n,
                          uint64_t* digests, uint64_t* lens, crdt_hip_stats* stats);
@@ -254,6 +261,11 @@ int crdt_hip_replica_info(const crdt_hip_replica* r, uint64_t* items,
 /* Merge the replica to its document (as crdt_hip_merge: out may be NULL). */
 int crdt_hip_replica_merge(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out, size_t cap,
                            size_t* out_len, uint64_t* digest);
+
+/* Downstream's len() (main.rs:68 asserts it; rope.rs:135 materialises): merge the replica and
+ * return the merged text's codepoints (counted on the device), UTF-8 bytes and tree digest. */
+int crdt_hip_replica_merge_len(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint64_t* codepoints,
+                               uint64_t* bytes, uint64_t* digest);
 
 /* ---- multi-GPU (RCCL over xGMI): digest/counter exchange only ----------------------------- */
 int crdt_hip_comm_unique_id(uint8_t id[128]);

@@ -358,3 +358,83 @@ def test_document_above_16mib_digest(ctx, oracle):
     ref = oracle.merge(to_anchor(log))
     assert int(lens[0]) == len(ref) == n
     assert int(dig[0]) == oracle.tree_digest(ref)
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3])
+def test_learnt_plan_merges_match_synchronous_ones(golden, lanes):
+    """A second merge of the same batch enqueues every wave with the plan the first merge
+    learnt (Engine::merge_async: no host wait after level 0); it must give the same digests,
+    lengths, codepoints and run counts as the synchronous path, for one and several lanes."""
+    bases = [resolved(n) for n in TRACES]
+    out = {}
+    for cache in (0, 1):
+        c = crdt_hip.Context(0)
+        c.set_param("lanes", lanes)
+        c.set_param("plan_cache", cache)
+        c.set_param("max_wave_slots", 1 << 20)  # several waves
+        b = c.batch(bases, replicas=3, relabel="rotate", seed=77)
+        res = [b.merge() for _ in range(3)]
+        for dig, lens, st in res:
+            assert st["waves"] >= 3
+            for r in range(b.docs):
+                name = TRACES[r % 4]
+                assert "%016x" % dig[r] == golden[name]["tree_digest"], (cache, r)
+                assert lens[r] == golden[name]["end_bytes"], (cache, r)
+        out[cache] = [(d.tolist(), l.tolist(), st["runs"], st["stage_launches"]) for d, l, st in res]
+        b.close()
+        c.close()
+    assert out[0] == out[1]
+
+
+def test_plan_that_no_longer_fits_is_redone():
+    """The device checks the enqueued plan (k_docmax flags C_REPLAN when the wave has more runs
+    than planned) and the host merges such a wave again: forced here with a plan of half size."""
+    bases = [resolved(n) for n in TRACES]
+    c = crdt_hip.Context(0)
+    c.set_param("max_wave_slots", 1 << 20)
+    b = c.batch(bases, replicas=2, relabel="rotate", seed=3)
+    d0, l0, s0 = b.merge()
+    c.set_param("plan_shrink", 1)
+    d1, l1, s1 = b.merge()
+    c.set_param("plan_shrink", 0)
+    d2, l2, s2 = b.merge()
+    assert np.array_equal(d0, d1) and np.array_equal(d0, d2)
+    assert np.array_equal(l0, l1) and np.array_equal(l0, l2)
+    assert s0["runs"] == s1["runs"] == s2["runs"]
+    b.close()
+    c.close()
+
+
+def test_merge_len_counts_codepoints_on_device(ctx, golden, py_trace):
+    """Upstream::len (rope.rs:16-19, 133-136): codepoints of the merged text, counted on the
+    device; multi-byte texts included."""
+    for name in TRACES:
+        cps, nbytes, dig = ctx.merge_len(resolved(name))
+        end = py_trace(name).end_content
+        assert (cps, nbytes) == (len(end), len(end.encode())), name
+        assert "%016x" % dig == golden[name]["tree_digest"]
+    rng = np.random.default_rng(3)
+    wide = crdt_hip.OpLog.synth_agents(30000, 8, 5).arrays()
+    wide.cp[:] = rng.choice([0x41, 0xE9, 0x2019, 0x4E2D, 0x1F600], wide.n)
+    text, _ = ctx.merge(wide)
+    cps, nbytes, _ = ctx.merge_len(wide)
+    assert nbytes == len(text) and cps == len(text.decode("utf-8"))
+    big = crdt_hip.LogArrays(np.arange(5_000_000, dtype=np.uint32),
+                             np.arange(1, 5_000_001, dtype=np.uint32),
+                             np.zeros(5_000_000, np.uint16), np.zeros(5_000_000, np.uint8),
+                             np.full(5_000_000, 0x4E2D, np.uint32))  # 15 MB: many leaves
+    cps, nbytes, _ = ctx.merge_len(big)
+    assert (cps, nbytes) == (5_000_000, 15_000_000)
+
+
+def test_rccl_single_rank_allgather(ctx):
+    """The engine's RCCL communicator (crdt_hip_comm_init + crdt_hip_allgather_u64) on one rank:
+    the digest / counter exchange bench.py runs after timing."""
+    c = crdt_hip.Context(0)
+    c.comm_init(1, 0, crdt_hip.Context.comm_unique_id())
+    v = np.array([1, 2**63 + 5, 0xDEADBEEF, 7], np.uint64)
+    out = c.allgather_u64(v, 1)
+    assert np.array_equal(out, v)
+    big = np.arange(16384, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    assert np.array_equal(c.allgather_u64(big, 1), big)
+    c.close()
