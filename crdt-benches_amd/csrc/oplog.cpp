@@ -359,23 +359,33 @@ std::string OpLog::apply_update(const uint8_t* buf, size_t len) {
     size_t need = 24 + (size_t)n * 16 + agent_bytes + (size_t)m * 4;
     if (len < need) return "truncated update";
     if (first == 0 || first > size() + 1) return "update is not causally ready (missing items)";
+    if (first_del > del_ops.size()) return "update is not causally ready (missing deletes)";
+    if ((uint64_t)first + n > 0xFFFFFFFFull) return "update item ids out of range";
     const uint8_t* P = buf + 24;
     const uint8_t* O = P + (size_t)n * 4;
     const uint8_t* L = O + (size_t)n * 4;
     const uint8_t* C = L + (size_t)n * 4;
     const uint8_t* A = C + (size_t)n * 4;
     const uint8_t* D = A + agent_bytes;
+    // validate everything before changing anything: a rejected update leaves the log as it was
+    // (as the device decoder does with a rejected batch)
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t id = first + k, par = get32(P + 4 * k);
+        if (id > size() && par >= id && par != 0) return "update item references an unknown parent";
+    }
+    const uint64_t known = std::max<uint64_t>(size(), n ? (uint64_t)first + n - 1 : 0);
+    for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t id = get32(D + 4 * k);
+        if (id == 0 || id > known) return "update deletes an unknown item";
+    }
     for (uint32_t k = 0; k < n; ++k) {
         uint32_t id = first + k;
         if (id <= size()) continue;  // already known (decode_and_add is idempotent)
-        uint32_t par = get32(P + 4 * k);
-        if (par >= id && par != 0) return "update item references an unknown parent";
-        push_item(par, get32(O + 4 * k), get32(L + 4 * k),
+        push_item(get32(P + 4 * k), get32(O + 4 * k), get32(L + 4 * k),
                   (uint16_t)(A[2 * k] | (A[2 * k + 1] << 8)), 0, get32(C + 4 * k));
     }
     for (uint32_t k = 0; k < m; ++k) {
-        uint32_t id = get32(D + 4 * k);
-        if (id == 0 || id > size()) return "update deletes an unknown item";
+        const uint32_t id = get32(D + 4 * k);
         if (first_del + k >= del_ops.size()) del_ops.push_back(id);
         mark_deleted(id);
     }

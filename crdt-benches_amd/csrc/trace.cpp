@@ -238,8 +238,8 @@ std::string chars_to_bytes(Trace& t) {
         size_t ncap = (len() + need) * 2 + 64;
         std::vector<uint8_t> nb(ncap);
         size_t tail = buf.size() - ge;
-        std::memcpy(nb.data(), buf.data(), gs);
-        std::memcpy(nb.data() + ncap - tail, buf.data() + ge, tail);
+        if (gs) std::memcpy(nb.data(), buf.data(), gs);  // (buf may still be empty: no null src)
+        if (tail) std::memcpy(nb.data() + ncap - tail, buf.data() + ge, tail);
         buf.swap(nb);
         ge = ncap - tail;
     };

@@ -193,3 +193,83 @@ def test_span_resolver_random_edits_match_oracle(oracle, seed):
     a, b = down.log.arrays(), up.arrays()
     for f in ("parent", "origin_right", "deleted", "cp"):
         assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_rejected_update_leaves_the_log_unchanged():
+    """The host decoder validates a whole update before applying any of it (as the device
+    decoder does with a batch): a bad parent, an unknown delete target or a delete index past
+    the log's deletes changes neither size() nor version()."""
+    import struct
+    up = crdt_hip.OpLog()
+    up.insert(0, "hello")
+    v0 = up.version()
+    up.insert(5, " world")
+    up.remove(0, 2)
+    good = up.encode_from(v0)
+    log = crdt_hip.OpLog()
+    log.insert(0, "hello")
+    before = (log.arrays().n, log.version())
+    words = list(struct.unpack(f"<{len(good) // 4}I", good))
+    n, m = words[3], words[5]
+    bad_parent = words.copy()
+    bad_parent[6 + n - 1] = 10_000  # the last new item's parent: unknown
+    bad_delete = words.copy()
+    bad_delete[-1] = 10_000  # the last delete: unknown item
+    bad_del_index = words.copy()
+    bad_del_index[4] = 7  # first_del beyond the log's deletes
+    for w in (bad_parent, bad_delete, bad_del_index):
+        with pytest.raises(crdt_hip.CrdtHipError):
+            log.apply_update(struct.pack(f"<{len(w)}I", *w))
+        assert (log.arrays().n, log.version()) == before
+    log.apply_update(good)
+    assert log.arrays().n == up.arrays().n and log.version() == up.version()
+    assert m == 2
+
+
+def test_parsers_survive_corrupted_inputs(tmp_path):
+    """Byte-flipped and truncated trace caches, op-log files and update buffers either parse or
+    fail with an error code; run under tools/asan_tests.sh (ASan + UBSan) nothing may overrun."""
+    rng = np.random.default_rng(2024)
+    t = crdt_hip.Trace(trace_path("sveltecomponent"))
+    cache = tmp_path / "t.bin"
+    t.save(str(cache))
+    log = t.resolve()
+    lpath = tmp_path / "l.bin"
+    log.save(str(lpath))
+    v0 = log.version()
+    up = log.clone()
+    up.insert(3, "xyzé’")
+    up.remove(10, 20)
+    upd = up.encode_from(v0)
+    for src, kind in ((cache.read_bytes(), "trace"), (lpath.read_bytes(), "log")):
+        for i in range(60):
+            b = bytearray(src)
+            if i % 3 == 0:
+                b = b[: int(rng.integers(0, len(b)))]
+            else:
+                for _ in range(int(rng.integers(1, 16))):
+                    k = int(rng.integers(0, min(len(b), 4096)))  # headers and index tables
+                    b[k] = int(rng.integers(0, 256))
+            p = tmp_path / f"bad_{kind}_{i}"
+            p.write_bytes(bytes(b))
+            try:
+                if kind == "trace":
+                    x = crdt_hip.Trace(str(p))
+                    len(x)
+                else:
+                    crdt_hip.OpLog.load(str(p))
+                    crdt_hip.LogFile(str(p)).close()
+            except crdt_hip.CrdtHipError:
+                pass
+    for i in range(300):
+        b = bytearray(upd)
+        if i % 4 == 0:
+            b = b[: int(rng.integers(0, len(b)))]
+        else:
+            for _ in range(int(rng.integers(1, 6))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        fresh = log.clone()
+        try:
+            fresh.apply_update(bytes(b))
+        except crdt_hip.CrdtHipError:
+            pass
