@@ -399,12 +399,16 @@ def roofline_fields(stats, batch, items_per_gpu, step_s) -> dict:
                       "alg_gbps": alg_bytes(k) / stage_ns[k] if stage_ns[k] and launches[k] else 0.0}
                   for k in stage_ns}
 
+    # one launch of a stage's main kernel per wave (a stage's helper kernels, e.g. k_doctotals
+    # beside k_doctree, are timed inside the stage: a few percent of it)
+    waves = max(1, stats[0]["waves"])
+
     def roof(k):
-        ns = stage_ns[k] / max(1, launches[k])
-        b = alg_bytes(k) / max(1, launches[k])
+        ns = stage_ns[k] / waves
+        b = alg_bytes(k) / waves
         return {"bound": "hbm", "kernel": STAGE_KERNEL.get(k, k), "achieved": b / ns,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": b / ns / HBM_PEAK_GBPS,
-                "traffic": measured_traffic(k, items_per_gpu / max(1, launches[k])),
+                "traffic": measured_traffic(k, items_per_gpu / waves),
                 "alg_bytes_per_launch": b, "launch_us": ns / 1e3}
 
     # the dominant kernel = the stage with the most device time per step (HIP events, summed

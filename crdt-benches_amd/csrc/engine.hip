@@ -1560,9 +1560,6 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // The sublist results (sum, next splitter) go to the ch region, which no walker reads.
     uint32_t runs = 0;
     uint32_t lane_steps = 0;
-#ifdef CRDT_HIP_PROBE
-    const uint64_t wc0 = clock64();
-#endif
     {
         uint32_t s = t;
         uint32_t s_next = atomicAdd(&qhead, 1u);  // the lane's next splitter, fetched ahead
@@ -1609,11 +1606,6 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     (void)lane_steps;
 #ifdef CRDT_HIP_PROBE
     if (a.probe && d == a.probe - 1u) {
-        const uint64_t wc1 = clock64();
-        uint32_t wm = lane_steps;
-        for (int o = 32; o; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, o));
-        if ((t & 63u) == 0) printf("[walkwave] %u iters %u cycles %llu\n", t >> 6, wm,
-                                   (unsigned long long)(wc1 - wc0));
         atomicMax(&probe_max, lane_steps);
         atomicAdd(&probe_sum, lane_steps);
     }
@@ -2251,6 +2243,7 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     p.dyn_bytes = p.fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
                                dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
                          : dbytes;
+    if (doctree_lds_max && p.lds1) p.dyn_bytes = kDocLds;  // experiment: one workgroup per CU
     return p;
 }
 

@@ -93,7 +93,8 @@ public:
     // Merges of logs merged before enqueue every wave with its learnt plan and wait once at the
     // end (merge_async) instead of after each wave's level 0.
     bool plan_cache = true;
-    bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
+    bool plan_shrink = false;
+    bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
