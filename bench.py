@@ -642,15 +642,18 @@ def downstream_workload(args) -> int:
         ok = True
         for name, npatch, init, src, _, dig, nbytes, ncp in work:
             t0 = time.perf_counter()
-            r = init.clone()
-            if args.pcie:
-                r.apply_packed(*src)
-            else:
-                r.apply_resident(src)
-            cps, n, d = r.merge_len()
+            if args.stepwise or args.pcie:
+                r = init.clone()
+                if args.pcie:
+                    r.apply_packed(*src)
+                else:
+                    r.apply_resident(src)
+                res = r.merge_len()
+                r.close()
+            else:  # the closure as one device call (crdt_hip_replica_replay)
+                res = init.replay(src)
             per[name] = per.get(name, 0.0) + time.perf_counter() - t0
-            ok &= (cps, n, d) == (ncp, nbytes, dig)
-            r.close()
+            ok &= res == (ncp, nbytes, dig)
         return ok
 
     for _ in range(args.warmup):
@@ -675,7 +678,9 @@ def downstream_workload(args) -> int:
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32", "data": "trace",
             "config": {"workload": "downstream (main.rs:63-69): clone + apply every update + len, "
-                                   "device decode, 4 traces one after the other",
+                                   "device decode, 4 traces one after the other, "
+                                   + ("clone / apply / merge_len calls" if args.stepwise or args.pcie
+                                      else "one crdt_hip_replica_replay call per closure"),
                        "updates": total_patches,
                        "encoded_bytes": int(sum(w[4] for w in work)),
                        "parallelism": f"replicas x{world} (no data-path collective)"},
@@ -705,6 +710,9 @@ def parse_args(argv=None):
     ap.add_argument("--pcie", action="store_true",
                     help="downstream: upload the encoded updates inside the timed region "
                          "(default: resident in HBM, as every other workload's inputs)")
+    ap.add_argument("--stepwise", action="store_true",
+                    help="downstream: clone, apply and merge as three calls (default: one "
+                         "crdt_hip_replica_replay call per closure)")
     ap.add_argument("--lane-gate", type=int, default=1, choices=[0, 1],
                     help="1: lanes take turns at level 0 (the HBM stream)")
     ap.add_argument("--lanes", type=int, default=2,

@@ -47,6 +47,7 @@ EXPORTS = [
     "crdt_hip_replica_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
     "crdt_hip_allgather_u64", "crdt_hip_comm_destroy", "crdt_hip_xxh64",
     "crdt_hip_tree_digest", "crdt_hip_merge_len", "crdt_hip_replica_merge_len",
+    "crdt_hip_replica_replay",
 ]
 
 
@@ -157,6 +158,7 @@ def lib() -> C.CDLL:
         "crdt_hip_replica_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_replica_merge": (i32, [vp, vp, vp, sz, P(sz), P(u64)]),
         "crdt_hip_replica_merge_len": (i32, [vp, vp, P(u64), P(u64), P(u64)]),
+        "crdt_hip_replica_replay": (i32, [vp, vp, vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_merge_len": (i32, [vp, P(View), P(u64), P(u64), P(u64)]),
         "crdt_hip_comm_unique_id": (i32, [vp]),
         "crdt_hip_comm_init": (i32, [vp, i32, i32, vp]),
@@ -665,6 +667,15 @@ class Replica:
         _check(lib().crdt_hip_replica_merge(self.ctx._h, self._h, None, 0, C.byref(n),
                                             C.byref(dig)), self.ctx._h)
         return int(n.value), int(dig.value)
+
+    def replay(self, batch: "UpdateBatch") -> tuple:
+        """The downstream closure (main.rs:63-69) in one device call: a copy of this replica
+        receives the whole resident batch and is merged; returns (codepoints, UTF-8 bytes, tree
+        digest) and leaves this replica unchanged (crdt_hip_replica_replay)."""
+        c, n, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().crdt_hip_replica_replay(self.ctx._h, self._h, batch._h, C.byref(c),
+                                             C.byref(n), C.byref(d)), self.ctx._h)
+        return int(c.value), int(n.value), int(d.value)
 
     def merge_len(self) -> tuple:
         """(codepoints, UTF-8 bytes, tree digest) of the merged document; the codepoints are

@@ -5,6 +5,7 @@
 
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -24,6 +25,9 @@ struct crdt_hip_ctx {
     crdt::DeviceLogs staging;
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0;
+    // replay sessions (crdt_hip_replica_replay): the work replica and learnt sizes per
+    // (initial replica, update batch), most recent first
+    std::vector<std::unique_ptr<crdt::ReplayState>> replays;
 };
 struct crdt_hip_oplog {
     crdt::OpLog log;
@@ -592,7 +596,17 @@ int crdt_hip_replica_clone(crdt_hip_ctx* ctx, const crdt_hip_replica* src,
         return 0;
     });
 }
+namespace {
+void drop_replays(crdt_hip_ctx* ctx, const void* init, const void* ub) {
+    if (!ctx) return;
+    auto& v = ctx->replays;
+    for (size_t i = v.size(); i-- > 0;)
+        if (v[i]->init == init || v[i]->ub == ub) v.erase(v.begin() + (long)i);
+}
+}  // namespace
+
 int crdt_hip_replica_free(crdt_hip_replica* r) {
+    if (r) drop_replays(r->ctx, &r->r, nullptr);
     delete r;
     return 0;
 }
@@ -620,8 +634,34 @@ int crdt_hip_updates_upload(crdt_hip_ctx* ctx, const uint8_t* buf, size_t len,
     });
 }
 int crdt_hip_updates_free(crdt_hip_updates* u) {
+    if (u) drop_replays(u->ctx, nullptr, &u->u);
     delete u;
     return 0;
+}
+
+int crdt_hip_replica_replay(crdt_hip_ctx* ctx, const crdt_hip_replica* init,
+                            const crdt_hip_updates* u, uint64_t* codepoints, uint64_t* bytes,
+                            uint64_t* digest) {
+    if (!ctx || !init || !u) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (init->ctx != ctx || u->ctx != ctx)
+        return set_err(ctx, CRDT_HIP_EINVAL, "replica or updates belong to another context");
+    return guard(ctx, [&] {
+        auto& v = ctx->replays;
+        size_t i = 0;
+        while (i < v.size() && !(v[i]->init == &init->r && v[i]->ub == &u->u)) ++i;
+        if (i == v.size()) {
+            if (v.size() >= 8) v.pop_back();
+            v.insert(v.begin(), std::make_unique<crdt::ReplayState>());
+            i = 0;
+        }
+        uint64_t c = 0, b = 0, d = 0;
+        const int rc = crdt::replica_replay(ctx->eng, init->r, u->u, *v[i], &c, &b, &d);
+        if (rc) return from_engine(ctx, rc);
+        if (codepoints) *codepoints = c;
+        if (bytes) *bytes = b;
+        if (digest) *digest = d;
+        return 0;
+    });
 }
 int crdt_hip_replica_apply_resident(crdt_hip_ctx* ctx, crdt_hip_replica* r,
                                     const crdt_hip_updates* u) {

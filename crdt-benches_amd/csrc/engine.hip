@@ -73,6 +73,14 @@ enum Ctl {
                     //   exits at once and the host merges the wave again with a fresh plan
 };
 
+// Level-0 scratch cleared in one launch: the wave's ctl words and its jump bitvector.
+__global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ ctl, uint4* __restrict__ bits,
+                                               uint32_t nq) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < 16) ctl[i] = 0;
+    for (uint32_t k = i; k < nq; k += gridDim.x * 256) bits[k] = make_uint4(0, 0, 0, 0);
+}
+
 // Every kernel after level 0 starts with this: a wave whose plan was too small does nothing.
 __device__ __forceinline__ bool replan(const uint32_t* ctl) { return ctl[C_REPLAN] != 0u; }
 
@@ -614,10 +622,10 @@ struct TreeArgs {
     uint32_t* loff;
     uint64_t* leafh;
     uint64_t* ghash;  // group digests of documents above 16 MiB (indexed like leafh)
-    uint64_t* dig;
     uint32_t* leafcp;  // per leaf: codepoints (UTF-8 bytes that are not continuation bytes)
     uint32_t* gcp;     // per group of a document above 16 MiB: codepoints
-    uint32_t* doccp;   // per document: codepoints of the merged text (Upstream::len)
+    uint4* res;        // per document {UTF-8 bytes, codepoints, digest lo, digest hi}: the wave's
+                       // results, after ctl in one block, copied to the host in one transfer
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
@@ -998,6 +1006,7 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
             const uint32_t end = d + 1 < a.ndocs ? a.doc_p0[d + 1] : wtotal;
             tl = end - a.doc_p0[d];
             a.tlen[d] = tl;
+            a.res[d] = make_uint4(tl, 0u, 0u, 0u);
         }
         const uint64_t sz = ((uint64_t)tl + am) & ~am;
         const uint32_t nl = a.align > 1 ? (tl + kLeaf - 1u) / kLeaf : 0u;
@@ -1095,8 +1104,12 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 // jumping) one pass turns them into document offsets.
 constexpr int kDocThreads = 1024;
 constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
-constexpr int kDocK = 5;           // splitters per thread: ceil(20480 / 4) = 5 * 1024
-constexpr uint32_t kDocLog2S = 2;  // splitters: the down arcs of the runs v % 4 == 0
+#ifndef CRDT_DOC_LOG2S
+#define CRDT_DOC_LOG2S 2
+#endif
+// splitters: the down arcs of the runs v % 2^kDocLog2S == 0; kDocK per thread
+constexpr uint32_t kDocLog2S = CRDT_DOC_LOG2S;
+constexpr int kDocK = (kDocJ + (1 << kDocLog2S) - 1) >> kDocLog2S;
 constexpr uint32_t kDocLds = 163840 - 1024;  // dynamic LDS budget (static arrays use the rest)
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
@@ -1153,7 +1166,7 @@ __device__ __forceinline__ uint64_t doc_key(const DocArgs& a, uint32_t base, uin
 constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
 __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t base, uint32_t R,
                                          const uint32_t (&ro)[kDocJ], uint8_t* st,
-                                         uint32_t* scan_lds) {
+                                         uint32_t* scan_lds, uint64_t* tprobe) {
     const uint32_t t = threadIdx.x;
     const uint32_t tl = a.tlen[d], p0 = a.doc_p0[d];
     const uint32_t sh = p0 & 15u;
@@ -1216,6 +1229,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
         }
     }
     __syncthreads();
+    if (tprobe) *tprobe = wall_clock64();
     // 3) the document in order, 16 bytes per lane per step (one bitvector word covers them)
     uint4* out = reinterpret_cast<uint4*>(a.text + a.toff[d]);  // 16-aligned
     for (uint32_t i = t; i < (tl + 15u) >> 4; i += kDocThreads) {
@@ -1248,7 +1262,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     const uint32_t t = threadIdx.x;
     const uint32_t base = a.doc_root[d];
     const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL]) - base;
-    const uint32_t S = (R + 3u) >> kDocLog2S;
+    const uint32_t S = (R + (1u << kDocLog2S) - 1u) >> kDocLog2S;
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
     uint16_t* ch = nx + a.rcap;
@@ -1260,7 +1274,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #ifdef CRDT_HIP_PROBE
     // phase timestamps of one document (probe build, CRDT_HIP_PROBE=<doc>)
     const bool probe = a.probe && d == a.probe - 1u && t == 0;
-    uint64_t tp[12];
+    uint64_t tp[20] = {};
     tp[0] = wall_clock64();
 #define PROBE(i) if (probe) tp[i] = wall_clock64()
 #else
@@ -1404,6 +1418,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         }
     }
     __syncthreads();
+    PROBE(12);
     {
         constexpr int kPairs = 8;
         const uint32_t np = npair;
@@ -1500,6 +1515,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         }
     }
     __syncthreads();
+    PROBE(13);
     if (flags) {
         if (t == 0) atomicOr(&a.ctl[C_ERR], (flags & 1u) ? 1u : 32u);
         return;
@@ -1525,6 +1541,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         }
     }
     __syncthreads();
+    PROBE(14);
     // ---- up links: a last child's up arc is followed by its parent's up arc (no weight, never a
     // splitter), so nx[v] = UP(p) may be replaced by nx[p].  In-place pointer jumping until no up
     // link is left: each thread keeps a bit per owned run still holding one and works only on
@@ -1659,26 +1676,47 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     __syncthreads();
     PROBE(9);
     if (a.text) {
-        const bool fused = doc_text(a, d, base, R, ro, reinterpret_cast<uint8_t*>(dyn), scan_lds);
-        if (!fused) {  // k_expand writes this document
+#ifdef CRDT_HIP_PROBE
+        uint64_t* tprobe = probe ? &tp[15] : nullptr;
+#else
+        uint64_t* tprobe = nullptr;
+#endif
+        const bool fused = doc_text(a, d, base, R, ro, reinterpret_cast<uint8_t*>(dyn), scan_lds,
+                                    tprobe);
+        if (!fused) {
+            // the text did not fit LDS: every run copies its bytes from the slot-order text to
+            // its document offset (byte stores; only documents above the LDS stage take this)
+            uint8_t* out = a.text + a.toff[d];
+            const uint32_t tl = a.tlen[d];
+            bool oob = false;
 #pragma unroll
-            for (int j = 0; j < kDocJ; ++j)
-                if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ro[j];
+            for (int j = 0; j < kDocJ; ++j) {
+                const uint32_t v = t + (uint32_t)j * kDocThreads;
+                if (ro[j] == kNil) continue;
+                const uint32_t ps = a.r_pstart[base + v], wv = a.r_w[base + v];
+                if ((uint64_t)ro[j] + wv > tl) {
+                    oob = true;
+                    continue;
+                }
+                for (uint32_t b = 0; b < wv; ++b) out[ro[j] + b] = a.sbytes[ps + b];
+            }
+            if (oob) atomicOr(&a.ctl[C_ERR], 8u);
             if (t == 0) atomicAdd(&a.ctl[C_UNFUSED], 1u);
         }
-        if (t == 0) a.fused[d] = fused ? 1u : 0u;
     }
     PROBE(10);
 #ifdef CRDT_HIP_PROBE
     if (probe) {
         printf("[doctree] doc %u R %u S %u us: load %.1f count %.1f scan %.1f place %.1f "
-               "sort %.1f (pairs %.1f) defer+fc %.1f walk1 %.1f jump %.1f offsets %.1f text %.1f | visited %u steps max %u "
-               "sum %u\n", d, R, S,
+               "glist %.1f pairs %.1f net3-8 %.1f wide9-64 %.1f fc %.1f uplinks %.1f walk1 %.1f "
+               "jump %.1f offsets %.1f text-stage %.1f text-out %.1f total %.1f | visited %u "
+               "steps max %u sum %u\n", d, R, S,
                (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
-               (tp[4] - tp[3]) / 100.0, (tp[5] - tp[4]) / 100.0, (tp[11] - tp[4]) / 100.0,
-               (tp[6] - tp[5]) / 100.0,
-               (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0, (tp[9] - tp[8]) / 100.0,
-               (tp[10] - tp[9]) / 100.0, visited_lds, probe_max, probe_sum);
+               (tp[4] - tp[3]) / 100.0, (tp[12] - tp[4]) / 100.0, (tp[11] - tp[12]) / 100.0,
+               (tp[5] - tp[11]) / 100.0, (tp[13] - tp[5]) / 100.0, (tp[14] - tp[13]) / 100.0,
+               (tp[6] - tp[14]) / 100.0, (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0,
+               (tp[9] - tp[8]) / 100.0, (tp[15] - tp[9]) / 100.0, (tp[10] - tp[15]) / 100.0,
+               (tp[10] - tp[0]) / 100.0, visited_lds, probe_max, probe_sum);
     }
 #endif
 #undef PROBE
@@ -1737,32 +1775,93 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
     return h;
 }
 
-// Codepoints of an 8-byte-aligned UTF-8 range: bytes minus continuation bytes (10xxxxxx).
-__device__ __forceinline__ uint32_t utf8_codepoints(const uint8_t* __restrict__ p, uint32_t len) {
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
-    uint32_t cont = 0, i = 0;
-    for (; i + 8 <= len; i += 8) {
-        const uint64_t x = w[i / 8];
-        cont += (uint32_t)__popcll(x & ~(x << 1) & 0x8080808080808080ull);
-    }
-    for (; i < len; ++i) cont += (p[i] & 0xC0u) == 0x80u ? 1u : 0u;
-    return len - cont;
-}
-
+// One wave per 4 KiB leaf: the leaf is loaded into LDS with 16-byte loads (the whole wave, one
+// round trip), then lanes 0-3 run xxh64's four stripe accumulators over it (lane i takes qword i
+// of every 32-byte stripe), lane 0 merges them and hashes the tail, and every lane counts the
+// codepoints of its 64 bytes.  The same digest as xxh64_aligned(leaf, len, 0), without a thread
+// walking 4 KiB alone.
+constexpr int kLeafWaves = kBlock / 64;
 __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_cap) {
-    const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
-    if (replan(a.ctl) || L >= leaf_cap || L >= a.loff[a.ndocs]) return;
+    __shared__ __attribute__((aligned(16))) uint64_t leaf[kLeafWaves][kLeaf / 8];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t L = blockIdx.x * kLeafWaves + wv;
+    if (replan(a.ctl) || L >= leaf_cap || L >= a.loff[a.ndocs]) return;  // wave-uniform
     uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (a.loff[mid] <= L) lo = mid; else hi = mid;
     }
     const uint32_t d = lo, j = L - a.loff[d];
-    const uint32_t tl = a.tlen[d];
-    const uint32_t len = min(kLeaf, tl - j * kLeaf);
-    const uint8_t* p = a.text + a.toff[d] + (uint64_t)j * kLeaf;
-    a.leafh[L] = xxh64_aligned(p, len, 0);
-    a.leafcp[L] = utf8_codepoints(p, len);
+    const uint32_t len = min(kLeaf, a.tlen[d] - j * kLeaf);
+    const uint4* src = reinterpret_cast<const uint4*>(a.text + a.toff[d] + (uint64_t)j * kLeaf);
+    uint4* dst = reinterpret_cast<uint4*>(leaf[wv]);
+    uint4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = lane + 64u * k;
+        q[k] = 16u * i < len ? src[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[lane + 64u * k] = q[k];
+    // codepoints: bytes minus continuation bytes, over this lane's 64 bytes (zero padding counts
+    // as non-continuation bytes, so count only up to len)
+    uint32_t cont = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t b0 = 16u * (lane + 64u * k);
+        const uint64_t w0 = ((uint64_t)q[k].y << 32) | q[k].x, w1 = ((uint64_t)q[k].w << 32) | q[k].z;
+        const uint32_t n0 = b0 >= len ? 0u : min(8u, len - b0);
+        const uint32_t n1 = b0 + 8u >= len ? 0u : min(8u, len - b0 - 8u);
+        const uint64_t m0 = n0 >= 8u ? ~0ull : ((1ull << (8u * n0)) - 1ull);
+        const uint64_t m1 = n1 >= 8u ? ~0ull : ((1ull << (8u * n1)) - 1ull);
+        cont += (uint32_t)__popcll(w0 & ~(w0 << 1) & 0x8080808080808080ull & m0);
+        cont += (uint32_t)__popcll(w1 & ~(w1 << 1) & 0x8080808080808080ull & m1);
+    }
+    const uint32_t cps = len - wave_sum(cont);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL,
+                   P3 = 0x165667B19E3779F9ULL, P4 = 0x85EBCA77C2B2AE63ULL,
+                   P5 = 0x27D4EB2F165667C5ULL;
+    const uint32_t nst = len / 32u;
+    uint64_t v = 0;
+    if (lane < 4u) {
+        v = lane == 0u ? P1 + P2 : lane == 1u ? P2 : lane == 2u ? 0ull : 0ull - P1;
+        const uint64_t* w = leaf[wv];
+        for (uint32_t k = 0; k < nst; ++k) v = xr(v, w[4u * k + lane]);
+    }
+    const uint64_t v1 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 0) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 0);
+    const uint64_t v2 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 1) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 1);
+    const uint64_t v3 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 2) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 2);
+    const uint64_t v4 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 3) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 3);
+    if (lane != 0u) return;
+    uint64_t h;
+    if (len >= 32u) {
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        h = xm(h, v1); h = xm(h, v2); h = xm(h, v3); h = xm(h, v4);
+    } else {
+        h = P5;
+    }
+    h += len;
+    const uint64_t* w = leaf[wv];
+    const uint8_t* pb = reinterpret_cast<const uint8_t*>(leaf[wv]);
+    uint32_t i = 32u * nst;
+    for (; i + 8u <= len; i += 8u) {
+        h ^= xr(0, w[i / 8u]);
+        h = rotl(h, 27) * P1 + P4;
+    }
+    if (i + 4u <= len) {
+        h ^= (uint64_t)(*reinterpret_cast<const uint32_t*>(pb + i)) * P1;
+        h = rotl(h, 23) * P2 + P3;
+        i += 4u;
+    }
+    for (; i < len; ++i) {
+        h ^= (uint64_t)pb[i] * P5;
+        h = rotl(h, 11) * P1;
+    }
+    h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+    a.leafh[L] = h;
+    a.leafcp[L] = cps;
 }
 
 // Documents of more than kGroup leaves (16 MiB): leaf digests hashed in groups of kGroup (seed =
@@ -1793,10 +1892,10 @@ __global__ __launch_bounds__(kBlock) void k_docdigest(TreeArgs a) {
     const uint64_t* h = nl > kGroup ? a.ghash + l0 : a.leafh + l0;
     const uint32_t* c = nl > kGroup ? a.gcp + l0 : a.leafcp + l0;
     const uint32_t nh = nl > kGroup ? (nl + kGroup - 1) / kGroup : nl;
-    a.dig[d] = xxh64_aligned(reinterpret_cast<const uint8_t*>(h), nh * 8u, a.tlen[d]);
+    const uint64_t dig = xxh64_aligned(reinterpret_cast<const uint8_t*>(h), nh * 8u, a.tlen[d]);
     uint32_t cps = 0;
     for (uint32_t i = 0; i < nh; ++i) cps += c[i];
-    a.doccp[d] = cps;
+    a.res[d] = make_uint4(a.tlen[d], cps, (uint32_t)dig, (uint32_t)(dig >> 32));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1934,6 +2033,7 @@ void DeviceLogs::release() {
     dfree(parent); dfree(lamport); dfree(agent); dfree(cp);
     dfree(docs_rel); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
+    tab_sig.clear();
 }
 
 Engine::~Engine() {
@@ -1943,14 +2043,11 @@ Engine::~Engine() {
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
-    dfree(ctl_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
+    dfree(out_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
     dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
-    dfree(dig_); dfree(leafh_); dfree(ghash_); dfree(text_);
-    dfree(leafcp_); dfree(gcp_); dfree(doccp_);
-    if (host_ctl_) (void)hipHostFree(host_ctl_);
-    if (host_dig_) (void)hipHostFree(host_dig_);
-    if (host_len_) (void)hipHostFree(host_len_);
-    if (host_cp_) (void)hipHostFree(host_cp_);
+    dfree(leafh_); dfree(ghash_); dfree(text_);
+    dfree(leafcp_); dfree(gcp_); dfree(tab_slot_); dfree(tab_local_);
+    if (host_out_) (void)hipHostFree(host_out_);
     for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : wev_) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1980,9 +2077,6 @@ std::string Engine::init(int dev) {
     ev_.resize(2 * S_N + 4);
     for (hipEvent_t& x : ev_)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hipGetErrorString(e);
-    if ((e = hipHostMalloc(reinterpret_cast<void**>(&host_ctl_), 64)) != hipSuccess)
-        return hipGetErrorString(e);
-    cap_host_ctl_ = 1;
     if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
         hipSuccess)
@@ -2027,6 +2121,16 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         slot += ds;
     }
     L.total_slots = slot;
+    for (Wave& w : L.waves) {  // a plan learnt on logs of the same shape
+        const WaveShape sh = shape_of(w);
+        for (const ShapeHint& h : shape_hints_)
+            if (h.shape == sh) {
+                w.hint_runs = h.runs;
+                w.hint_rmax = h.rmax;
+                w.hint_lds = true;
+                break;
+            }
+    }
     const uint64_t nchunks = slot / M;
     if (slot > L.cap_slots) {
         dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.cp);
@@ -2035,15 +2139,20 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         HIPCHK(dalloc(&L.agent, slot), "hipMalloc logs.agent");
         HIPCHK(dalloc(&L.cp, slot), "hipMalloc logs.cp");
         L.cap_slots = slot;
+        gen_++;
     }
     if (docs.size() > L.cap_docs) {
+        L.tab_sig.clear();
         dfree(L.docs_rel);
         HIPCHK(dalloc(&L.docs_rel, docs.size()), "hipMalloc logs.docs");
+        gen_++;
         L.cap_docs = docs.size();
     }
     if (nchunks > L.cap_chunks) {
+        L.tab_sig.clear();
         dfree(L.chunk_doc);
         HIPCHK(dalloc(&L.chunk_doc, nchunks), "hipMalloc logs.chunk_doc");
+        gen_++;
         L.cap_chunks = nchunks;
     }
     return upload_tables(L);
@@ -2052,6 +2161,17 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
 int Engine::upload_tables(DeviceLogs& L) {
     const uint32_t nd = (uint32_t)L.docs.size();
     if (nd == 0) return CRDT_HIP_OK;
+    // the same plan as the tables on the device (a replica merged again at the same size)
+    std::vector<uint64_t> sig;
+    sig.reserve(2 * nd + L.waves.size() + 1);
+    sig.push_back(L.total_slots);
+    for (uint32_t d = 0; d < nd; ++d) {
+        sig.push_back(L.docs[d].n);
+        sig.push_back(L.doc_slot[d]);
+    }
+    for (const Wave& w : L.waves) sig.push_back(w.first_doc);
+    if (sig == L.tab_sig) return CRDT_HIP_OK;
+    L.tab_sig.clear();
     std::vector<uint2> rel(nd);
     std::vector<uint32_t> local(nd);
     for (const Wave& w : L.waves)
@@ -2060,25 +2180,33 @@ int Engine::upload_tables(DeviceLogs& L) {
             rel[d] = make_uint2((uint32_t)(L.doc_slot[d] - w.slot0), L.docs[d].n);
             local[d] = k;
         }
+    // (pageable sources: hipMemcpyAsync has copied them when it returns; the tables are
+    // consumed in stream order, so no wait here)
     HIPCHK(hipMemcpyAsync(L.docs_rel, rel.data(), nd * sizeof(uint2), hipMemcpyHostToDevice, stream),
            "upload docs");
-    uint64_t* dslot = nullptr;
-    uint32_t* dlocal = nullptr;
-    HIPCHK(dalloc(&dslot, nd), "hipMalloc doc_slot");
-    HIPCHK(dalloc(&dlocal, nd), "hipMalloc doc_local");
-    hipError_t e = hipMemcpyAsync(dslot, L.doc_slot.data(), nd * 8, hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(dlocal, local.data(), nd * 4, hipMemcpyHostToDevice, stream);
     const uint64_t nchunks = L.total_slots >> L.log2m;
-    if (e == hipSuccess) {
-        k_chunk_doc<<<grid_for(nchunks), kBlock, 0, stream>>>(dslot, dlocal, nd, nchunks, L.log2m,
-                                                              L.chunk_doc);
-        e = hipGetLastError();
+    if (nd == 1) {  // one document: every chunk is document 0
+        HIPCHK(hipMemsetAsync(L.chunk_doc, 0, nchunks * 4, stream), "chunk table");
+        L.tab_sig = std::move(sig);
+        return CRDT_HIP_OK;
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    dfree(dslot);
-    dfree(dlocal);
-    if (e != hipSuccess) return fail("chunk table", e);
+    if (nd > cap_tab_) {
+        (void)hipStreamSynchronize(stream);
+        dfree(tab_slot_);
+        dfree(tab_local_);
+        cap_tab_ = 0;
+        HIPCHK(dalloc(&tab_slot_, nd), "hipMalloc doc_slot");
+        HIPCHK(dalloc(&tab_local_, nd), "hipMalloc doc_local");
+        cap_tab_ = nd;
+    }
+    HIPCHK(hipMemcpyAsync(tab_slot_, L.doc_slot.data(), nd * 8, hipMemcpyHostToDevice, stream),
+           "upload doc slots");
+    HIPCHK(hipMemcpyAsync(tab_local_, local.data(), nd * 4, hipMemcpyHostToDevice, stream),
+           "upload doc index");
+    k_chunk_doc<<<grid_for(nchunks), kBlock, 0, stream>>>(tab_slot_, tab_local_, nd, nchunks,
+                                                          L.log2m, L.chunk_doc);
+    HIPCHK(hipGetLastError(), "chunk table");
+    L.tab_sig = std::move(sig);
     return CRDT_HIP_OK;
 }
 
@@ -2103,13 +2231,13 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
     return CRDT_HIP_OK;
 }
 
-int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
+int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
         dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hrank_); dfree(stile_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
-        HIPCHK(dalloc(&jbits_, slots / 32 + 4), "hipMalloc jump bits");
+        HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
         HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
         HIPCHK(dalloc(&seqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
@@ -2119,32 +2247,36 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
         HIPCHK(dalloc(&tile_hw_, tiles), "hipMalloc tile totals");
         HIPCHK(dalloc(&tile_sums_, tiles / kScanTile + 2), "hipMalloc tile sums");
         cap_slots0_ = slots;
+        gen_++;
     }
     if (w.text_cap + 64 > cap_sbytes_) {
         dfree(sbytes_);
         HIPCHK(dalloc(&sbytes_, w.text_cap + 64), "hipMalloc slot-order text");
         cap_sbytes_ = w.text_cap + 64;
+        gen_++;
     }
-    if (!ctl_) HIPCHK(dalloc(&ctl_, 16), "hipMalloc ctl");
     if (w.ndocs + 1 > cap_docs_) {
-        dfree(tlen_); dfree(loff_); dfree(toff_); dfree(dig_); dfree(doc_root_); dfree(doc_p0_);
-        dfree(doc_fused_); dfree(doccp_);
+        dfree(tlen_); dfree(loff_); dfree(toff_); dfree(out_); dfree(doc_root_); dfree(doc_p0_);
+        dfree(doc_fused_);
         const uint64_t nd = w.ndocs + 1;
-        HIPCHK(dalloc(&doccp_, nd), "hipMalloc doc codepoints");
+        HIPCHK(dalloc(&out_, 16 + 4 * nd), "hipMalloc results");  // ctl + one uint4 per document
+        ctl_ = out_;
+        res_ = reinterpret_cast<uint4*>(out_ + 16);
         HIPCHK(dalloc(&tlen_, nd), "hipMalloc tlen");
         HIPCHK(dalloc(&loff_, nd), "hipMalloc loff");
         HIPCHK(dalloc(&toff_, nd), "hipMalloc toff");
-        HIPCHK(dalloc(&dig_, nd), "hipMalloc dig");
         HIPCHK(dalloc(&doc_root_, nd), "hipMalloc doc_root");
         HIPCHK(dalloc(&doc_p0_, nd), "hipMalloc doc_p0");
         HIPCHK(dalloc(&doc_fused_, nd), "hipMalloc doc_fused");
         cap_docs_ = nd;
+        gen_++;
     }
     const uint64_t tb = std::max<uint64_t>(w.text_cap, w.order_cap * 4) + 64;
     if (tb > cap_text_) {
         dfree(text_);
         HIPCHK(dalloc(&text_, tb), "hipMalloc text");
         cap_text_ = tb;
+        gen_++;
     }
     if (w.leaf_cap + 1 > cap_leaves_) {
         dfree(leafh_);
@@ -2156,15 +2288,7 @@ int Engine::ensure_scratch(const Wave& w, uint32_t ndocs_total) {
         HIPCHK(dalloc(&leafcp_, w.leaf_cap + 1), "hipMalloc leaf codepoints");
         HIPCHK(dalloc(&gcp_, w.leaf_cap + 1), "hipMalloc group codepoints");
         cap_leaves_ = w.leaf_cap + 1;
-    }
-    if (ndocs_total > cap_host_docs_) {
-        if (host_dig_) (void)hipHostFree(host_dig_);
-        if (host_len_) (void)hipHostFree(host_len_);
-        if (host_cp_) (void)hipHostFree(host_cp_);
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_dig_), ndocs_total * 8ull), "pinned dig");
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_len_), ndocs_total * 4ull), "pinned len");
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_cp_), ndocs_total * 4ull), "pinned cps");
-        cap_host_docs_ = ndocs_total;
+        gen_++;
     }
     return CRDT_HIP_OK;
 }
@@ -2189,6 +2313,7 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
         HIPCHK(dalloc(&scan_sums_, r / kScanTile + 2), "hipMalloc scan sums");
         HIPCHK(dalloc(&rec_, r), "hipMalloc run records");
         cap_runs_ = r;
+        gen_++;
     }
     if (S > cap_splitters_) {
         dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_); dfree(v1_); dfree(p0_); dfree(p1_);
@@ -2201,17 +2326,22 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
         HIPCHK(dalloc(&p0_, sc), "hipMalloc p0");
         HIPCHK(dalloc(&p1_, sc), "hipMalloc p1");
         cap_splitters_ = sc;
+        gen_++;
     }
     return CRDT_HIP_OK;
 }
 
-int Engine::ensure_host_ctl(uint32_t waves) {
-    if (waves <= cap_host_ctl_) return CRDT_HIP_OK;
-    if (host_ctl_) (void)hipHostFree(host_ctl_);
-    host_ctl_ = nullptr;
-    cap_host_ctl_ = 0;
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_ctl_), waves * 64ull), "pinned ctl");
-    cap_host_ctl_ = waves;
+// Pinned host image of every wave's result block: wave i's ctl (64 B) then one uint4 per
+// document, at byte 64 i + 16 first_doc (one device-to-host copy per wave).
+int Engine::ensure_host_out(const DeviceLogs& L) {
+    const uint64_t need = 64ull * L.waves.size() + 16ull * L.docs.size() + 64;
+    if (need <= cap_host_out_) return CRDT_HIP_OK;
+    if (host_out_) (void)hipHostFree(host_out_);
+    host_out_ = nullptr;
+    cap_host_out_ = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&host_out_), need), "pinned results");
+    cap_host_out_ = need;
+    gen_++;
     return CRDT_HIP_OK;
 }
 
@@ -2231,7 +2361,7 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     p.R = R;
     p.rmax = rmax;
     p.rcap = (rmax + 2u + 7u) & ~7u;
-    p.scap = (((rmax + 3u) >> kDocLog2S) + 8u) & ~7u;
+    p.scap = (((rmax + (1u << kDocLog2S) - 1u) >> kDocLog2S) + 8u) & ~7u;
     const uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap);
     // per-document LDS path when the largest document's run tree fits one workgroup (sublist
     // offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
@@ -2247,8 +2377,20 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     return p;
 }
 
-#define BEGIN(st) HIPCHK(hipEventRecord(ev[2 * (st)], s), "event record")
-#define END(st) HIPCHK(hipEventRecord(ev[2 * (st) + 1], s), "event record")
+// Stage timing: an event at the start of the wave and after every stage that ran; a stage's time
+// is the interval since the event before it.  (Two events per stage, recorded whether the stage
+// ran or not, cost several microseconds of host time each on a one-document merge.)
+int Engine::clock_mark(StageClock& c, int stage) {
+    if (!c.ev || c.n >= kClockEvents) return CRDT_HIP_OK;  // untimed (a captured graph)
+    if (c.n) c.stage[c.n - 1] = (uint8_t)stage;
+    HIPCHK(hipEventRecord(c.ev[c.n], stream), "event record");
+    ++c.n;
+    return CRDT_HIP_OK;
+}
+#define MARK(st)                                       \
+    do {                                               \
+        if (const int _rc = clock_mark(ck, (st))) return _rc; \
+    } while (0)
 
 // Level-0 argument block of a wave (device pointers of L and of this engine's scratch).
 #define L0ARGS(a0)                                                  \
@@ -2299,50 +2441,44 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;     \
     a.roff = roff_;                                                                   \
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
-    a.dig = dig_; a.leafcp = leafcp_; a.gcp = gcp_; a.doccp = doccp_;                 \
+    a.leafcp = leafcp_; a.gcp = gcp_; a.res = res_;                                   \
     a.text = text_;                                                                   \
     a.text_cap = ord ? w.order_cap : cap_text_ - 64;                                  \
     a.align = ord ? 1u : 16u
 
 int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs,
-                          uint32_t cap_rmax, hipEvent_t* ev) {
+                          uint32_t cap_rmax, StageClock& ck) {
     hipStream_t s = stream;
     L0ARGS(a0);
     a0.cap_runs = cap_runs;
     a0.cap_rmax = cap_rmax;
     const uint32_t ntiles = a0.ntiles;
     const uint32_t nsums = (ntiles + kScanTile - 1) / kScanTile;
-    HIPCHK(hipMemsetAsync(ctl_, 0, 64, s), "memset ctl");
-    HIPCHK(hipMemsetAsync(jbits_, 0, (w.nslots / 32 + 4) * 4ull, s), "memset jump bits");
-    BEGIN(S_CLASSIFY);
+    const uint32_t nq = (uint32_t)((w.nslots / 32 + 4 + 3) / 4);  // jump-bit words, in uint4
+    k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
+    MARK(-1);
     k_classify<<<ntiles, kBlock, 0, s>>>(a0);
-    END(S_CLASSIFY);
-    BEGIN(S_RUNS);
+    MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
     k_tiles_top<<<1, 1024, 0, s>>>(a0, nsums);
     k_tiles_apply<<<nsums, kBlock, 0, s>>>(a0);
     k_runs<<<ntiles, kBlock, 0, s>>>(a0);
     k_docmax<<<1, 1024, 0, s>>>(a0);
-    END(S_RUNS);
+    MARK(S_RUNS);
     HIPCHK(hipGetLastError(), "level-0 launch");
     return CRDT_HIP_OK;
 }
 
 // k_run_parent, k_doctotals, k_doctree (and k_expand for documents whose text did not fit).
 int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
-                              hipEvent_t* ev) {
+                              StageClock& ck) {
     hipStream_t s = stream;
     L0ARGS(a0);
     TREEARGS(a);
-    BEGIN(S_RPARENT);
     k_run_parent<<<std::min<uint32_t>(grid_for(p.R, kBlock * kRunsPerThread), 8192u) + 1u, kBlock,
                    0, s>>>(a0);
-    END(S_RPARENT);
-    for (int st = S_COUNT; st <= S_WALK2; ++st) {
-        BEGIN(st);
-        END(st);
-    }
+    MARK(S_RPARENT);
     DocArgs da{};
     da.ndocs = w.ndocs;
     da.rcap = p.rcap;
@@ -2362,11 +2498,10 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.text = p.fuse ? text_ : nullptr;
     da.fused = doc_fused_;
     da.lds_bytes = (uint32_t)p.dyn_bytes;
-    if (const char* pe = getenv("CRDT_HIP_PROBE")) da.probe = 1u + (uint32_t)atoi(pe);
-    BEGIN(S_DOCTREE);
+    da.probe = probe_doc_;
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
-    END(S_DOCTREE);
+    MARK(S_DOCTREE);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
 }
@@ -2374,7 +2509,7 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
 // The global (grid-wide) level 1, for waves whose documents do not fit the LDS path.  Grids are
 // sized by the exact run count (the caller waited for level 0).
 int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
-                                 hipEvent_t* ev, uint32_t& rounds) {
+                                 StageClock& ck, uint32_t& rounds) {
     hipStream_t s = stream;
     L0ARGS(a0);
     TREEARGS(a);
@@ -2391,32 +2526,23 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     a.step_limit = 2u * R + 4u;
     const uint32_t gR = grid_for(R), gS = grid_for(S);
     const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
-    BEGIN(S_RPARENT);
     k_run_parent<<<std::min<uint32_t>(grid_for(R, kBlock * kRunsPerThread), 8192u) + 1u, kBlock,
                    0, s>>>(a0);
-    END(S_RPARENT);
-    BEGIN(S_DOCTREE);
-    END(S_DOCTREE);
-    BEGIN(S_COUNT);
+    MARK(S_RPARENT);
     k_count<<<gR, kBlock, 0, s>>>(a);
-    END(S_COUNT);
-    BEGIN(S_SCAN);
+    MARK(S_COUNT);
     k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_);
     k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, R);
     k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_, cstart_);
-    END(S_SCAN);
-    BEGIN(S_PLACE);
+    MARK(S_SCAN);
     k_place<<<gR, kBlock, 0, s>>>(a);
-    END(S_PLACE);
-    BEGIN(S_LINK);
+    MARK(S_PLACE);
     k_link<<<gR, kBlock, 0, s>>>(a);
     k_sortmid<<<kMidGrid, kBlock, 0, s>>>(a);
     k_sortbig<<<kBigGrid, kBigThreads, 0, s>>>(a);
-    END(S_LINK);
-    BEGIN(S_WALK1);
+    MARK(S_LINK);
     k_walk1<<<gS, kBlock, 0, s>>>(a);
-    END(S_WALK1);
-    BEGIN(S_RANK);
+    MARK(S_WALK1);
     HIPCHK(hipMemsetAsync(pred_, 0xFF, S * 4ull, s), "memset pred");
     k_pred<<<gS, kBlock, 0, s>>>(snext_, S, pred_);
     k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, S, v0_, p0_);
@@ -2429,19 +2555,18 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         std::swap(pi, po);
     }
     const uint32_t* spref = vi;
-    END(S_RANK);
-    BEGIN(S_WALK2);
+    MARK(S_RANK);
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
-    END(S_WALK2);
+    MARK(S_WALK2);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
 }
 
-// Expansion (documents k_doctree did not write), digest, and the copies of the wave's results
-// into the pinned host arrays (lengths, digests, codepoints per document; ctl into hctl).
-int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, hipEvent_t* ev,
-                        uint32_t* hctl) {
+// Expansion (documents k_doctree did not write), digest, and one copy of the wave's result block
+// (ctl + a {bytes, codepoints, digest} record per document) into the pinned host image.
+int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, StageClock& ck,
+                        uint32_t* hblock) {
     hipStream_t s = stream;
     L0ARGS(a0);
     TREEARGS(a);
@@ -2459,60 +2584,59 @@ int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, hipE
     ea.sbytes = sbytes_;
     ea.text = text_;
     ea.ctl = ctl_;
-    ea.fused = fused ? doc_fused_ : nullptr;
-    BEGIN(S_EXPAND);
-    k_expand<<<4096, kBlock, 0, s>>>(ea);
-    END(S_EXPAND);
-    BEGIN(S_DIGEST);
+    ea.fused = nullptr;
+    if (!fused) {  // (a fused k_doctree writes every document itself)
+        k_expand<<<4096, kBlock, 0, s>>>(ea);
+        MARK(S_EXPAND);
+    }
     if (!ord) {
-        k_leafhash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
+        k_leafhash<<<grid_for(w.leaf_cap + 1, kLeafWaves), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
         if (w.max_doc_text > (uint64_t)kLeaf * kGroup)
             k_grouphash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
         k_docdigest<<<grid_for(w.ndocs), kBlock, 0, s>>>(a);
+        MARK(S_DIGEST);
     }
-    END(S_DIGEST);
     HIPCHK(hipGetLastError(), "kernel launch");
-    HIPCHK(hipMemcpyAsync(host_len_ + w.first_doc, tlen_, w.ndocs * 4ull, hipMemcpyDeviceToHost, s),
-           "copy lens");
-    if (!ord) {
-        HIPCHK(hipMemcpyAsync(host_dig_ + w.first_doc, dig_, w.ndocs * 8ull, hipMemcpyDeviceToHost, s),
-               "copy digests");
-        HIPCHK(hipMemcpyAsync(host_cp_ + w.first_doc, doccp_, w.ndocs * 4ull, hipMemcpyDeviceToHost, s),
-               "copy codepoints");
-    }
-    HIPCHK(hipMemcpyAsync(hctl, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
+    HIPCHK(hipMemcpyAsync(hblock, out_, 64 + 16ull * w.ndocs, hipMemcpyDeviceToHost, s),
+           "copy results");
     return CRDT_HIP_OK;
 }
-#undef BEGIN
-#undef END
+#undef MARK
 #undef L0ARGS
 #undef TREEARGS
 
 int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t rounds,
-                        const hipEvent_t* ev, const uint32_t* hctl, std::vector<float>& stage_ms,
+                        const StageClock& ck, const uint32_t* hctl, std::vector<float>& stage_ms,
                         std::vector<uint32_t>& stage_launches) {
     const uint32_t g1 = p.lds1 ? 0u : 1u;
-    const bool expand_run = !p.fuse || hctl[C_UNFUSED] != 0;
+    const bool expand_run = !p.fuse;
     const uint32_t launches[S_N] = {1, 6, 1, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
                                     p.lds1 ? 2u : 0u};
-    for (int i = 0; i < S_N; ++i) {
+    for (uint32_t i = 0; i + 1 < ck.n; ++i) {
+        if (ck.stage[i] >= S_N) continue;  // not a stage (a host wait between two launches)
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]), "event time");
-        stage_ms[i] += ms;
-        stage_launches[i] += launches[i];
+        HIPCHK(hipEventElapsedTime(&ms, ck.ev[i], ck.ev[i + 1]), "event time");
+        stage_ms[ck.stage[i]] += ms;
     }
+    for (int i = 0; i < S_N; ++i) stage_launches[i] += launches[i];
     return CRDT_HIP_OK;
+}
+
+uint32_t* Engine::host_block(const DeviceLogs& L, uint32_t wi) const {
+    return host_out_ + (64ull * wi + 16ull * L.waves[wi].first_doc) / 4;
 }
 
 // One wave, waiting for level 0 to learn its run counts (the first merge of a set of logs, the
 // global level-1 path, ORDER mode).  Records the wave's launch plan for later merges.
-int Engine::run_wave(DeviceLogs& L, Wave& w, Mode mode, std::vector<float>& stage_ms,
+int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& stage_ms,
                      std::vector<uint32_t>& stage_launches, bool force_global) {
+    Wave& w = L.waves[wi];
     hipStream_t s = stream;
     const bool ord = mode == ORDER;
-    hipEvent_t* ev = ev_.data();
+    StageClock ck{ev_.data(), 0, {}};
+    uint32_t* hctl = host_block(L, wi);
     // run records are written before the run count is known: runs <= slots
     if (w.nslots > cap_heads_) {
         dfree(r_head_); dfree(r_pstart_);
@@ -2525,36 +2649,37 @@ int Engine::run_wave(DeviceLogs& L, Wave& w, Mode mode, std::vector<float>& stag
     // level 1.
     std::unique_lock<std::mutex> gate;
     if (l0_gate_) gate = std::unique_lock<std::mutex>(*l0_gate_);
-    int rc = launch_level0(L, w, ord, 0xFFFFFFFFu, 0xFFFFFFFFu, ev);
+    int rc = launch_level0(L, w, ord, 0xFFFFFFFFu, 0xFFFFFFFFu, ck);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(host_ctl_, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
+    HIPCHK(hipMemcpyAsync(hctl, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "level-0 sync");
     if (gate.owns_lock()) gate.unlock();
-    if (host_ctl_[C_ERR]) {
-        err = host_ctl_[C_ERR] & 4u ? "op log holds more text than planned"
-                                    : "malformed op log: parent id out of range";
+    if (hctl[C_ERR]) {
+        err = hctl[C_ERR] & 4u ? "op log holds more text than planned"
+                               : "malformed op log: parent id out of range";
         return CRDT_HIP_EBADLOG;
     }
-    const L1Plan p = plan_level1(w, host_ctl_[C_RTOTAL], host_ctl_[C_RMAX], ord, force_global);
+    const L1Plan p = plan_level1(w, hctl[C_RTOTAL], hctl[C_RMAX], ord, force_global);
     const uint32_t lg = log2m_set ? log2m : (p.R > (1u << 24) ? 6u : 4u);
     const uint32_t Sreg = 2 * ((p.R + (1u << lg) - 1) >> lg);
     rc = ensure_runs(p.R, Sreg + w.ndocs);
     if (rc) return rc;
+    if ((rc = clock_mark(ck, 0xFF))) return rc;  // the host wait above is no stage's time
     uint32_t rounds = 0;
-    rc = p.lds1 ? launch_lds_level1(L, w, ord, p, ev) : launch_global_level1(L, w, ord, p, ev, rounds);
+    rc = p.lds1 ? launch_lds_level1(L, w, ord, p, ck) : launch_global_level1(L, w, ord, p, ck, rounds);
     if (rc) return rc;
-    rc = launch_tail(L, w, ord, p.fuse, ev, host_ctl_);
+    rc = launch_tail(L, w, ord, p.fuse, ck, hctl);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s), "merge wave");
-    uint32_t errs = host_ctl_[C_ERR];
+    uint32_t errs = hctl[C_ERR];
     if (p.lds1 && (errs & 32u)) {
         // a sibling group wider than the LDS path sorts: redo the wave on the global path
-        return run_wave(L, w, mode, stage_ms, stage_launches, true);
+        return run_wave(L, wi, mode, stage_ms, stage_launches, true);
     }
-    rc = finish_wave(w, ord, p, rounds, ev, host_ctl_, stage_ms, stage_launches);
+    rc = finish_wave(w, ord, p, rounds, ck, hctl, stage_ms, stage_launches);
     if (rc) return rc;
     runs_ += p.R;
-    if (!errs && host_ctl_[C_VISITED] != p.R) errs |= 16u;  // unreachable runs: a cycle
+    if (!errs && hctl[C_VISITED] != p.R) errs |= 16u;  // unreachable runs: a cycle
     if (errs) {
         (void)hipMemset(deg_, 0, (cap_runs_ + 16) * 4);  // restore the all-zero invariant
         err = "malformed op log detected on device (flags " + std::to_string(errs) + ")";
@@ -2563,17 +2688,36 @@ int Engine::run_wave(DeviceLogs& L, Wave& w, Mode mode, std::vector<float>& stag
     w.hint_runs = p.R;
     w.hint_rmax = p.rmax;
     w.hint_lds = p.lds1 && p.fuse && !ord;
+    if (w.hint_lds) learn_shape(w);
     return CRDT_HIP_OK;
+}
+
+void Engine::learn_shape(const Wave& w) {
+    const WaveShape sh = shape_of(w);
+    forget_shape(w);
+    shape_hints_.insert(shape_hints_.begin(), ShapeHint{sh, w.hint_runs, w.hint_rmax});
+    if (shape_hints_.size() > kShapeHints) shape_hints_.pop_back();
+}
+
+void Engine::forget_shape(const Wave& w) {
+    const WaveShape sh = shape_of(w);
+    for (size_t i = 0; i < shape_hints_.size(); ++i)
+        if (shape_hints_[i].shape == sh) {
+            shape_hints_.erase(shape_hints_.begin() + (long)i);
+            return;
+        }
 }
 
 void Engine::collect(const DeviceLogs& L, uint32_t wi, uint64_t* digests, uint64_t* lens,
                      uint64_t* cps, uint64_t& text_bytes) const {
     const Wave& w = L.waves[wi];
-    for (uint32_t d = w.first_doc; d < w.first_doc + w.ndocs; ++d) {
-        if (lens) lens[d] = host_len_[d];
-        if (digests) digests[d] = host_dig_[d];
-        if (cps) cps[d] = host_cp_[d];
-        text_bytes += host_len_[d];
+    const uint4* r = reinterpret_cast<const uint4*>(host_block(L, wi) + 16);
+    for (uint32_t k = 0; k < w.ndocs; ++k) {
+        const uint32_t d = w.first_doc + k;
+        if (lens) lens[d] = r[k].x;
+        if (cps) cps[d] = r[k].y;
+        if (digests) digests[d] = ((uint64_t)r[k].w << 32) | r[k].z;
+        text_bytes += r[k].x;
     }
 }
 
@@ -2585,6 +2729,7 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         err = "text output needs a single-wave merge";
         return CRDT_HIP_EINVAL;
     }
+    if (const char* pe = getenv("CRDT_HIP_PROBE")) probe_doc_ = 1u + (uint32_t)atoi(pe);
     bool hinted = plan_cache && mode == TEXT && !text_out && !text_offsets && !L.waves.empty();
     for (const Wave& w : L.waves) hinted = hinted && w.hint_lds;
     if (hinted) return merge_async(L, digests, lens, cps, st);
@@ -2593,14 +2738,14 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
     std::vector<uint32_t> stage_launches(S_N, 0);
     const uint32_t ndocs = (uint32_t)L.docs.size();
     runs_ = 0;
-    if (const int hc = ensure_host_ctl(1)) return hc;
+    if (const int rc = ensure_host_out(L)) return rc;
     HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
     uint64_t text_bytes = 0;
     for (uint32_t wi = 0; wi < L.waves.size(); ++wi) {
-        Wave& w = L.waves[wi];
-        int rc = ensure_scratch(w, ndocs);
+        const Wave& w = L.waves[wi];
+        int rc = ensure_scratch(w);
         if (rc) return rc;
-        rc = run_wave(L, w, mode, stage_ms, stage_launches);
+        rc = run_wave(L, wi, mode, stage_ms, stage_launches);
         if (rc) return rc;
         collect(L, wi, digests, lens, cps, text_bytes);
         if (text_out) {
@@ -2635,45 +2780,48 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
     return CRDT_HIP_OK;
 }
 
-// Every wave of a merge whose launch plans are known (an earlier merge of the same logs learnt
-// them), enqueued without waiting: wave i goes to lane i % K (this engine or a helper engine:
-// own stream and scratch), one host thread enqueues them all.  With the level-0 gate, a wave's
-// level 0 waits (hipStreamWaitEvent) for the previous wave's level 0 to end, so level 0 of one
-// wave runs beside the latency-bound level 1 of another, as merge_lanes' mutex does.  The host
-// waits once, at the end; a wave whose device check failed (C_REPLAN, or a sibling group too wide
-// for the LDS path) is merged again on the synchronous path.
-int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64_t* cps,
-                        crdt_hip_stats* st) {
+// Every wave of a merge whose launch plans are known (an earlier merge of the same logs, or of
+// logs of the same shape, learnt them), enqueued without waiting: wave i goes to lane i % K (this
+// engine or a helper engine: own stream and scratch), one host thread enqueues them all.  With
+// the level-0 gate, a wave's level 0 waits (hipStreamWaitEvent) for the previous wave's level 0
+// to end, so level 0 of one wave runs beside the latency-bound level 1 of another, as
+// merge_lanes' mutex does.  The host waits once, at the end; a wave whose device check failed
+// (C_REPLAN, or a sibling group too wide for the LDS path) is merged again synchronously.
+// Three phases, so that a caller can capture the launches in a graph: prepare (lanes, plans,
+// every allocation), enqueue (launches and copies only), finish (after the wait: errors, redo,
+// results).
+int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
     const uint32_t nw = (uint32_t)L.waves.size();
-    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>(lanes, nw));
-    while (lane_eng_.size() + 1 < K) {
+    m.K = std::max<uint32_t>(1, std::min<uint32_t>(lanes, nw));
+    m.timed = timed;
+    while (lane_eng_.size() + 1 < m.K) {
         auto e = std::make_unique<Engine>();
-        const std::string m = e->init(device);
-        if (!m.empty()) {
-            err = "lane engine: " + m;
+        const std::string msg = e->init(device);
+        if (!msg.empty()) {
+            err = "lane engine: " + msg;
             return CRDT_HIP_EDEVICE;
         }
         lane_eng_.push_back(std::move(e));
     }
-    std::vector<Engine*> eng(K, this);
-    for (uint32_t i = 1; i < K; ++i) {
-        eng[i] = lane_eng_[i - 1].get();
-        eng[i]->log2m = log2m;
-        eng[i]->log2m_set = log2m_set;
-        eng[i]->level1_global = level1_global;
+    m.eng.assign(m.K, this);
+    for (uint32_t i = 1; i < m.K; ++i) {
+        m.eng[i] = lane_eng_[i - 1].get();
+        m.eng[i]->log2m = log2m;
+        m.eng[i]->log2m_set = log2m_set;
+        m.eng[i]->level1_global = level1_global;
+        m.eng[i]->probe_doc_ = probe_doc_;
     }
-    const uint32_t ndocs = (uint32_t)L.docs.size();
     // every allocation before the first launch (a pool free waits for the device)
-    const uint32_t per_lane = (nw + K - 1) / K;
-    std::vector<L1Plan> plans(nw);
+    const uint32_t per_lane = (nw + m.K - 1) / m.K;
+    m.plans.assign(nw, L1Plan{});
     for (uint32_t wi = 0; wi < nw; ++wi) {
-        Engine& E = *eng[wi % K];
+        Engine& E = *m.eng[wi % m.K];
         Wave& w = L.waves[wi];
         // test hook: a plan too small for the wave (the device must flag it, the host redo it)
         const uint32_t cr = plan_shrink ? w.hint_runs / 2 : w.hint_runs;
         const uint32_t cm = plan_shrink ? w.hint_rmax / 2 : w.hint_rmax;
-        plans[wi] = E.plan_level1(w, cr, cm, false, false);
-        int rc = E.ensure_scratch(w, ndocs);
+        m.plans[wi] = E.plan_level1(w, cr, cm, false, false);
+        int rc = E.ensure_scratch(w);
         if (rc) return rc;
         rc = E.ensure_runs(cr, 0);
         if (rc) return rc;
@@ -2682,54 +2830,65 @@ int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64
             HIPCHK(dalloc(&E.r_head_, w.nslots + 64ull), "hipMalloc r_head");
             HIPCHK(dalloc(&E.r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
             E.cap_heads_ = w.nslots;
+            E.gen_++;
         }
     }
-    for (uint32_t i = 0; i < K; ++i) {
-        int rc = eng[i]->ensure_host_ctl(per_lane);
+    for (uint32_t i = 0; i < m.K; ++i) {
+        int rc = m.eng[i]->ensure_host_out(L);
         if (rc) return rc;
-        rc = eng[i]->ensure_events(eng[i]->wev_, per_lane * 2ull * S_N);
+        rc = m.eng[i]->ensure_events(m.eng[i]->wev_, per_lane * (size_t)kClockEvents);
         if (rc) return rc;
-        eng[i]->runs_ = 0;
+        m.eng[i]->runs_ = 0;
     }
-    HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
+    m.clocks.assign(nw, StageClock{});
+    return CRDT_HIP_OK;
+}
+
+int Engine::merge_async_enqueue(DeviceLogs& L, AsyncMerge& m) {
+    const uint32_t nw = (uint32_t)L.waves.size();
+    const uint32_t K = m.K;
+    if (m.timed || K > 1) HIPCHK(hipEventRecord(ev_[2 * S_N + 1], stream), "event record");
     // the other lanes start after the merge's start event
     for (uint32_t i = 1; i < K; ++i)
-        HIPCHK(hipStreamWaitEvent(eng[i]->stream, ev_[2 * S_N + 1], 0), "stream wait");
+        HIPCHK(hipStreamWaitEvent(m.eng[i]->stream, ev_[2 * S_N + 1], 0), "stream wait");
     hipEvent_t prev_l0 = nullptr;
     for (uint32_t wi = 0; wi < nw; ++wi) {
-        Engine& E = *eng[wi % K];
+        Engine& E = *m.eng[wi % K];
         const Wave& w = L.waves[wi];
-        const uint32_t slot = wi / K;
-        hipEvent_t* ev = E.wev_.data() + slot * 2ull * S_N;
+        StageClock& ck = m.clocks[wi];
+        ck.ev = m.timed || K > 1 ? E.wev_.data() + (size_t)(wi / K) * kClockEvents : nullptr;
         if (l0_gated && prev_l0 && K > 1)
             HIPCHK(hipStreamWaitEvent(E.stream, prev_l0, 0), "stream wait");
-        // the plan's capacity: the learnt run counts exactly (the logs have not changed)
-        int rc = E.launch_level0(L, w, false, plans[wi].R, plans[wi].rmax, ev);
+        int rc = E.launch_level0(L, w, false, m.plans[wi].R, m.plans[wi].rmax, ck);
         if (rc) return rc;
-        prev_l0 = ev[2 * S_RUNS + 1];
-        rc = E.launch_lds_level1(L, w, false, plans[wi], ev);
+        prev_l0 = ck.ev ? ck.ev[ck.n - 1] : nullptr;  // the end of level 0
+        rc = E.launch_lds_level1(L, w, false, m.plans[wi], ck);
         if (rc) return rc;
-        rc = E.launch_tail(L, w, false, true, ev, E.host_ctl_ + 16ull * slot);
+        rc = E.launch_tail(L, w, false, true, ck, E.host_block(L, wi));
         if (rc) return rc;
     }
     // join: the merge's end event on this stream after every lane's last launch
     for (uint32_t i = 1; i < K; ++i) {
-        hipEvent_t done = eng[i]->ev_[2 * S_N + 3];
-        HIPCHK(hipEventRecord(done, eng[i]->stream), "event record");
+        hipEvent_t done = m.eng[i]->ev_[2 * S_N + 3];
+        HIPCHK(hipEventRecord(done, m.eng[i]->stream), "event record");
         HIPCHK(hipStreamWaitEvent(stream, done, 0), "stream wait");
     }
-    HIPCHK(hipEventRecord(ev_[2 * S_N + 2], stream), "event record");
-    HIPCHK(hipEventSynchronize(ev_[2 * S_N + 2]), "event sync");
+    if (m.timed) HIPCHK(hipEventRecord(ev_[2 * S_N + 2], stream), "event record");
+    return CRDT_HIP_OK;
+}
 
+int Engine::merge_async_finish(DeviceLogs& L, AsyncMerge& m, uint64_t* digests, uint64_t* lens,
+                               uint64_t* cps, crdt_hip_stats* st) {
+    const uint32_t nw = (uint32_t)L.waves.size();
+    const uint32_t ndocs = (uint32_t)L.docs.size();
     std::vector<float> stage_ms(S_N, 0.f);
     std::vector<uint32_t> stage_launches(S_N, 0);
     uint64_t text_bytes = 0, runs = 0;
     std::vector<uint32_t> redo;
     uint32_t bad = 0;
     for (uint32_t wi = 0; wi < nw; ++wi) {
-        Engine& E = *eng[wi % K];
-        const uint32_t slot = wi / K;
-        const uint32_t* hctl = E.host_ctl_ + 16ull * slot;
+        Engine& E = *m.eng[wi % m.K];
+        const uint32_t* hctl = E.host_block(L, wi);
         const Wave& w = L.waves[wi];
         uint32_t errs = hctl[C_ERR];
         if (hctl[C_REPLAN] || (errs & 32u)) {
@@ -2741,8 +2900,9 @@ int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64
             bad |= errs;
             continue;
         }
-        int rc = E.finish_wave(w, false, plans[wi], 0, E.wev_.data() + slot * 2ull * S_N, hctl,
-                               stage_ms, stage_launches);
+        StageClock ck = m.clocks[wi];
+        if (!m.timed) ck.n = 0;
+        int rc = E.finish_wave(w, false, m.plans[wi], 0, ck, hctl, stage_ms, stage_launches);
         if (rc) return rc;
         runs += hctl[C_RTOTAL];
         E.collect(L, wi, digests, lens, cps, text_bytes);
@@ -2753,11 +2913,11 @@ int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64
     }
     for (uint32_t wi : redo) {  // the logs changed under the plan: learn it again
         L.waves[wi].hint_lds = false;
-        if (const int hc = ensure_host_ctl(1)) return hc;
+        forget_shape(L.waves[wi]);
         runs_ = 0;
-        int rc = ensure_scratch(L.waves[wi], ndocs);
+        int rc = ensure_scratch(L.waves[wi]);
         if (rc) return rc;
-        rc = run_wave(L, L.waves[wi], TEXT, stage_ms, stage_launches);
+        rc = run_wave(L, wi, TEXT, stage_ms, stage_launches);
         if (rc) return rc;
         runs += runs_;
         collect(L, wi, digests, lens, cps, text_bytes);
@@ -2775,11 +2935,24 @@ int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64
             st->stage_ns[i] = (uint64_t)((double)stage_ms[i] * 1e6);
             st->stage_launches[i] = stage_launches[i];
         }
-        float tot = 0;
-        HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N + 1], ev_[2 * S_N + 2]), "event time");
-        st->total_ns = (uint64_t)((double)tot * 1e6);
+        if (m.timed) {
+            float tot = 0;
+            HIPCHK(hipEventElapsedTime(&tot, ev_[2 * S_N + 1], ev_[2 * S_N + 2]), "event time");
+            st->total_ns = (uint64_t)((double)tot * 1e6);
+        }
     }
     return CRDT_HIP_OK;
+}
+
+int Engine::merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64_t* cps,
+                        crdt_hip_stats* st) {
+    AsyncMerge m;
+    int rc = merge_async_prepare(L, m, true);
+    if (rc) return rc;
+    rc = merge_async_enqueue(L, m);
+    if (rc) return rc;
+    HIPCHK(hipEventSynchronize(ev_[2 * S_N + 2]), "event sync");
+    return merge_async_finish(L, m, digests, lens, cps, st);
 }
 
 // Multi-wave merge over lanes, synchronous per wave: wave i runs on lane i % K, every lane in its
@@ -2790,6 +2963,8 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
                         uint64_t* cps, crdt_hip_stats* st) {
     const uint32_t nw = (uint32_t)L.waves.size();
     const uint32_t K = std::min<uint32_t>(lanes, nw);
+    // the lanes' streams do not wait for this one: let its queued table uploads finish
+    HIPCHK(hipStreamSynchronize(stream), "table sync");
     while (lane_eng_.size() + 1 < K) {
         auto e = std::make_unique<Engine>();
         const std::string m = e->init(device);
@@ -2806,11 +2981,13 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         eng[i]->log2m = log2m;
         eng[i]->log2m_set = log2m_set;
         eng[i]->level1_global = level1_global;
+        eng[i]->probe_doc_ = probe_doc_;
     }
-    const uint32_t ndocs = (uint32_t)L.docs.size();
     std::vector<int> rc(K, CRDT_HIP_OK);
     std::vector<std::vector<float>> ms(K, std::vector<float>(S_N, 0.f));
     std::vector<std::vector<uint32_t>> nl(K, std::vector<uint32_t>(S_N, 0));
+    for (uint32_t i = 0; i < K; ++i)
+        if ((rc[0] = eng[i]->ensure_host_out(L))) return rc[0];
     auto lane = [&](uint32_t i) {
         Engine& E = *eng[i];
         const hipError_t e = hipSetDevice(device);  // the current device is per host thread
@@ -2821,8 +2998,8 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         E.runs_ = 0;
         E.l0_gate_ = l0_gated ? &gate : nullptr;
         for (uint32_t wi = i; wi < nw && rc[i] == CRDT_HIP_OK; wi += K) {
-            rc[i] = E.ensure_scratch(L.waves[wi], ndocs);
-            if (rc[i] == CRDT_HIP_OK) rc[i] = E.run_wave(L, L.waves[wi], mode, ms[i], nl[i]);
+            rc[i] = E.ensure_scratch(L.waves[wi]);
+            if (rc[i] == CRDT_HIP_OK) rc[i] = E.run_wave(L, wi, mode, ms[i], nl[i]);
         }
     };
     const auto t0 = std::chrono::steady_clock::now();
@@ -2839,6 +3016,7 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
             if (i) err = eng[i]->err;
             return rc[i];
         }
+    const uint32_t ndocs = (uint32_t)L.docs.size();
     uint64_t text_bytes = 0, runs = 0;
     for (uint32_t wi = 0; wi < nw; ++wi) eng[wi % K]->collect(L, wi, digests, lens, cps, text_bytes);
     for (uint32_t i = 0; i < K; ++i) runs += eng[i]->runs_;

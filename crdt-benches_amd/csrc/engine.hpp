@@ -40,6 +40,14 @@ struct Wave {
     bool hint_lds = false;  // the wave took the per-document LDS level 1 with fused text
 };
 
+// Stage timing of one wave: an event at its start and after every stage that ran.
+constexpr uint32_t kClockEvents = 24;
+struct StageClock {
+    hipEvent_t* ev = nullptr;              // kClockEvents events
+    uint32_t n = 0;                        // events recorded
+    uint8_t stage[kClockEvents] = {};      // stage timed by the interval ev[i] -> ev[i + 1]
+};
+
 // Level-1 launch configuration of a wave, from its run count and largest document.
 struct L1Plan {
     uint32_t R = 0, rmax = 0;
@@ -68,6 +76,7 @@ struct DeviceLogs {
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
     uint64_t cap_docs = 0, cap_chunks = 0;
+    std::vector<uint64_t> tab_sig;  // the plan docs_rel / chunk_doc were last built for
 
     void release();
     ~DeviceLogs() { release(); }
@@ -113,6 +122,27 @@ public:
               std::vector<uint8_t>* text_out = nullptr,
               std::vector<uint64_t>* text_offsets = nullptr, uint64_t* cps = nullptr);
 
+    // merge() of logs whose every wave has a learnt plan, in three phases so that the launches
+    // can be captured in a graph: prepare (every allocation), enqueue (launches and copies only;
+    // untimed: no events), then, after the caller waited for the stream, finish.
+    struct AsyncMerge {
+        uint32_t K = 1;
+        bool timed = true;
+        std::vector<Engine*> eng;
+        std::vector<L1Plan> plans;
+        std::vector<StageClock> clocks;
+    };
+    bool plans_known(const DeviceLogs& L) const {
+        bool ok = plan_cache && !L.waves.empty();
+        for (const Wave& w : L.waves) ok = ok && w.hint_lds;
+        return ok;
+    }
+    int merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed);
+    int merge_async_enqueue(DeviceLogs& L, AsyncMerge& m);
+    int merge_async_finish(DeviceLogs& L, AsyncMerge& m, uint64_t* digests, uint64_t* lens,
+                           uint64_t* cps, crdt_hip_stats* st);
+    uint64_t generation() const { return gen_; }  // bumped by every (re)allocation of scratch
+
     // One config-5 document generated on the device (synth.cpp synth_tree_item, item by item).
     int synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t del_pct,
                    uint64_t seed);
@@ -133,8 +163,12 @@ private:
     uint64_t cap_sbytes_ = 0;
     // per document
     uint32_t *doc_root_ = nullptr, *doc_p0_ = nullptr, *tlen_ = nullptr, *loff_ = nullptr;
-    uint64_t *toff_ = nullptr, *dig_ = nullptr, *leafh_ = nullptr, *ghash_ = nullptr;
-    uint32_t *leafcp_ = nullptr, *gcp_ = nullptr, *doccp_ = nullptr;
+    uint64_t *toff_ = nullptr, *leafh_ = nullptr, *ghash_ = nullptr;
+    uint32_t *leafcp_ = nullptr, *gcp_ = nullptr;
+    // result block of a wave: ctl (16 words) then one uint4 per document {bytes, codepoints,
+    // digest lo, digest hi}; ctl_ and res_ point into it
+    uint32_t* out_ = nullptr;
+    uint4* res_ = nullptr;
     uint8_t* text_ = nullptr;
     uint8_t* doc_fused_ = nullptr;
     // level-1 scratch (per run / per splitter), grown on demand
@@ -147,40 +181,66 @@ private:
     uint4* rec_ = nullptr;
     uint32_t *sw_ = nullptr, *snext_ = nullptr, *pred_ = nullptr, *v0_ = nullptr, *v1_ = nullptr,
              *p0_ = nullptr, *p1_ = nullptr;
-    uint32_t* host_ctl_ = nullptr;       // pinned, 16 words per wave slot
-    uint32_t cap_host_ctl_ = 0;          // wave slots
-    uint64_t* host_dig_ = nullptr;       // pinned
-    uint32_t* host_len_ = nullptr;       // pinned
-    uint32_t* host_cp_ = nullptr;        // pinned
-    uint64_t cap_host_docs_ = 0;
+    uint32_t* host_out_ = nullptr;       // pinned image of every wave's result block
+    uint64_t cap_host_out_ = 0;          // bytes
+    uint32_t probe_doc_ = 0;             // 1 + document whose k_doctree phases are printed
     uint64_t runs_ = 0;
-    std::vector<hipEvent_t> ev_;         // stage events of a synchronous wave
-    std::vector<hipEvent_t> wev_;        // stage events of every enqueued wave (merge_async)
+    uint64_t gen_ = 0;
+    std::vector<hipEvent_t> ev_;         // stage clock of a synchronous wave; merge start/end
+    std::vector<hipEvent_t> wev_;        // stage clocks of every enqueued wave (merge_async)
     std::vector<std::unique_ptr<Engine>> lane_eng_;  // lanes 1..lanes-1 (lane 0 = this)
     std::mutex* l0_gate_ = nullptr;                  // set by merge_lanes
+
+    // Launch plans learnt per wave shape (documents, slots, text bound, items): a new set of
+    // logs of the same shape (the downstream loop merges a fresh clone every iteration) starts
+    // from the plan an earlier merge learnt; the device checks it (C_REPLAN) as for any plan.
+    struct WaveShape {
+        uint32_t ndocs, nslots;
+        uint64_t text_cap, order_cap, max_doc_text;
+        bool operator==(const WaveShape& o) const {
+            return ndocs == o.ndocs && nslots == o.nslots && text_cap == o.text_cap &&
+                   order_cap == o.order_cap && max_doc_text == o.max_doc_text;
+        }
+    };
+    struct ShapeHint {
+        WaveShape shape;
+        uint32_t runs, rmax;
+    };
+    std::vector<ShapeHint> shape_hints_;  // most recent first, at most kShapeHints
+    static constexpr size_t kShapeHints = 64;
+    static WaveShape shape_of(const Wave& w) {
+        return WaveShape{w.ndocs, w.nslots, w.text_cap, w.order_cap, w.max_doc_text};
+    }
+    void learn_shape(const Wave& w);
+    void forget_shape(const Wave& w);
+    uint64_t* tab_slot_ = nullptr;   // upload_tables scratch (grown, never freed mid-merge)
+    uint32_t* tab_local_ = nullptr;
+    uint64_t cap_tab_ = 0;
 
     int merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, uint64_t* cps,
                     crdt_hip_stats* st);
     int merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64_t* cps,
                     crdt_hip_stats* st);
     int ensure_runs(uint64_t runs, uint64_t splitters);
-    int ensure_scratch(const Wave& w, uint32_t ndocs_total);
-    int ensure_host_ctl(uint32_t waves);
+    int ensure_scratch(const Wave& w);
+    int ensure_host_out(const DeviceLogs& L);
+    uint32_t* host_block(const DeviceLogs& L, uint32_t wi) const;
     int ensure_events(std::vector<hipEvent_t>& ev, size_t n);
     L1Plan plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord, bool force_global) const;
-    // The launches of one wave, in stream order.  ev: 2 events per stage (begin, end).
+    int clock_mark(StageClock& c, int stage);
+    // The launches of one wave, in stream order.
     int launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs, uint32_t cap_rmax,
-                      hipEvent_t* ev);
-    int launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p, hipEvent_t* ev);
+                      StageClock& ck);
+    int launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p, StageClock& ck);
     int launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
-                             hipEvent_t* ev, uint32_t& rounds);
-    int launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, hipEvent_t* ev,
-                    uint32_t* hctl);
-    // After the wave's stream has drained: stage times, launch counts, error flags.
-    int finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t rounds, const hipEvent_t* ev,
+                             StageClock& ck, uint32_t& rounds);
+    int launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, StageClock& ck,
+                    uint32_t* hblock);
+    // After the wave's stream has drained: stage times, launch counts.
+    int finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t rounds, const StageClock& ck,
                     const uint32_t* hctl, std::vector<float>& stage_ms,
                     std::vector<uint32_t>& stage_launches);
-    int run_wave(DeviceLogs& L, Wave& w, Mode mode, std::vector<float>& stage_ms,
+    int run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& stage_ms,
                  std::vector<uint32_t>& stage_launches, bool force_global = false);
     void collect(const DeviceLogs& L, uint32_t wi, uint64_t* digests, uint64_t* lens,
                  uint64_t* cps, uint64_t& text_bytes) const;

@@ -36,7 +36,9 @@ constexpr uint32_t kCpMaskR = 0x001FFFFFu;
 constexpr uint32_t kMaxGrid = 1024;  // write passes: one counter atomic per block
 
 // device counters (u64)
-enum UCtl { U_ERR = 0, U_ITEMS, U_DELS, U_MAXID, U_ADD_CP, U_ADD_B, U_DEL_CP, U_DEL_B, U_N };
+enum UCtl { U_ERR = 0, U_ITEMS, U_DELS, U_MAXID, U_ADD_CP, U_ADD_B, U_DEL_CP, U_DEL_B,
+            U_PLAN,  // replay: the decode's sizes differ from the ones the merge was planned with
+            U_N };
 // U_ERR bits
 constexpr uint64_t E_HEADER = 1, E_NOT_READY = 2, E_PARENT = 4, E_DELETE = 8, E_BOUNDS = 16;
 
@@ -105,6 +107,8 @@ struct UpdArgs {
     uint16_t* agent;
     uint32_t* cp;  // codepoint | kDelBit
     uint64_t cap_slots;
+    uint32_t* imap;  // per flattened item / delete: its update (found by the check pass, reused
+    uint32_t* dmap;  //   by the write pass instead of a second binary search)
 };
 
 __global__ __launch_bounds__(kUB) void k_upd_parse(UpdArgs a) {
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
     uint64_t err = 0;
     const uint32_t stride = gridDim.x * kUB * kItemsPerThread;
     for (uint32_t j0 = (blockIdx.x * kUB + threadIdx.x) * kItemsPerThread; j0 < T; j0 += stride) {
-        uint32_t u = find_update<0>(a.scan, a.n, j0);
+        uint32_t u = WRITE ? a.imap[j0] : find_update<0>(a.scan, a.n, j0);
         uint4 h = a.hdr[u], s = a.scan[u];
 #pragma unroll
         for (int q = 0; q < kItemsPerThread; ++q) {
@@ -225,6 +229,7 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
                 h = a.hdr[u];
                 s = a.scan[u];
             }
+            if (!WRITE) a.imap[j] = u;
             const uint32_t k = j - s.x, id = h.x + k;
             if (id <= s.z) continue;  // already known (decode_and_add is idempotent)
             const uint32_t par = a.buf[h.w + k];
@@ -265,7 +270,8 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
     uint32_t del_cp = 0, del_b = 0;
     uint64_t err = 0;
     for (uint32_t j = blockIdx.x * kUB + threadIdx.x; j < Dm; j += gridDim.x * kUB) {
-        const uint32_t u = find_update<1>(a.scan, a.n, j);
+        const uint32_t u = WRITE ? a.dmap[j] : find_update<1>(a.scan, a.n, j);
+        if (!WRITE) a.dmap[j] = u;
         const uint4 h = a.hdr[u], s = a.scan[u];
         const uint32_t dw = h.w + 4u * h.y + (2u * h.y + 3u) / 4u;
         const uint32_t id = a.buf[dw + (j - s.y)];
@@ -305,6 +311,34 @@ __global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint32_t* lam
     cp[g] = kDelBit;
 }
 
+// Replica clone: the four slot arrays in one launch (main.rs:64).
+__global__ __launch_bounds__(kUB) void k_rep_copy(const uint32_t* __restrict__ sp,
+                                                  const uint32_t* __restrict__ sl,
+                                                  const uint16_t* __restrict__ sa,
+                                                  const uint32_t* __restrict__ sc,
+                                                  uint32_t* __restrict__ dp, uint32_t* __restrict__ dl,
+                                                  uint16_t* __restrict__ da, uint32_t* __restrict__ dc,
+                                                  uint64_t n) {
+    for (uint64_t g = (uint64_t)blockIdx.x * kUB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * kUB) {
+        dp[g] = sp[g];
+        dl[g] = sl[g];
+        da[g] = sa[g];
+        dc[g] = sc[g];
+    }
+}
+
+// Replay: the sizes the enqueued merge was planned with (n items, visible bytes) against the
+// ones the decode produced.
+__global__ void k_replay_check(uint64_t* ctl, uint32_t n0, uint64_t bytes0, uint32_t n_plan,
+                               uint64_t bytes_plan) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t n = ctl[U_MAXID] > n0 ? ctl[U_MAXID] : n0;
+    const uint64_t bytes = bytes0 + ctl[U_ADD_B] - ctl[U_DEL_B];
+    ctl[U_PLAN] = (n != n_plan || bytes != bytes_plan || ctl[U_ERR]) ? 1u : 0u;
+}
+
+thread_local uint64_t grow_gen = 0;  // counts grow() reallocations (replica generations)
+
 int hip_fail(Engine& E, const char* what, hipError_t e) {
     E.err = std::string(what) + ": " + hipGetErrorString(e);
     (void)hipGetLastError();
@@ -320,6 +354,7 @@ int hip_fail(Engine& E, const char* what, hipError_t e) {
 template <class T>
 hipError_t grow(T** p, uint64_t& cap, uint64_t need) {
     if (need <= cap) return hipSuccess;
+    ++grow_gen;
     dfree(*p);
     cap = 0;
     hipError_t e = dalloc(p, need);
@@ -330,11 +365,14 @@ hipError_t grow(T** p, uint64_t& cap, uint64_t need) {
 }  // namespace
 
 Replica::~Replica() {
+    for (void* p : graveyard) pool_free(p);
     dfree(ubuf);
     dfree(uoff);
     dfree(uhdr);
     dfree(uscan);
     dfree(ublk);
+    dfree(imap);
+    dfree(dmap);
     dfree(uctl);
     pool_free(hctl, true);
 }
@@ -367,17 +405,21 @@ int replica_reserve(Engine& E, Replica& r, uint64_t items) {
         k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, lam, ag, c, old, cap);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
+        (void)hipStreamSynchronize(s);
         dfree(par); dfree(lam); dfree(ag); dfree(c);
         return hip_fail(E, "replica reserve", e);
     }
-    dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.cp);
+    // the old arrays may still be read by queued work: freed at the replica's next wait
+    for (void* p : {(void*)L.parent, (void*)L.lamport, (void*)L.agent, (void*)L.cp})
+        if (p) r.graveyard.push_back(p);
+    L.parent = nullptr; L.lamport = nullptr; L.agent = nullptr; L.cp = nullptr;
     L.parent = par;
     L.lamport = lam;
     L.agent = ag;
     L.cp = c;
     L.cap_slots = cap;
+    r.gen++;
     return CRDT_HIP_OK;
 }
 
@@ -388,6 +430,7 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     if (rc) return rc;
     r.n = n;
     r.vis_cp = r.vis_bytes = 0;
+    r.version++;
     if (!n) return CRDT_HIP_OK;
     DeviceLogs& L = r.logs;
     RCHK(hipMemcpy(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice), "upload parent");
@@ -407,6 +450,10 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
 
 int replica_copy(Engine& E, const Replica& src, Replica& dst) {
     RCHK(hipSetDevice(E.device), "hipSetDevice");
+    if (src.pending) {
+        E.err = "replica has an unsettled decode";
+        return CRDT_HIP_EINVAL;
+    }
     const uint64_t cap = src.logs.cap_slots;
     int rc = replica_reserve(E, dst, cap ? cap - 1 : 0);
     if (rc) return rc;
@@ -414,15 +461,15 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst) {
     DeviceLogs& D = dst.logs;
     hipStream_t s = E.stream;
     if (cap) {
-        RCHK(hipMemcpyAsync(D.parent, S.parent, cap * 4, hipMemcpyDeviceToDevice, s), "copy parent");
-        RCHK(hipMemcpyAsync(D.lamport, S.lamport, cap * 4, hipMemcpyDeviceToDevice, s), "copy lamport");
-        RCHK(hipMemcpyAsync(D.agent, S.agent, cap * 2, hipMemcpyDeviceToDevice, s), "copy agent");
-        RCHK(hipMemcpyAsync(D.cp, S.cp, cap * 4, hipMemcpyDeviceToDevice, s), "copy cp");
-        RCHK(hipStreamSynchronize(s), "copy sync");
+        // (no wait: every later use of the copy, decode and merge, is on the same stream)
+        k_rep_copy<<<(uint32_t)std::min<uint64_t>(grid_for(cap, kUB), 4096), kUB, 0, s>>>(
+            S.parent, S.lamport, S.agent, S.cp, D.parent, D.lamport, D.agent, D.cp, cap);
+        RCHK(hipGetLastError(), "replica copy");
     }
     dst.n = src.n;
     dst.vis_cp = src.vis_cp;
     dst.vis_bytes = src.vis_bytes;
+    dst.version++;
     return CRDT_HIP_OK;
 }
 
@@ -443,6 +490,20 @@ int updates_upload(Engine& E, UpdateBatch& ub, const uint8_t* buf, uint64_t len,
     if (n) RCHK(hipMemcpy(ub.off, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice), "upload offsets");
     ub.len = len;
     ub.n = n;
+    // the largest id the batch carries, from its headers (first id, items at words 2, 3); a
+    // malformed header leaves it unknown (the device decoder rejects such a batch anyway)
+    ub.max_id = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t o0 = offsets[i], o1 = offsets[i + 1];
+        if (o0 > o1 || o1 > len || o1 - o0 < 24) {
+            ub.max_id = 0;
+            break;
+        }
+        uint32_t first, items;
+        std::memcpy(&first, buf + o0 + 8, 4);
+        std::memcpy(&items, buf + o0 + 12, 4);
+        if (items) ub.max_id = std::max<uint32_t>(ub.max_id, first + items - 1);
+    }
     return CRDT_HIP_OK;
 }
 
@@ -457,25 +518,36 @@ int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
 }
 
 int replica_apply_resident(Engine& E, Replica& r, const UpdateBatch& ub) {
-    return replica_decode(E, r, ub.buf, ub.len, ub.off, ub.n, true);
+    int rc = replica_settle(E, r);
+    if (rc) return rc;
+    rc = replica_decode_enqueue(E, r, ub.buf, ub.len, ub.off, ub.n, true, ub.max_id, true);
+    if (rc) return rc;
+    return replica_settle(E, r);
 }
 
 int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
                    const uint64_t* offsets, uint32_t n, bool resident) {
-    if (n == 0) return CRDT_HIP_OK;
-    if (!buf || !offsets) {
-        E.err = "null update buffer or offsets";
-        return CRDT_HIP_EINVAL;
-    }
+    int rc = replica_settle(E, r);
+    if (rc) return rc;
+    rc = replica_decode_enqueue(E, r, buf, len, offsets, n, resident, 0, true);
+    if (rc) return rc;
+    return replica_settle(E, r);
+}
+
+// Everything a decode may allocate (or wait for), before its launches.
+int decode_prepare(Engine& E, Replica& r, uint64_t len, uint32_t n, bool resident,
+                   uint32_t max_id) {
     if (len >= (1ull << 32) - 16) {
         E.err = "update batch of 4 GiB or more";
         return CRDT_HIP_ERANGE;
     }
     RCHK(hipSetDevice(E.device), "hipSetDevice");
-    hipStream_t s = E.stream;
-    // ids a batch can add: every item takes at least 16 bytes of it
-    int rc = replica_reserve(E, r, (uint64_t)r.n + len / 16 + 1);
+    // ids a batch can add: up to its largest id if known, else every item takes at least 16
+    // bytes of it
+    int rc = replica_reserve(E, r, max_id ? std::max<uint64_t>(r.n, max_id)
+                                          : (uint64_t)r.n + len / 16 + 1);
     if (rc) return rc;
+    const uint64_t g0 = grow_gen;
     const uint32_t nblk = (n + kUB - 1) / kUB;
     if (!resident) RCHK(grow(&r.ubuf, r.ubuf_cap, (len + 4) & ~3ull), "hipMalloc update buffer");
     if (n + 1ull > r.ucap) {
@@ -486,10 +558,46 @@ int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
         RCHK(dalloc(&r.uhdr, c), "hipMalloc update headers");
         RCHK(dalloc(&r.uscan, c), "hipMalloc update scan");
         r.ucap = c;
+        r.gen++;
     }
     RCHK(grow(&r.ublk, r.ublk_cap, (uint64_t)nblk), "hipMalloc update blocks");
-    if (!r.uctl) RCHK(dalloc(&r.uctl, (uint64_t)U_N), "hipMalloc update counters");
-    if (!r.hctl) RCHK(pool_alloc(reinterpret_cast<void**>(&r.hctl), U_N * 8, true), "hipHostMalloc");
+    // every item takes at least 16 bytes of the batch, every delete 4
+    RCHK(grow(&r.imap, r.imap_cap, len / 16 + 1), "hipMalloc item map");
+    RCHK(grow(&r.dmap, r.dmap_cap, len / 4 + 1), "hipMalloc delete map");
+    if (!r.uctl) {
+        RCHK(dalloc(&r.uctl, (uint64_t)U_N), "hipMalloc update counters");
+        r.gen++;
+    }
+    if (!r.hctl) {
+        RCHK(pool_alloc(reinterpret_cast<void**>(&r.hctl), U_N * 8, true), "hipHostMalloc");
+        r.gen++;
+    }
+    if (grow_gen != g0) r.gen++;
+    return CRDT_HIP_OK;
+}
+
+// The decode's launches (capturable: no allocation, no wait).
+int decode_launch(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                  const uint64_t* offsets, uint32_t n, bool resident, bool copy_counters);
+
+int replica_decode_enqueue(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                           const uint64_t* offsets, uint32_t n, bool resident, uint32_t max_id,
+                           bool copy_counters) {
+    if (n == 0) return CRDT_HIP_OK;
+    if (!buf || !offsets) {
+        E.err = "null update buffer or offsets";
+        return CRDT_HIP_EINVAL;
+    }
+    int rc = decode_prepare(E, r, len, n, resident, max_id);
+    if (rc) return rc;
+    return decode_launch(E, r, buf, len, offsets, n, resident, copy_counters);
+}
+
+int decode_launch(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                  const uint64_t* offsets, uint32_t n, bool resident, bool copy_counters) {
+    if (n == 0) return CRDT_HIP_OK;
+    hipStream_t s = E.stream;
+    const uint32_t nblk = (n + kUB - 1) / kUB;
     if (!resident) {
         RCHK(hipMemcpyAsync(r.ubuf, buf, len, hipMemcpyHostToDevice, s), "upload updates");
         RCHK(hipMemcpyAsync(r.uoff, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice, s),
@@ -513,6 +621,8 @@ int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     a.agent = L.agent;
     a.cp = L.cp;
     a.cap_slots = L.cap_slots;
+    a.imap = r.imap;
+    a.dmap = r.dmap;
     const uint32_t gi = std::min<uint64_t>(kMaxGrid, grid_for(len / 16 / kItemsPerThread + 1, kUB));
     const uint32_t gd = std::min<uint64_t>(kMaxGrid, grid_for(len / 4 + 1, kUB));
     k_upd_parse<<<nblk, kUB, 0, s>>>(a);
@@ -523,8 +633,20 @@ int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     k_upd_items<true><<<gi, kUB, 0, s>>>(a);
     k_upd_dels<true><<<gd, kUB, 0, s>>>(a);
     RCHK(hipGetLastError(), "update kernels");
-    RCHK(hipMemcpyAsync(r.hctl, r.uctl, U_N * 8, hipMemcpyDeviceToHost, s), "copy update counters");
-    RCHK(hipStreamSynchronize(s), "update sync");
+    if (copy_counters)
+        RCHK(hipMemcpyAsync(r.hctl, r.uctl, U_N * 8, hipMemcpyDeviceToHost, s), "copy update counters");
+    r.pending = true;
+    return CRDT_HIP_OK;
+}
+
+int replica_settle(Engine& E, Replica& r) {
+    if (!r.pending && r.graveyard.empty()) return CRDT_HIP_OK;
+    RCHK(hipStreamSynchronize(E.stream), "update sync");
+    for (void* p : r.graveyard) pool_free(p, false, true);
+    r.graveyard.clear();
+    if (!r.pending) return CRDT_HIP_OK;
+    r.pending = false;
+    r.version++;
     const uint64_t* c = r.hctl;
     if (c[U_ERR]) {
         const uint64_t e = c[U_ERR];
@@ -543,12 +665,140 @@ int replica_decode(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
 
 int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* len,
                   uint64_t* digest, crdt_hip_stats* st, uint64_t* cps) {
-    int rc = replica_reserve(E, r, r.n);
+    int rc = replica_settle(E, r);
+    if (rc) return rc;
+    rc = replica_reserve(E, r, r.n);
     if (rc) return rc;
     std::vector<DocInfo> docs{DocInfo{r.n, r.vis_bytes}};
     rc = E.plan(r.logs, docs);
     if (rc) return rc;
     return E.merge(r.logs, Engine::TEXT, digest, len, st, text, nullptr, cps);
+}
+
+ReplayState::~ReplayState() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+}
+
+namespace {
+void drop_graph(ReplayState& st) {
+    if (st.exec) (void)hipGraphExecDestroy(st.exec);
+    if (st.graph) (void)hipGraphDestroy(st.graph);
+    st.exec = nullptr;
+    st.graph = nullptr;
+    st.key.clear();
+}
+}  // namespace
+
+int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, ReplayState& st,
+                   uint64_t* cps, uint64_t* bytes, uint64_t* digest) {
+    if (st.init != &init || st.ub != &ub || st.init_version != init.version) {
+        st.init = &init;
+        st.ub = &ub;
+        st.init_version = init.version;
+        st.known = false;
+        drop_graph(st);
+    }
+    Replica& w = st.work;
+    int rc = replica_settle(E, w);
+    if (rc) return rc;
+    if (init.pending) {
+        E.err = "replica has an unsettled decode";
+        return CRDT_HIP_EINVAL;
+    }
+    if (st.known && E.plan_cache && ub.n && ub.buf && ub.off) {
+        // ---- the sizes are known: one graph for the closure ---------------------------------
+        // prepare (everything that may allocate, upload or wait), then the launches
+        const uint64_t cap = init.logs.cap_slots;
+        rc = replica_reserve(E, w, cap ? cap - 1 : 0);
+        if (rc) return rc;
+        w.n = init.n;  // the copy below
+        rc = decode_prepare(E, w, ub.len, ub.n, true, ub.max_id);
+        if (rc) return rc;
+        // (test hook: with plan_shrink the planned sizes are off by one, forcing the fallback)
+        const uint64_t b_plan = st.bytes_after + (E.plan_shrink ? 1u : 0u);
+        std::vector<DocInfo> docs{DocInfo{st.n_after, b_plan}};
+        rc = E.plan(w.logs, docs);
+        if (rc) return rc;
+        if (!E.plans_known(w.logs)) {
+            st.known = false;  // the shape's plan was forgotten: learn it again below
+        } else {
+            Engine::AsyncMerge m;
+            rc = E.merge_async_prepare(w.logs, m, false);
+            if (rc) return rc;
+            const std::vector<uint64_t> key = {
+                E.generation(), w.gen, init.gen, (uint64_t)(uintptr_t)&init, init.n, init.vis_bytes,
+                cap, (uint64_t)(uintptr_t)&ub, ub.len, ub.n, st.n_after, b_plan};
+            hipStream_t s = E.stream;
+            if (key != st.key || !st.exec) {
+                drop_graph(st);
+                RCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), "begin capture");
+                rc = CRDT_HIP_OK;
+                if (cap) {
+                    const DeviceLogs& S = init.logs;
+                    DeviceLogs& D = w.logs;
+                    k_rep_copy<<<(uint32_t)std::min<uint64_t>(grid_for(cap, kUB), 4096), kUB, 0, s>>>(
+                        S.parent, S.lamport, S.agent, S.cp, D.parent, D.lamport, D.agent, D.cp, cap);
+                }
+                if (!rc) rc = decode_launch(E, w, ub.buf, ub.len, ub.off, ub.n, true, false);
+                if (!rc) {
+                    k_replay_check<<<1, 64, 0, s>>>(w.uctl, init.n, init.vis_bytes, st.n_after,
+                                                    b_plan);
+                    if (hipMemcpyAsync(w.hctl, w.uctl, U_N * 8, hipMemcpyDeviceToHost, s) !=
+                        hipSuccess)
+                        rc = hip_fail(E, "copy update counters", hipGetLastError());
+                }
+                if (!rc) rc = E.merge_async_enqueue(w.logs, m);
+                hipGraph_t g = nullptr;
+                const hipError_t ce = hipStreamEndCapture(s, &g);
+                if (rc) {
+                    if (g) (void)hipGraphDestroy(g);
+                    w.pending = false;
+                    return rc;
+                }
+                if (ce != hipSuccess) return hip_fail(E, "end capture", ce);
+                st.graph = g;
+                RCHK(hipGraphInstantiate(&st.exec, g, nullptr, nullptr, 0), "graph instantiate");
+                st.key = key;
+            }
+            w.pending = true;  // the graph holds the decode
+            RCHK(hipGraphLaunch(st.exec, s), "graph launch");
+            RCHK(hipStreamSynchronize(s), "replay sync");
+            w.vis_cp = init.vis_cp;
+            w.vis_bytes = init.vis_bytes;
+            uint64_t c1 = 0, b1 = 0, d1 = 0;
+            const int mrc = E.merge_async_finish(w.logs, m, &d1, &b1, &c1, nullptr);
+            if (w.hctl[U_PLAN] == 0 && mrc == CRDT_HIP_OK) {
+                rc = replica_settle(E, w);  // no wait left: applies the counters
+                if (rc) return rc;
+                if (cps) *cps = c1;
+                if (bytes) *bytes = b1;
+                if (digest) *digest = d1;
+                return CRDT_HIP_OK;
+            }
+            // the sizes changed (or the batch was rejected): merge again from the decode's counts
+            rc = replica_settle(E, w);
+            if (rc) return rc;
+            rc = replica_merge(E, w, nullptr, bytes, digest, nullptr, cps);
+            if (rc) return rc;
+            st.n_after = w.n;
+            st.bytes_after = w.vis_bytes;
+            return CRDT_HIP_OK;
+        }
+    }
+    // ---- first replay (or sizes unknown): clone, decode, wait, merge -----------------------
+    rc = replica_copy(E, init, w);  // main.rs:64
+    if (rc) return rc;
+    rc = replica_decode_enqueue(E, w, ub.buf, ub.len, ub.off, ub.n, true, ub.max_id, true);
+    if (rc) return rc;
+    rc = replica_settle(E, w);  // main.rs:65-67 (a rejected batch changes nothing)
+    if (rc) return rc;
+    rc = replica_merge(E, w, nullptr, bytes, digest, nullptr, cps);  // main.rs:68
+    if (rc) return rc;
+    st.known = true;
+    st.n_after = w.n;
+    st.bytes_after = w.vis_bytes;
+    return CRDT_HIP_OK;
 }
 
 }  // namespace crdt

@@ -9,6 +9,7 @@
 // merged by the engine like any resident document (one document, slot k = item id k).
 #pragma once
 #include <cstdint>
+#include <vector>
 
 #include "engine.hpp"
 
@@ -28,8 +29,15 @@ struct Replica {
     uint64_t ucap = 0;
     uint4* ublk = nullptr;     // per 256-update block aggregates
     uint64_t ublk_cap = 0;
+    uint32_t* imap = nullptr;  // per flattened item / delete of a batch: its update
+    uint32_t* dmap = nullptr;
+    uint64_t imap_cap = 0, dmap_cap = 0;
     uint64_t* uctl = nullptr;  // device counters (see replica.hip)
     uint64_t* hctl = nullptr;  // pinned host copy
+    bool pending = false;      // a decode was enqueued and its counters not yet applied
+    uint64_t gen = 0;          // bumped by every (re)allocation of the replica's device arrays
+    uint64_t version = 0;      // bumped by every change of the contents
+    std::vector<void*> graveyard;  // arrays replaced by a regrow, freed at the next wait
 
     Replica() = default;
     Replica(const Replica&) = delete;
@@ -44,6 +52,8 @@ struct UpdateBatch {
     uint64_t* off = nullptr;  // n + 1 byte offsets
     uint64_t len = 0;
     uint32_t n = 0;
+    uint32_t max_id = 0;      // largest item id the batch carries (read from the headers on the
+                              // host at upload; 0 = unknown): sizes a replica before the decode
 
     UpdateBatch() = default;
     UpdateBatch(const UpdateBatch&) = delete;
@@ -69,6 +79,41 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst);
 // OpLog::apply_update's semantics.  A batch that fails validation changes nothing.
 int replica_apply(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
                   const uint64_t* offsets, uint32_t n);
+// The decode without the wait: counters are copied to r.hctl in stream order (copy_counters)
+// and applied by replica_settle.  max_id: the batch's largest id if known (0: bound from len).
+int replica_decode_enqueue(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
+                           const uint64_t* offsets, uint32_t n, bool resident, uint32_t max_id,
+                           bool copy_counters);
+// Wait for an enqueued decode and apply its counters (errors: the batch changed nothing).
+int replica_settle(Engine& E, Replica& r);
+
+// The downstream closure (main.rs:63-69: clone the initial replica, apply every update, len())
+// in one call: `work` receives a copy of `init`, the resident batch is decoded into it and it is
+// merged.  The merge is planned with the sizes the previous replay of the same init and batch
+// produced, enqueued right behind the decode (one wait for the whole closure); a device check
+// compares those sizes with the decode's counters, and on a mismatch the host merges again with
+// the real ones.
+// Once the sizes are known the whole closure (copy, decode, check, merge, result copies) is
+// captured as a hipGraph and replayed while nothing it points to is reallocated.
+struct ReplayState {
+    Replica work;
+    const Replica* init = nullptr;
+    const UpdateBatch* ub = nullptr;
+    uint64_t init_version = 0;
+    bool known = false;
+    uint32_t n_after = 0;
+    uint64_t bytes_after = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<uint64_t> key;  // what the graph was captured with
+    ReplayState() = default;
+    ReplayState(const ReplayState&) = delete;
+    ReplayState& operator=(const ReplayState&) = delete;
+    ~ReplayState();
+};
+int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, ReplayState& st,
+                   uint64_t* cps, uint64_t* bytes, uint64_t* digest);
+
 // Merge the replica's document (text may be null: length and digest only; cps: codepoints of
 // the merged text, counted on the device).
 int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* len,

@@ -132,7 +132,7 @@ hipError_t pool_alloc(void** p, size_t bytes, bool host) {
     return hipSuccess;
 }
 
-void pool_free(void* p, bool host) {
+void pool_free(void* p, bool host, bool synced) {
     if (!p) return;
     Pool& P = pool(host);
     uint64_t key = 0;
@@ -148,7 +148,7 @@ void pool_free(void* p, bool host) {
         raw_free(p, host);
         return;
     }
-    (void)hipDeviceSynchronize();  // what hipFree would wait for
+    if (!synced) (void)hipDeviceSynchronize();  // what hipFree would wait for
     const size_t c = (size_t)(key & ((1ull << 48) - 1));
     {
         std::lock_guard<std::mutex> g(P.mu);

@@ -16,7 +16,8 @@ constexpr uint32_t NIL = 0xFFFFFFFFu;
 // drops it) do not pay hipMalloc / hipFree each time.  pool_free synchronises the device before
 // caching a block, as hipFree would, so a cached block is never still in use by queued work.
 hipError_t pool_alloc(void** p, size_t bytes, bool host = false);
-void pool_free(void* p, bool host = false);
+// synced: the caller has already waited for every use of the block (no device wait here)
+void pool_free(void* p, bool host = false, bool synced = false);
 
 inline size_t utf8_len_cp(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
 

@@ -262,6 +262,16 @@ int crdt_hip_replica_info(const crdt_hip_replica* r, uint64_t* items,
 int crdt_hip_replica_merge(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out, size_t cap,
                            size_t* out_len, uint64_t* digest);
 
+/* The downstream closure (main.rs:63-69) in one call: a copy of `init` (clone, :64) receives
+ * every update of the resident batch `u` (apply_update, :65-67) and is merged (len(), :68).
+ * Returns the merged text's codepoints, UTF-8 bytes and tree digest; `init` is unchanged.  The
+ * context keeps a work replica per (init, u) and the sizes the last replay produced: the merge
+ * is planned with them and enqueued right behind the decode (one host wait for the closure), a
+ * device check compares them with the decode's counters, and on a mismatch the replica is merged
+ * again with the real sizes.  A batch that fails validation returns EBADLOG. */
+int crdt_hip_replica_replay(crdt_hip_ctx* ctx, const crdt_hip_replica* init,
+                            const crdt_hip_updates* u, uint64_t* codepoints, uint64_t* bytes,
+                            uint64_t* digest);
 /* Downstream's len() (main.rs:68 asserts it; rope.rs:135 materialises): merge the replica and
  * return the merged text's codepoints (counted on the device), UTF-8 bytes and tree digest. */
 int crdt_hip_replica_merge_len(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint64_t* codepoints,

@@ -222,3 +222,72 @@ def test_resident_update_batch_rejects_bad_updates(ctx):
         r.apply_resident(ub)
     assert e.value.code == -5 and r.info()[0] == 0
     ub.close()
+
+
+@pytest.mark.parametrize("name", TRACES)
+def test_replay_closure_matches_golden(ctx, golden, py_trace, name):
+    """crdt_hip_replica_replay: the downstream closure (main.rs:63-69) in one call.  The first
+    call learns the sizes, later ones merge right behind the decode (speculated sizes checked on
+    the device); every call must give the trace's document, and init must stay unchanged."""
+    t = crdt_hip.Trace(trace_path(name))
+    patches = [t.patch(i) for i in range(len(t))]
+    up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
+    init = crdt_hip.Replica(ctx, up.log if up.log.view().n else None)
+    ub = crdt_hip.UpdateBatch(ctx, *crdt_hip.pack_updates(updates))
+    end = py_trace(name).end_content
+    want = (len(end), len(end.encode()), int(golden[name]["tree_digest"], 16))
+    before = init.info()
+    for _ in range(4):
+        assert init.replay(ub) == want
+    assert init.info() == before
+    # the same closure as three calls agrees
+    r = init.clone()
+    r.apply_resident(ub)
+    assert r.merge_len() == want
+    r.close()
+    ub.close()
+    init.close()
+
+
+def test_replay_falls_back_when_sizes_change(ctx, golden):
+    """Speculated sizes that no longer hold (forced with the plan_shrink hook) are caught by the
+    device check and the closure is merged again with the real ones; a changed init starts over."""
+    name = "sveltecomponent"
+    t = crdt_hip.Trace(trace_path(name))
+    patches = [t.patch(i) for i in range(len(t))]
+    up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
+    init = crdt_hip.Replica(ctx, None)
+    half = len(updates) // 2
+    ub = crdt_hip.UpdateBatch(ctx, *crdt_hip.pack_updates(updates))
+    want = init.replay(ub)
+    assert want[1] == golden[name]["end_bytes"]
+    ctx.set_param("plan_shrink", 1)
+    try:
+        assert init.replay(ub) == want
+    finally:
+        ctx.set_param("plan_shrink", 0)
+    assert init.replay(ub) == want
+    # init receives the first half itself: the learnt sizes no longer apply, the result is the same
+    init.apply_updates(updates[:half])
+    assert init.replay(ub) == want
+    assert init.replay(ub) == want
+    ub.close()
+    init.close()
+
+
+def test_replay_rejects_a_bad_batch_and_keeps_init(ctx):
+    log = crdt_hip.OpLog()
+    log.insert(0, "hello")
+    v0 = log.version()
+    log.insert(5, " world")
+    good = log.encode_from(v0)
+    init = crdt_hip.Replica(ctx, None)
+    bad = bytearray(good)
+    bad[8:12] = (50).to_bytes(4, "little")  # first id far beyond the replica: not causally ready
+    ub = crdt_hip.UpdateBatch(ctx, *crdt_hip.pack_updates([bytes(bad)]))
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        init.replay(ub)
+    assert e.value.code == -5
+    assert init.info() == (0, 0, 0)
+    ub.close()
+    init.close()
