@@ -702,7 +702,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--replicas", type=int, default=4096, help="replicas of each trace per GPU")
     ap.add_argument("--relabel", default="rotate", choices=["none", "rotate", "shuffle"])
-    ap.add_argument("--companion-replicas", type=int, default=0,
+    ap.add_argument("--companion-replicas", type=int, default=1024,
                     help="replicas per trace of the relabel=shuffle companion line (0: none)")
     ap.add_argument("--splitter-stride", type=int, default=0)
     ap.add_argument("--wave-slots-log2", type=int, default=30,
