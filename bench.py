@@ -59,8 +59,8 @@ MIN_B_PER_TEXT = 1.0
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
     "classify": (8.625, 0.0, 1.0),   # parent, cp|tombstone bit; seq bits, weight nibbles; tile UTF-8
-    "runs": (1.0, 8.0, 2.0),         # seq/jump/head bits, nibbles, rank words; run records; text move
-    "run_parent": (0.0, 28.0, 0.0),  # run head/prefix, parent lookup (+ rank word); weight, parent
+    # head/seq bits, nibbles; per run: key + parent slot + rank lookup in, record row out; text move
+    "runs": (0.75, 38.0, 2.0),
     "count": (0.0, 8.0, 0.0),
     "scan": (0.0, 8.0, 0.0),
     "place": (0.0, 12.0, 0.0),
@@ -72,7 +72,7 @@ KERNEL_BYTES = {
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out
 }
-STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs", "run_parent": "k_run_parent",
+STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs",
                 "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
 # HBM bytes per item of each kernel from rocprofv3 PMC passes of this build (FETCH_SIZE x2 for
 # gfx950 wide reads + WRITE_SIZE, one pass each: tools/profile.sh + tools/pmc_summary.py).

@@ -15,8 +15,8 @@
 //    k_classify    seq/jump bits, weight nibbles, each tile's UTF-8 compacted in slot order
 //    k_heads       head bitvector words, per-tile head counts
 //    k_tiles_*     exclusive scan of the per-tile (heads, weight) pairs
-//    k_runs        rank words, run records (head slot, weight prefix), slot-order UTF-8
-//    k_run_parent  parent run (rank lookup), key and weight of every run
+//    k_runs        run records (head slot, weight prefix, key, parent run by rank lookup),
+//                  slot-order UTF-8
 //  Level 1 merges the tree of runs:
 //    k_count / k_scan_* / k_place        children grouped by parent run
 //    k_link / k_sortmid / k_sortbig      sibling order -> first-child / next-sibling
@@ -117,16 +117,16 @@ struct L0Args {
     uint2* tile_hw;             // per tile {heads, weight}: totals, then exclusive prefixes
     uint2* tile_sums;           // per 4096 tiles: scan carries
     uint64_t* hbits;            // per 64 slots: run-head bits
-    uint32_t* hrank;            // per 64 slots: heads before the word (wave-relative)
+    uint16_t* hloc;             // per 64 slots: heads before the word inside its tile
     uint32_t* r_head;           // per run: head slot
-    uint32_t* r_pstart;         // per run: weight prefix at its head
+    uint32_t* r_pstart;         // per run: weight prefix at its head; [R] = the wave's weight
     uint32_t* r_parent;         // per run: parent run (kNil for a document start)
-    uint32_t* r_w;              // per run: weight
     uint64_t* r_key;            // per run: (lamport << 16 | agent) of the head
     uint32_t* doc_root;         // per document: its document-start run
     uint32_t* doc_p0;           // per document: weight prefix at its start
     uint32_t* ctl;
     uint32_t cap_runs, cap_rmax;  // capacity of the launch plan (k_docmax flags C_REPLAN above)
+    uint32_t cap_rows;            // rows allocated in r_parent / r_key (more runs: not written)
 };
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
@@ -246,7 +246,10 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 
 // k_heads: one thread per 64-slot word of the rank bitvector (a word is inside one document),
 // one wave per tile.  head(g) = document start, or an item that does not continue the run of
-// the slot before it: continue(g) = seq(g) && !jump(g-1).
+// the slot before it: continue(g) = seq(g) && !jump(g-1).  Besides the words: the heads before
+// each word inside its tile (hloc), so that the run of any slot s is
+// tile_hw[s / 4096].x + hloc[s / 64] + popcount(hbits[s / 64] up to s) - 1 once the tile
+// prefixes are scanned.
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
@@ -268,7 +271,10 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
         }
         a.hbits[wi] = hw;
     }
-    const uint32_t th = wave_sum((uint32_t)__popcll(hw));
+    const uint32_t c = (uint32_t)__popcll(hw);
+    const uint32_t inc = wave_incl_scan(c);
+    if (gs < a.nslots) a.hloc[wi] = (uint16_t)(inc - c);
+    const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     const uint32_t tile = wi >> 6;  // 64 words per tile: one wave
     if ((threadIdx.x & 63u) == 0 && tile < a.ntiles) a.tile_hw[tile].x = th;
 }
@@ -333,27 +339,37 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
         }
 }
 
-// k_runs: rank words, one record per run head (head slot, weight prefix), document starts, and
-// the tile's UTF-8 moved from its stile segment to its place in sbytes.  One packed scan,
-// heads << 16 | weight (a tile holds at most 4096 heads and 16,384 bytes).  The run records
-// are assembled in LDS (tile-local slot << 16 | tile-local weight prefix) and stored as
-// contiguous dword rows: storing them from the thread that found them costs one vector store
-// instruction per head position with lanes scattered over many lines, and the address unit,
-// not HBM, bounded the kernel.
+// k_runs: one record per run head and the tile's UTF-8 moved from its stile segment to its place
+// in sbytes.  One packed scan, heads << 16 | weight (a tile holds at most 4096 heads and 16,384
+// bytes).  The run records are assembled in LDS (tile-local slot << 16 | tile-local weight
+// prefix), then one thread per run of the tile writes its record row: head slot, weight prefix
+// (r_pstart; the last tile adds the sentinel r_pstart[R] = the wave's weight, so a run's weight
+// is always r_pstart[rho + 1] - r_pstart[rho]), key (lamport, agent of the head) and parent
+// run.  A head whose parent is the slot before it (a seq head, cut by a jump) has the previous
+// run as parent; any other head looks up the run of its parent slot in the head bitvector
+// (tile prefix + hloc + popcount).  Storing the rows from the thread that found each head costs
+// one vector store instruction per head position with lanes scattered over many lines (the
+// address unit, not HBM, bounded that form); one thread per run stores them as contiguous rows.
 __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     constexpr int NW = kBlock / 64;
     __shared__ uint32_t lsum[NW];
     __shared__ uint32_t rec[kScanTile];
+    __shared__ uint16_t lseq[kBlock];  // seq bits of every thread's 16 slots
+    __shared__ uint2 ldoc[kBlock];     // every thread's document {base slot, items}
     const uint32_t tile = blockIdx.x;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
     uint32_t hm = 0;
     uint64_t nib = 0;
+    uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
     if (gs < a.nslots) {
         hm = (uint32_t)(a.hbits[gs >> 6] >> (gs & 63u)) & 0xFFFFu;
         nib = a.wnib[gs >> 4];
+        doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        lseq[threadIdx.x] = a.seqb[gs >> 4];
     }
+    ldoc[threadIdx.x] = doc;
     // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
     // offset is known: thread t's destination dword needs source dwords t and t+1 whatever the
     // offset's alignment (the segment is kTileBytes long, so both are in bounds).
@@ -380,7 +396,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     }
     const uint32_t ex = off + inc - x;
     const uint32_t nh = tot >> 16;
-    uint32_t tw = tot & 0xFFFFu;
+    const uint32_t tw_all = tot & 0xFFFFu;
+    uint32_t tw = tw_all;
     if (a.mode == 0 && tw && (uint64_t)pre.y + tw > a.sbytes_cap) {  // more text than the host bound
         if (threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 4u);
         tw = 0;
@@ -398,14 +415,12 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             p += (uint32_t)(nib >> (4 * j)) & 15u;
         }
     }
-    if (gs < a.nslots && (threadIdx.x & 3u) == 0) a.hrank[gs >> 6] = pre.x + (ex >> 16);
-    if ((hm & 1u) && (gs & 63u) == 0) {  // document starts are 64-aligned
+    if ((hm & 1u) && (gs & 63u) == 0 && doc.x == gs) {  // document starts are 64-aligned
         const uint32_t d = a.chunk_doc[gs >> a.log2m];
-        if (a.docs[d].x == gs) {
-            a.doc_root[d] = pre.x + (ex >> 16);
-            a.doc_p0[d] = pre.y + (ex & 0xFFFFu);
-        }
+        a.doc_root[d] = pre.x + (ex >> 16);
+        a.doc_p0[d] = pre.y + (ex & 0xFFFFu);
     }
+    if (tile + 1u == a.ntiles && threadIdx.x == 0) a.r_pstart[pre.x + nh] = pre.y + tw_all;
     if (a.mode == 0) {
         uint32_t* d32 = reinterpret_cast<uint32_t*>(a.sbytes);
         if (m < hi) d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
@@ -420,11 +435,36 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             for (uint32_t g = max(hi, lo); g < D + tw; ++g) a.sbytes[g] = src[g - D];
     }
     __syncthreads();
+    // one thread per run: every gather of a stage issued before any is used
     const uint32_t tbase = tile * kScanTile;
     for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
-        const uint32_t v = rec[i];
-        a.r_head[pre.x + i] = tbase + (v >> 16);
-        a.r_pstart[pre.x + i] = pre.y + (v & 0xFFFFu);
+        const uint32_t rv = rec[i];
+        const uint32_t li = rv >> 16, g = tbase + li, rho = pre.x + i;
+        const uint2 dc = ldoc[li >> 4];
+        const bool sq = (lseq[li >> 4] >> (li & 15u)) & 1u;
+        const bool root = g == dc.x;
+        const uint32_t lam = a.in_lamport[g];
+        const uint32_t ag = a.in_agent[g];
+        uint32_t p = (!sq && !root) ? a.in_parent[g] : 0u;
+        a.r_head[rho] = g;
+        a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
+        uint32_t pr = kNil;
+        if (sq) {
+            pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
+        } else if (!root) {
+            if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
+            const uint32_t ps = dc.x + p;
+            const uint64_t hb = a.hbits[ps >> 6];
+            const uint32_t hl = a.hloc[ps >> 6];
+            const uint32_t tp = a.tile_hw[ps / kScanTile].x;
+            const uint32_t b = ps & 63u;
+            const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
+            pr = tp + hl + (uint32_t)__popcll(hb & mask) - 1u;
+        }
+        if (rho < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
+            a.r_parent[rho] = pr;
+            a.r_key[rho] = root ? 0ull : (((uint64_t)lam << 16) | ag);
+        }
     }
 }
 
@@ -446,77 +486,6 @@ __global__ __launch_bounds__(1024) void k_docmax(L0Args a) {
     }
 }
 
-// Per run: weight (next run's prefix - own prefix) and parent run (rank lookup of the head's
-// parent item; the parent item is always the last item of its run; a head whose parent is the
-// slot before it has the previous run as parent).  kRunsPerThread runs per thread, every load of
-// a stage issued before any is used, so that enough gathers are in flight to cover HBM latency.
-// The run count comes from level 0 on the device (ctl); the grid strides over it.
-constexpr int kRunsPerThread = 4;
-__global__ __launch_bounds__(kBlock) void k_run_parent(L0Args a) {
-    constexpr int K = kRunsPerThread;
-    if (replan(a.ctl)) return;
-    const uint32_t R = a.ctl[C_RTOTAL], wtotal = a.ctl[C_WTOTAL];
-    for (uint32_t r0 = blockIdx.x * (kBlock * K) + threadIdx.x; r0 < R;
-         r0 += gridDim.x * (kBlock * K)) {
-        uint32_t h[K], ps[K], nx[K], sq[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t rho = min(r0 + (uint32_t)k * kBlock, R - 1u);
-            h[k] = a.r_head[rho];
-            ps[k] = a.r_pstart[rho];
-            nx[k] = rho + 1 < R ? a.r_pstart[rho + 1] : wtotal;
-        }
-        uint32_t dx[K], dy[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            sq[k] = a.seqb[h[k] >> 4];
-            const uint2 doc = a.docs[a.chunk_doc[h[k] >> a.log2m]];
-            dx[k] = doc.x;
-            dy[k] = doc.y;
-        }
-        uint32_t lam[K], ag[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            lam[k] = a.in_lamport[h[k]];
-            ag[k] = a.in_agent[h[k]];
-        }
-        uint32_t ps_slot[K];  // parent slot of a non-seq head (0: none)
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            sq[k] = (sq[k] >> (h[k] & 15u)) & 1u;
-            uint32_t p = (!sq[k] && h[k] != dx[k]) ? a.in_parent[h[k]] : 0u;
-            if (p > dy[k] || p == h[k] - dx[k]) p = 0;  // flagged by k_classify
-            ps_slot[k] = dx[k] + p;
-        }
-        uint64_t hb[K];
-        uint32_t hr[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {  // rank lookups (only non-seq heads use them)
-            hb[k] = a.hbits[ps_slot[k] >> 6];
-            hr[k] = a.hrank[ps_slot[k] >> 6];
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t rho = r0 + (uint32_t)k * kBlock;
-            if (rho >= R) break;
-            uint32_t pr = kNil;
-            uint64_t key = 0;
-            if (sq[k]) {
-                pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
-                key = ((uint64_t)lam[k] << 16) | ag[k];
-            } else if (h[k] != dx[k]) {
-                const uint32_t b = ps_slot[k] & 63u;
-                const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
-                pr = hr[k] + (uint32_t)__popcll(hb[k] & mask) - 1u;
-                key = ((uint64_t)lam[k] << 16) | ag[k];
-            }
-            a.r_w[rho] = nx[k] - ps[k];
-            a.r_parent[rho] = pr;
-            a.r_key[rho] = key;
-        }
-    }
-}
-
 // Expansion, one wave per 64 consecutive runs.  Their bytes are contiguous in sbytes (runs are
 // numbered in slot order), so the wave streams them with unit-stride loads and each byte goes
 // to its run's place in the document: text[toff[d] + roff[run] + i].  ORDER mode writes the
@@ -526,8 +495,7 @@ struct ExpandArgs {
     const uint32_t* chunk_doc;
     const uint2* docs;
     const uint32_t* r_head;
-    const uint32_t* r_pstart;
-    const uint32_t* r_w;
+    const uint32_t* r_pstart;  // weight of run rho: r_pstart[rho + 1] - r_pstart[rho]
     const uint32_t* roff;
     const uint32_t* tlen;
     const uint64_t* toff;
@@ -550,7 +518,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a) {
         uint64_t dst = 0;
         if (rho < R) {
             src = a.r_pstart[rho];
-            w = a.r_w[rho];
+            w = a.r_pstart[rho + 1] - src;
             if (w) {
                 const uint32_t h = a.r_head[rho];
                 const uint32_t d = a.chunk_doc[h >> a.log2m];
@@ -604,7 +572,7 @@ struct TreeArgs {
     uint32_t step_limit;
     const uint32_t* in_parent;   // parent run (kNil: document start)
     const uint64_t* key;         // sibling key: (lamport, agent) of the run's head
-    const uint32_t* in_w;        // run weight
+    const uint32_t* pstart;      // weight prefix per run (+ sentinel): weight = [g + 1] - [g]
     const uint32_t* doc_root;    // per document: its document-start run
     const uint32_t* doc_p0;      // per document: weight prefix at its start
     uint32_t* deg;
@@ -776,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
     bool defer = false;
     if (g < a.R) {
-        const uint32_t w = a.in_w[g];
+        const uint32_t w = a.pstart[g + 1] - a.pstart[g];
         if (a.in_parent[g] == kNil) set_up(a, g, kNil, kNil);  // no sibling, no parent
         const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
         uint32_t fc = kNil;
@@ -1122,7 +1090,6 @@ struct DocArgs {
     uint32_t probe;  // 1 + document whose phase times are printed (0: none)
     const uint32_t* doc_root;
     const uint32_t* r_parent;
-    const uint32_t* r_w;
     const uint64_t* r_key;
     uint32_t* roff;
     uint32_t* ctl;
@@ -1303,7 +1270,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             gp[j] = v < R ? a.r_parent[base + v] : 0u;
-            gw[j] = v < R ? a.r_w[base + v] : 1u;
+            gw[j] = v < R ? a.r_pstart[base + v + 1] - a.r_pstart[base + v] : 1u;
         }
         for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
         uint32_t bad = 0;
@@ -1693,7 +1660,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             for (int j = 0; j < kDocJ; ++j) {
                 const uint32_t v = t + (uint32_t)j * kDocThreads;
                 if (ro[j] == kNil) continue;
-                const uint32_t ps = a.r_pstart[base + v], wv = a.r_w[base + v];
+                const uint32_t ps = a.r_pstart[base + v], wv = a.r_pstart[base + v + 1] - ps;
                 if ((uint64_t)ro[j] + wv > tl) {
                     oob = true;
                     continue;
@@ -2038,10 +2005,10 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hrank_); dfree(stile_);
+    dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hloc_); dfree(stile_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
-    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
+    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(out_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
     dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
@@ -2234,7 +2201,7 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hrank_); dfree(stile_);
+        dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hloc_); dfree(stile_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
@@ -2242,7 +2209,7 @@ int Engine::ensure_scratch(const Wave& w) {
         HIPCHK(dalloc(&seqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
         HIPCHK(dalloc(&hbits_, slots / 64 + 2), "hipMalloc hbits");
-        HIPCHK(dalloc(&hrank_, slots / 64 + 2), "hipMalloc hrank");
+        HIPCHK(dalloc(&hloc_, slots / 64 + 2), "hipMalloc hloc");
         HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
         HIPCHK(dalloc(&tile_hw_, tiles), "hipMalloc tile totals");
         HIPCHK(dalloc(&tile_sums_, tiles / kScanTile + 2), "hipMalloc tile sums");
@@ -2296,12 +2263,11 @@ int Engine::ensure_scratch(const Wave& w) {
 // Level-1 scratch, sized by the runs of the wave (known after level 0).
 int Engine::ensure_runs(uint64_t R, uint64_t S) {
     if (R > cap_runs_) {
-        dfree(r_parent_); dfree(r_w_); dfree(roff_); dfree(r_key_);
+        dfree(r_parent_); dfree(roff_); dfree(r_key_);
         dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_);
         dfree(scan_sums_); dfree(rec_);
         const uint64_t r = R + (R >> 3) + 4096;  // headroom against regrowth
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
-        HIPCHK(dalloc(&r_w_, r), "hipMalloc r_w");
         HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
         HIPCHK(dalloc(&deg_, r + 16), "hipMalloc deg");
@@ -2416,17 +2382,17 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.tile_hw = tile_hw_;                                          \
     a0.tile_sums = tile_sums_;                                      \
     a0.hbits = hbits_;                                              \
-    a0.hrank = hrank_;                                              \
+    a0.hloc = hloc_;                                                \
     a0.doc_root = doc_root_;                                        \
     a0.doc_p0 = doc_p0_;                                            \
     a0.ctl = ctl_;                                                  \
     a0.r_head = r_head_;                                            \
     a0.r_pstart = r_pstart_;                                        \
     a0.r_parent = r_parent_;                                        \
-    a0.r_w = r_w_;                                                  \
     a0.r_key = r_key_;                                              \
     a0.cap_runs = 0xFFFFFFFFu;                                      \
-    a0.cap_rmax = 0xFFFFFFFFu
+    a0.cap_rmax = 0xFFFFFFFFu;                                      \
+    a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull)
 
 // Tree / digest argument block (run counts come from ctl where the kernels need them).
 #define TREEARGS(a)                                                                   \
@@ -2434,7 +2400,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.ndocs = w.ndocs;                                                                \
     a.in_parent = r_parent_;                                                          \
     a.key = r_key_;                                                                   \
-    a.in_w = r_w_;                                                                    \
+    a.pstart = r_pstart_;                                                             \
     a.doc_root = doc_root_;                                                           \
     a.doc_p0 = doc_p0_;                                                               \
     a.deg = deg_; a.cstart = cstart_; a.child = child_; a.rec = rec_;                 \
@@ -2470,15 +2436,19 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
     return CRDT_HIP_OK;
 }
 
-// k_run_parent, k_doctotals, k_doctree (and k_expand for documents whose text did not fit).
+// k_runs alone (run_wave: the run rows did not fit the rows allocated when level 0 ran).
+int Engine::launch_runs(DeviceLogs& L, const Wave& w, bool ord) {
+    L0ARGS(a0);
+    k_runs<<<a0.ntiles, kBlock, 0, stream>>>(a0);
+    HIPCHK(hipGetLastError(), "k_runs launch");
+    return CRDT_HIP_OK;
+}
+
+// k_doctotals, k_doctree (k_expand for documents whose text did not fit runs in the tail).
 int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
                               StageClock& ck) {
     hipStream_t s = stream;
-    L0ARGS(a0);
     TREEARGS(a);
-    k_run_parent<<<std::min<uint32_t>(grid_for(p.R, kBlock * kRunsPerThread), 8192u) + 1u, kBlock,
-                   0, s>>>(a0);
-    MARK(S_RPARENT);
     DocArgs da{};
     da.ndocs = w.ndocs;
     da.rcap = p.rcap;
@@ -2486,7 +2456,6 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.chbytes = doctree_ch_bytes(p.rcap, p.scap);
     da.doc_root = doc_root_;
     da.r_parent = r_parent_;
-    da.r_w = r_w_;
     da.r_key = r_key_;
     da.roff = roff_;
     da.ctl = ctl_;
@@ -2511,7 +2480,6 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
 int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
                                  StageClock& ck, uint32_t& rounds) {
     hipStream_t s = stream;
-    L0ARGS(a0);
     TREEARGS(a);
     const uint32_t R = p.R;
     // splitter stride: longer sublists once the pointer jumping over the splitter lists
@@ -2526,9 +2494,6 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     a.step_limit = 2u * R + 4u;
     const uint32_t gR = grid_for(R), gS = grid_for(S);
     const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
-    k_run_parent<<<std::min<uint32_t>(grid_for(R, kBlock * kRunsPerThread), 8192u) + 1u, kBlock,
-                   0, s>>>(a0);
-    MARK(S_RPARENT);
     k_count<<<gR, kBlock, 0, s>>>(a);
     MARK(S_COUNT);
     k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_);
@@ -2577,7 +2542,6 @@ int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, Stag
     ea.docs = a0.docs;
     ea.r_head = r_head_;
     ea.r_pstart = r_pstart_;
-    ea.r_w = r_w_;
     ea.roff = roff_;
     ea.tlen = tlen_;
     ea.toff = toff_;
@@ -2610,7 +2574,7 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
                         std::vector<uint32_t>& stage_launches) {
     const uint32_t g1 = p.lds1 ? 0u : 1u;
     const bool expand_run = !p.fuse;
-    const uint32_t launches[S_N] = {1, 6, 1, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
+    const uint32_t launches[S_N] = {1, 6, 0, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
                                     p.lds1 ? 2u : 0u};
@@ -2662,8 +2626,14 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     const L1Plan p = plan_level1(w, hctl[C_RTOTAL], hctl[C_RMAX], ord, force_global);
     const uint32_t lg = log2m_set ? log2m : (p.R > (1u << 24) ? 6u : 4u);
     const uint32_t Sreg = 2 * ((p.R + (1u << lg) - 1) >> lg);
+    const uint64_t rows = cap_runs_;  // run rows k_runs could write
     rc = ensure_runs(p.R, Sreg + w.ndocs);
     if (rc) return rc;
+    if (p.R > rows) {
+        // more runs than rows: the run records again, now that they fit (k_runs only reads
+        // level-0 outputs, so it can run twice)
+        if ((rc = launch_runs(L, w, ord))) return rc;
+    }
     if ((rc = clock_mark(ck, 0xFF))) return rc;  // the host wait above is no stage's time
     uint32_t rounds = 0;
     rc = p.lds1 ? launch_lds_level1(L, w, ord, p, ck) : launch_global_level1(L, w, ord, p, ck, rounds);

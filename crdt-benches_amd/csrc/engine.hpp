@@ -157,7 +157,7 @@ private:
     uint32_t *jbits_ = nullptr, *jloc_ = nullptr;
     uint16_t* seqb_ = nullptr;
     uint64_t *hbits_ = nullptr, *wnib_ = nullptr;
-    uint32_t* hrank_ = nullptr;
+    uint16_t* hloc_ = nullptr;
     uint8_t *stile_ = nullptr, *sbytes_ = nullptr;
     uint2 *tile_hw_ = nullptr, *tile_sums_ = nullptr;
     uint64_t cap_sbytes_ = 0;
@@ -173,7 +173,7 @@ private:
     uint8_t* doc_fused_ = nullptr;
     // level-1 scratch (per run / per splitter), grown on demand
     uint64_t cap_heads_ = 0, cap_runs_ = 0, cap_splitters_ = 0;
-    uint32_t *r_head_ = nullptr, *r_pstart_ = nullptr, *r_parent_ = nullptr, *r_w_ = nullptr,
+    uint32_t *r_head_ = nullptr, *r_pstart_ = nullptr, *r_parent_ = nullptr,
              *roff_ = nullptr;
     uint64_t* r_key_ = nullptr;
     uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
@@ -229,6 +229,7 @@ private:
     L1Plan plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord, bool force_global) const;
     int clock_mark(StageClock& c, int stage);
     // The launches of one wave, in stream order.
+    int launch_runs(DeviceLogs& L, const Wave& w, bool ord);
     int launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs, uint32_t cap_rmax,
                       StageClock& ck);
     int launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p, StageClock& ck);
