@@ -1054,30 +1054,57 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 // r_parent and r_w (coalesced) and r_key (sibling groups of two or more only); it writes the
 // run offsets roff exactly as the global path's k_walk2 does.
 //
-// LDS image (u16 arrays indexed by the local run v in [0, R); run 0 is the document start):
+// LDS image until the siblings are sorted (u16 arrays indexed by the local run v in [0, R); run 0
+// is the document start):
 //   D[v]   child count -> segment start (exclusive scan) -> segment end (after placement)
-//          -> first child (kNil16: a leaf) once the siblings are sorted
 //   nx[v]  parent until placement, then the tour successor of v's up arc: the next sibling's
 //          down arc, (parent | kUp16) = the parent's up arc, or kNil16 for the root
-//   ch[]   children grouped by parent (segment of v = [D[v-1], D[v])), sorted by key desc;
-//          reused for the splitter lists (u32 sums + u16 links) once the first children are known
-//   w[v]   the deferred sort list during the sort, then the weight (0xFFFF: look it up in
-//          r_w), then, once walk 1 has passed v, the splitter whose sublist holds v (kNil16 for
-//          weightless runs)
-// Splitters are the down arcs of the runs v with v % 4 == 0 (splitter v / 4).  Up arcs carry no
+//   ch[]   children grouped by parent (segment of v = [D[v-1], D[v])), sorted by key desc
+//   w[v]   the weight (0xFFFF: look it up in the LDS side table of big runs)
+//   gl[]   the work list of sibling groups of two or more
+// then one 8-byte record per run over the D / nx / ch / w arrays, so that a walk step is one
+// LDS read:
+//   rec[v] = {first child | nx << 16, weight | spare << 16}; once walk 1 has passed v's down
+//            arc the second word holds v's offset inside its sublist (18 bits) and the sublist
+//            (14 bits); 0xFFFFFFFF for weightless runs
+// and the splitter records (u32 sublist sum << 14 | next splitter) in the gl region.
+// Splitters are the down arcs of one run per block of 4 (splitter_run: block b, hashed offset).  Up arcs carry no
 // weight and never split: pointer jumping over the last-child up links until none is left makes
 // the tour a list of down arcs only (a leaf goes straight to the next sibling of its nearest
 // ancestor-or-self that has one).  A walker that passes v's down arc leaves v's offset inside its
 // sublist and the sublist's id in v's LDS entries, and once the splitter list is ranked (pointer
 // jumping) one pass turns them into document offsets.
+// Volatile LDS accesses through LDS-typed pointers: a volatile access through a generic pointer
+// is not narrowed to the LDS aperture by the compiler and becomes a system-coherent flat access.
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t* p) { return *(volatile lds_u32_t*)p; }
+__device__ __forceinline__ void lds_st32(uint32_t* p, uint32_t v) { *(volatile lds_u32_t*)p = v; }
+__device__ __forceinline__ uint32_t lds_ld16(uint16_t* p) { return *(volatile lds_u16_t*)p; }
+__device__ __forceinline__ void lds_st16(uint16_t* p, uint32_t v) { *(volatile lds_u16_t*)p = (uint16_t)v; }
+
 constexpr int kDocThreads = 1024;
 constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
 #ifndef CRDT_DOC_LOG2S
 #define CRDT_DOC_LOG2S 2
 #endif
-// splitters: the down arcs of the runs v % 2^kDocLog2S == 0; kDocK per thread
+// splitters: one run per block of 2^kDocLog2S consecutive runs, at a hashed position inside the
+// block (block 0: the document start), so that no chain of the tour whose run indices share a
+// residue can miss every splitter; splitter b = block b; kDocK per thread
 constexpr uint32_t kDocLog2S = CRDT_DOC_LOG2S;
 constexpr int kDocK = (kDocJ + (1 << kDocLog2S) - 1) >> kDocLog2S;
+#ifndef CRDT_DOC_HASHSPLIT
+#define CRDT_DOC_HASHSPLIT 1
+#endif
+#ifndef CRDT_DOC_WALK_WAVES
+#define CRDT_DOC_WALK_WAVES 16
+#endif
+__device__ __forceinline__ uint32_t splitter_off(uint32_t b) {
+    return (CRDT_DOC_HASHSPLIT && b) ? (b * 0x9E3779B1u) >> (32u - kDocLog2S) : 0u;
+}
+__device__ __forceinline__ uint32_t splitter_run(uint32_t b) {
+    return (b << kDocLog2S) | splitter_off(b);
+}
 constexpr uint32_t kDocLds = 163840 - 1024;  // dynamic LDS budget (static arrays use the rest)
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
@@ -1104,16 +1131,20 @@ struct DocArgs {
     uint32_t lds_bytes;   // dynamic LDS of the launch
 };
 
-// LDS bytes of a document with up to rcap - 2 runs: D, nx, w (2 B/run each), the ch region,
-// which later holds the splitter records (4 B per splitter: sublist sum << 14 | next splitter),
-// and the work list of sibling groups of two or more (at most one per two runs).
-__host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t scap) {
-    return ((2u * rcap > 4u * scap ? 2u * rcap : 4u * scap) + 15u) & ~15u;
+// LDS bytes of a document with up to rcap - 2 runs: D, nx, ch, w (2 B/run each; together the
+// 8-byte run records later) and the gl region: the work list of sibling groups of two or more
+// (at most one per two runs), later the splitter records (4 B per splitter).
+__host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t) {
+    return (2u * rcap + 15u) & ~15u;
 }
 // sibling groups of two or more: at most one per two runs
 __host__ __device__ constexpr uint32_t doctree_defer_cap(uint32_t rcap) { return rcap / 2u + 8u; }
+__host__ __device__ constexpr uint32_t doctree_gl_bytes(uint32_t rcap, uint32_t scap) {
+    return ((2u * doctree_defer_cap(rcap) > 4u * scap ? 2u * doctree_defer_cap(rcap) : 4u * scap) +
+            15u) & ~15u;
+}
 __host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap) {
-    return 6ull * rcap + doctree_ch_bytes(rcap, scap) + 2ull * doctree_defer_cap(rcap);
+    return 6ull * rcap + doctree_ch_bytes(rcap, scap) + doctree_gl_bytes(rcap, scap);
 }
 
 // Sort key: (lamport, agent) of the run's head (48 bits) and the local run index (15 bits), so
@@ -1219,7 +1250,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
 __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
-    __shared__ uint32_t npair, nwide, flags, visited_lds, pruned_any, nbig, qhead;
+    __shared__ uint32_t npair, nwide, flags, visited_lds, pruned_any, nbig;
 #ifdef CRDT_HIP_PROBE
     __shared__ uint32_t probe_max, probe_sum;
 #endif
@@ -1233,9 +1264,11 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
     uint16_t* ch = nx + a.rcap;
-    uint32_t* srec = reinterpret_cast<uint32_t*>(ch);  // splitter records, once ch is dead
     uint16_t* w = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(ch) + a.chbytes);
     uint16_t* glist = w + a.rcap;  // sibling-group work list (pairs front, 3..64 back)
+    uint32_t* srec = reinterpret_cast<uint32_t*>(glist);  // splitter records, once gl is dead
+    uint2* rec = reinterpret_cast<uint2*>(dyn);           // run records, once D..w are dead
+    uint32_t* rec32 = dyn;
     const uint32_t gcap = doctree_defer_cap(a.rcap);
     uint32_t* D32 = dyn;
 #ifdef CRDT_HIP_PROBE
@@ -1252,7 +1285,6 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         flags = 0;
         visited_lds = 0;
         pruned_any = 0;
-        qhead = kDocThreads;
 #ifdef CRDT_HIP_PROBE
         probe_max = probe_sum = 0;
 #endif
@@ -1265,12 +1297,23 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // ---- parents and weightless flags (all loads first), cleared counts --------------------
     uint32_t zw = 0, pruned = 0;  // bit j: run t + 1024 j has no visible bytes / was pruned
     {
-        uint32_t gp[kDocJ], gw[kDocJ];
+        // weights are differences of consecutive weight prefixes: the next run's prefix is the
+        // next lane's (lane 63 loads it; v = R - 1 reads the next document's first run or the
+        // sentinel)
+        uint32_t gp[kDocJ], gw[kDocJ], gn[kDocJ];
+        const bool l63 = (t & 63u) == 63u;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             gp[j] = v < R ? a.r_parent[base + v] : 0u;
-            gw[j] = v < R ? a.r_pstart[base + v + 1] - a.r_pstart[base + v] : 1u;
+            gw[j] = v <= R ? a.r_pstart[base + v] : 0u;  // (v = R: the next lane's successor)
+            gn[j] = (l63 && v < R) ? a.r_pstart[base + v + 1] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            const uint32_t nxt = (uint32_t)__shfl_down((int)gw[j], 1);
+            gw[j] = v < R ? (l63 ? gn[j] : nxt) - gw[j] : 1u;
         }
         for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
         uint32_t bad = 0;
@@ -1372,17 +1415,27 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // work list and groups of 3..64 to its back, and the list is sorted in passes whose key
     // loads are issued together: pairs (kPairs per thread at once), 3..8 (one register network
     // per thread), 9..64 (one wave per group).  Wider groups hand the wave to the global path.
+    // fcs[j]: the first child of run t + 1024 j (kNil16: a leaf), or 0x10000 | its segment start
+    // while its group is still to be sorted
+    uint32_t fcs[kDocJ];
     if (t == 0) nx[0] = kNil16;
 #pragma unroll
     for (int j = 0; j < kDocJ; ++j) {
         const uint32_t p = t + (uint32_t)j * kDocThreads;
+        uint32_t f = kNil16;
         if (p < R) {
             const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
-            if (cnt == 1u) nx[ch[s0]] = (uint16_t)(p | kUp16);
-            else if (cnt == 2u) glist[atomicAdd(&npair, 1u)] = (uint16_t)p;
-            else if (cnt > 64u) atomicOr(&flags, 2u);
-            else if (cnt > 2u) glist[gcap - 1u - atomicAdd(&nwide, 1u)] = (uint16_t)p;
+            if (cnt == 1u) {
+                f = ch[s0];
+                nx[f] = (uint16_t)(p | kUp16);
+            } else if (cnt >= 2u) {
+                f = 0x10000u | s0;
+                if (cnt == 2u) glist[atomicAdd(&npair, 1u)] = (uint16_t)p;
+                else if (cnt > 64u) atomicOr(&flags, 2u);
+                else glist[gcap - 1u - atomicAdd(&nwide, 1u)] = (uint16_t)p;
+            }
         }
+        fcs[j] = f;
     }
     __syncthreads();
     PROBE(12);
@@ -1487,24 +1540,28 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         if (t == 0) atomicOr(&a.ctl[C_ERR], (flags & 1u) ? 1u : 32u);
         return;
     }
-    // ---- first children (into D) --------------------------------------------------------------
+    // ---- first children of the sorted groups; the run records --------------------------------
+    uint32_t act = 0;  // bit j: run t + 1024 j still has an up link (see below)
     {
-        uint32_t fc[kDocJ];
+        uint32_t fx[kDocJ], wx[kDocJ];
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            uint32_t f = kNil16;
+            uint32_t f = fcs[j], n = 0, ww = 0;
             if (v < R) {
-                const uint32_t s0 = v ? D[v - 1] : 0u;
-                if (s0 < D[v]) f = ch[s0];
+                if (f & 0x10000u) f = ch[f & 0xFFFFu];
+                n = nx[v];
+                ww = w[v];
+                if ((n & kUp16) && n < kDead16) act |= 1u << j;
             }
-            fc[j] = f;
+            fx[j] = (f & 0xFFFFu) | (n << 16);
+            wx[j] = ww | 0xFFFF0000u;  // spare: "not reached" until walk 1 passes v
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            if (v < R) D[v] = (uint16_t)fc[j];
+            if (v < R) rec[v] = make_uint2(fx[j], wx[j]);
         }
     }
     __syncthreads();
@@ -1512,57 +1569,61 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // ---- up links: a last child's up arc is followed by its parent's up arc (no weight, never a
     // splitter), so nx[v] = UP(p) may be replaced by nx[p].  In-place pointer jumping until no up
     // link is left: each thread keeps a bit per owned run still holding one and works only on
-    // those; a concurrent reader sees an old or a new link, both correct successors, so a round
-    // needs no barrier between its reads and writes, only the block-wide "anything left" test.
+    // those.  A concurrent reader sees an old or a new link, both correct successors, so there
+    // is no barrier at all until every thread's own links are resolved; every pass advances a
+    // link by at least one level, so R passes bound it (more: a parent cycle, flagged).
     {
-        uint32_t act = 0;
-#pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t v = t + (uint32_t)j * kDocThreads;
-            if (v < R) {
-                const uint32_t x = nx[v];
-                if ((x & kUp16) && x < kDead16) act |= 1u << j;
+        uint16_t* vnx = reinterpret_cast<uint16_t*>(dyn) + 1;  // nx of v: [4 v]
+        for (uint32_t pass = 0; act; ++pass) {
+            if (pass > R) {
+                atomicOr(&flags, 4u);
+                break;
             }
-        }
-        volatile uint16_t* vnx = nx;
-        while (__syncthreads_or(act != 0u)) {
             for (uint32_t m = act; m; m &= m - 1u) {
                 const uint32_t j = (uint32_t)__ffs(m) - 1u;
                 const uint32_t v = t + j * kDocThreads;
-                const uint32_t y = vnx[vnx[v] & 0x7FFFu];  // an internal run: never dead
-                vnx[v] = (uint16_t)y;
+                // (the parent is an internal run: never dead)
+                const uint32_t y = lds_ld16(vnx + 4u * (lds_ld16(vnx + 4u * v) & 0x7FFFu));
+                lds_st16(vnx + 4u * v, y);
                 if (!((y & kUp16) && y < kDead16)) act &= ~(1u << j);
             }
         }
     }
+    __syncthreads();
     PROBE(6);
-    // ---- walk 1: one walker per lane, splitters handed out by an LDS queue ----------------
-    // A step at v's down arc reads fc, nx and w of v together: v's weight is added, v's offset
-    // inside the sublist and the sublist go to v's D and w entries, and the walk goes to the
-    // first child, or for a leaf to nx (a down arc, or the end of the tour).  A lane whose
-    // sublist ends takes the next splitter, so the lanes stay busy until the queue runs dry.
-    // The sublist results (sum, next splitter) go to the ch region, which no walker reads.
+    // ---- walk 1: one walker per lane, each wave over its own range of splitters ---------------
+    // A step at v's down arc reads v's record (first child, nx, weight: one 8-byte LDS read):
+    // v's weight is added, v's offset inside the sublist and the sublist go to the record's
+    // second word, and the walk goes to the first child, or for a leaf to nx (a down arc, or the
+    // end of the tour).  A lane whose sublist ends takes the next splitter of its wave's range
+    // (a wave-uniform cursor advanced by ballot: no LDS atomic in the loop), so the lanes stay
+    // busy until the range runs dry.  The sublist results (sum, next splitter) go to the gl
+    // region, which no walker reads.
     uint32_t runs = 0;
     uint32_t lane_steps = 0;
     {
-        uint32_t s = t;
-        uint32_t s_next = atomicAdd(&qhead, 1u);  // the lane's next splitter, fetched ahead
-        uint32_t V = s << kDocLog2S, SUM = 0, steps = 0;
+        constexpr uint32_t NWV = CRDT_DOC_WALK_WAVES;  // walking waves (the others wait)
+        const uint32_t lane = t & 63u, wv = t >> 6;
+        const uint32_t lo = wv < NWV ? (S * wv) / NWV : S, hi = wv < NWV ? (S * (wv + 1u)) / NWV : S;
+        uint32_t cur = lo + 64u;  // the wave's next unassigned splitter (uniform over its lanes)
+        uint32_t s = lo + lane < hi ? lo + lane : S;
+        uint32_t V = splitter_run(s), SUM = 0, steps = 0;
         const uint32_t step_limit = R + S + 4u;
         while (s < S) {
-            const uint32_t f = D[V], n = nx[V], ww = w[V];
-            const bool dn = n != kDead16;  // a pruned run (only ever a splitter's own) ends it
+            const uint2 r = rec[V < R ? V : 0u];
+            const uint32_t f = r.x & 0xFFFFu, n = r.x >> 16, ww = r.y & 0xFFFFu;
+            // a pruned run (only ever a splitter's own) ends it, and so does the splitter run of
+            // the last block when it falls beyond the document
+            const bool dn = V < R && n != kDead16;
             uint32_t wt = ww;
             if (dn && ww == 0xFFFFu)  // a run of 64 KiB or more: the LDS side table
                 for (uint32_t i = 0; i < nbig; ++i)
                     if (bigv[i] == V) wt = bigw[i];
             wt = dn ? wt : 0u;
             if (dn) {
-                // v's down arc is the last use of D[v] (first child) and w[v] (weight): they now
-                // hold v's offset inside this sublist (18 bits) and the sublist (14 bits)
-                const uint32_t pk = wt ? (SUM | (s << 18)) : 0xFFFFFFFFu;
-                D[V] = (uint16_t)pk;
-                w[V] = (uint16_t)(pk >> 16);
+                // v's down arc is the last use of its record: the second word now holds v's
+                // offset inside this sublist (18 bits) and the sublist (14 bits)
+                rec32[2u * V + 1u] = wt ? (SUM | (s << 18)) : 0xFFFFFFFFu;
             }
             SUM += wt;
             runs += dn ? 1u : 0u;
@@ -1570,16 +1631,22 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             const uint32_t go = !dn ? kNil16 : (f != kNil16 ? f : n);
             constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
             const bool end = go == kNil16;
-            const bool split = !end && (go & mm) == 0;  // a splitter's down arc
-            if (end || split) {
+            const bool split = !end && (go & mm) == splitter_off(go >> kDocLog2S);  // a splitter's
+            const bool need = end || split;
+            if (need) {
                 srec[s] = (SUM << 14) | (split ? go >> kDocLog2S : kNil14);
-                s = s_next;
-                s_next = atomicAdd(&qhead, 1u);
-                V = s << kDocLog2S;
                 SUM = 0;
             } else {
                 V = go;
             }
+            const uint64_t m = __ballot(need);
+            if (need) {
+                const uint32_t ns = cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                s = ns < hi ? ns : S;
+                V = splitter_run(s);
+            }
+            cur += (uint32_t)__popcll(m);
             if (++steps > step_limit) {
                 atomicOr(&flags, 4u);
                 break;
@@ -1596,29 +1663,42 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #endif
     __syncthreads();
     PROBE(7);
-    // ---- pointer jumping: record = (sum from the splitter to the end of the tour) << 14 | next
-    for (uint32_t r = 1; r < S; r <<= 1) {
-        uint32_t nr[kDocK];
+    // ---- pointer jumping: record = (sum from the splitter to the end of the tour) << 14 | next.
+    // A record always describes a valid stretch of the tour (sum up to its next splitter, read
+    // and written as one dword), so joining it with an old or a new record of its successor is
+    // equally right: the jumping runs without barriers, each thread until its own records reach
+    // the end (every pass advances a record by at least one splitter: S passes bound it).
+    {
+        uint32_t x[kDocK], live = 0;
 #pragma unroll
         for (int k = 0; k < kDocK; ++k) {
             const uint32_t s = t + (uint32_t)k * kDocThreads;
-            uint32_t x = 0;
-            if (s < S) {
-                x = srec[s];
-                const uint32_t p = x & kNil14;
-                if (p != kNil14) x = (x & ~kNil14) + srec[p];  // sums add, the link jumps
+            x[k] = s < S ? srec[s] : kNil14;
+            live |= ((x[k] & kNil14) != kNil14 ? 1u : 0u) << k;
+        }
+        for (uint32_t pass = 0; live; ++pass) {
+            if (pass > S) {
+                atomicOr(&flags, 4u);
+                break;
             }
-            nr[k] = x;
-        }
-        __syncthreads();
+            uint32_t y[kDocK];
 #pragma unroll
-        for (int k = 0; k < kDocK; ++k) {
-            const uint32_t s = t + (uint32_t)k * kDocThreads;
-            if (s < S) srec[s] = nr[k];
+            for (int k = 0; k < kDocK; ++k) y[k] = ((live >> k) & 1u) ? lds_ld32(srec + (x[k] & kNil14)) : 0u;
+#pragma unroll
+            for (int k = 0; k < kDocK; ++k) {
+                if (!((live >> k) & 1u)) continue;
+                x[k] = (x[k] & ~kNil14) + y[k];  // sums add, the link jumps
+                lds_st32(srec + t + (uint32_t)k * kDocThreads, x[k]);
+                if ((x[k] & kNil14) == kNil14) live &= ~(1u << k);
+            }
         }
-        __syncthreads();
     }
+    __syncthreads();
     PROBE(8);
+    if (flags) {  // a walk or a jumping that did not end: a cycle (the log is malformed)
+        if (t == 0) atomicOr(&a.ctl[C_ERR], 2u);
+        return;
+    }
     // ---- run offsets: sublist offset (total - suffix of its splitter) + offset inside ------
     uint32_t ro[kDocJ];  // document offset of every owned run with visible bytes, else kNil
     {
@@ -1627,7 +1707,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t pk = 0xFFFFFFFFu;
-            if (v < R && !(pruned & (1u << j))) pk = (uint32_t)D[v] | ((uint32_t)w[v] << 16);
+            if (v < R && !(pruned & (1u << j))) pk = rec32[2u * v + 1u];
             const uint32_t sid = pk >> 18;
             // weightless, pruned (or never reached: flagged below)
             ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (srec[sid] >> 14) : kNil;

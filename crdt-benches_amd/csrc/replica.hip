@@ -433,9 +433,12 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     r.version++;
     if (!n) return CRDT_HIP_OK;
     DeviceLogs& L = r.logs;
-    RCHK(hipMemcpy(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice), "upload parent");
-    RCHK(hipMemcpy(L.lamport + 1, v->lamport, n * 4ull, hipMemcpyHostToDevice), "upload lamport");
-    RCHK(hipMemcpy(L.agent + 1, v->agent, n * 2ull, hipMemcpyHostToDevice), "upload agent");
+    // on the engine stream, after the padding kernel replica_reserve may have queued there (a
+    // null-stream copy does not wait for a non-blocking stream and could be overwritten by it)
+    hipStream_t s = E.stream;
+    RCHK(hipMemcpyAsync(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice, s), "upload parent");
+    RCHK(hipMemcpyAsync(L.lamport + 1, v->lamport, n * 4ull, hipMemcpyHostToDevice, s), "upload lamport");
+    RCHK(hipMemcpyAsync(L.agent + 1, v->agent, n * 2ull, hipMemcpyHostToDevice, s), "upload agent");
     std::vector<uint32_t> c(n);
     for (uint32_t i = 0; i < n; ++i) {
         c[i] = (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u);
@@ -444,7 +447,8 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
             r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
         }
     }
-    RCHK(hipMemcpy(L.cp + 1, c.data(), n * 4ull, hipMemcpyHostToDevice), "upload cp");
+    RCHK(hipMemcpyAsync(L.cp + 1, c.data(), n * 4ull, hipMemcpyHostToDevice, s), "upload cp");
+    RCHK(hipStreamSynchronize(s), "upload sync");  // (c and the caller's view are released)
     return CRDT_HIP_OK;
 }
 
