@@ -441,6 +441,8 @@ def traces_workload(args) -> int:
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
+    if args.l1_split != 1:  # (the engine's default; builds before the parameter lack it)
+        ctx.set_param("l1_split", args.l1_split)
 
     def make_batch(bases, replicas, relabel, seed):
         return ctx.batch(bases, replicas=replicas, relabel=relabel, seed=seed)
@@ -721,6 +723,9 @@ def parse_args(argv=None):
     ap.add_argument("--plan-cache", type=int, default=1, choices=[0, 1],
                     help="1: merges after the first enqueue every wave with its learnt launch "
                          "plan and wait once (Engine::merge_async); 0: wait after each level 0")
+    ap.add_argument("--l1-split", type=int, default=1, choices=[0, 1],
+                    help="1: enqueued waves run level 1 on a low-priority stream of their lane "
+                         "(level 0 of the next wave is favoured for the CUs); 0: one stream")
     ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
                     help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

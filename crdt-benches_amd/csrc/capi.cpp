@@ -51,6 +51,9 @@ struct crdt_hip_updates {
 };
 
 namespace {
+
+// device bytes per op-log slot: parent (4) + key (lamport << 16 | agent, 8) + codepoint word (4)
+constexpr uint64_t kSlotBytes = 16;
 thread_local std::string g_err;
 
 int set_err(crdt_hip_ctx* ctx, int code, const std::string& msg) {
@@ -172,6 +175,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
     if (k == "lane_gate") {
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "lane_gate must be 0 or 1");
         ctx->eng.l0_gated = value == 1;
+        return 0;
+    }
+    if (k == "l1_split") {
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "l1_split must be 0 or 1");
+        ctx->eng.l1_split = value == 1;
         return 0;
     }
     if (k == "plan_cache") {
@@ -514,7 +522,7 @@ int crdt_hip_batch_create(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* bases, u
             delete b;
             return from_engine(ctx, rc);
         }
-        b->device_bytes = b->logs.total_slots * 15 + (b->logs.total_slots >> b->logs.log2m) * 4;
+        b->device_bytes = b->logs.total_slots * kSlotBytes + (b->logs.total_slots >> b->logs.log2m) * 4;
         *out = b;
         return 0;
     });
@@ -532,7 +540,7 @@ int crdt_hip_batch_synth_tree(crdt_hip_ctx* ctx, uint32_t n_items, uint32_t p_ch
             delete b;
             return from_engine(ctx, rc);
         }
-        b->device_bytes = b->logs.total_slots * 15 + (b->logs.total_slots >> b->logs.log2m) * 4;
+        b->device_bytes = b->logs.total_slots * kSlotBytes + (b->logs.total_slots >> b->logs.log2m) * 4;
         *out = b;
         return 0;
     });

@@ -104,8 +104,7 @@ struct L0Args {
     const uint32_t* chunk_doc;  // per 64 slots: wave-local document
     const uint2* docs;          // per document {wave-relative base slot, n items}
     const uint32_t* in_parent;
-    const uint32_t* in_lamport;
-    const uint16_t* in_agent;
+    const uint64_t* in_key;     // lamport << 16 | agent (one gather per run head)
     const uint32_t* in_cp;
     uint32_t* jbits;            // per slot bit: has a non-consecutive child in a later tile
     uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
@@ -116,8 +115,8 @@ struct L0Args {
     uint64_t sbytes_cap;
     uint2* tile_hw;             // per tile {heads, weight}: totals, then exclusive prefixes
     uint2* tile_sums;           // per 4096 tiles: scan carries
-    uint64_t* hbits;            // per 64 slots: run-head bits
-    uint16_t* hloc;             // per 64 slots: heads before the word inside its tile
+    uint4* hrec;                // per 64 slots: run-head bits (x, y) and the heads before the
+                                //   word inside its tile (z): a rank lookup is one 16-byte load
     uint32_t* r_head;           // per run: head slot
     uint32_t* r_pstart;         // per run: weight prefix at its head; [R] = the wave's weight
     uint32_t* r_parent;         // per run: parent run (kNil for a document start)
@@ -247,8 +246,8 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 // k_heads: one thread per 64-slot word of the rank bitvector (a word is inside one document),
 // one wave per tile.  head(g) = document start, or an item that does not continue the run of
 // the slot before it: continue(g) = seq(g) && !jump(g-1).  Besides the words: the heads before
-// each word inside its tile (hloc), so that the run of any slot s is
-// tile_hw[s / 4096].x + hloc[s / 64] + popcount(hbits[s / 64] up to s) - 1 once the tile
+// each word inside its tile (hrec .z), so that the run of any slot s is
+// tile_hw[s / 4096].x + hrec[s / 64].z + popcount(bits of hrec[s / 64] up to s) - 1 once the tile
 // prefixes are scanned.
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
@@ -269,11 +268,10 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
             hw = root | (item & ~(seq & ~prevj));
         }
-        a.hbits[wi] = hw;
     }
     const uint32_t c = (uint32_t)__popcll(hw);
     const uint32_t inc = wave_incl_scan(c);
-    if (gs < a.nslots) a.hloc[wi] = (uint16_t)(inc - c);
+    if (gs < a.nslots) a.hrec[wi] = make_uint4((uint32_t)hw, (uint32_t)(hw >> 32), inc - c, 0u);
     const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     const uint32_t tile = wi >> 6;  // 64 words per tile: one wave
     if ((threadIdx.x & 63u) == 0 && tile < a.ntiles) a.tile_hw[tile].x = th;
@@ -364,7 +362,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
     if (gs < a.nslots) {
-        hm = (uint32_t)(a.hbits[gs >> 6] >> (gs & 63u)) & 0xFFFFu;
+        const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
+        hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
         nib = a.wnib[gs >> 4];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         lseq[threadIdx.x] = a.seqb[gs >> 4];
@@ -443,8 +442,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const uint2 dc = ldoc[li >> 4];
         const bool sq = (lseq[li >> 4] >> (li & 15u)) & 1u;
         const bool root = g == dc.x;
-        const uint32_t lam = a.in_lamport[g];
-        const uint32_t ag = a.in_agent[g];
+        const uint64_t key = a.in_key[g];
         uint32_t p = (!sq && !root) ? a.in_parent[g] : 0u;
         a.r_head[rho] = g;
         a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
@@ -454,8 +452,9 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         } else if (!root) {
             if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
             const uint32_t ps = dc.x + p;
-            const uint64_t hb = a.hbits[ps >> 6];
-            const uint32_t hl = a.hloc[ps >> 6];
+            const uint4 hr = a.hrec[ps >> 6];
+            const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
+            const uint32_t hl = hr.z;
             const uint32_t tp = a.tile_hw[ps / kScanTile].x;
             const uint32_t b = ps & 63u;
             const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
@@ -463,7 +462,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         }
         if (rho < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
             a.r_parent[rho] = pr;
-            a.r_key[rho] = root ? 0ull : (((uint64_t)lam << 16) | ag);
+            a.r_key[rho] = root ? 0ull : key;
         }
     }
 }
@@ -1163,8 +1162,8 @@ __device__ __forceinline__ uint64_t doc_key(const DocArgs& a, uint32_t base, uin
 // at or before y.  Returns false (nothing written) when the document does not fit.
 constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
 __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t base, uint32_t R,
-                                         const uint32_t (&ro)[kDocJ], uint8_t* st,
-                                         uint32_t* scan_lds, uint64_t* tprobe) {
+                                         const uint32_t (&ro)[kDocJ], const uint32_t (&ps)[kDocJ],
+                                         uint8_t* st, uint32_t* scan_lds, uint64_t* tprobe) {
     const uint32_t t = threadIdx.x;
     const uint32_t tl = a.tlen[d], p0 = a.doc_p0[d];
     const uint32_t sh = p0 & 15u;
@@ -1181,17 +1180,15 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
     uint32_t* bits = reinterpret_cast<uint32_t*>(st + o_bits);
     uint16_t* pref = reinterpret_cast<uint16_t*>(st + o_pref);
     uint32_t* delta = reinterpret_cast<uint32_t*>(st + o_delta);
-    // 1) staging (every load first; clamped indices keep the arrays in registers)
+    // 1) staging (every load first; the run prefixes ps were loaded before the offsets)
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.sbytes + (p0 - sh));
         uint4 q[kDocQ];
 #pragma unroll
-        for (int k = 0; k < kDocQ; ++k)
-            q[k] = src[min(t + (uint32_t)k * kDocThreads, nq ? nq - 1u : 0u)];
-        uint32_t ps[kDocJ];
-#pragma unroll
-        for (int j = 0; j < kDocJ; ++j)
-            ps[j] = a.r_pstart[base + min(t + (uint32_t)j * kDocThreads, R - 1u)];
+        for (int k = 0; k < kDocQ; ++k) {
+            const uint32_t i = t + (uint32_t)k * kDocThreads;
+            q[k] = i < nq ? src[i] : make_uint4(0, 0, 0, 0);
+        }
         for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
         uint4* stq = reinterpret_cast<uint4*>(st);
 #pragma unroll
@@ -1630,7 +1627,9 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             // the next down arc: the first child, or for a leaf nx (kNil16 at the tour's end)
             const uint32_t go = !dn ? kNil16 : (f != kNil16 ? f : n);
             constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
-            const bool end = go == kNil16;
+            // (kNil16 is the tour's end; any other value >= R is an up link a parent cycle left
+            // unresolved: the walk ends there and the runs it misses are reported)
+            const bool end = go >= R;
             const bool split = !end && (go & mm) == splitter_off(go >> kDocLog2S);  // a splitter's
             const bool need = end || split;
             if (need) {
@@ -1663,6 +1662,14 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #endif
     __syncthreads();
     PROBE(7);
+    // the slot-order text prefixes of the owned runs, for phase C: loaded now, so that the
+    // pointer jumping and the offsets cover their latency
+    uint32_t ps[kDocJ];
+#pragma unroll
+    for (int j = 0; j < kDocJ; ++j) {
+        const uint32_t v = t + (uint32_t)j * kDocThreads;
+        ps[j] = (a.text && v < R) ? a.r_pstart[base + v] : 0u;
+    }
     // ---- pointer jumping: record = (sum from the splitter to the end of the tour) << 14 | next.
     // A record always describes a valid stretch of the tour (sum up to its next splitter, read
     // and written as one dword), so joining it with an old or a new record of its successor is
@@ -1728,8 +1735,8 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #else
         uint64_t* tprobe = nullptr;
 #endif
-        const bool fused = doc_text(a, d, base, R, ro, reinterpret_cast<uint8_t*>(dyn), scan_lds,
-                                    tprobe);
+        const bool fused = doc_text(a, d, base, R, ro, ps, reinterpret_cast<uint8_t*>(dyn),
+                                    scan_lds, tprobe);
         if (!fused) {
             // the text did not fit LDS: every run copies its bytes from the slot-order text to
             // its document offset (byte stores; only documents above the LDS stage take this)
@@ -1740,12 +1747,12 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             for (int j = 0; j < kDocJ; ++j) {
                 const uint32_t v = t + (uint32_t)j * kDocThreads;
                 if (ro[j] == kNil) continue;
-                const uint32_t ps = a.r_pstart[base + v], wv = a.r_pstart[base + v + 1] - ps;
+                const uint32_t wv = a.r_pstart[base + v + 1] - ps[j];
                 if ((uint64_t)ro[j] + wv > tl) {
                     oob = true;
                     continue;
                 }
-                for (uint32_t b = 0; b < wv; ++b) out[ro[j] + b] = a.sbytes[ps + b];
+                for (uint32_t b = 0; b < wv; ++b) out[ro[j] + b] = a.sbytes[ps[j] + b];
             }
             if (oob) atomicOr(&a.ctl[C_ERR], 8u);
             if (t == 0) atomicAdd(&a.ctl[C_UNFUSED], 1u);
@@ -2012,10 +2019,10 @@ __device__ __forceinline__ Perm replica_perm(uint32_t kind, uint32_t n, uint64_t
 // blockIdx.x x 256 threads over a document's items.  Replica r is a relabelled copy of base
 // r % nb: item k goes to slot perm(k) and its parent is relabelled the same way.
 __global__ __launch_bounds__(kBlock) void k_replicate(
-    const uint32_t* __restrict__ bp, const uint32_t* __restrict__ bl,
-    const uint16_t* __restrict__ ba, const uint32_t* __restrict__ bc,
+    const uint32_t* __restrict__ bp, const uint64_t* __restrict__ bk,
+    const uint32_t* __restrict__ bc,
     const uint64_t* __restrict__ bslot, const uint32_t* __restrict__ bn, uint32_t nb,
-    uint32_t* __restrict__ rp, uint32_t* __restrict__ rl, uint16_t* __restrict__ ra,
+    uint32_t* __restrict__ rp, uint64_t* __restrict__ rk,
     uint32_t* __restrict__ rc, const uint64_t* __restrict__ rslot, uint64_t ndocs,
     uint32_t kind, uint64_t seed) {
     for (uint64_t r = blockIdx.y; r < ndocs; r += gridDim.y) {
@@ -2027,8 +2034,7 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
         for (uint32_t k = blockIdx.x * kBlock + threadIdx.x + 1; k <= n; k += gridDim.x * kBlock) {
             const uint64_t o = dst + perm_apply(P, k);
             rp[o] = perm_apply(P, bp[src + k]);
-            rl[o] = bl[src + k];
-            ra[o] = ba[src + k];
+            rk[o] = bk[src + k];
             rc[o] = bc[src + k];
         }
     }
@@ -2038,8 +2044,7 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
 // counter-based hashes), so a device batch equals the host log of the same seed.  Slot 0 is the
 // document start; padding slots are deleted, parentless.
 __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ par,
-                                                        uint32_t* __restrict__ lam,
-                                                        uint16_t* __restrict__ ag,
+                                                        uint64_t* __restrict__ key,
                                                         uint32_t* __restrict__ cp, uint32_t n,
                                                         uint64_t nslots, uint32_t p_chain_pct,
                                                         uint32_t del_pct, uint64_t seed) {
@@ -2060,8 +2065,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ pa
         a = (uint16_t)(i % 64);
     }
     par[g] = p;
-    lam[g] = l;
-    ag[g] = a;
+    key[g] = ((uint64_t)l << 16) | a;
     cp[g] = c | (d ? kDelBit : 0u);
 }
 
@@ -2077,7 +2081,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 // host side
 // =============================================================================================
 void DeviceLogs::release() {
-    dfree(parent); dfree(lamport); dfree(agent); dfree(cp);
+    dfree(parent); dfree(key); dfree(cp);
     dfree(docs_rel); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
@@ -2085,7 +2089,7 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hloc_); dfree(stile_);
+    dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
@@ -2097,6 +2101,12 @@ Engine::~Engine() {
     if (host_out_) (void)hipHostFree(host_out_);
     for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : wev_) (void)hipEventDestroy(e);
+    if (ev_l0_) (void)hipEventDestroy(ev_l0_);
+    if (ev_l1_) (void)hipEventDestroy(ev_l1_);
+    if (stream_l1) {
+        (void)hipStreamSynchronize(stream_l1);
+        (void)hipStreamDestroy(stream_l1);
+    }
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -2119,8 +2129,17 @@ std::string Engine::init(int dev) {
     if (dev < 0 || dev >= n) return "device index out of range";
     device = dev;
     if ((e = hipSetDevice(dev)) != hipSuccess) return hipGetErrorString(e);
-    if ((e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess)
+    int prio_lo = 0, prio_hi = 0;  // (numerically: least >= greatest)
+    if ((e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess)
         return hipGetErrorString(e);
+    if ((e = hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_hi)) != hipSuccess)
+        return hipGetErrorString(e);
+    if ((e = hipStreamCreateWithPriority(&stream_l1, hipStreamNonBlocking, prio_lo)) != hipSuccess)
+        return hipGetErrorString(e);
+    if ((e = hipEventCreateWithFlags(&ev_l0_, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ev_l1_, hipEventDisableTiming)) != hipSuccess)
+        return hipGetErrorString(e);
+    cur_ = stream;
     ev_.resize(2 * S_N + 4);
     for (hipEvent_t& x : ev_)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hipGetErrorString(e);
@@ -2180,10 +2199,9 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     }
     const uint64_t nchunks = slot / M;
     if (slot > L.cap_slots) {
-        dfree(L.parent); dfree(L.lamport); dfree(L.agent); dfree(L.cp);
+        dfree(L.parent); dfree(L.key); dfree(L.cp);
         HIPCHK(dalloc(&L.parent, slot), "hipMalloc logs.parent");
-        HIPCHK(dalloc(&L.lamport, slot), "hipMalloc logs.lamport");
-        HIPCHK(dalloc(&L.agent, slot), "hipMalloc logs.agent");
+        HIPCHK(dalloc(&L.key, slot), "hipMalloc logs.key");
         HIPCHK(dalloc(&L.cp, slot), "hipMalloc logs.cp");
         L.cap_slots = slot;
         gen_++;
@@ -2259,21 +2277,20 @@ int Engine::upload_tables(DeviceLogs& L) {
 
 int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) {
     const uint64_t S = L.total_slots;
-    std::vector<uint32_t> par(S, 0), lam(S, 0), c(S, kDelBit);
-    std::vector<uint16_t> ag(S, 0);
+    std::vector<uint32_t> par(S, 0), c(S, kDelBit);
+    std::vector<uint64_t> key(S, 0);
     for (uint32_t d = 0; d < n; ++d) {
         const crdt_hip_oplog_view& v = views[d];
         const uint64_t b = L.doc_slot[d] + 1;
         if (v.n == 0) continue;
         std::memcpy(&par[b], v.parent, v.n * 4ull);
-        std::memcpy(&lam[b], v.lamport, v.n * 4ull);
-        std::memcpy(&ag[b], v.agent, v.n * 2ull);
-        for (uint32_t i = 0; i < v.n; ++i)
+        for (uint32_t i = 0; i < v.n; ++i) {
+            key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
             c[b + i] = (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u);
+        }
     }
     HIPCHK(hipMemcpy(L.parent, par.data(), S * 4, hipMemcpyHostToDevice), "upload parent");
-    HIPCHK(hipMemcpy(L.lamport, lam.data(), S * 4, hipMemcpyHostToDevice), "upload lamport");
-    HIPCHK(hipMemcpy(L.agent, ag.data(), S * 2, hipMemcpyHostToDevice), "upload agent");
+    HIPCHK(hipMemcpy(L.key, key.data(), S * 8, hipMemcpyHostToDevice), "upload key");
     HIPCHK(hipMemcpy(L.cp, c.data(), S * 4, hipMemcpyHostToDevice), "upload cp");
     return CRDT_HIP_OK;
 }
@@ -2281,15 +2298,14 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hbits_); dfree(hloc_); dfree(stile_);
+        dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
         HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
         HIPCHK(dalloc(&seqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
-        HIPCHK(dalloc(&hbits_, slots / 64 + 2), "hipMalloc hbits");
-        HIPCHK(dalloc(&hloc_, slots / 64 + 2), "hipMalloc hloc");
+        HIPCHK(dalloc(&hrec_, slots / 64 + 2), "hipMalloc head records");
         HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
         HIPCHK(dalloc(&tile_hw_, tiles), "hipMalloc tile totals");
         HIPCHK(dalloc(&tile_sums_, tiles / kScanTile + 2), "hipMalloc tile sums");
@@ -2429,7 +2445,7 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
 int Engine::clock_mark(StageClock& c, int stage) {
     if (!c.ev || c.n >= kClockEvents) return CRDT_HIP_OK;  // untimed (a captured graph)
     if (c.n) c.stage[c.n - 1] = (uint8_t)stage;
-    HIPCHK(hipEventRecord(c.ev[c.n], stream), "event record");
+    HIPCHK(hipEventRecord(c.ev[c.n], cur_), "event record");
     ++c.n;
     return CRDT_HIP_OK;
 }
@@ -2449,8 +2465,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);              \
     a0.docs = L.docs_rel + w.first_doc;                             \
     a0.in_parent = L.parent + w.slot0;                              \
-    a0.in_lamport = L.lamport + w.slot0;                            \
-    a0.in_agent = L.agent + w.slot0;                                \
+    a0.in_key = L.key + w.slot0;                                    \
     a0.in_cp = L.cp + w.slot0;                                      \
     a0.jbits = jbits_;                                              \
     a0.jloc = jloc_;                                                \
@@ -2461,8 +2476,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.sbytes_cap = cap_sbytes_ - 64;                               \
     a0.tile_hw = tile_hw_;                                          \
     a0.tile_sums = tile_sums_;                                      \
-    a0.hbits = hbits_;                                              \
-    a0.hloc = hloc_;                                                \
+    a0.hrec = hrec_;                                                \
     a0.doc_root = doc_root_;                                        \
     a0.doc_p0 = doc_p0_;                                            \
     a0.ctl = ctl_;                                                  \
@@ -2494,7 +2508,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
 
 int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs,
                           uint32_t cap_rmax, StageClock& ck) {
-    hipStream_t s = stream;
+    hipStream_t s = cur_;
     L0ARGS(a0);
     a0.cap_runs = cap_runs;
     a0.cap_rmax = cap_rmax;
@@ -2519,7 +2533,7 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
 // k_runs alone (run_wave: the run rows did not fit the rows allocated when level 0 ran).
 int Engine::launch_runs(DeviceLogs& L, const Wave& w, bool ord) {
     L0ARGS(a0);
-    k_runs<<<a0.ntiles, kBlock, 0, stream>>>(a0);
+    k_runs<<<a0.ntiles, kBlock, 0, cur_>>>(a0);
     HIPCHK(hipGetLastError(), "k_runs launch");
     return CRDT_HIP_OK;
 }
@@ -2527,7 +2541,7 @@ int Engine::launch_runs(DeviceLogs& L, const Wave& w, bool ord) {
 // k_doctotals, k_doctree (k_expand for documents whose text did not fit runs in the tail).
 int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
                               StageClock& ck) {
-    hipStream_t s = stream;
+    hipStream_t s = cur_;
     TREEARGS(a);
     DocArgs da{};
     da.ndocs = w.ndocs;
@@ -2559,7 +2573,7 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
 // sized by the exact run count (the caller waited for level 0).
 int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
                                  StageClock& ck, uint32_t& rounds) {
-    hipStream_t s = stream;
+    hipStream_t s = cur_;
     TREEARGS(a);
     const uint32_t R = p.R;
     // splitter stride: longer sublists once the pointer jumping over the splitter lists
@@ -2612,7 +2626,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
 // (ctl + a {bytes, codepoints, digest} record per document) into the pinned host image.
 int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, StageClock& ck,
                         uint32_t* hblock) {
-    hipStream_t s = stream;
+    hipStream_t s = cur_;
     L0ARGS(a0);
     TREEARGS(a);
     ExpandArgs ea{};
@@ -2859,6 +2873,7 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         m.eng[i]->log2m = log2m;
         m.eng[i]->log2m_set = log2m_set;
         m.eng[i]->level1_global = level1_global;
+        m.eng[i]->l1_split = l1_split;
         m.eng[i]->probe_doc_ = probe_doc_;
     }
     // every allocation before the first launch (a pool free waits for the device)
@@ -2902,6 +2917,8 @@ int Engine::merge_async_enqueue(DeviceLogs& L, AsyncMerge& m) {
     for (uint32_t i = 1; i < K; ++i)
         HIPCHK(hipStreamWaitEvent(m.eng[i]->stream, ev_[2 * S_N + 1], 0), "stream wait");
     hipEvent_t prev_l0 = nullptr;
+    const bool split = l1_split;
+    for (uint32_t i = 0; i < K; ++i) m.eng[i]->l1_pending_ = false;
     for (uint32_t wi = 0; wi < nw; ++wi) {
         Engine& E = *m.eng[wi % K];
         const Wave& w = L.waves[wi];
@@ -2909,18 +2926,38 @@ int Engine::merge_async_enqueue(DeviceLogs& L, AsyncMerge& m) {
         ck.ev = m.timed || K > 1 ? E.wev_.data() + (size_t)(wi / K) * kClockEvents : nullptr;
         if (l0_gated && prev_l0 && K > 1)
             HIPCHK(hipStreamWaitEvent(E.stream, prev_l0, 0), "stream wait");
+        // level 0 overwrites the lane's scratch: after the lane's previous level 1
+        if (E.l1_pending_) HIPCHK(hipStreamWaitEvent(E.stream, E.ev_l1_, 0), "stream wait");
+        E.cur_ = E.stream;
         int rc = E.launch_level0(L, w, false, m.plans[wi].R, m.plans[wi].rmax, ck);
         if (rc) return rc;
         prev_l0 = ck.ev ? ck.ev[ck.n - 1] : nullptr;  // the end of level 0
+        if (split) {
+            HIPCHK(hipEventRecord(E.ev_l0_, E.stream), "event record");
+            HIPCHK(hipStreamWaitEvent(E.stream_l1, E.ev_l0_, 0), "stream wait");
+            E.cur_ = E.stream_l1;
+        }
         rc = E.launch_lds_level1(L, w, false, m.plans[wi], ck);
-        if (rc) return rc;
-        rc = E.launch_tail(L, w, false, true, ck, E.host_block(L, wi));
+        if (!rc) rc = E.launch_tail(L, w, false, true, ck, E.host_block(L, wi));
+        if (split) {
+            E.cur_ = E.stream;
+            if (!rc) {
+                HIPCHK(hipEventRecord(E.ev_l1_, E.stream_l1), "event record");
+                E.l1_pending_ = true;
+            }
+        }
         if (rc) return rc;
     }
     // join: the merge's end event on this stream after every lane's last launch
-    for (uint32_t i = 1; i < K; ++i) {
-        hipEvent_t done = m.eng[i]->ev_[2 * S_N + 3];
-        HIPCHK(hipEventRecord(done, m.eng[i]->stream), "event record");
+    for (uint32_t i = 0; i < K; ++i) {
+        Engine& E = *m.eng[i];
+        if (E.l1_pending_) {
+            HIPCHK(hipStreamWaitEvent(E.stream, E.ev_l1_, 0), "stream wait");
+            E.l1_pending_ = false;
+        }
+        if (i == 0) continue;
+        hipEvent_t done = E.ev_[2 * S_N + 3];
+        HIPCHK(hipEventRecord(done, E.stream), "event record");
         HIPCHK(hipStreamWaitEvent(stream, done, 0), "stream wait");
     }
     if (m.timed) HIPCHK(hipEventRecord(ev_[2 * S_N + 2], stream), "event record");
@@ -3102,7 +3139,7 @@ int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t
     int rc = plan(R, docs);
     if (rc) return rc;
     k_synth_tree<<<grid_for(R.total_slots), kBlock, 0, stream>>>(
-        R.parent, R.lamport, R.agent, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
+        R.parent, R.key, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
     HIPCHK(hipGetLastError(), "synth launch");
     HIPCHK(hipStreamSynchronize(stream), "synth");
     return CRDT_HIP_OK;
@@ -3137,8 +3174,8 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
         // serialising every dispatch, slow at 16,384 replicas)
         const dim3 grid(std::min<uint32_t>(grid_for(nmax), 1024u),
                         (uint32_t)std::min<uint64_t>(total, 65535u));
-        k_replicate<<<grid, kBlock, 0, stream>>>(B.parent, B.lamport, B.agent, B.cp, dbslot, dbn,
-                                                 nb, R.parent, R.lamport, R.agent, R.cp, drslot,
+        k_replicate<<<grid, kBlock, 0, stream>>>(B.parent, B.key, B.cp, dbslot, dbn,
+                                                 nb, R.parent, R.key, R.cp, drslot,
                                                  total, relabel, seed);
         e = hipGetLastError();
     }

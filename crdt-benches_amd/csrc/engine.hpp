@@ -70,8 +70,7 @@ struct DeviceLogs {
     uint64_t items = 0;
     // device arrays (slot-indexed)
     uint32_t* parent = nullptr;
-    uint32_t* lamport = nullptr;
-    uint16_t* agent = nullptr;
+    uint64_t* key = nullptr;       // the item's id as a sibling key: lamport << 16 | agent
     uint32_t* cp = nullptr;        // codepoint (bits 0-20) | tombstone (bit 31, kDelBit)
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
@@ -89,7 +88,8 @@ public:
     std::string init(int device);
 
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;     // every launch of the engine (high priority)
+    hipStream_t stream_l1 = nullptr;  // level 1 + tail of enqueued waves (low priority: l1_split)
     uint32_t log2m = 4;                    // level-1 splitter stride M = 2^log2m
     bool log2m_set = false;                // set by the caller; else chosen per wave from R
     uint64_t max_wave_slots = 1ull << 30;
@@ -99,11 +99,15 @@ public:
     // of one wave then overlaps the HBM-bound level 0 of another.
     uint32_t lanes = 2;
     bool l0_gated = true;  // lanes take turns at level 0 (see run_wave)
+    // Enqueued waves (merge_async) run level 1 and the tail on stream_l1, created with the lowest
+    // stream priority, so that when one wave's latency-bound level 1 and the next wave's HBM-bound
+    // level 0 compete for the CUs, the dispatcher favours level 0 (the chain that bounds a merge).
+    bool l1_split = true;
     // Merges of logs merged before enqueue every wave with its learnt plan and wait once at the
     // end (merge_async) instead of after each wave's level 0.
     bool plan_cache = true;
-    bool plan_shrink = false;
-    bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
+    bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
+    bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -152,12 +156,17 @@ public:
                   uint64_t seed);
 
 private:
+    // the stream the launch functions and the stage clock use (stream, or stream_l1 while an
+    // enqueued wave's level 1 and tail are launched); events ordering the two streams
+    hipStream_t cur_ = nullptr;
+    hipEvent_t ev_l0_ = nullptr, ev_l1_ = nullptr;
+    bool l1_pending_ = false;  // ev_l1_ marks this merge's last level 1 on stream_l1
     // level-0 scratch (per slot / per tile), grown on demand
     uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
     uint32_t *jbits_ = nullptr, *jloc_ = nullptr;
     uint16_t* seqb_ = nullptr;
-    uint64_t *hbits_ = nullptr, *wnib_ = nullptr;
-    uint16_t* hloc_ = nullptr;
+    uint64_t* wnib_ = nullptr;
+    uint4* hrec_ = nullptr;
     uint8_t *stile_ = nullptr, *sbytes_ = nullptr;
     uint2 *tile_hw_ = nullptr, *tile_sums_ = nullptr;
     uint64_t cap_sbytes_ = 0;

@@ -103,9 +103,8 @@ struct UpdArgs {
     uint64_t* ctl;
     // replica slot arrays (slot = id)
     uint32_t* parent;
-    uint32_t* lamport;
-    uint16_t* agent;
-    uint32_t* cp;  // codepoint | kDelBit
+    uint64_t* key;  // lamport << 16 | agent
+    uint32_t* cp;   // codepoint | kDelBit
     uint64_t cap_slots;
     uint32_t* imap;  // per flattened item / delete: its update (found by the check pass, reused
     uint32_t* dmap;  //   by the write pass instead of a second binary search)
@@ -244,9 +243,9 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
                 }
                 const uint32_t c = a.buf[h.w + 3u * h.y + k];
                 a.parent[id] = par;
-                a.lamport[id] = a.buf[h.w + 2u * h.y + k];
+                a.key[id] = ((uint64_t)a.buf[h.w + 2u * h.y + k] << 16) |
+                            reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
                 a.cp[id] = c & kCpMaskR;  // live
-                a.agent[id] = reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
                 add_cp += 1u;
                 add_b += utf8_len(c & kCpMaskR);
             }
@@ -300,29 +299,24 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
 
 // padding / unused slots: a tombstoned child of the document start with key 0 (never visible,
 // pruned by the merge)
-__global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint32_t* lamport,
-                                                 uint16_t* agent, uint32_t* cp,
+__global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint64_t* key, uint32_t* cp,
                                                  uint64_t s0, uint64_t s1) {
     const uint64_t g = s0 + (uint64_t)blockIdx.x * kUB + threadIdx.x;
     if (g >= s1) return;
     parent[g] = 0;
-    lamport[g] = 0;
-    agent[g] = 0;
+    key[g] = 0;
     cp[g] = kDelBit;
 }
 
-// Replica clone: the four slot arrays in one launch (main.rs:64).
+// Replica clone: the three slot arrays in one launch (main.rs:64).
 __global__ __launch_bounds__(kUB) void k_rep_copy(const uint32_t* __restrict__ sp,
-                                                  const uint32_t* __restrict__ sl,
-                                                  const uint16_t* __restrict__ sa,
+                                                  const uint64_t* __restrict__ sk,
                                                   const uint32_t* __restrict__ sc,
-                                                  uint32_t* __restrict__ dp, uint32_t* __restrict__ dl,
-                                                  uint16_t* __restrict__ da, uint32_t* __restrict__ dc,
-                                                  uint64_t n) {
+                                                  uint32_t* __restrict__ dp, uint64_t* __restrict__ dk,
+                                                  uint32_t* __restrict__ dc, uint64_t n) {
     for (uint64_t g = (uint64_t)blockIdx.x * kUB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * kUB) {
         dp[g] = sp[g];
-        dl[g] = sl[g];
-        da[g] = sa[g];
+        dk[g] = sk[g];
         dc[g] = sc[g];
     }
 }
@@ -387,36 +381,32 @@ int replica_reserve(Engine& E, Replica& r, uint64_t items) {
     if (need <= L.cap_slots) return CRDT_HIP_OK;
     const uint64_t cap = std::min<uint64_t>((1ull << 31) - 64,
                                             std::max<uint64_t>({need, 2 * L.cap_slots, 4096}));
-    uint32_t *par = nullptr, *lam = nullptr, *c = nullptr;
-    uint16_t* ag = nullptr;
+    uint32_t *par = nullptr, *c = nullptr;
+    uint64_t* key = nullptr;
     hipError_t e = dalloc(&par, cap);
-    if (e == hipSuccess) e = dalloc(&lam, cap);
-    if (e == hipSuccess) e = dalloc(&ag, cap);
+    if (e == hipSuccess) e = dalloc(&key, cap);
     if (e == hipSuccess) e = dalloc(&c, cap);
     const uint64_t old = L.cap_slots;
     hipStream_t s = E.stream;
     if (e == hipSuccess && old) {
         e = hipMemcpyAsync(par, L.parent, old * 4, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(lam, L.lamport, old * 4, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(ag, L.agent, old * 2, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(key, L.key, old * 8, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(c, L.cp, old * 4, hipMemcpyDeviceToDevice, s);
     }
     if (e == hipSuccess) {
-        k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, lam, ag, c, old, cap);
+        k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, key, c, old, cap);
         e = hipGetLastError();
     }
     if (e != hipSuccess) {
         (void)hipStreamSynchronize(s);
-        dfree(par); dfree(lam); dfree(ag); dfree(c);
+        dfree(par); dfree(key); dfree(c);
         return hip_fail(E, "replica reserve", e);
     }
     // the old arrays may still be read by queued work: freed at the replica's next wait
-    for (void* p : {(void*)L.parent, (void*)L.lamport, (void*)L.agent, (void*)L.cp})
+    for (void* p : {(void*)L.parent, (void*)L.key, (void*)L.cp})
         if (p) r.graveyard.push_back(p);
-    L.parent = nullptr; L.lamport = nullptr; L.agent = nullptr; L.cp = nullptr;
     L.parent = par;
-    L.lamport = lam;
-    L.agent = ag;
+    L.key = key;
     L.cp = c;
     L.cap_slots = cap;
     r.gen++;
@@ -437,18 +427,19 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     // null-stream copy does not wait for a non-blocking stream and could be overwritten by it)
     hipStream_t s = E.stream;
     RCHK(hipMemcpyAsync(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice, s), "upload parent");
-    RCHK(hipMemcpyAsync(L.lamport + 1, v->lamport, n * 4ull, hipMemcpyHostToDevice, s), "upload lamport");
-    RCHK(hipMemcpyAsync(L.agent + 1, v->agent, n * 2ull, hipMemcpyHostToDevice, s), "upload agent");
     std::vector<uint32_t> c(n);
+    std::vector<uint64_t> key(n);
     for (uint32_t i = 0; i < n; ++i) {
+        key[i] = ((uint64_t)v->lamport[i] << 16) | v->agent[i];
         c[i] = (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u);
         if (!v->deleted[i]) {
             r.vis_cp += 1;
             r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
         }
     }
+    RCHK(hipMemcpyAsync(L.key + 1, key.data(), n * 8ull, hipMemcpyHostToDevice, s), "upload key");
     RCHK(hipMemcpyAsync(L.cp + 1, c.data(), n * 4ull, hipMemcpyHostToDevice, s), "upload cp");
-    RCHK(hipStreamSynchronize(s), "upload sync");  // (c and the caller's view are released)
+    RCHK(hipStreamSynchronize(s), "upload sync");  // (key, c and the caller's view are released)
     return CRDT_HIP_OK;
 }
 
@@ -467,7 +458,7 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst) {
     if (cap) {
         // (no wait: every later use of the copy, decode and merge, is on the same stream)
         k_rep_copy<<<(uint32_t)std::min<uint64_t>(grid_for(cap, kUB), 4096), kUB, 0, s>>>(
-            S.parent, S.lamport, S.agent, S.cp, D.parent, D.lamport, D.agent, D.cp, cap);
+            S.parent, S.key, S.cp, D.parent, D.key, D.cp, cap);
         RCHK(hipGetLastError(), "replica copy");
     }
     dst.n = src.n;
@@ -621,8 +612,7 @@ int decode_launch(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     a.known0 = r.n;
     a.ctl = r.uctl;
     a.parent = L.parent;
-    a.lamport = L.lamport;
-    a.agent = L.agent;
+    a.key = L.key;
     a.cp = L.cp;
     a.cap_slots = L.cap_slots;
     a.imap = r.imap;
@@ -742,7 +732,7 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
                     const DeviceLogs& S = init.logs;
                     DeviceLogs& D = w.logs;
                     k_rep_copy<<<(uint32_t)std::min<uint64_t>(grid_for(cap, kUB), 4096), kUB, 0, s>>>(
-                        S.parent, S.lamport, S.agent, S.cp, D.parent, D.lamport, D.agent, D.cp, cap);
+                        S.parent, S.key, S.cp, D.parent, D.key, D.cp, cap);
                 }
                 if (!rc) rc = decode_launch(E, w, ub.buf, ub.len, ub.off, ub.n, true, false);
                 if (!rc) {

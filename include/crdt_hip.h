@@ -119,7 +119,9 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * merge run concurrently on that many streams, each with its own scratch (1 = one after the
  * other), "lane_gate" (default 1: lanes take turns at the HBM-bound level 0), "plan_cache"
  * (default 1: a merge of logs merged before enqueues every wave with the launch plan the earlier
- * merge learnt, checked on the device, and waits once instead of after each wave's level 0).
+ * merge learnt, checked on the device, and waits once instead of after each wave's level 0),
+ * "l1_split" (default 1: such enqueued waves run level 1 on a low-priority stream of their lane,
+ * so that the next wave's level 0 is favoured when the two compete for the CUs).
  * Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 

@@ -321,6 +321,13 @@ def test_malformed_logs_are_rejected(ctx):
     with pytest.raises(crdt_hip.CrdtHipError) as e:
         ctx.merge(cycle)
     assert e.value.code == -5
+    # two runs that are each other's parent (neither reachable from the document start): their
+    # up links never resolve, so the LDS path's pointer jumping has to give up, not spin
+    cycle2 = crdt_hip.LogArrays([0, 4, 1, 2], [1, 2, 3, 4], [0, 0, 0, 0], [0, 0, 0, 0],
+                                [97, 98, 99, 100])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        ctx.merge(cycle2)
+    assert e.value.code == -5
     ok = crdt_hip.LogArrays([0, 1], [1, 2], [0, 0], [0, 0], [97, 98])
     assert ctx.merge(ok)[0] == b"ab"  # the engine recovers after an error
 
