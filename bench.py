@@ -569,9 +569,11 @@ def side_workload(args) -> int:
     elif args.workload == "agents64":
         n = args.items or 10_000_000
         lg = crdt_hip.OpLog.synth_agents(n, 64, 0x5EED0001).arrays()
-        # expected length = the log's visible items (each item is one 1-byte codepoint here);
+        # expected length = the UTF-8 bytes of the log's visible items (counted without merging);
         # the digest itself is checked against the oracle by tests/test_gpu_scale.py
-        expect = (None, int(np.count_nonzero(lg.deleted == 0)))
+        cp = lg.cp[lg.deleted == 0].astype(np.uint64)
+        expect = (None, int(cp.size + np.count_nonzero(cp >= 0x80) + np.count_nonzero(cp >= 0x800)
+                            + np.count_nonzero(cp >= 0x10000)))
         batch = ctx.batch([lg], replicas=1, relabel="none")
         desc = f"config 4: 64-agent concurrent log, {n} items, seed 0x5EED0001"
     else:
