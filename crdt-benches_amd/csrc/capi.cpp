@@ -167,6 +167,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.max_wave_slots = value;
         return 0;
     }
+    if (k == "tail_wave_div") {
+        if (value > 64) return set_err(ctx, CRDT_HIP_EINVAL, "tail_wave_div must be in [0, 64]");
+        ctx->eng.tail_wave_div = (uint32_t)value;
+        return 0;
+    }
     if (k == "lanes") {
         if (value < 1 || value > 8) return set_err(ctx, CRDT_HIP_EINVAL, "lanes must be in [1, 8]");
         ctx->eng.lanes = (uint32_t)value;

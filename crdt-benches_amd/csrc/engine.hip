@@ -2159,6 +2159,21 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     L.items = 0;
     uint64_t slot = 0;
     const uint64_t hard_max = (1ull << 31) - M;
+    // The last wave's level 1 overlaps nothing, so a merge of several waves ends with a small
+    // one: the trailing documents that fit max_wave_slots / tail_wave_div go to a wave of their
+    // own (from `tail0` on) when the whole merge needs more than one wave.
+    uint64_t total = 0;
+    for (const DocInfo& di : docs) total += (di.n + 1 + M - 1) / M * M;
+    uint32_t tail0 = (uint32_t)docs.size();
+    if (tail_wave_div && total > max_wave_slots) {
+        uint64_t sfx = 0;
+        while (tail0 > 1) {
+            const uint64_t ds = (docs[tail0 - 1].n + 1 + M - 1) / M * M;
+            if (sfx + ds > max_wave_slots / tail_wave_div && sfx) break;
+            sfx += ds;
+            --tail0;
+        }
+    }
     for (uint32_t d = 0; d < docs.size(); ++d) {
         const uint64_t ds = (docs[d].n + 1 + M - 1) / M * M;
         if (ds > hard_max) { err = "document too large for one wave"; return CRDT_HIP_ERANGE; }
@@ -2168,7 +2183,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         }
         const uint64_t dt = (docs[d].text_cap + 15) & ~15ull;
         if (L.waves.empty() || (uint64_t)L.waves.back().nslots + ds > max_wave_slots ||
-            L.waves.back().text_cap + dt > kMaxWaveText) {
+            L.waves.back().text_cap + dt > kMaxWaveText || d == tail0) {
             Wave w{};
             w.first_doc = d;
             w.slot0 = slot;

@@ -93,6 +93,7 @@ public:
     uint32_t log2m = 4;                    // level-1 splitter stride M = 2^log2m
     bool log2m_set = false;                // set by the caller; else chosen per wave from R
     uint64_t max_wave_slots = 1ull << 30;
+    uint32_t tail_wave_div = 4;            // last wave of a multi-wave merge <= max / div (0: off)
     bool level1_global = false;            // never use the per-document LDS level 1
     // Waves merged at once by a multi-wave merge, each on a lane of its own: a helper engine
     // (non-blocking stream + scratch) driven by its own host thread.  The latency-bound level 1

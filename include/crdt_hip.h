@@ -121,7 +121,9 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * (default 1: a merge of logs merged before enqueues every wave with the launch plan the earlier
  * merge learnt, checked on the device, and waits once instead of after each wave's level 0),
  * "l1_split" (default 1: such enqueued waves run level 1 on a low-priority stream of their lane,
- * so that the next wave's level 0 is favoured when the two compete for the CUs).
+ * so that the next wave's level 0 is favoured when the two compete for the CUs), "tail_wave_div"
+ * (default 4: a merge of several waves ends with a wave of at most max_wave_slots / 4 slots,
+ * whose level 1 is the only part of the merge that overlaps nothing; 0 = plain greedy waves).
  * Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 

@@ -393,6 +393,38 @@ def test_learnt_plan_merges_match_synchronous_ones(golden, lanes):
     assert out[0] == out[1]
 
 
+@pytest.mark.parametrize("l1_split,tail_div", [(0, 0), (1, 0), (1, 4), (1, 2)])
+def test_scheduling_knobs_do_not_change_results(golden, l1_split, tail_div):
+    """Level 1 on the lane's low-priority stream (l1_split) and the small trailing wave
+    (tail_wave_div) only reorder work: digests, lengths and runs stay those of the traces, in the
+    first (synchronous) merge and in the learnt-plan merges after it."""
+    bases = [resolved(n) for n in TRACES]
+    c = crdt_hip.Context(0)
+    c.set_param("lanes", 2)
+    c.set_param("l1_split", l1_split)
+    c.set_param("tail_wave_div", tail_div)
+    c.set_param("max_wave_slots", 1 << 20)
+    b = c.batch(bases, replicas=3, relabel="rotate", seed=5)
+    runs = set()
+    for _ in range(3):
+        dig, lens, st = b.merge()
+        runs.add(st["runs"])
+        for r in range(b.docs):
+            name = TRACES[r % 4]
+            assert "%016x" % dig[r] == golden[name]["tree_digest"], r
+            assert lens[r] == golden[name]["end_bytes"], r
+    assert len(runs) == 1
+    waves = st["waves"]
+    b.close()
+    c.set_param("tail_wave_div", 0)
+    b = c.batch(bases, replicas=3, relabel="rotate", seed=5)
+    greedy = b.merge()[2]["waves"]
+    b.close()
+    c.close()
+    # a separate trailing wave (its documents would otherwise have filled the last greedy wave)
+    assert waves == greedy or (tail_div and waves == greedy + 1)
+
+
 def test_plan_that_no_longer_fits_is_redone():
     """The device checks the enqueued plan (k_docmax flags C_REPLAN when the wave has more runs
     than planned) and the host merges such a wave again: forced here with a plan of half size."""
