@@ -334,9 +334,12 @@ int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out) {
         crdt_hip_oplog* L = new crdt_hip_oplog();
         const crdt::Trace& T = t->t;
         std::string e;
-        size_t ins_bytes = T.start_content.size();
-        for (const crdt::Patch& p : T.patches) ins_bytes += p.ins_len;
-        L->log.reserve(ins_bytes);  // >= items (one per codepoint)
+        size_t ins_bytes = T.start_content.size(), dels = 0;
+        for (const crdt::Patch& p : T.patches) {
+            ins_bytes += p.ins_len;
+            dels += p.del;
+        }
+        L->log.reserve(ins_bytes, dels);  // >= items (one per codepoint), = delete ops
         // from_str(start_content), then replace() every patch (main.rs:29-33, rope.rs:21-32)
         if (!T.start_content.empty())
             e = L->log.insert_utf8(0, T.start_content.data(), T.start_content.size());

@@ -1,6 +1,8 @@
 // oplog.cpp — order-statistic resolver over a chunked span sequence (runs of consecutive ids,
 // chunks of <= 64 spans + a Fenwick tree of per-chunk visible counts): O(log C + 64) per
 // positional lookup, O(1) amortised appends while typing on (the span of the last item grows).
+// A chunk hint and a span hint make the lookup of an edit next to the previous one O(1); the
+// Fenwick tree is rebuilt only when a lookup misses the hints after chunks were split.
 #include "oplog.hpp"
 
 #include <algorithm>
@@ -28,7 +30,8 @@ OpLog::OpLog() {
     fen_build();
 }
 
-void OpLog::reserve(size_t items) {
+void OpLog::reserve(size_t items, size_t dels) {
+    del_ops.reserve(dels);
     parent.reserve(items);
     oright.reserve(items);
     lamport.reserve(items);
@@ -43,7 +46,8 @@ OpLog::Chunk OpLog::new_chunk() const {
     return c;
 }
 
-void OpLog::fen_build() {
+void OpLog::fen_build() const {
+    fen_dirty_ = false;
     fen_.assign(chunks_.size() + 1, 0);
     for (size_t i = 0; i < chunks_.size(); ++i) {
         size_t j = i + 1;
@@ -54,10 +58,12 @@ void OpLog::fen_build() {
 }
 
 void OpLog::fen_add(size_t i, int64_t d) {
+    if (fen_dirty_) return;  // (the rebuild counts the chunks as they are then)
     for (size_t j = i + 1; j < fen_.size(); j += j & (~j + 1)) fen_[j] += d;
 }
 
 size_t OpLog::fen_find(uint64_t& p) const {
+    if (fen_dirty_) fen_build();
     size_t pos = 0;
     size_t step = 1;
     while (step * 2 < fen_.size()) step *= 2;
@@ -82,16 +88,25 @@ bool OpLog::find_visible(uint64_t p, size_t& c, size_t& si, uint32_t& off) const
         if (c >= chunks_.size()) return false;
         hint_c_ = c;
         hint_base_ = p - r;
+        hint_si_ = SIZE_MAX;
     }
     const std::vector<Span>& v = chunks_[c].s;
-    for (si = 0; si < v.size(); ++si) {
+    si = 0;
+    uint64_t vb = 0;  // visible items of the chunk before span si
+    if (hint_si_ < v.size() && r > hint_vb_) {
+        si = hint_si_;
+        vb = hint_vb_;
+    }
+    for (; si < v.size(); ++si) {
         if (v[si].del()) continue;
-        uint32_t len = v[si].len();
-        if (r <= len) {
-            off = (uint32_t)r - 1;
+        const uint32_t len = v[si].len();
+        if (r - vb <= len) {
+            off = (uint32_t)(r - vb) - 1;
+            hint_si_ = si;
+            hint_vb_ = vb;
             return true;
         }
-        r -= len;
+        vb += len;
     }
     return false;
 }
@@ -113,7 +128,9 @@ bool OpLog::split_chunk(size_t c) {
         if (!x.del()) hi.vis += x.len();
     chunks_[c].vis -= hi.vis;
     chunks_.insert(chunks_.begin() + c + 1, std::move(hi));
-    fen_build();
+    fen_dirty_ = true;
+    if (hint_c_ == c && hint_si_ >= half) hint_si_ = SIZE_MAX;  // the span moved to chunk c + 1
+    if (hint_c_ != SIZE_MAX && hint_c_ > c) hint_c_++;         // (its visible base is unchanged)
     return true;
 }
 
@@ -133,6 +150,7 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
         right = first_id_from(0, 0);
         hint_c_ = 0;  // chunk 0 changes: keep the hint on it
         hint_base_ = 0;
+        hint_si_ = SIZE_MAX;
     } else {
         size_t si;
         uint32_t off;
@@ -150,14 +168,32 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
         }
         at = si + 1;
     }
-    for (size_t j = 0; j < k; ++j) {
-        uint32_t id = first + (uint32_t)j;
-        parent.push_back(j == 0 ? left : id - 1);
+    if (k == 1) {  // typing: one item
+        parent.push_back(left);
         oright.push_back(right);
         lamport.push_back(++max_lamport);
         agent.push_back(local_agent);
         deleted.push_back(0);
-        cp.push_back(cps[j]);
+        cp.push_back(cps[0]);
+    } else {  // a paste: every column grown once, then filled
+        const size_t n0 = parent.size();
+        parent.resize(n0 + k);
+        oright.resize(n0 + k);
+        lamport.resize(n0 + k);
+        agent.resize(n0 + k, local_agent);
+        deleted.resize(n0 + k, 0);
+        cp.resize(n0 + k);
+        uint32_t* P = parent.data() + n0;
+        uint32_t* O = oright.data() + n0;
+        uint32_t* L = lamport.data() + n0;
+        P[0] = left;
+        for (size_t j = 1; j < k; ++j) P[j] = first + (uint32_t)j - 1;
+        for (size_t j = 0; j < k; ++j) {
+            O[j] = right;
+            L[j] = max_lamport + 1 + (uint32_t)j;
+        }
+        max_lamport += (uint32_t)k;
+        std::memcpy(cp.data() + n0, cps, k * sizeof(uint32_t));
     }
     std::vector<Span>& v = chunks_[c].s;
     if (extend)
@@ -183,9 +219,14 @@ size_t OpLog::delete_in_span(Chunk& ch, size_t si, uint32_t off, uint32_t take) 
     std::vector<Span>& v = ch.s;
     const Span S = v[si];
     const uint32_t len = S.len(), did = S.id + off, dend = did + take;
-    for (uint32_t id = did; id < dend; ++id) {
-        deleted[id - 1] = 1;
-        del_ops.push_back(id);
+    if (take == 1) {  // backspace
+        deleted[did - 1] = 1;
+        del_ops.push_back(did);
+    } else {
+        std::memset(deleted.data() + did - 1, 1, take);
+        const size_t m0 = del_ops.size();
+        del_ops.resize(m0 + take);
+        for (uint32_t j = 0; j < take; ++j) del_ops[m0 + j] = did + j;
     }
     Span rep[3];
     int nr = 0;
@@ -289,6 +330,7 @@ std::string OpLog::rebuild_index() {
     chunks_.push_back(new_chunk());
     nvis_ = 0;
     hint_c_ = SIZE_MAX;
+    hint_si_ = SIZE_MAX;
     std::vector<uint32_t> stack;
     stack.reserve(n + 1);
     stack.push_back(0);

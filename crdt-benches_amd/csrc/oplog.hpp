@@ -52,7 +52,7 @@ public:
     // For bulk builders that fill the SoA directly.
     void mark_stale() { stale_ = true; }
     void reset_visible(uint64_t v) { nvis_ = v; }
-    void reserve(size_t items);
+    void reserve(size_t items, size_t dels = 0);
 
 private:
     // Positional index: the document sequence (tombstones included) as spans of consecutive
@@ -69,16 +69,24 @@ private:
         uint32_t vis = 0;
     };
     std::vector<Chunk> chunks_;
-    std::vector<int64_t> fen_;  // Fenwick tree over chunks_[i].vis
+    // Fenwick tree over chunks_[i].vis; a chunk split shifts every later chunk, so the tree is
+    // rebuilt lazily, at the next lookup that misses the hints (not at every split)
+    mutable std::vector<int64_t> fen_;
+    mutable bool fen_dirty_ = false;
     std::vector<uint32_t> cps_;  // scratch for insert_utf8
     uint64_t nvis_ = 0;
     // Chunk of the last lookup and the visible items before it.  Edits only change counts at or
     // after the chunk they start in and splits append after it, so the hint stays exact.
     mutable size_t hint_c_ = SIZE_MAX;
     mutable uint64_t hint_base_ = 0;
+    // Span of the last lookup inside hint_c_ and the visible items of the chunk before it: edits
+    // change spans only at or after it (tombstone spans merging into it count 0), so a lookup at
+    // or after it scans on from there.  Dropped when a split moves it to another chunk.
+    mutable size_t hint_si_ = SIZE_MAX;
+    mutable uint64_t hint_vb_ = 0;
     bool stale_ = false;  // positional index must be rebuilt (after remote items arrived)
 
-    void fen_build();
+    void fen_build() const;
     void fen_add(size_t i, int64_t d);
     size_t fen_find(uint64_t& p) const;  // chunk holding the p-th visible item (p >= 1)
     Chunk new_chunk() const;
