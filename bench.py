@@ -227,8 +227,8 @@ def load_bases():
     with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
         golden = json.load(f)
     bases, patches, items, survivors, digests, resolve_ms = [], [], [], [], [], []
-    for name in TRACES:
-        t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
+    traces = [crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz")) for name in TRACES]
+    for name, t in zip(TRACES, traces):
         t0 = time.perf_counter()
         lg = t.resolve()
         resolve_ms.append((time.perf_counter() - t0) * 1e3)
@@ -237,8 +237,12 @@ def load_bases():
         items.append(bases[-1].n)
         survivors.append(golden[name]["end_bytes"])
         digests.append(int(golden[name]["tree_digest"], 16))
+    # the same four documents resolved at once, one host thread each (crdt_hip_trace_resolve_many)
+    t0 = time.perf_counter()
+    crdt_hip.Trace.resolve_many(traces, len(traces))
+    parallel_ms = (time.perf_counter() - t0) * 1e3
     return {"bases": bases, "patches": patches, "items": items, "survivors": survivors,
-            "digests": digests, "resolve_ms": resolve_ms}
+            "digests": digests, "resolve_ms": resolve_ms, "resolve_parallel_ms": parallel_ms}
 
 
 def host_cpus() -> dict:
@@ -504,6 +508,8 @@ def traces_workload(args) -> int:
             "pipeline": rf["pipeline"],
             "resolve": {"ms_per_trace": dict(zip(TRACES, inputs["resolve_ms"])),
                         "ms_total_one_core": sum(inputs["resolve_ms"]),
+                        "ms_all_parallel": inputs["resolve_parallel_ms"],
+                        "threads_parallel": len(TRACES),
                         "note": "host resolver (positional patches -> anchor log), untimed "
                                 "setup of the batch; once per trace"},
             "per_rank": res["per_rank"],

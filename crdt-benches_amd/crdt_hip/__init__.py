@@ -36,7 +36,8 @@ EXPORTS = [
     "crdt_hip_oplog_version", "crdt_hip_oplog_encode_from", "crdt_hip_oplog_apply_update",
     "crdt_hip_trace_load", "crdt_hip_trace_free", "crdt_hip_trace_len", "crdt_hip_trace_txns",
     "crdt_hip_trace_patch", "crdt_hip_trace_start_content", "crdt_hip_trace_end_content",
-    "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_trace_save",
+    "crdt_hip_trace_chars_to_bytes", "crdt_hip_trace_resolve", "crdt_hip_trace_resolve_many",
+    "crdt_hip_trace_save",
     "crdt_hip_oplog_save", "crdt_hip_oplog_load", "crdt_hip_logfile_open",
     "crdt_hip_logfile_close", "crdt_hip_synth_agents",
     "crdt_hip_synth_tree", "crdt_hip_synth_tree_visible", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
@@ -132,6 +133,7 @@ def lib() -> C.CDLL:
         "crdt_hip_trace_end_content": (i32, [vp, P(vp), P(sz)]),
         "crdt_hip_trace_chars_to_bytes": (i32, [vp]),
         "crdt_hip_trace_resolve": (i32, [vp, P(vp)]),
+        "crdt_hip_trace_resolve_many": (i32, [P(vp), u32, u32, P(vp)]),
         "crdt_hip_trace_save": (i32, [vp, C.c_char_p]),
         "crdt_hip_oplog_save": (i32, [vp, C.c_char_p]),
         "crdt_hip_oplog_load": (i32, [C.c_char_p, P(vp)]),
@@ -367,6 +369,15 @@ class Trace:
         h = C.c_void_p()
         _check(lib().crdt_hip_trace_resolve(self._h, C.byref(h)))
         return OpLog(h)
+
+    @staticmethod
+    def resolve_many(traces, threads: int = 0):
+        """resolve() of every trace, on up to `threads` host threads (0: one per trace)."""
+        n = len(traces)
+        ins = (C.c_void_p * n)(*[t._h for t in traces])
+        outs = (C.c_void_p * n)()
+        _check(lib().crdt_hip_trace_resolve_many(ins, n, threads, outs))
+        return [OpLog(C.c_void_p(outs[i])) for i in range(n)]
 
     def save(self, path: str) -> None:
         """Trace cache (crdt_hip_trace_save); Trace(path) reads it back without gunzip + JSON."""

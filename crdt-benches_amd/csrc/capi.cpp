@@ -3,11 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <exception>
 #include <memory>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "crdt_hip.h"
@@ -355,6 +358,40 @@ int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out) {
         *out = L;
         return 0;
     });
+}
+
+int crdt_hip_trace_resolve_many(const crdt_hip_trace* const* traces, uint32_t n, uint32_t threads,
+                                crdt_hip_oplog** out) {
+    if ((n && (!traces || !out))) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i) {
+        out[i] = nullptr;
+        if (!traces[i]) return set_err(nullptr, CRDT_HIP_EINVAL, "null trace");
+    }
+    uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    uint32_t k = threads ? threads : std::min(n, hw);
+    k = std::max(1u, std::min(k, n ? n : 1u));
+    std::vector<int> rc(n, 0);
+    std::vector<std::string> msg(n);
+    std::atomic<uint32_t> next{0};
+    auto work = [&] {
+        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+            rc[i] = crdt_hip_trace_resolve(traces[i], &out[i]);
+            if (rc[i]) msg[i] = crdt_hip_last_error(nullptr);  // (thread-local: read it here)
+        }
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t j = 1; j < k; ++j) pool.emplace_back(work);
+    work();
+    for (std::thread& th : pool) th.join();
+    for (uint32_t i = 0; i < n; ++i)
+        if (rc[i]) {
+            for (uint32_t j = 0; j < n; ++j) {
+                if (out[j]) crdt_hip_oplog_free(out[j]);
+                out[j] = nullptr;
+            }
+            return set_err(nullptr, rc[i], "trace " + std::to_string(i) + ": " + msg[i]);
+        }
+    return 0;
 }
 
 // ---- binary files ----------------------------------------------------------------------------

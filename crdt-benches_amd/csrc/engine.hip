@@ -1252,11 +1252,13 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     __shared__ uint32_t probe_max, probe_sum;
 #endif
     __shared__ uint32_t bigv[kDocBig], bigw[kDocBig];
-    if (replan(a.ctl)) return;
     const uint32_t d = blockIdx.x;
     const uint32_t t = threadIdx.x;
+    // the plan check and the document's run range in one round of loads (not one after the other)
     const uint32_t base = a.doc_root[d];
-    const uint32_t R = (d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL]) - base;
+    const uint32_t end = d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL];
+    if (replan(a.ctl)) return;
+    const uint32_t R = end - base;
     const uint32_t S = (R + (1u << kDocLog2S) - 1u) >> kDocLog2S;
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
@@ -1355,7 +1357,10 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // ---- pruning: a weightless leaf adds nothing to the document and is dropped from its
     // parent's children; a parent that loses its last child may go in the same pass (the
     // outcome depends on timing, never the text).  Repeated while it finds anything.
-    for (int round = 0; round < 2; ++round) {
+#ifndef CRDT_DOC_PRUNE_ROUNDS
+#define CRDT_DOC_PRUNE_ROUNDS 1  // (a second round: no measurable change)
+#endif
+    for (int round = 0; round < CRDT_DOC_PRUNE_ROUNDS; ++round) {
         uint32_t found = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {

@@ -166,6 +166,11 @@ int crdt_hip_trace_end_content(const crdt_hip_trace* t, const char** s, size_t* 
 int crdt_hip_trace_chars_to_bytes(crdt_hip_trace* t);
 /* Replay every patch into a fresh op log (the upstream loop body of main.rs:29-34). */
 int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out);
+/* crdt_hip_trace_resolve of n traces on up to `threads` host threads (0: one per trace, capped
+ * by the hardware), documents being independent.  out[i] receives trace
+ * i's op log; on an error every out[i] is null and the first error is reported. */
+int crdt_hip_trace_resolve_many(const crdt_hip_trace* const* traces, uint32_t n, uint32_t threads,
+                                crdt_hip_oplog** out);
 
 /* ---- binary files (skip gunzip + JSON; map resolved logs) ------------
  * Trace cache: the parsed trace in one flat file; crdt_hip_trace_load reads either format

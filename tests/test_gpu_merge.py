@@ -57,9 +57,9 @@ def test_merge_order_matches_oracle_preorder(ctx, oracle, name):
     assert np.array_equal(order, ref)
 
 
-def test_upstream_bench_loop_semantics(ctx, golden, py_trace):
-    """The reference's upstream closure (main.rs:28-36) with HipMerge as R."""
-    name = "sveltecomponent"
+@pytest.mark.parametrize("name", TRACES)
+def test_upstream_bench_loop_semantics(ctx, golden, py_trace, name):
+    """The reference's upstream closure (main.rs:28-36) with HipMerge as R, every trace."""
     t = crdt_hip.Trace(trace_path(name))
     rope = crdt_hip.HipMerge.from_str(t.start_content)
     for i in range(len(t)):

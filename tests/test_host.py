@@ -68,6 +68,20 @@ def test_native_resolver_matches_oracle_bit_exact(name, oracle, py_trace):
     assert oracle.merge(to_anchor(log)) == py_trace(name).end_content.encode()
 
 
+@pytest.mark.parametrize("threads", [0, 1, 3])
+def test_parallel_resolve_matches_sequential(threads):
+    """crdt_hip_trace_resolve_many (documents resolved in parallel) gives
+    every trace's log exactly as resolve() does, whatever the thread count."""
+    traces = [crdt_hip.Trace(trace_path(n)) for n in TRACES] * 2
+    logs = crdt_hip.Trace.resolve_many(traces, threads)
+    for t, lg in zip(traces, logs):
+        a, b = lg.arrays(), t.resolve().arrays()
+        assert a.n == b.n
+        for f in ("parent", "lamport", "agent", "deleted", "cp", "origin_right"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert crdt_hip.Trace.resolve_many([], 2) == []
+
+
 def test_resolver_upstream_api_semantics(oracle):
     log = crdt_hip.OpLog()
     log.insert(0, "hello")
