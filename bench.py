@@ -20,11 +20,11 @@ and its per-document digests are all-gathered over RCCL through the engine's C A
 golden digest of the trace's endContent.  torch.distributed (gloo) is the control plane only:
 the barriers around the timed region and the RCCL unique-id broadcast.
 
-cpu_baseline: the oracle's sequential RGA merge (oracle/oracle.c orc_merge_many), one document
-per thread over every CPU this process may run on, on a bounded sample of the same documents.
-config1: the oracle's positional replay (orc_replay, one core) of automerge-paper, timed like the
-reference's upstream closure (main.rs:28-36), beside the engine's own upstream path (host
-resolve + device merge of the same trace).
+cpu_baseline (rank 0 of an N=1 run only): the oracle's sequential RGA merge (oracle/oracle.c
+orc_merge_many), one document per thread over every CPU this process may run on, on a bounded
+sample of the same documents.  config1 (likewise): the oracle's positional replay (orc_replay,
+one core) of automerge-paper, timed like the reference's upstream closure (main.rs:28-36),
+beside the engine's own upstream path (host resolve + device merge of the same trace).
 """
 from __future__ import annotations
 
@@ -539,7 +539,7 @@ def traces_workload(args) -> int:
             out["digests_ok"] = out["digests_ok"] and cres["digests_ok"]
             cb.close()
     if rank == 0:
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # (the CPU lines belong to the N=1 run)
             threads = args.cpu_threads or host_cpus()["threads"]
             out["cpu_baseline"] = cpu_baseline(inputs["bases"], inputs["patches"],
                                                args.cpu_seconds, threads)
