@@ -1839,88 +1839,99 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 // of every 32-byte stripe), lane 0 merges them and hashes the tail, and every lane counts the
 // codepoints of its 64 bytes.  The same digest as xxh64_aligned(leaf, len, 0), without a thread
 // walking 4 KiB alone.
-constexpr int kLeafWaves = kBlock / 64;
+// Leaf digests, 16 leaves per wave: lanes 4g..4g+3 run the four stripe accumulators of leaf g
+// (every lane of the wave busy in the 128 rounds, instead of 4 of 64 with a wave per leaf),
+// reading their 8-byte words straight from the merged text (8 rounds of loads in flight), and
+// counting the leaf's codepoints on the way; the first lane of each group adds the tail (< 32
+// bytes), finalises and writes leafh / leafcp.  Leaf -> document by a binary search over loff.
+constexpr uint32_t kLeafGroup = 16;  // leaves per wave
+__device__ __forceinline__ uint32_t cont_bytes(uint64_t w, uint32_t n) {  // in the first n bytes
+    const uint64_t m = n >= 8u ? ~0ull : ((1ull << (8u * n)) - 1ull);
+    return (uint32_t)__popcll(w & ~(w << 1) & 0x8080808080808080ull & m);
+}
 __global__ __launch_bounds__(kBlock) void k_leafhash(TreeArgs a, uint32_t leaf_cap) {
-    __shared__ __attribute__((aligned(16))) uint64_t leaf[kLeafWaves][kLeaf / 8];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t L = blockIdx.x * kLeafWaves + wv;
-    if (replan(a.ctl) || L >= leaf_cap || L >= a.loff[a.ndocs]) return;  // wave-uniform
-    uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.loff[mid] <= L) lo = mid; else hi = mid;
+    const uint32_t lane = threadIdx.x & 63u, g = lane >> 2, acc = lane & 3u;
+    const uint32_t L = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kLeafGroup + g;
+    if (replan(a.ctl)) return;
+    const uint32_t nleaves = min(leaf_cap, a.loff[a.ndocs]);
+    const bool live = L < nleaves;
+    uint32_t d = 0, j = 0, len = 0;
+    if (live) {
+        uint32_t lo = 0, hi = a.ndocs;  // last d with loff[d] <= L
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.loff[mid] <= L) lo = mid; else hi = mid;
+        }
+        d = lo;
+        j = L - a.loff[d];
+        len = min(kLeaf, a.tlen[d] - j * kLeaf);
     }
-    const uint32_t d = lo, j = L - a.loff[d];
-    const uint32_t len = min(kLeaf, a.tlen[d] - j * kLeaf);
-    const uint4* src = reinterpret_cast<const uint4*>(a.text + a.toff[d] + (uint64_t)j * kLeaf);
-    uint4* dst = reinterpret_cast<uint4*>(leaf[wv]);
-    uint4 q[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t i = lane + 64u * k;
-        q[k] = 16u * i < len ? src[i] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) dst[lane + 64u * k] = q[k];
-    // codepoints: bytes minus continuation bytes, over this lane's 64 bytes (zero padding counts
-    // as non-continuation bytes, so count only up to len)
-    uint32_t cont = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t b0 = 16u * (lane + 64u * k);
-        const uint64_t w0 = ((uint64_t)q[k].y << 32) | q[k].x, w1 = ((uint64_t)q[k].w << 32) | q[k].z;
-        const uint32_t n0 = b0 >= len ? 0u : min(8u, len - b0);
-        const uint32_t n1 = b0 + 8u >= len ? 0u : min(8u, len - b0 - 8u);
-        const uint64_t m0 = n0 >= 8u ? ~0ull : ((1ull << (8u * n0)) - 1ull);
-        const uint64_t m1 = n1 >= 8u ? ~0ull : ((1ull << (8u * n1)) - 1ull);
-        cont += (uint32_t)__popcll(w0 & ~(w0 << 1) & 0x8080808080808080ull & m0);
-        cont += (uint32_t)__popcll(w1 & ~(w1 << 1) & 0x8080808080808080ull & m1);
-    }
-    const uint32_t cps = len - wave_sum(cont);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(a.text + (live ? a.toff[d] : 0ull) +
+                                                          (uint64_t)j * kLeaf);
     const uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL,
                    P3 = 0x165667B19E3779F9ULL, P4 = 0x85EBCA77C2B2AE63ULL,
                    P5 = 0x27D4EB2F165667C5ULL;
     const uint32_t nst = len / 32u;
-    uint64_t v = 0;
-    if (lane < 4u) {
-        v = lane == 0u ? P1 + P2 : lane == 1u ? P2 : lane == 2u ? 0ull : 0ull - P1;
-        const uint64_t* w = leaf[wv];
-        for (uint32_t k = 0; k < nst; ++k) v = xr(v, w[4u * k + lane]);
+    uint64_t v = acc == 0u ? P1 + P2 : acc == 1u ? P2 : acc == 2u ? 0ull : 0ull - P1;
+    uint32_t cont = 0;
+    uint32_t k = 0;
+    for (; k + 8u <= nst; k += 8u) {
+        uint64_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = w[4u * (k + u) + acc];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            v = xr(v, x[u]);
+            cont += cont_bytes(x[u], 8u);
+        }
     }
-    const uint64_t v1 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 0) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 0);
-    const uint64_t v2 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 1) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 1);
-    const uint64_t v3 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 2) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 2);
-    const uint64_t v4 = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), 3) << 32) | (uint32_t)__shfl((int)(uint32_t)v, 3);
-    if (lane != 0u) return;
+    for (; k < nst; ++k) {
+        const uint64_t x = w[4u * k + acc];
+        v = xr(v, x);
+        cont += cont_bytes(x, 8u);
+    }
+    // the group's four accumulators and continuation counts (every lane takes part)
+    const uint32_t b = lane & ~3u;
+    uint64_t vv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        vv[q] = ((uint64_t)(uint32_t)__shfl((int)(v >> 32), (int)(b + q)) << 32) |
+                (uint32_t)__shfl((int)(uint32_t)v, (int)(b + q));
+    cont += (uint32_t)__shfl_xor((int)cont, 1);
+    cont += (uint32_t)__shfl_xor((int)cont, 2);
+    if (!live || acc != 0u) return;
     uint64_t h;
     if (len >= 32u) {
-        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
-        h = xm(h, v1); h = xm(h, v2); h = xm(h, v3); h = xm(h, v4);
+        h = rotl(vv[0], 1) + rotl(vv[1], 7) + rotl(vv[2], 12) + rotl(vv[3], 18);
+        h = xm(h, vv[0]); h = xm(h, vv[1]); h = xm(h, vv[2]); h = xm(h, vv[3]);
     } else {
         h = P5;
     }
     h += len;
-    const uint64_t* w = leaf[wv];
-    const uint8_t* pb = reinterpret_cast<const uint8_t*>(leaf[wv]);
+    const uint8_t* pb = reinterpret_cast<const uint8_t*>(w);
     uint32_t i = 32u * nst;
     for (; i + 8u <= len; i += 8u) {
-        h ^= xr(0, w[i / 8u]);
+        const uint64_t x = w[i / 8u];
+        cont += cont_bytes(x, 8u);
+        h ^= xr(0, x);
         h = rotl(h, 27) * P1 + P4;
     }
     if (i + 4u <= len) {
-        h ^= (uint64_t)(*reinterpret_cast<const uint32_t*>(pb + i)) * P1;
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(pb + i);
+        cont += cont_bytes(x, 4u);
+        h ^= (uint64_t)x * P1;
         h = rotl(h, 23) * P2 + P3;
         i += 4u;
     }
     for (; i < len; ++i) {
-        h ^= (uint64_t)pb[i] * P5;
+        const uint32_t x = pb[i];
+        cont += (x & 0xC0u) == 0x80u ? 1u : 0u;
+        h ^= (uint64_t)x * P5;
         h = rotl(h, 11) * P1;
     }
     h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
     a.leafh[L] = h;
-    a.leafcp[L] = cps;
+    a.leafcp[L] = len - cont;
 }
 
 // Documents of more than kGroup leaves (16 MiB): leaf digests hashed in groups of kGroup (seed =
@@ -2668,7 +2679,8 @@ int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, Stag
         MARK(S_EXPAND);
     }
     if (!ord) {
-        k_leafhash<<<grid_for(w.leaf_cap + 1, kLeafWaves), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
+        k_leafhash<<<grid_for(w.leaf_cap + 1, (kBlock / 64) * kLeafGroup), kBlock, 0, s>>>(
+            a, (uint32_t)(w.leaf_cap + 1));
         if (w.max_doc_text > (uint64_t)kLeaf * kGroup)
             k_grouphash<<<grid_for(w.leaf_cap + 1), kBlock, 0, s>>>(a, (uint32_t)(w.leaf_cap + 1));
         k_docdigest<<<grid_for(w.ndocs), kBlock, 0, s>>>(a);
