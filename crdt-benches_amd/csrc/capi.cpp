@@ -55,8 +55,8 @@ struct crdt_hip_updates {
 
 namespace {
 
-// device bytes per op-log slot: parent (4) + key (lamport << 16 | agent, 8) + codepoint word (4)
-constexpr uint64_t kSlotBytes = 16;
+// device bytes per op-log slot: parent (4) + key (lamport << 16 | agent, 8) + codepoint (3)
+constexpr uint64_t kSlotBytes = 15;
 thread_local std::string g_err;
 
 int set_err(crdt_hip_ctx* ctx, int code, const std::string& msg) {

@@ -105,7 +105,7 @@ struct L0Args {
     const uint2* docs;          // per document {wave-relative base slot, n items}
     const uint32_t* in_parent;
     const uint64_t* in_key;     // lamport << 16 | agent (one gather per run head)
-    const uint32_t* in_cp;
+    const uint8_t* in_cp;       // 3 bytes per slot (cp3_get)
     uint32_t* jbits;            // per slot bit: has a non-consecutive child in a later tile
     uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
     uint16_t* seqb;             // per slot bit, 16 per thread: parent is the previous slot
@@ -130,8 +130,8 @@ struct L0Args {
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 
-// k_classify: parents and characters (tombstone in bit 31) of 16 slots per thread (4 + 4 x 16-byte
-// loads).
+// k_classify: parents and characters (3 bytes each, tombstone in bit 23) of 16 slots per thread
+// (4 + 3 x 16-byte loads).
 //  * "parent is the previous slot" bits (one u16 store per thread);
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
     const bool live = gs < a.nslots;
     // every load first (8 x 16 B per thread); padding slots hold junk and are masked below
-    uint4 pq[4], cq[4];
+    uint4 pq[4], cq[3];
     uint32_t base = 0, n = 0, l0 = 0;
     if (live) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
@@ -156,16 +156,24 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         n = doc.y;
         l0 = gs - base;
         const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
-        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + gs);
+        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B, 16-aligned
 #pragma unroll
         for (int q = 0; q < 4; ++q) pq[q] = pv[q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cq[q] = cv[q];
+        for (int q = 0; q < 3; ++q) cq[q] = cv[q];
     }
     const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
                             pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
-    const uint32_t C[16] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z, cq[1].w,
-                            cq[2].x, cq[2].y, cq[2].z, cq[2].w, cq[3].x, cq[3].y, cq[3].z, cq[3].w};
+    // the 16 three-byte values from 12 dwords (constant shifts: value k at byte 3k)
+    const uint32_t CW[13] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z,
+                             cq[1].w, cq[2].x, cq[2].y, cq[2].z, cq[2].w, 0u};
+    uint32_t C[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
+        const uint32_t lo = CW[wd] >> sh, hi = sh > 8 ? CW[wd + 1] << (32 - sh) : 0u;
+        C[k] = (lo | hi) & 0x00FFFFFFu;
+    }
     // branch-free classification of the 16 slots
     uint32_t seq = 0, jmp = 0, bad = 0, W = 0;
     uint32_t w[16];
@@ -2036,10 +2044,10 @@ __device__ __forceinline__ Perm replica_perm(uint32_t kind, uint32_t n, uint64_t
 // r % nb: item k goes to slot perm(k) and its parent is relabelled the same way.
 __global__ __launch_bounds__(kBlock) void k_replicate(
     const uint32_t* __restrict__ bp, const uint64_t* __restrict__ bk,
-    const uint32_t* __restrict__ bc,
+    const uint8_t* __restrict__ bc,
     const uint64_t* __restrict__ bslot, const uint32_t* __restrict__ bn, uint32_t nb,
     uint32_t* __restrict__ rp, uint64_t* __restrict__ rk,
-    uint32_t* __restrict__ rc, const uint64_t* __restrict__ rslot, uint64_t ndocs,
+    uint8_t* __restrict__ rc, const uint64_t* __restrict__ rslot, uint64_t ndocs,
     uint32_t kind, uint64_t seed) {
     for (uint64_t r = blockIdx.y; r < ndocs; r += gridDim.y) {
         const uint32_t b = (uint32_t)(r % nb);
@@ -2051,7 +2059,7 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
             const uint64_t o = dst + perm_apply(P, k);
             rp[o] = perm_apply(P, bp[src + k]);
             rk[o] = bk[src + k];
-            rc[o] = bc[src + k];
+            cp3_put(rc, o, cp3_get(bc, src + k));
         }
     }
 }
@@ -2061,7 +2069,7 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
 // document start; padding slots are deleted, parentless.
 __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ par,
                                                         uint64_t* __restrict__ key,
-                                                        uint32_t* __restrict__ cp, uint32_t n,
+                                                        uint8_t* __restrict__ cp, uint32_t n,
                                                         uint64_t nslots, uint32_t p_chain_pct,
                                                         uint32_t del_pct, uint64_t seed) {
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -2082,7 +2090,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ pa
     }
     par[g] = p;
     key[g] = ((uint64_t)l << 16) | a;
-    cp[g] = c | (d ? kDelBit : 0u);
+    cp3_put(cp, g, c | (d ? kDelBit : 0u));
 }
 
 inline uint32_t ceil_log2(uint64_t x) {
@@ -2233,7 +2241,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         dfree(L.parent); dfree(L.key); dfree(L.cp);
         HIPCHK(dalloc(&L.parent, slot), "hipMalloc logs.parent");
         HIPCHK(dalloc(&L.key, slot), "hipMalloc logs.key");
-        HIPCHK(dalloc(&L.cp, slot), "hipMalloc logs.cp");
+        HIPCHK(dalloc(&L.cp, cp3_bytes(slot)), "hipMalloc logs.cp");
         L.cap_slots = slot;
         gen_++;
     }
@@ -2308,7 +2316,9 @@ int Engine::upload_tables(DeviceLogs& L) {
 
 int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) {
     const uint64_t S = L.total_slots;
-    std::vector<uint32_t> par(S, 0), c(S, kDelBit);
+    std::vector<uint32_t> par(S, 0);
+    std::vector<uint8_t> c(cp3_bytes(S), 0);
+    for (uint64_t g = 0; g < S; ++g) cp3_put(c.data(), g, kDelBit);
     std::vector<uint64_t> key(S, 0);
     for (uint32_t d = 0; d < n; ++d) {
         const crdt_hip_oplog_view& v = views[d];
@@ -2317,12 +2327,12 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
         std::memcpy(&par[b], v.parent, v.n * 4ull);
         for (uint32_t i = 0; i < v.n; ++i) {
             key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
-            c[b + i] = (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u);
+            cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u));
         }
     }
     HIPCHK(hipMemcpy(L.parent, par.data(), S * 4, hipMemcpyHostToDevice), "upload parent");
     HIPCHK(hipMemcpy(L.key, key.data(), S * 8, hipMemcpyHostToDevice), "upload key");
-    HIPCHK(hipMemcpy(L.cp, c.data(), S * 4, hipMemcpyHostToDevice), "upload cp");
+    HIPCHK(hipMemcpy(L.cp, c.data(), c.size(), hipMemcpyHostToDevice), "upload cp");
     return CRDT_HIP_OK;
 }
 
@@ -2497,7 +2507,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.docs = L.docs_rel + w.first_doc;                             \
     a0.in_parent = L.parent + w.slot0;                              \
     a0.in_key = L.key + w.slot0;                                    \
-    a0.in_cp = L.cp + w.slot0;                                      \
+    a0.in_cp = L.cp + 3ull * w.slot0;                               \
     a0.jbits = jbits_;                                              \
     a0.jloc = jloc_;                                                \
     a0.seqb = seqb_;                                                \

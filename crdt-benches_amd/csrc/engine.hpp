@@ -56,9 +56,21 @@ struct L1Plan {
     uint64_t dyn_bytes = 0;
 };
 
-// Tombstone flag of a device slot, folded into its codepoint word (one 4-byte stream instead of
-// a 4-byte and a 1-byte one; codepoints use 21 bits).
-constexpr uint32_t kDelBit = 0x80000000u;
+// The codepoint column: 3 bytes per slot, the codepoint (bits 0-20) and the tombstone flag (bit
+// 23) in one 24-bit value (a 3-byte stream instead of a 4-byte codepoint and a 1-byte flag; the
+// level-0 stream reads 7 instead of 8 bytes per slot).
+constexpr uint32_t kDelBit = 0x00800000u;
+__host__ __device__ inline void cp3_put(uint8_t* b, uint64_t slot, uint32_t v) {
+    b[3 * slot] = (uint8_t)v;
+    b[3 * slot + 1] = (uint8_t)(v >> 8);
+    b[3 * slot + 2] = (uint8_t)(v >> 16);
+}
+__host__ __device__ inline uint32_t cp3_get(const uint8_t* b, uint64_t slot) {
+    return (uint32_t)b[3 * slot] | ((uint32_t)b[3 * slot + 1] << 8) | ((uint32_t)b[3 * slot + 2] << 16);
+}
+// bytes of the column for n slots (padded so that 16-byte loads of whole 16-slot groups and
+// 16-byte copies stay inside it)
+__host__ __device__ inline uint64_t cp3_bytes(uint64_t n) { return (3 * n + 63) & ~15ull; }
 
 // Device-resident op logs in slot layout, planned into waves.
 struct DeviceLogs {
@@ -71,7 +83,7 @@ struct DeviceLogs {
     // device arrays (slot-indexed)
     uint32_t* parent = nullptr;
     uint64_t* key = nullptr;       // the item's id as a sibling key: lamport << 16 | agent
-    uint32_t* cp = nullptr;        // codepoint (bits 0-20) | tombstone (bit 31, kDelBit)
+    uint8_t* cp = nullptr;         // 3 bytes per slot: codepoint (bits 0-20) | tombstone (bit 23)
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
     uint64_t cap_docs = 0, cap_chunks = 0;

@@ -104,7 +104,7 @@ struct UpdArgs {
     // replica slot arrays (slot = id)
     uint32_t* parent;
     uint64_t* key;  // lamport << 16 | agent
-    uint32_t* cp;   // codepoint | kDelBit
+    uint8_t* cp;    // 3 bytes per slot: codepoint | kDelBit (cp3_put / cp3_get)
     uint64_t cap_slots;
     uint32_t* imap;  // per flattened item / delete: its update (found by the check pass, reused
     uint32_t* dmap;  //   by the write pass instead of a second binary search)
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
                 a.parent[id] = par;
                 a.key[id] = ((uint64_t)a.buf[h.w + 2u * h.y + k] << 16) |
                             reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
-                a.cp[id] = c & kCpMaskR;  // live
+                cp3_put(a.cp, id, c & kCpMaskR);  // live
                 add_cp += 1u;
                 add_b += utf8_len(c & kCpMaskR);
             }
@@ -279,10 +279,13 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
             continue;
         }
         if (WRITE) {
-            const uint32_t old = atomicOr(a.cp + id, kDelBit);
-            if (!(old & kDelBit)) {  // newly tombstoned
+            // the tombstone bit is bit 7 of the slot's third byte: one atomic on its dword
+            const uint64_t b = 3ull * id + 2u;
+            const uint32_t sh = 8u * (uint32_t)(b & 3u) + 7u;
+            const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(a.cp + (b & ~3ull)), 1u << sh);
+            if (!((old >> sh) & 1u)) {  // newly tombstoned
                 del_cp += 1u;
-                del_b += utf8_len(old & kCpMaskR);
+                del_b += utf8_len(cp3_get(a.cp, id) & kCpMaskR);
             }
         }
     }
@@ -299,25 +302,31 @@ __global__ __launch_bounds__(kUB) void k_upd_dels(UpdArgs a) {
 
 // padding / unused slots: a tombstoned child of the document start with key 0 (never visible,
 // pruned by the merge)
-__global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint64_t* key, uint32_t* cp,
+__global__ __launch_bounds__(kUB) void k_rep_pad(uint32_t* parent, uint64_t* key, uint8_t* cp,
                                                  uint64_t s0, uint64_t s1) {
     const uint64_t g = s0 + (uint64_t)blockIdx.x * kUB + threadIdx.x;
     if (g >= s1) return;
     parent[g] = 0;
     key[g] = 0;
-    cp[g] = kDelBit;
+    cp3_put(cp, g, kDelBit);
 }
 
-// Replica clone: the three slot arrays in one launch (main.rs:64).
+// Replica clone: the three slot arrays in one launch (main.rs:64); the codepoint column as the
+// dwords of its padded byte size.
 __global__ __launch_bounds__(kUB) void k_rep_copy(const uint32_t* __restrict__ sp,
                                                   const uint64_t* __restrict__ sk,
-                                                  const uint32_t* __restrict__ sc,
+                                                  const uint8_t* __restrict__ sc,
                                                   uint32_t* __restrict__ dp, uint64_t* __restrict__ dk,
-                                                  uint32_t* __restrict__ dc, uint64_t n) {
-    for (uint64_t g = (uint64_t)blockIdx.x * kUB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * kUB) {
-        dp[g] = sp[g];
-        dk[g] = sk[g];
-        dc[g] = sc[g];
+                                                  uint8_t* __restrict__ dc, uint64_t n) {
+    const uint64_t nw = cp3_bytes(n) / 4;
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sc);
+    uint32_t* dw = reinterpret_cast<uint32_t*>(dc);
+    for (uint64_t g = (uint64_t)blockIdx.x * kUB + threadIdx.x; g < nw; g += (uint64_t)gridDim.x * kUB) {
+        if (g < n) {
+            dp[g] = sp[g];
+            dk[g] = sk[g];
+        }
+        dw[g] = sw[g];
     }
 }
 
@@ -381,17 +390,18 @@ int replica_reserve(Engine& E, Replica& r, uint64_t items) {
     if (need <= L.cap_slots) return CRDT_HIP_OK;
     const uint64_t cap = std::min<uint64_t>((1ull << 31) - 64,
                                             std::max<uint64_t>({need, 2 * L.cap_slots, 4096}));
-    uint32_t *par = nullptr, *c = nullptr;
+    uint32_t* par = nullptr;
+    uint8_t* c = nullptr;
     uint64_t* key = nullptr;
     hipError_t e = dalloc(&par, cap);
     if (e == hipSuccess) e = dalloc(&key, cap);
-    if (e == hipSuccess) e = dalloc(&c, cap);
+    if (e == hipSuccess) e = dalloc(&c, cp3_bytes(cap));
     const uint64_t old = L.cap_slots;
     hipStream_t s = E.stream;
     if (e == hipSuccess && old) {
         e = hipMemcpyAsync(par, L.parent, old * 4, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(key, L.key, old * 8, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(c, L.cp, old * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(c, L.cp, old * 3, hipMemcpyDeviceToDevice, s);
     }
     if (e == hipSuccess) {
         k_rep_pad<<<grid_for(cap - old, kUB), kUB, 0, s>>>(par, key, c, old, cap);
@@ -427,18 +437,18 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     // null-stream copy does not wait for a non-blocking stream and could be overwritten by it)
     hipStream_t s = E.stream;
     RCHK(hipMemcpyAsync(L.parent + 1, v->parent, n * 4ull, hipMemcpyHostToDevice, s), "upload parent");
-    std::vector<uint32_t> c(n);
+    std::vector<uint8_t> c(3ull * n);
     std::vector<uint64_t> key(n);
     for (uint32_t i = 0; i < n; ++i) {
         key[i] = ((uint64_t)v->lamport[i] << 16) | v->agent[i];
-        c[i] = (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u);
+        cp3_put(c.data(), i, (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u));
         if (!v->deleted[i]) {
             r.vis_cp += 1;
             r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
         }
     }
     RCHK(hipMemcpyAsync(L.key + 1, key.data(), n * 8ull, hipMemcpyHostToDevice, s), "upload key");
-    RCHK(hipMemcpyAsync(L.cp + 1, c.data(), n * 4ull, hipMemcpyHostToDevice, s), "upload cp");
+    RCHK(hipMemcpyAsync(L.cp + 3, c.data(), c.size(), hipMemcpyHostToDevice, s), "upload cp");
     RCHK(hipStreamSynchronize(s), "upload sync");  // (key, c and the caller's view are released)
     return CRDT_HIP_OK;
 }
