@@ -130,40 +130,31 @@ struct L0Args {
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 
-// k_classify: parents and characters (3 bytes each, tombstone in bit 23) of 16 slots per thread
-// (4 + 3 x 16-byte loads).
-//  * "parent is the previous slot" bits (one u16 store per thread);
-//  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
-//    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
+// k_classify: the characters of 16 slots per thread (3 x 16-byte loads of the codepoint column:
+// codepoint, tombstone, "parent is the previous slot" flag).
+//  * "parent is the previous slot" bits (one u16 store per thread), straight from the flags;
 //  * per-slot weights as nibbles, the tile's weight total, and the tile's visible UTF-8
 //    compacted in slot order: assembled in LDS, stored to its stile segment in 16-byte pieces.
-// A parent out of range (or an item that is its own parent) is flagged; such an item becomes a
-// run head under the document start, and the merge reports CRDT_HIP_EBADLOG.
+// No parent is read here: the parents of the slots without the flag (a few percent) are k_jumps'
+// work, so this stream reads 3 bytes per slot and waits for one round trip.
 __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint32_t lds[kBlock / 64];
-    __shared__ uint32_t jl[kScanTile / 32];
     __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes];
     const uint32_t tile = blockIdx.x;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
-    if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
     const bool live = gs < a.nslots;
-    // every load first (8 x 16 B per thread); padding slots hold junk and are masked below
-    uint4 pq[4], cq[3];
-    uint32_t base = 0, n = 0, l0 = 0;
+    // the codepoint column first (its address does not wait for the document lookup); padding
+    // slots hold junk and are masked below
+    uint4 cq[3] = {};
+    uint32_t n = 0, l0 = 0;
     if (live) {
-        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        base = doc.x;
-        n = doc.y;
-        l0 = gs - base;
-        const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
         const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B, 16-aligned
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pq[q] = pv[q];
-#pragma unroll
         for (int q = 0; q < 3; ++q) cq[q] = cv[q];
+        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        n = doc.y;
+        l0 = gs - doc.x;
     }
-    const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
-                            pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
     // the 16 three-byte values from 12 dwords (constant shifts: value k at byte 3k)
     const uint32_t CW[13] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z,
                              cq[1].w, cq[2].x, cq[2].y, cq[2].z, cq[2].w, 0u};
@@ -174,40 +165,19 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         const uint32_t lo = CW[wd] >> sh, hi = sh > 8 ? CW[wd + 1] << (32 - sh) : 0u;
         C[k] = (lo | hi) & 0x00FFFFFFu;
     }
-    // branch-free classification of the 16 slots
-    uint32_t seq = 0, jmp = 0, bad = 0, W = 0;
-    uint32_t w[16];
+    // branch-free classification of the 16 slots; weights straight into their nibbles
+    uint32_t seq = 0, W = 0;
+    uint64_t nib = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const uint32_t local = l0 + k, p = P[k];
-        const bool it = live && (local - 1u) < n;  // an item (not the document start / padding)
+        const bool it = live && (l0 + k - 1u) < n;  // an item (not the document start / padding)
         const bool del = (C[k] & kDelBit) != 0u;
-        const bool b = p > n || p == local;
-        const bool sq = p == local - 1u;
-        w[k] = it ? (a.mode ? 1u : (del ? 0u : utf8_len(C[k] & kCpMask))) : 0u;
-        W += w[k];
-        bad |= (it && b) ? 1u : 0u;
-        seq |= (it && !b && sq ? 1u : 0u) << k;
-        jmp |= (it && !b && !sq ? 1u : 0u) << k;
-    }
-    __syncthreads();  // jl cleared
-    // jump bits: parents in this tile in LDS; parents in earlier tiles by global atomics, issued
-    // last so that no wait in this kernel ever has to cover them
-    uint32_t remote = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (jmp & (1u << k)) {
-            const uint32_t ps = base + P[k];
-            if (ps / kScanTile == tile)
-                atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
-            else
-                remote |= 1u << k;
-        }
+        const uint32_t w = it ? (a.mode ? 1u : (del ? 0u : utf8_len(C[k] & kCpMask))) : 0u;
+        W += w;
+        nib |= (uint64_t)w << (4 * k);
+        seq |= (it && (C[k] & kSeqBit) ? 1u : 0u) << k;
     }
     if (live) {
-        uint64_t nib = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) nib |= (uint64_t)w[k] << (4 * k);
         a.seqb[gs >> 4] = (uint16_t)seq;
         a.wnib[gs >> 4] = nib;
     }
@@ -217,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         uint8_t* o = sb + ex;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const uint32_t L = w[k], c = C[k] & kCpMask;
+            const uint32_t L = (uint32_t)(nib >> (4 * k)) & 15u, c = C[k] & kCpMask;
             if (L) {
                 // UTF-8: lead byte = length prefix | top bits, then 6-bit continuation bytes
                 const uint32_t s0 = 6u * (L - 1u);
@@ -231,19 +201,63 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     }
     __syncthreads();
     if (threadIdx.x == 0) a.tile_hw[tile].y = tw;
-    if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
     if (a.mode == 0) {
         uint4* dst = reinterpret_cast<uint4*>(a.stile + (uint64_t)tile * kTileBytes);
         const uint4* src = reinterpret_cast<const uint4*>(sb);
         for (uint32_t i = threadIdx.x; i < (tw + 15u) / 16u; i += kBlock) dst[i] = src[i];
     }
+}
+
+// k_jumps: the parents of the items without the previous-slot flag (k_classify's seq bits),
+// 16 slots per thread, read only by the threads holding one (4 x 16 B):
+//  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
+//    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
+//  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
+//    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG.
+__global__ __launch_bounds__(kBlock) void k_jumps(L0Args a) {
+    __shared__ uint32_t jl[kScanTile / 32];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
+    if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
+    uint32_t need = 0, base = 0, n = 0, l0 = 0;
+    uint4 pq[4] = {};
+    if (gs < a.nslots) {
+        const uint32_t seq = a.seqb[gs >> 4];
+        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        base = doc.x;
+        n = doc.y;
+        l0 = gs - base;
+        uint32_t items = 0;  // the group's items: locals 1..n
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (remote & (1u << k)) {
-            const uint32_t ps = base + P[k];
-            atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+        for (int k = 0; k < 16; ++k) items |= ((l0 + k - 1u) < n ? 1u : 0u) << k;
+        need = items & ~seq;
+        if (need) {
+            const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pq[q] = pv[q];
         }
     }
+    const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
+                            pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
+    __syncthreads();  // jl cleared
+    uint32_t bad = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (need & (1u << k)) {
+            const uint32_t p = P[k], local = l0 + k;
+            if (p > n || p == local) {
+                bad = 1u;
+            } else {
+                const uint32_t ps = base + p;
+                if (ps / kScanTile == tile)
+                    atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
+                else
+                    atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
@@ -2056,10 +2070,11 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
         const Perm P = replica_perm(kind, n, seed, r);
         const uint64_t src = bslot[b], dst = rslot[r];
         for (uint32_t k = blockIdx.x * kBlock + threadIdx.x + 1; k <= n; k += gridDim.x * kBlock) {
-            const uint64_t o = dst + perm_apply(P, k);
-            rp[o] = perm_apply(P, bp[src + k]);
+            const uint32_t lk = perm_apply(P, k), pk = perm_apply(P, bp[src + k]);
+            const uint64_t o = dst + lk;
+            rp[o] = pk;
             rk[o] = bk[src + k];
-            cp3_put(rc, o, cp3_get(bc, src + k));
+            cp3_put(rc, o, (cp3_get(bc, src + k) & ~kSeqBit) | (pk == lk - 1u ? kSeqBit : 0u));
         }
     }
 }
@@ -2084,7 +2099,8 @@ __global__ __launch_bounds__(kBlock) void k_synth_tree(uint32_t* __restrict__ pa
         const uint64_t h2 = mix64(seed ^ 0x5A5A5A5A5A5A5A5AULL, i);
         p = (h0 % 100 < p_chain_pct) ? i - 1 : (uint32_t)(h1 % i);
         d = (uint8_t)((h2 % 100) < del_pct);
-        c = 'a' + (uint32_t)((h2 >> 32) % 26);
+        if (p == i - 1) c |= kSeqBit;
+        c |= 'a' + (uint32_t)((h2 >> 32) % 26);
         l = i;
         a = (uint16_t)(i % 64);
     }
@@ -2327,7 +2343,8 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
         std::memcpy(&par[b], v.parent, v.n * 4ull);
         for (uint32_t i = 0; i < v.n; ++i) {
             key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
-            cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u));
+            cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
+                                         (v.parent[i] == i ? kSeqBit : 0u));
         }
     }
     HIPCHK(hipMemcpy(L.parent, par.data(), S * 4, hipMemcpyHostToDevice), "upload parent");
@@ -2559,6 +2576,7 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
     k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
     MARK(-1);
     k_classify<<<ntiles, kBlock, 0, s>>>(a0);
+    k_jumps<<<ntiles, kBlock, 0, s>>>(a0);
     MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);

@@ -56,10 +56,13 @@ struct L1Plan {
     uint64_t dyn_bytes = 0;
 };
 
-// The codepoint column: 3 bytes per slot, the codepoint (bits 0-20) and the tombstone flag (bit
-// 23) in one 24-bit value (a 3-byte stream instead of a 4-byte codepoint and a 1-byte flag; the
-// level-0 stream reads 7 instead of 8 bytes per slot).
+// The codepoint column: 3 bytes per slot, the codepoint (bits 0-20), the tombstone flag (bit 23)
+// and a "parent is the previous slot" flag (bit 22) in one 24-bit value.  The level-0 stream
+// reads this column and only the parents of slots without the flag: 3 + a few bytes per slot
+// instead of 8.  The flag is a hint written with the parent: set only when the parent column
+// holds the previous slot; a slot without it has its parent read and classified in full.
 constexpr uint32_t kDelBit = 0x00800000u;
+constexpr uint32_t kSeqBit = 0x00400000u;
 __host__ __device__ inline void cp3_put(uint8_t* b, uint64_t slot, uint32_t v) {
     b[3 * slot] = (uint8_t)v;
     b[3 * slot + 1] = (uint8_t)(v >> 8);

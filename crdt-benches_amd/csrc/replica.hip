@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
                 a.parent[id] = par;
                 a.key[id] = ((uint64_t)a.buf[h.w + 2u * h.y + k] << 16) |
                             reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
-                cp3_put(a.cp, id, c & kCpMaskR);  // live
+                cp3_put(a.cp, id, (c & kCpMaskR) | (par == id - 1u ? kSeqBit : 0u));  // live
                 add_cp += 1u;
                 add_b += utf8_len(c & kCpMaskR);
             }
@@ -441,7 +441,8 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     std::vector<uint64_t> key(n);
     for (uint32_t i = 0; i < n; ++i) {
         key[i] = ((uint64_t)v->lamport[i] << 16) | v->agent[i];
-        cp3_put(c.data(), i, (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u));
+        cp3_put(c.data(), i, (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u) |
+                                 (v->parent[i] == i ? kSeqBit : 0u));
         if (!v->deleted[i]) {
             r.vis_cp += 1;
             r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
