@@ -12,7 +12,9 @@
 //  the document; on the josephg traces they hold 93-98 % of all items.  Run heads are recorded
 //  in a rank bitvector (1 bit/slot + a u32 rank per 64 slots) and every run gets its parent run,
 //  its key (lamport, agent of the head) and its weight (visible UTF-8 bytes).
-//    k_classify    seq/jump bits, weight nibbles, each tile's UTF-8 compacted in slot order
+//    k_classify    non-seq item bits (from the codepoint column's previous-slot flags), weight
+//                  nibbles, each tile's UTF-8 compacted in slot order
+//    k_jumps       jump bits from the parents of the non-seq items
 //    k_heads       head bitvector words, per-tile head counts
 //    k_tiles_*     exclusive scan of the per-tile (heads, weight) pairs
 //    k_runs        run records (head slot, weight prefix, key, parent run by rank lookup),
@@ -108,7 +110,8 @@ struct L0Args {
     const uint8_t* in_cp;       // 3 bytes per slot (cp3_get)
     uint32_t* jbits;            // per slot bit: has a non-consecutive child in a later tile
     uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
-    uint16_t* seqb;             // per slot bit, 16 per thread: parent is the previous slot
+    uint16_t* nsqb;             // per slot bit, 16 per thread: an item whose parent is not the
+                                //   previous slot (no previous-slot flag)
     uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
     uint8_t* stile;             // per tile: its visible UTF-8 in slot order (kTileBytes each)
     uint8_t* sbytes;            // the wave's visible UTF-8 in slot order (= weight order)
@@ -132,7 +135,8 @@ constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-by
 
 // k_classify: the characters of 16 slots per thread (3 x 16-byte loads of the codepoint column:
 // codepoint, tombstone, "parent is the previous slot" flag).
-//  * "parent is the previous slot" bits (one u16 store per thread), straight from the flags;
+//  * "item whose parent is not the previous slot" bits (one u16 store per thread), straight from
+//    the flags;
 //  * per-slot weights as nibbles, the tile's weight total, and the tile's visible UTF-8
 //    compacted in slot order: assembled in LDS, stored to its stile segment in 16-byte pieces.
 // No parent is read here: the parents of the slots without the flag (a few percent) are k_jumps'
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         C[k] = (lo | hi) & 0x00FFFFFFu;
     }
     // branch-free classification of the 16 slots; weights straight into their nibbles
-    uint32_t seq = 0, W = 0;
+    uint32_t nsq = 0, W = 0;
     uint64_t nib = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -175,10 +179,10 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         const uint32_t w = it ? (a.mode ? 1u : (del ? 0u : utf8_len(C[k] & kCpMask))) : 0u;
         W += w;
         nib |= (uint64_t)w << (4 * k);
-        seq |= (it && (C[k] & kSeqBit) ? 1u : 0u) << k;
+        nsq |= (it && !(C[k] & kSeqBit) ? 1u : 0u) << k;
     }
     if (live) {
-        a.seqb[gs >> 4] = (uint16_t)seq;
+        a.nsqb[gs >> 4] = (uint16_t)nsq;
         a.wnib[gs >> 4] = nib;
     }
     uint32_t tw;
@@ -208,8 +212,9 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     }
 }
 
-// k_jumps: the parents of the items without the previous-slot flag (k_classify's seq bits),
-// 16 slots per thread, read only by the threads holding one (4 x 16 B):
+// k_jumps: the parents of the items without the previous-slot flag (k_classify's nsq bits),
+// 16 slots per thread; a thread with none reads nothing else, the others read their 16 parents
+// (4 x 16 B) and the document together:
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
 //  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
@@ -219,23 +224,17 @@ __global__ __launch_bounds__(kBlock) void k_jumps(L0Args a) {
     const uint32_t tile = blockIdx.x;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
     if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
-    uint32_t need = 0, base = 0, n = 0, l0 = 0;
+    const uint32_t need = gs < a.nslots ? (uint32_t)a.nsqb[gs >> 4] : 0u;
+    uint32_t base = 0, n = 0, l0 = 0;
     uint4 pq[4] = {};
-    if (gs < a.nslots) {
-        const uint32_t seq = a.seqb[gs >> 4];
+    if (need) {
+        const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pq[q] = pv[q];
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         base = doc.x;
         n = doc.y;
         l0 = gs - base;
-        uint32_t items = 0;  // the group's items: locals 1..n
-#pragma unroll
-        for (int k = 0; k < 16; ++k) items |= ((l0 + k - 1u) < n ? 1u : 0u) << k;
-        need = items & ~seq;
-        if (need) {
-            const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) pq[q] = pv[q];
-        }
     }
     const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
                             pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
@@ -279,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         const uint32_t l0 = gs - doc.x, n = doc.y;
         if (l0 <= n) {
-            const uint64_t seq = *reinterpret_cast<const uint64_t*>(a.seqb + (gs >> 4));
+            const uint64_t nsq = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
             const uint2 jr = *reinterpret_cast<const uint2*>(a.jbits + (gs >> 5));
             const uint2 jq = *reinterpret_cast<const uint2*>(a.jloc + (gs >> 5));
             const uint64_t jw = ((uint64_t)(jr.y | jq.y) << 32) | (uint64_t)(jr.x | jq.x);
@@ -288,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint64_t prevj = (jw << 1) | pj;  // bit k = jump(gs + k - 1)
             const uint64_t item = low_mask64(n + 1u - l0) & ~low_mask64(l0 == 0 ? 1u : 0u);
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
-            hw = root | (item & ~(seq & ~prevj));
+            hw = root | (item & (nsq | prevj));
         }
     }
     const uint32_t c = (uint32_t)__popcll(hw);
@@ -374,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     constexpr int NW = kBlock / 64;
     __shared__ uint32_t lsum[NW];
     __shared__ uint32_t rec[kScanTile];
-    __shared__ uint16_t lseq[kBlock];  // seq bits of every thread's 16 slots
+    __shared__ uint16_t lnsq[kBlock];  // nsq bits of every thread's 16 slots
     __shared__ uint2 ldoc[kBlock];     // every thread's document {base slot, items}
     const uint32_t tile = blockIdx.x;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -388,7 +387,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
         nib = a.wnib[gs >> 4];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        lseq[threadIdx.x] = a.seqb[gs >> 4];
+        lnsq[threadIdx.x] = a.nsqb[gs >> 4];
     }
     ldoc[threadIdx.x] = doc;
     // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
@@ -462,8 +461,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const uint32_t rv = rec[i];
         const uint32_t li = rv >> 16, g = tbase + li, rho = pre.x + i;
         const uint2 dc = ldoc[li >> 4];
-        const bool sq = (lseq[li >> 4] >> (li & 15u)) & 1u;
         const bool root = g == dc.x;
+        const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
         const uint64_t key = a.in_key[g];
         uint32_t p = (!sq && !root) ? a.in_parent[g] : 0u;
         a.r_head[rho] = g;
@@ -2129,7 +2128,7 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
+    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
@@ -2356,12 +2355,12 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(seqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
+        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
         HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
-        HIPCHK(dalloc(&seqb_, slots / 16 + 4), "hipMalloc seq bits");
+        HIPCHK(dalloc(&nsqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
         HIPCHK(dalloc(&hrec_, slots / 64 + 2), "hipMalloc head records");
         HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
@@ -2527,7 +2526,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.in_cp = L.cp + 3ull * w.slot0;                               \
     a0.jbits = jbits_;                                              \
     a0.jloc = jloc_;                                                \
-    a0.seqb = seqb_;                                                \
+    a0.nsqb = nsqb_;                                                \
     a0.wnib = wnib_;                                                \
     a0.stile = stile_;                                              \
     a0.sbytes = sbytes_;                                            \

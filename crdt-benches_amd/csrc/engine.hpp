@@ -180,7 +180,7 @@ private:
     // level-0 scratch (per slot / per tile), grown on demand
     uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
     uint32_t *jbits_ = nullptr, *jloc_ = nullptr;
-    uint16_t* seqb_ = nullptr;
+    uint16_t* nsqb_ = nullptr;
     uint64_t* wnib_ = nullptr;
     uint4* hrec_ = nullptr;
     uint8_t *stile_ = nullptr, *sbytes_ = nullptr;
