@@ -212,42 +212,53 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     }
 }
 
-// k_jumps: the parents of the items without the previous-slot flag (k_classify's nsq bits),
-// 16 slots per thread; a thread with none reads nothing else, the others read their 16 parents
-// (4 x 16 B) and the document together:
+// k_jumps: the parents of the items without the previous-slot flag (k_classify's nsq bits), one
+// wave per tile, 64 slots (one 64-aligned word of nsq bits, inside one document) per thread.  A
+// thread with no such item reads nothing else; the others read those parents, four loads in
+// flight at a time, and their document record:
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
 //  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
 //    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG.
-__global__ __launch_bounds__(kBlock) void k_jumps(L0Args a) {
+constexpr uint32_t kJumpBlock = kScanTile / 64;
+__global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
     __shared__ uint32_t jl[kScanTile / 32];
     const uint32_t tile = blockIdx.x;
-    const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
-    if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
-    const uint32_t need = gs < a.nslots ? (uint32_t)a.nsqb[gs >> 4] : 0u;
-    uint32_t base = 0, n = 0, l0 = 0;
-    uint4 pq[4] = {};
+    const uint32_t gs = tile * kScanTile + threadIdx.x * 64u;
+    jl[threadIdx.x] = 0;
+    jl[threadIdx.x + kJumpBlock] = 0;
+    // the bits and the chunk's document index together, then the parents and the record
+    uint64_t need = 0;
+    uint32_t di = 0;
+    if (gs < a.nslots) {
+        need = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
+        di = a.chunk_doc[gs >> a.log2m];
+    }
+    uint32_t base = 0, n = 0;
     if (need) {
-        const uint4* pv = reinterpret_cast<const uint4*>(a.in_parent + gs);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pq[q] = pv[q];
-        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        const uint2 doc = a.docs[di];
         base = doc.x;
         n = doc.y;
-        l0 = gs - base;
     }
-    const uint32_t P[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
-                            pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
     __syncthreads();  // jl cleared
+    const uint32_t l0 = gs - base;
     uint32_t bad = 0;
+    while (need) {
+        uint32_t k[4], p[4];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (need & (1u << k)) {
-            const uint32_t p = P[k], local = l0 + k;
-            if (p > n || p == local) {
+        for (int j = 0; j < 4; ++j) {
+            k[j] = need ? (uint32_t)__builtin_ctzll(need) : 64u;
+            need &= need - 1ull;  // (0 stays 0)
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = k[j] < 64u ? a.in_parent[gs + k[j]] : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (k[j] >= 64u) continue;
+            if (p[j] > n || p[j] == l0 + k[j]) {
                 bad = 1u;
             } else {
-                const uint32_t ps = base + p;
+                const uint32_t ps = base + p[j];
                 if (ps / kScanTile == tile)
                     atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
                 else
@@ -256,7 +267,8 @@ __global__ __launch_bounds__(kBlock) void k_jumps(L0Args a) {
         }
     }
     __syncthreads();
-    if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
+    a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
+    a.jloc[tile * (kScanTile / 32) + kJumpBlock + threadIdx.x] = jl[kJumpBlock + threadIdx.x];
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
@@ -2575,7 +2587,7 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
     k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
     MARK(-1);
     k_classify<<<ntiles, kBlock, 0, s>>>(a0);
-    k_jumps<<<ntiles, kBlock, 0, s>>>(a0);
+    k_jumps<<<ntiles, kJumpBlock, 0, s>>>(a0);
     MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
