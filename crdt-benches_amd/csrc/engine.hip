@@ -213,52 +213,67 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
 }
 
 // k_jumps: the parents of the items without the previous-slot flag (k_classify's nsq bits), one
-// wave per tile, 64 slots (one 64-aligned word of nsq bits, inside one document) per thread.  A
-// thread with no such item reads nothing else; the others read those parents, four loads in
-// flight at a time, and their document record:
+// wave per tile.  Each thread reads the nsq word of 64 slots (inside one document) and, if it
+// has any, its document record; the tile's items are listed in LDS in slot order and their
+// parents read by the whole wave, four loads per thread in flight at a time (the items cluster:
+// without the list one thread could hold 64 of them; a tile with more than kJumpList of them,
+// rare, has each thread read its own):
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
 //  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
 //    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG.
 constexpr uint32_t kJumpBlock = kScanTile / 64;
+constexpr uint32_t kJumpList = 1024;  // (the LDS list's size: 2 KiB keeps 8 waves per SIMD)
 __global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
     __shared__ uint32_t jl[kScanTile / 32];
-    const uint32_t tile = blockIdx.x;
-    const uint32_t gs = tile * kScanTile + threadIdx.x * 64u;
-    jl[threadIdx.x] = 0;
-    jl[threadIdx.x + kJumpBlock] = 0;
-    // the bits and the chunk's document index together, then the parents and the record
+    __shared__ uint16_t lst[kJumpList];  // tile offsets of the items, in slot order
+    __shared__ uint2 ldoc[kJumpBlock];   // per thread: its document {base slot, items}
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    const uint32_t t0 = tile * kScanTile, gs = t0 + lane * 64u;
+    jl[lane] = 0;
+    jl[lane + kJumpBlock] = 0;
     uint64_t need = 0;
     uint32_t di = 0;
-    if (gs < a.nslots) {
+    if (gs < a.nslots) {  // the bits and the chunk's document index together
         need = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
         di = a.chunk_doc[gs >> a.log2m];
     }
-    uint32_t base = 0, n = 0;
-    if (need) {
-        const uint2 doc = a.docs[di];
-        base = doc.x;
-        n = doc.y;
-    }
-    __syncthreads();  // jl cleared
-    const uint32_t l0 = gs - base;
+    uint2 doc = make_uint2(0, 0);
+    if (need) doc = a.docs[di];
+    ldoc[lane] = doc;
+    const uint32_t c = (uint32_t)__popcll(need);
+    const uint32_t inc = wave_incl_scan(c);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    const bool listed = T <= kJumpList;  // (wave-uniform)
+    if (listed)
+        for (uint32_t i = inc - c; need; need &= need - 1ull)
+            lst[i++] = (uint16_t)(lane * 64u + (uint32_t)__builtin_ctzll(need));
+    __syncthreads();  // jl cleared, list and records written
     uint32_t bad = 0;
-    while (need) {
-        uint32_t k[4], p[4];
+    // listed: item q of the list at t + 64 j; else this thread's own items, four at a time
+    for (uint32_t t = listed ? lane : 0u; listed ? t < T : need != 0ull;
+         t += 4u * kJumpBlock) {
+        uint32_t o[4], p[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            k[j] = need ? (uint32_t)__builtin_ctzll(need) : 64u;
-            need &= need - 1ull;  // (0 stays 0)
+            const uint32_t q = t + (uint32_t)j * kJumpBlock;
+            if (listed) {
+                o[j] = q < T ? lst[q] : 0xFFFFu;
+            } else {
+                o[j] = need ? lane * 64u + (uint32_t)__builtin_ctzll(need) : 0xFFFFu;
+                need &= need - 1ull;
+            }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] = k[j] < 64u ? a.in_parent[gs + k[j]] : 0u;
+        for (int j = 0; j < 4; ++j) p[j] = o[j] != 0xFFFFu ? a.in_parent[t0 + o[j]] : 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (k[j] >= 64u) continue;
-            if (p[j] > n || p[j] == l0 + k[j]) {
+            if (o[j] == 0xFFFFu) continue;
+            const uint2 d = ldoc[o[j] >> 6];
+            if (p[j] > d.y || p[j] == t0 + o[j] - d.x) {
                 bad = 1u;
             } else {
-                const uint32_t ps = base + p[j];
+                const uint32_t ps = d.x + p[j];
                 if (ps / kScanTile == tile)
                     atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
                 else
@@ -267,8 +282,8 @@ __global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
         }
     }
     __syncthreads();
-    a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
-    a.jloc[tile * (kScanTile / 32) + kJumpBlock + threadIdx.x] = jl[kJumpBlock + threadIdx.x];
+    a.jloc[tile * (kScanTile / 32) + lane] = jl[lane];
+    a.jloc[tile * (kScanTile / 32) + kJumpBlock + lane] = jl[kJumpBlock + lane];
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
