@@ -58,7 +58,7 @@ MIN_B_PER_TEXT = 1.0
 # Per-kernel algorithmic bytes: each kernel's declared inputs read once +
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
-    "classify": (3.875, 4.0, 1.0),   # 3-byte cp|flags, parents of unflagged items (k_jumps); seq bits, weight nibbles; tile UTF-8
+    "classify": (3.875, 8.0, 1.0),   # 3-byte cp|flags, parents of unflagged items read + listed (k_jumps); seq bits, weight nibbles; tile UTF-8
     # head/seq bits, nibbles; per run: key + parent slot + rank lookup in, record row out; text move
     "runs": (0.75, 38.0, 2.0),
     "count": (0.0, 8.0, 0.0),

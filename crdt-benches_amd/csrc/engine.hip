@@ -114,6 +114,8 @@ struct L0Args {
                                 //   previous slot (no previous-slot flag)
     uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
     uint8_t* stile;             // per tile: its visible UTF-8 in slot order (kTileBytes each)
+    uint32_t* plist;            // per tile (kScanTile each): the parents of its non-seq items in
+                                //   slot order (k_jumps reads them, k_runs reads them back)
     uint8_t* sbytes;            // the wave's visible UTF-8 in slot order (= weight order)
     uint64_t sbytes_cap;
     uint2* tile_hw;             // per tile {heads, weight}: totals, then exclusive prefixes
@@ -221,7 +223,9 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
 //  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
-//    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG.
+//    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG;
+//  * the parents themselves, in slot order, to the tile's plist segment: every non-seq item is
+//    a run head, and k_runs reads its parent there (coalesced) instead of gathering it.
 constexpr uint32_t kJumpBlock = kScanTile / 64;
 constexpr uint32_t kJumpList = 1024;  // (the LDS list's size: 2 KiB keeps 8 waves per SIMD)
 __global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
@@ -251,15 +255,19 @@ __global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
     __syncthreads();  // jl cleared, list and records written
     uint32_t bad = 0;
     // listed: item q of the list at t + 64 j; else this thread's own items, four at a time
+    uint32_t* pl = a.plist + t0;
+    uint32_t own = inc - c;  // (unlisted: the list index of this thread's next item)
     for (uint32_t t = listed ? lane : 0u; listed ? t < T : need != 0ull;
          t += 4u * kJumpBlock) {
-        uint32_t o[4], p[4];
+        uint32_t o[4], p[4], q[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t q = t + (uint32_t)j * kJumpBlock;
             if (listed) {
-                o[j] = q < T ? lst[q] : 0xFFFFu;
+                q[j] = t + (uint32_t)j * kJumpBlock;
+                o[j] = q[j] < T ? lst[q[j]] : 0xFFFFu;
             } else {
+                q[j] = own;
+                own += need ? 1u : 0u;
                 o[j] = need ? lane * 64u + (uint32_t)__builtin_ctzll(need) : 0xFFFFu;
                 need &= need - 1ull;
             }
@@ -269,6 +277,7 @@ __global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (o[j] == 0xFFFFu) continue;
+            pl[q[j]] = p[j];
             const uint2 d = ldoc[o[j] >> 6];
             if (p[j] > d.y || p[j] == t0 + o[j] - d.x) {
                 bad = 1u;
@@ -402,10 +411,12 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     __shared__ uint32_t rec[kScanTile];
     __shared__ uint16_t lnsq[kBlock];  // nsq bits of every thread's 16 slots
     __shared__ uint2 ldoc[kBlock];     // every thread's document {base slot, items}
+    __shared__ uint32_t lsq[NW];
+    __shared__ uint16_t lnpf[kBlock];  // non-seq items of the tile before every thread
     const uint32_t tile = blockIdx.x;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
-    uint32_t hm = 0;
+    uint32_t hm = 0, nsq = 0;
     uint64_t nib = 0;
     uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
@@ -414,7 +425,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
         nib = a.wnib[gs >> 4];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        lnsq[threadIdx.x] = a.nsqb[gs >> 4];
+        nsq = a.nsqb[gs >> 4];
+        lnsq[threadIdx.x] = (uint16_t)nsq;
     }
     ldoc[threadIdx.x] = doc;
     // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
@@ -432,15 +444,21 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     for (int j = 0; j < 16; ++j) W += (uint32_t)(nib >> (4 * j)) & 15u;
     const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;
     const uint32_t inc = wave_incl_scan(x);
-    if (lane == 63u) lsum[wv] = inc;
+    const uint32_t cq = (uint32_t)__popc(nsq), incq = wave_incl_scan(cq);
+    if (lane == 63u) {
+        lsum[wv] = inc;
+        lsq[wv] = incq;
+    }
     __syncthreads();
-    uint32_t off = 0, tot = 0;
+    uint32_t off = 0, tot = 0, offq = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
         const uint32_t v = lsum[i];
         off += (i < (int)wv) ? v : 0u;
+        offq += (i < (int)wv) ? lsq[i] : 0u;
         tot += v;
     }
+    lnpf[threadIdx.x] = (uint16_t)(offq + incq - cq);
     const uint32_t ex = off + inc - x;
     const uint32_t nh = tot >> 16;
     const uint32_t tw_all = tot & 0xFFFFu;
@@ -491,14 +509,18 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const bool root = g == dc.x;
         const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
         const uint64_t key = a.in_key[g];
-        uint32_t p = (!sq && !root) ? a.in_parent[g] : 0u;
+        // a non-seq head's parent from the tile's list: its index = the non-seq items before it
+        const uint32_t nw = lnsq[li >> 4];
+        uint32_t p = (!sq && !root)
+                         ? a.plist[tbase + lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u))]
+                         : 0u;
         a.r_head[rho] = g;
         a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
         uint32_t pr = kNil;
         if (sq) {
             pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
         } else if (!root) {
-            if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
+            if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_jumps
             const uint32_t ps = dc.x + p;
             const uint4 hr = a.hrec[ps >> 6];
             const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
@@ -2155,7 +2177,7 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
+    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
@@ -2382,7 +2404,7 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_);
+        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
@@ -2391,6 +2413,7 @@ int Engine::ensure_scratch(const Wave& w) {
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
         HIPCHK(dalloc(&hrec_, slots / 64 + 2), "hipMalloc head records");
         HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
+        HIPCHK(dalloc(&plist_, tiles * kScanTile), "hipMalloc parent lists");
         HIPCHK(dalloc(&tile_hw_, tiles), "hipMalloc tile totals");
         HIPCHK(dalloc(&tile_sums_, tiles / kScanTile + 2), "hipMalloc tile sums");
         cap_slots0_ = slots;
@@ -2556,6 +2579,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.nsqb = nsqb_;                                                \
     a0.wnib = wnib_;                                                \
     a0.stile = stile_;                                              \
+    a0.plist = plist_;                                              \
     a0.sbytes = sbytes_;                                            \
     a0.sbytes_cap = cap_sbytes_ - 64;                               \
     a0.tile_hw = tile_hw_;                                          \

@@ -184,6 +184,7 @@ private:
     uint64_t* wnib_ = nullptr;
     uint4* hrec_ = nullptr;
     uint8_t *stile_ = nullptr, *sbytes_ = nullptr;
+    uint32_t* plist_ = nullptr;
     uint2 *tile_hw_ = nullptr, *tile_sums_ = nullptr;
     uint64_t cap_sbytes_ = 0;
     // per document
