@@ -60,7 +60,7 @@ MIN_B_PER_TEXT = 1.0
 # Per-kernel algorithmic bytes: each kernel's declared inputs read once +
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
-    "classify": (3.875, 8.0, 1.0),   # 3-byte cp|flags, parents of unflagged items read + listed (k_jumps); seq bits, weight nibbles; tile UTF-8
+    "classify": (3.75, 8.0, 1.0),    # 3-byte cp|flags; nsq bits, weight nibbles, jump bits; parents of the nsq items read + listed; tile UTF-8
     # head/seq bits, nibbles; per run: key + parent slot + rank lookup in, record row out; text move
     "runs": (0.75, 38.0, 2.0),
     "count": (0.0, 8.0, 0.0),
@@ -74,7 +74,7 @@ KERNEL_BYTES = {
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out
 }
-STAGE_KERNEL = {"classify": "k_classify+k_jumps", "runs": "k_runs",
+STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs",
                 "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
 # HBM bytes per item of each kernel from rocprofv3 PMC passes of this build (FETCH_SIZE x2 for
 # gfx950 wide reads + WRITE_SIZE, one pass each: tools/profile.sh + tools/pmc_summary.py).
@@ -84,7 +84,7 @@ COUNTERS = ["patches", "items", "runs", "text_bytes", "docs", "elapsed_ns", "dev
 
 
 # kernels whose PMC traffic makes up a stage's (the stage clock times them together)
-STAGE_PMC_KERNELS = {"classify": ["k_clear", "k_classify", "k_jumps"]}
+STAGE_PMC_KERNELS = {"classify": ["k_clear", "k_classify"]}
 
 
 def measured_traffic(stage: str, items_per_launch: float):

@@ -13,8 +13,8 @@
 //  in a rank bitvector (1 bit/slot + a u32 rank per 64 slots) and every run gets its parent run,
 //  its key (lamport, agent of the head) and its weight (visible UTF-8 bytes).
 //    k_classify    non-seq item bits (from the codepoint column's previous-slot flags), weight
-//                  nibbles, each tile's UTF-8 compacted in slot order
-//    k_jumps       jump bits from the parents of the non-seq items
+//                  nibbles, each tile's UTF-8 compacted in slot order; jump bits and the
+//                  tile's parent list from the parents of its non-seq items
 //    k_heads       head bitvector words, per-tile head counts
 //    k_tiles_*     exclusive scan of the per-tile (heads, weight) pairs
 //    k_runs        run records (head slot, weight prefix, key, parent run by rank lookup),
@@ -115,7 +115,7 @@ struct L0Args {
     uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
     uint8_t* stile;             // per tile: its visible UTF-8 in slot order (kTileBytes each)
     uint32_t* plist;            // per tile (kScanTile each): the parents of its non-seq items in
-                                //   slot order (k_jumps reads them, k_runs reads them back)
+                                //   slot order (k_classify reads them, k_runs reads them back)
     uint8_t* sbytes;            // the wave's visible UTF-8 in slot order (= weight order)
     uint64_t sbytes_cap;
     uint2* tile_hw;             // per tile {heads, weight}: totals, then exclusive prefixes
@@ -136,31 +136,43 @@ struct L0Args {
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 
 // k_classify: the characters of 16 slots per thread (3 x 16-byte loads of the codepoint column:
-// codepoint, tombstone, "parent is the previous slot" flag).
-//  * "item whose parent is not the previous slot" bits (one u16 store per thread), straight from
-//    the flags;
+// codepoint, tombstone, "parent is the previous slot" flag), then the parents of the tile's
+// items without the flag (a few percent):
+//  * "item whose parent is not the previous slot" (nsq) bits, one u16 store per thread;
 //  * per-slot weights as nibbles, the tile's weight total, and the tile's visible UTF-8
-//    compacted in slot order: assembled in LDS, stored to its stile segment in 16-byte pieces.
-// No parent is read here: the parents of the slots without the flag (a few percent) are k_jumps'
-// work, so this stream reads 3 bytes per slot and waits for one round trip.
+//    compacted in slot order: assembled in LDS, stored to its stile segment in 16-byte pieces;
+//  * the nsq items listed in LDS in slot order (the text stage's LDS, once stored) and their
+//    parents read by the whole block, four loads per thread in flight at a time (the items
+//    cluster; listing them spreads the loads over the block);
+//  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
+//    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
+//  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
+//    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG;
+//  * the parents themselves, in slot order, to the tile's plist segment: every nsq item is a run
+//    head, and k_runs reads its parent there (coalesced) instead of gathering it.
+// The stream part reads 3 bytes per slot and waits for one round trip; the parent part is one
+// more round trip at the end of the block, hidden behind the other blocks' streams.
 __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint32_t lds[kBlock / 64];
+    __shared__ uint32_t jl[kScanTile / 32];
+    __shared__ uint2 ldoc[kBlock];  // per thread: its document {base slot, items}
     __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes];
     const uint32_t tile = blockIdx.x;
-    const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
+    const uint32_t t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
     const bool live = gs < a.nslots;
+    if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
     // the codepoint column first (its address does not wait for the document lookup); padding
     // slots hold junk and are masked below
     uint4 cq[3] = {};
-    uint32_t n = 0, l0 = 0;
+    uint2 doc = make_uint2(0, 0);
     if (live) {
         const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B, 16-aligned
 #pragma unroll
         for (int q = 0; q < 3; ++q) cq[q] = cv[q];
-        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        n = doc.y;
-        l0 = gs - doc.x;
+        doc = a.docs[a.chunk_doc[gs >> a.log2m]];
     }
+    const uint32_t n = doc.y, l0 = gs - doc.x;
+    ldoc[threadIdx.x] = doc;
     // the 16 three-byte values from 12 dwords (constant shifts: value k at byte 3k)
     const uint32_t CW[13] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z,
                              cq[1].w, cq[2].x, cq[2].y, cq[2].z, cq[2].w, 0u};
@@ -187,10 +199,12 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
         a.wnib[gs >> 4] = nib;
     }
-    uint32_t tw;
-    const uint32_t ex = block_excl_scan<kBlock / 64>(W, lds, tw);
+    // one scan for both: nsq items << 16 | weight (a tile holds at most 4096 and 16,384)
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<kBlock / 64>(((uint32_t)__popc(nsq) << 16) | W, lds, tot);
+    const uint32_t tw = tot & 0xFFFFu, T = tot >> 16;
     if (a.mode == 0 && W) {
-        uint8_t* o = sb + ex;
+        uint8_t* o = sb + (ex & 0xFFFFu);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t L = (uint32_t)(nib >> (4 * k)) & 15u, c = C[k] & kCpMask;
@@ -212,73 +226,31 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         const uint4* src = reinterpret_cast<const uint4*>(sb);
         for (uint32_t i = threadIdx.x; i < (tw + 15u) / 16u; i += kBlock) dst[i] = src[i];
     }
-}
-
-// k_jumps: the parents of the items without the previous-slot flag (k_classify's nsq bits), one
-// wave per tile.  Each thread reads the nsq word of 64 slots (inside one document) and, if it
-// has any, its document record; the tile's items are listed in LDS in slot order and their
-// parents read by the whole wave, four loads per thread in flight at a time (the items cluster:
-// without the list one thread could hold 64 of them; a tile with more than kJumpList of them,
-// rare, has each thread read its own):
-//  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
-//    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
-//  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
-//    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG;
-//  * the parents themselves, in slot order, to the tile's plist segment: every non-seq item is
-//    a run head, and k_runs reads its parent there (coalesced) instead of gathering it.
-constexpr uint32_t kJumpBlock = kScanTile / 64;
-constexpr uint32_t kJumpList = 1024;  // (the LDS list's size: 2 KiB keeps 8 waves per SIMD)
-__global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
-    __shared__ uint32_t jl[kScanTile / 32];
-    __shared__ uint16_t lst[kJumpList];  // tile offsets of the items, in slot order
-    __shared__ uint2 ldoc[kJumpBlock];   // per thread: its document {base slot, items}
-    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
-    const uint32_t t0 = tile * kScanTile, gs = t0 + lane * 64u;
-    jl[lane] = 0;
-    jl[lane + kJumpBlock] = 0;
-    uint64_t need = 0;
-    uint32_t di = 0;
-    if (gs < a.nslots) {  // the bits and the chunk's document index together
-        need = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
-        di = a.chunk_doc[gs >> a.log2m];
+    if (T == 0) {  // (block-uniform) no nsq item: no jump bit from this tile
+        if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = 0u;
+        return;
     }
-    uint2 doc = make_uint2(0, 0);
-    if (need) doc = a.docs[di];
-    ldoc[lane] = doc;
-    const uint32_t c = (uint32_t)__popcll(need);
-    const uint32_t inc = wave_incl_scan(c);
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    const bool listed = T <= kJumpList;  // (wave-uniform)
-    if (listed)
-        for (uint32_t i = inc - c; need; need &= need - 1ull)
-            lst[i++] = (uint16_t)(lane * 64u + (uint32_t)__builtin_ctzll(need));
-    __syncthreads();  // jl cleared, list and records written
+    __syncthreads();  // the text stage is stored: its LDS holds the list
+    uint16_t* lst = reinterpret_cast<uint16_t*>(sb);
+    for (uint32_t i = ex >> 16; nsq; nsq &= nsq - 1u)
+        lst[i++] = (uint16_t)(threadIdx.x * kScanItems + (uint32_t)__builtin_ctz(nsq));
+    __syncthreads();
     uint32_t bad = 0;
-    // listed: item q of the list at t + 64 j; else this thread's own items, four at a time
     uint32_t* pl = a.plist + t0;
-    uint32_t own = inc - c;  // (unlisted: the list index of this thread's next item)
-    for (uint32_t t = listed ? lane : 0u; listed ? t < T : need != 0ull;
-         t += 4u * kJumpBlock) {
-        uint32_t o[4], p[4], q[4];
+    for (uint32_t t = threadIdx.x; t < T; t += 4u * kBlock) {
+        uint32_t o[4], p[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (listed) {
-                q[j] = t + (uint32_t)j * kJumpBlock;
-                o[j] = q[j] < T ? lst[q[j]] : 0xFFFFu;
-            } else {
-                q[j] = own;
-                own += need ? 1u : 0u;
-                o[j] = need ? lane * 64u + (uint32_t)__builtin_ctzll(need) : 0xFFFFu;
-                need &= need - 1ull;
-            }
+            const uint32_t q = t + (uint32_t)j * kBlock;
+            o[j] = q < T ? lst[q] : 0xFFFFu;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) p[j] = o[j] != 0xFFFFu ? a.in_parent[t0 + o[j]] : 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (o[j] == 0xFFFFu) continue;
-            pl[q[j]] = p[j];
-            const uint2 d = ldoc[o[j] >> 6];
+            pl[t + (uint32_t)j * kBlock] = p[j];
+            const uint2 d = ldoc[o[j] / kScanItems];
             if (p[j] > d.y || p[j] == t0 + o[j] - d.x) {
                 bad = 1u;
             } else {
@@ -291,8 +263,7 @@ __global__ __launch_bounds__(kJumpBlock) void k_jumps(L0Args a) {
         }
     }
     __syncthreads();
-    a.jloc[tile * (kScanTile / 32) + lane] = jl[lane];
-    a.jloc[tile * (kScanTile / 32) + kJumpBlock + lane] = jl[kJumpBlock + lane];
+    if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
@@ -520,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         if (sq) {
             pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
         } else if (!root) {
-            if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_jumps
+            if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
             const uint32_t ps = dc.x + p;
             const uint4 hr = a.hrec[ps >> 6];
             const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
@@ -2626,7 +2597,6 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
     k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
     MARK(-1);
     k_classify<<<ntiles, kBlock, 0, s>>>(a0);
-    k_jumps<<<ntiles, kJumpBlock, 0, s>>>(a0);
     MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
