@@ -113,6 +113,7 @@ struct L0Args {
     uint16_t* nsqb;             // per slot bit, 16 per thread: an item whose parent is not the
                                 //   previous slot (no previous-slot flag)
     uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
+    uint16_t* visb;             // per slot bit, 16 per thread: an item with a nonzero weight
     uint8_t* stile;             // per tile: its visible UTF-8 in slot order (kTileBytes each)
     uint32_t* plist;            // per tile (kScanTile each): the parents of its non-seq items in
                                 //   slot order (k_classify reads them, k_runs reads them back)
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         C[k] = (lo | hi) & 0x00FFFFFFu;
     }
     // branch-free classification of the 16 slots; weights straight into their nibbles
-    uint32_t nsq = 0, W = 0;
+    uint32_t nsq = 0, W = 0, vis = 0;
     uint64_t nib = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -194,10 +195,12 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         W += w;
         nib |= (uint64_t)w << (4 * k);
         nsq |= (it && !(C[k] & kSeqBit) ? 1u : 0u) << k;
+        vis |= (w ? 1u : 0u) << k;
     }
     if (live) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
         a.wnib[gs >> 4] = nib;
+        a.visb[gs >> 4] = (uint16_t)vis;
     }
     // one scan for both: nsq items << 16 | weight (a tile holds at most 4096 and 16,384)
     uint32_t tot;
@@ -277,15 +280,27 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 // each word inside its tile (hrec .z), so that the run of any slot s is
 // tile_hw[s / 4096].x + hrec[s / 64].z + popcount(bits of hrec[s / 64] up to s) - 1 once the tile
 // prefixes are scanned.
+// Dead runs are dropped here: a run none of whose items is visible and whose last item has no
+// child adds nothing to the document and is nobody's parent (on the traces 40-50 % of the runs:
+// typed-then-deleted text).  Its items are "live" neither by weight nor by a jump bit (inside a
+// run only the last item can have a non-consecutive child, and a last item has a child at all
+// only through its jump bit), so a head survives iff a live slot lies between it and the next
+// head: a segmented OR, smeared down from every live slot to the head of its run in six
+// shift steps.  A run that goes on into the next word takes that word's live slots before its
+// first head (the next lane's word; the last lane of the wave, or a word without a head, keeps
+// the run).  Without its head the dead run's items count as the previous run's, which changes
+// nothing: they weigh nothing, and no parent lookup lands on them.  Nothing else moves: seq heads
+// still follow their parent's run (rho - 1), whose last item is live by its jump bit.
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
-    uint64_t hw = 0;
+    uint64_t hw = 0, lv = 0;
     if (gs < a.nslots) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         const uint32_t l0 = gs - doc.x, n = doc.y;
         if (l0 <= n) {
             const uint64_t nsq = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
+            const uint64_t vis = *reinterpret_cast<const uint64_t*>(a.visb + (gs >> 4));
             const uint2 jr = *reinterpret_cast<const uint2*>(a.jbits + (gs >> 5));
             const uint2 jq = *reinterpret_cast<const uint2*>(a.jloc + (gs >> 5));
             const uint64_t jw = ((uint64_t)(jr.y | jq.y) << 32) | (uint64_t)(jr.x | jq.x);
@@ -295,7 +310,23 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint64_t item = low_mask64(n + 1u - l0) & ~low_mask64(l0 == 0 ? 1u : 0u);
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
             hw = root | (item & (nsq | prevj));
+            lv = root | vis | (item & jw);
         }
+    }
+    {
+        // the next word's live slots before its first head keep this word's last run
+        const uint64_t hn = (uint64_t)__shfl_down((long long)hw, 1);
+        const uint64_t ln = (uint64_t)__shfl_down((long long)lv, 1);
+        const bool carry = (threadIdx.x & 63u) == 63u || hn == 0ull ||
+                           (ln & low_mask64((uint32_t)__builtin_ctzll(hn))) != 0ull;
+        uint64_t z = lv | (carry ? (1ull << 63) : 0ull);
+        uint64_t pm = ~(hw >> 1);  // bit i: slot i + 1 is not a head (the OR may pass down)
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            z |= (z >> k) & pm;
+            pm &= pm >> k;
+        }
+        hw &= z;
     }
     const uint32_t c = (uint32_t)__popcll(hw);
     const uint32_t inc = wave_incl_scan(c);
@@ -2148,7 +2179,7 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
+    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
@@ -2375,13 +2406,14 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
+        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
         HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
         HIPCHK(dalloc(&nsqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
+        HIPCHK(dalloc(&visb_, slots / 16 + 4), "hipMalloc visible bits");
         HIPCHK(dalloc(&hrec_, slots / 64 + 2), "hipMalloc head records");
         HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
         HIPCHK(dalloc(&plist_, tiles * kScanTile), "hipMalloc parent lists");
@@ -2549,6 +2581,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.jloc = jloc_;                                                \
     a0.nsqb = nsqb_;                                                \
     a0.wnib = wnib_;                                                \
+    a0.visb = visb_;                                                \
     a0.stile = stile_;                                              \
     a0.plist = plist_;                                              \
     a0.sbytes = sbytes_;                                            \
