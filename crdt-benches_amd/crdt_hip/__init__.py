@@ -30,7 +30,8 @@ STAGES = ["classify", "runs", "run_parent", "count", "scan", "place", "link", "w
 # Every symbol include/crdt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "crdt_hip_abi_version", "crdt_hip_device_count", "crdt_hip_init", "crdt_hip_destroy",
-    "crdt_hip_last_error", "crdt_hip_set_param", "crdt_hip_oplog_new", "crdt_hip_oplog_clone",
+    "crdt_hip_last_error", "crdt_hip_set_param", "crdt_hip_oplog_new", "crdt_hip_oplog_set_fugue",
+    "crdt_hip_oplog_clone", "crdt_hip_trace_resolve_fugue",
     "crdt_hip_oplog_free", "crdt_hip_oplog_insert", "crdt_hip_oplog_remove",
     "crdt_hip_oplog_replace", "crdt_hip_oplog_visible_len", "crdt_hip_oplog_get_view",
     "crdt_hip_oplog_version", "crdt_hip_oplog_encode_from", "crdt_hip_oplog_apply_update",
@@ -67,6 +68,7 @@ class View(C.Structure):
         ("agent", C.POINTER(C.c_uint16)),
         ("deleted", C.POINTER(C.c_uint8)),
         ("cp", C.POINTER(C.c_uint32)),
+        ("side", C.POINTER(C.c_uint8)),  # Fugue (NULL: RGA)
     ]
 
 
@@ -114,6 +116,7 @@ def lib() -> C.CDLL:
         "crdt_hip_last_error": (C.c_char_p, [vp]),
         "crdt_hip_set_param": (i32, [vp, C.c_char_p, u64]),
         "crdt_hip_oplog_new": (i32, [P(vp)]),
+        "crdt_hip_oplog_set_fugue": (i32, [vp, i32]),
         "crdt_hip_oplog_clone": (i32, [vp, P(vp)]),
         "crdt_hip_oplog_free": (None, [vp]),
         "crdt_hip_oplog_insert": (i32, [vp, sz, C.c_char_p, sz]),
@@ -133,6 +136,7 @@ def lib() -> C.CDLL:
         "crdt_hip_trace_end_content": (i32, [vp, P(vp), P(sz)]),
         "crdt_hip_trace_chars_to_bytes": (i32, [vp]),
         "crdt_hip_trace_resolve": (i32, [vp, P(vp)]),
+        "crdt_hip_trace_resolve_fugue": (i32, [vp, P(vp)]),
         "crdt_hip_trace_resolve_many": (i32, [P(vp), u32, u32, P(vp)]),
         "crdt_hip_trace_save": (i32, [vp, C.c_char_p]),
         "crdt_hip_oplog_save": (i32, [vp, C.c_char_p]),
@@ -199,11 +203,12 @@ def tree_digest(data: bytes) -> int:
 
 # ------------------------------------------------------------------------------------------------
 class LogArrays:
-    """Anchor op log as numpy SoA (ids 1..n).  Keeps the arrays alive for a View."""
+    """Anchor op log as numpy SoA (ids 1..n).  Keeps the arrays alive for a View.  `side`
+    (optional): 1 = the item is a LEFT child of its parent (Fugue order); None = RGA."""
 
     FIELDS = ("parent", "origin_right", "lamport", "agent", "deleted", "cp")
 
-    def __init__(self, parent, lamport, agent, deleted, cp, origin_right=None):
+    def __init__(self, parent, lamport, agent, deleted, cp, origin_right=None, side=None):
         self.parent = np.ascontiguousarray(parent, dtype=np.uint32)
         n = self.parent.size
         self.lamport = np.ascontiguousarray(lamport, dtype=np.uint32)
@@ -212,8 +217,10 @@ class LogArrays:
         self.cp = np.ascontiguousarray(cp, dtype=np.uint32)
         self.origin_right = (np.full(n, 0xFFFFFFFF, np.uint32) if origin_right is None
                              else np.ascontiguousarray(origin_right, dtype=np.uint32))
+        self.side = None if side is None else np.ascontiguousarray(side, dtype=np.uint8)
         for f in self.FIELDS:
             assert getattr(self, f).size == n, f
+        assert self.side is None or self.side.size == n
 
     @property
     def n(self) -> int:
@@ -222,23 +229,27 @@ class LogArrays:
     def view(self) -> View:
         def p(a, t):
             return a.ctypes.data_as(C.POINTER(t)) if a.size else None
+        side = None if self.side is None else p(self.side, C.c_uint8)
         return View(self.n, p(self.parent, C.c_uint32), p(self.origin_right, C.c_uint32),
                     p(self.lamport, C.c_uint32), p(self.agent, C.c_uint16),
-                    p(self.deleted, C.c_uint8), p(self.cp, C.c_uint32))
+                    p(self.deleted, C.c_uint8), p(self.cp, C.c_uint32), side)
 
     def copy(self) -> "LogArrays":
         return LogArrays(self.parent.copy(), self.lamport.copy(), self.agent.copy(),
-                         self.deleted.copy(), self.cp.copy(), self.origin_right.copy())
+                         self.deleted.copy(), self.cp.copy(), self.origin_right.copy(),
+                         None if self.side is None else self.side.copy())
 
 
 class OpLog:
     """Host-side resolver (positional patches -> anchor op log), crdt_hip_oplog_*."""
 
-    def __init__(self, handle=None):
+    def __init__(self, handle=None, fugue: bool = False):
         if handle is None:
             h = C.c_void_p()
             _check(lib().crdt_hip_oplog_new(C.byref(h)))
             handle = h
+            if fugue:
+                _check(lib().crdt_hip_oplog_set_fugue(h, 1))
         self._h = handle
 
     def __del__(self):
@@ -278,9 +289,12 @@ class OpLog:
             if n == 0:
                 return np.zeros(0, dt)
             return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
+        side = None
+        if v.side:
+            side = arr(v.side, np.uint8)
         return LogArrays(arr(v.parent, np.uint32), arr(v.lamport, np.uint32),
                          arr(v.agent, np.uint16), arr(v.deleted, np.uint8),
-                         arr(v.cp, np.uint32), arr(v.origin_right, np.uint32))
+                         arr(v.cp, np.uint32), arr(v.origin_right, np.uint32), side)
 
     def version(self) -> int:
         return int(lib().crdt_hip_oplog_version(self._h))
@@ -365,9 +379,11 @@ class Trace:
     def chars_to_bytes(self) -> None:
         _check(lib().crdt_hip_trace_chars_to_bytes(self._h))
 
-    def resolve(self) -> OpLog:
+    def resolve(self, fugue: bool = False) -> OpLog:
+        """Positional patches -> anchor op log (RGA anchors; `fugue`: Fugue anchors)."""
         h = C.c_void_p()
-        _check(lib().crdt_hip_trace_resolve(self._h, C.byref(h)))
+        fn = lib().crdt_hip_trace_resolve_fugue if fugue else lib().crdt_hip_trace_resolve
+        _check(fn(self._h, C.byref(h)))
         return OpLog(h)
 
     @staticmethod

@@ -216,6 +216,12 @@ int crdt_hip_oplog_new(crdt_hip_oplog** out) {
     if (!out) return set_err(nullptr, CRDT_HIP_EINVAL, "null out");
     return guard(nullptr, [&] { *out = new crdt_hip_oplog(); return 0; });
 }
+int crdt_hip_oplog_set_fugue(crdt_hip_oplog* log, int on) {
+    if (!log) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    if (log->log.size()) return set_err(nullptr, CRDT_HIP_EINVAL, "set_fugue needs an empty log");
+    log->log.fugue = on != 0;
+    return 0;
+}
 int crdt_hip_oplog_clone(const crdt_hip_oplog* src, crdt_hip_oplog** out) {
     if (!src || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
     return guard(nullptr, [&] { *out = new crdt_hip_oplog(*src); return 0; });
@@ -257,6 +263,7 @@ int crdt_hip_oplog_get_view(const crdt_hip_oplog* log, crdt_hip_oplog_view* out)
     out->agent = L.agent.data();
     out->deleted = L.deleted.data();
     out->cp = L.cp.data();
+    out->side = L.fugue ? L.side.data() : nullptr;
     return 0;
 }
 uint64_t crdt_hip_oplog_version(const crdt_hip_oplog* log) { return log ? log->log.version() : 0; }
@@ -264,6 +271,7 @@ uint64_t crdt_hip_oplog_version(const crdt_hip_oplog* log) { return log ? log->l
 int crdt_hip_oplog_encode_from(const crdt_hip_oplog* log, uint64_t version, uint8_t* buf,
                                size_t cap, size_t* out_len) {
     if (!log || !out_len) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    if (log->log.fugue) return set_err(nullptr, CRDT_HIP_EINVAL, "Fugue logs have no update wire format");
     return guard(nullptr, [&] {
         std::vector<uint8_t> u = log->log.encode_from(version);
         *out_len = u.size();
@@ -274,6 +282,7 @@ int crdt_hip_oplog_encode_from(const crdt_hip_oplog* log, uint64_t version, uint
 }
 int crdt_hip_oplog_apply_update(crdt_hip_oplog* log, const uint8_t* buf, size_t len) {
     if (!log || (!buf && len)) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    if (log->log.fugue) return set_err(nullptr, CRDT_HIP_EINVAL, "Fugue logs have no update wire format");
     return guard(nullptr, [&] {
         std::string e = log->log.apply_update(buf, len);
         return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EINVAL, e);
@@ -328,13 +337,24 @@ int crdt_hip_trace_chars_to_bytes(crdt_hip_trace* t) {
         return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_ERANGE, e);
     });
 }
+namespace {
+int trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out, bool fugue);
+}
 int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out) {
+    return trace_resolve(t, out, false);
+}
+int crdt_hip_trace_resolve_fugue(const crdt_hip_trace* t, crdt_hip_oplog** out) {
+    return trace_resolve(t, out, true);
+}
+namespace {
+int trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out, bool fugue) {
     if (!t || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
     if (t->t.byte_offsets)
         return set_err(nullptr, CRDT_HIP_EINVAL, "resolve needs codepoint offsets (EDITS_USE_BYTE_OFFSETS = false)");
     *out = nullptr;
     return guard(nullptr, [&] {
         crdt_hip_oplog* L = new crdt_hip_oplog();
+        L->log.fugue = fugue;
         const crdt::Trace& T = t->t;
         std::string e;
         size_t ins_bytes = T.start_content.size(), dels = 0;
@@ -359,6 +379,7 @@ int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out) {
         return 0;
     });
 }
+}  // namespace
 
 int crdt_hip_trace_resolve_many(const crdt_hip_trace* const* traces, uint32_t n, uint32_t threads,
                                 crdt_hip_oplog** out) {
@@ -408,6 +429,7 @@ int crdt_hip_trace_save(const crdt_hip_trace* t, const char* path) {
 }
 int crdt_hip_oplog_save(const crdt_hip_oplog* log, const char* path) {
     if (!log || !path) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    if (log->log.fugue) return set_err(nullptr, CRDT_HIP_EINVAL, "the op-log file format has no side column");
     return guard(nullptr, [&] {
         std::string e = crdt::save_oplog(log->log, path);
         return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EIO, e);
@@ -444,6 +466,7 @@ int crdt_hip_logfile_open(const char* path, crdt_hip_logfile** out, crdt_hip_opl
         view->agent = f->m.agent;
         view->deleted = f->m.deleted;
         view->cp = f->m.cp;
+        view->side = nullptr;
         *out = f;
         return 0;
     });
@@ -616,6 +639,8 @@ int crdt_hip_replica_new(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* init,
                          crdt_hip_replica** out) {
     if (!ctx || !out) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
     *out = nullptr;
+    if (init && init->side)
+        return set_err(ctx, CRDT_HIP_EINVAL, "Fugue logs have no update wire format (replicas are RGA)");
     if (init) {
         int rc = check_view(ctx, init);
         if (rc) return rc;

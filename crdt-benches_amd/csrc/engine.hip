@@ -114,6 +114,9 @@ struct L0Args {
                                 //   previous slot (no previous-slot flag)
     uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
     uint16_t* visb;             // per slot bit, 16 per thread: an item with a nonzero weight
+    uint32_t* lbits;            // Fugue: per slot bit, has a left child (its run gets a content
+                                //   node; see k_runs)
+    uint32_t fugue;             // the wave holds Fugue logs (left children)
     uint8_t* stile;             // per tile: its visible UTF-8 in slot order (kTileBytes each)
     uint32_t* plist;            // per tile (kScanTile each): the parents of its non-seq items in
                                 //   slot order (k_classify reads them, k_runs reads them back)
@@ -135,6 +138,19 @@ struct L0Args {
 };
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
+// Fugue (left children).  A run whose head has left children is numbered as two rows: a content
+// row (the run's text, weight only) and then its tree row (no weight; its parent, key and every
+// child: the head's left children, the content row, the last item's right children).  The
+// content row sorts between the two sides: left children carry kLeftKey in their key (bit 48),
+// the content row kMidKey, right children neither; siblings sort by key descending, so the
+// weighted pre-order of the rows is the Fugue in-order (lamport < 0xFFFFFFFF).  The tree row is
+// the last row of its run, so "the run of slot s" (a rank lookup) and "the previous run" of a seq
+// head both land on it.
+constexpr uint64_t kLeftKey = 1ull << 48;
+// words of the jump bitvector of a wave (a multiple of 4: the left-child bits follow it aligned)
+__host__ __device__ constexpr uint64_t jbits_words(uint64_t slots) { return (slots / 32 + 8 + 3) & ~3ull; }
+constexpr uint64_t kMidKey = (1ull << 48) - 1ull;
+constexpr uint32_t kRecContent = 1u << 30, kRecTree = 1u << 31;
 
 // k_classify: the characters of 16 slots per thread (3 x 16-byte loads of the codepoint column:
 // codepoint, tombstone, "parent is the previous slot" flag), then the parents of the tile's
@@ -185,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         C[k] = (lo | hi) & 0x00FFFFFFu;
     }
     // branch-free classification of the 16 slots; weights straight into their nibbles
-    uint32_t nsq = 0, W = 0, vis = 0;
+    uint32_t nsq = 0, W = 0, vis = 0, lm = 0;
     uint64_t nib = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -196,6 +212,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         nib |= (uint64_t)w << (4 * k);
         nsq |= (it && !(C[k] & kSeqBit) ? 1u : 0u) << k;
         vis |= (w ? 1u : 0u) << k;
+        lm |= (it && (C[k] & kLeftBit) ? 1u : 0u) << k;
     }
     if (live) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
@@ -234,9 +251,12 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         return;
     }
     __syncthreads();  // the text stage is stored: its LDS holds the list
+    // list entries: tile-local slot, bit 15 = a left child (Fugue)
     uint16_t* lst = reinterpret_cast<uint16_t*>(sb);
-    for (uint32_t i = ex >> 16; nsq; nsq &= nsq - 1u)
-        lst[i++] = (uint16_t)(threadIdx.x * kScanItems + (uint32_t)__builtin_ctz(nsq));
+    for (uint32_t i = ex >> 16; nsq; nsq &= nsq - 1u) {
+        const uint32_t b = (uint32_t)__builtin_ctz(nsq);
+        lst[i++] = (uint16_t)((threadIdx.x * kScanItems + b) | (((lm >> b) & 1u) << 15));
+    }
     __syncthreads();
     uint32_t bad = 0;
     uint32_t* pl = a.plist + t0;
@@ -248,20 +268,32 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
             o[j] = q < T ? lst[q] : 0xFFFFu;
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] = o[j] != 0xFFFFu ? a.in_parent[t0 + o[j]] : 0u;
+        for (int j = 0; j < 4; ++j) p[j] = o[j] != 0xFFFFu ? a.in_parent[t0 + (o[j] & 0x7FFFu)] : 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (o[j] == 0xFFFFu) continue;
+            const uint32_t oi = o[j] & 0x7FFFu;
             pl[t + (uint32_t)j * kBlock] = p[j];
-            const uint2 d = ldoc[o[j] / kScanItems];
-            if (p[j] > d.y || p[j] == t0 + o[j] - d.x) {
-                bad = 1u;
+            const uint2 d = ldoc[oi / kScanItems];
+            const bool left = (o[j] >> 15) != 0u;
+            if (p[j] > d.y || p[j] == t0 + oi - d.x || (left && p[j] == 0u)) {
+                bad = 1u;  // (the document start has no left children)
             } else {
                 const uint32_t ps = d.x + p[j];
                 if (ps / kScanTile == tile)
                     atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
                 else
                     atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
+                if (left) {
+                    // Fugue: the parent's run node holds its left children, so the parent must
+                    // head its run: a jump bit on the slot before it cuts the run there
+                    atomicOr(&a.lbits[ps >> 5], 1u << (ps & 31u));
+                    const uint32_t pv = ps - 1u;
+                    if (pv / kScanTile == tile)
+                        atomicOr(&jl[(pv % kScanTile) >> 5], 1u << (pv & 31u));
+                    else
+                        atomicOr(&a.jbits[pv >> 5], 1u << (pv & 31u));
+                }
             }
         }
     }
@@ -294,7 +326,7 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
-    uint64_t hw = 0, lv = 0;
+    uint64_t hw = 0, lv = 0, lb = 0;
     if (gs < a.nslots) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         const uint32_t l0 = gs - doc.x, n = doc.y;
@@ -311,6 +343,7 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
             hw = root | (item & (nsq | prevj));
             lv = root | vis | (item & jw);
+            if (a.fugue) lb = *reinterpret_cast<const uint64_t*>(a.lbits + (gs >> 5));
         }
     }
     {
@@ -328,7 +361,8 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
         }
         hw &= z;
     }
-    const uint32_t c = (uint32_t)__popcll(hw);
+    // Fugue: a head with left children numbers two run rows (k_runs)
+    const uint32_t c = (uint32_t)__popcll(hw) + (uint32_t)__popcll(hw & lb);
     const uint32_t inc = wave_incl_scan(c);
     if (gs < a.nslots) a.hrec[wi] = make_uint4((uint32_t)hw, (uint32_t)(hw >> 32), inc - c, 0u);
     const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
@@ -407,10 +441,13 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
 // (tile prefix + hloc + popcount).  Storing the rows from the thread that found each head costs
 // one vector store instruction per head position with lanes scattered over many lines (the
 // address unit, not HBM, bounded that form); one thread per run stores them as contiguous rows.
+// FUGUE: the wave has left children; a tile then holds up to two rows per head (the RGA build
+// keeps its 16 KiB of records and its occupancy).
+template <bool FUGUE>
 __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     constexpr int NW = kBlock / 64;
     __shared__ uint32_t lsum[NW];
-    __shared__ uint32_t rec[kScanTile];
+    __shared__ uint32_t rec[FUGUE ? 2 * kScanTile : kScanTile];
     __shared__ uint16_t lnsq[kBlock];  // nsq bits of every thread's 16 slots
     __shared__ uint2 ldoc[kBlock];     // every thread's document {base slot, items}
     __shared__ uint32_t lsq[NW];
@@ -418,13 +455,14 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     const uint32_t tile = blockIdx.x;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
-    uint32_t hm = 0, nsq = 0;
+    uint32_t hm = 0, nsq = 0, dm = 0;
     uint64_t nib = 0;
     uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
     if (gs < a.nslots) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
+        if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
         nib = a.wnib[gs >> 4];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         nsq = a.nsqb[gs >> 4];
@@ -444,7 +482,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     uint32_t W = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) W += (uint32_t)(nib >> (4 * j)) & 15u;
-    const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;
+    const uint32_t x = ((uint32_t)(__popc(hm) + __popc(dm)) << 16) | W;
     const uint32_t inc = wave_incl_scan(x);
     const uint32_t cq = (uint32_t)__popc(nsq), incq = wave_incl_scan(cq);
     if (lane == 63u) {
@@ -478,7 +516,15 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         uint32_t r = ex >> 16, p = ex & 0xFFFFu;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            if (hm & (1u << j)) rec[r++] = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p;
+            if (hm & (1u << j)) {
+                const uint32_t rv = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p;
+                if (dm & (1u << j)) {  // Fugue: content row, then the run's tree row
+                    rec[r++] = rv | kRecContent;
+                    rec[r++] = rv | kRecTree;
+                } else {
+                    rec[r++] = rv;
+                }
+            }
             p += (uint32_t)(nib >> (4 * j)) & 15u;
         }
     }
@@ -506,7 +552,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     const uint32_t tbase = tile * kScanTile;
     for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
         const uint32_t rv = rec[i];
-        const uint32_t li = rv >> 16, g = tbase + li, rho = pre.x + i;
+        const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li, rho = pre.x + i;
+        const bool content = (rv & kRecContent) != 0u, treerow = (rv & kRecTree) != 0u;
         const uint2 dc = ldoc[li >> 4];
         const bool root = g == dc.x;
         const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
@@ -517,10 +564,16 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
                          ? a.plist[tbase + lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u))]
                          : 0u;
         a.r_head[rho] = g;
-        a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
+        // a tree row weighs nothing: its prefix is the next row's (the content row's end)
+        a.r_pstart[rho] = pre.y + (treerow ? (i + 1u < nh ? rec[i + 1u] & 0xFFFFu : tw_all)
+                                           : (rv & 0xFFFFu));
         uint32_t pr = kNil;
-        if (sq) {
-            pr = rho - 1u;  // the parent is the slot before the head: the previous run's last
+        if (content) {
+            pr = rho + 1u;  // the run's text, a child of its tree row between the left and the
+                            // right children (kMidKey)
+        } else if (sq) {
+            // the parent is the slot before the head: the previous run's last row
+            pr = rho - (treerow ? 2u : 1u);
         } else if (!root) {
             if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
             const uint32_t ps = dc.x + p;
@@ -530,11 +583,16 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             const uint32_t tp = a.tile_hw[ps / kScanTile].x;
             const uint32_t b = ps & 63u;
             const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
-            pr = tp + hl + (uint32_t)__popcll(hb & mask) - 1u;
+            uint32_t rows = (uint32_t)__popcll(hb & mask);
+            if (FUGUE) {  // (rows of the parent slot's run: its tree row is its last)
+                const uint64_t lw = *reinterpret_cast<const uint64_t*>(a.lbits + ((ps >> 5) & ~1u));
+                rows += (uint32_t)__popcll(hb & lw & mask);
+            }
+            pr = tp + hl + rows - 1u;
         }
         if (rho < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
             a.r_parent[rho] = pr;
-            a.r_key[rho] = root ? 0ull : key;
+            a.r_key[rho] = root ? 0ull : (content ? kMidKey : key);
         }
     }
 }
@@ -2124,7 +2182,8 @@ __global__ __launch_bounds__(kBlock) void k_replicate(
             const uint64_t o = dst + lk;
             rp[o] = pk;
             rk[o] = bk[src + k];
-            cp3_put(rc, o, (cp3_get(bc, src + k) & ~kSeqBit) | (pk == lk - 1u ? kSeqBit : 0u));
+            const uint32_t c = cp3_get(bc, src + k);
+            cp3_put(rc, o, (c & ~kSeqBit) | (pk == lk - 1u && !(c & kLeftBit) ? kSeqBit : 0u));
         }
     }
 }
@@ -2386,11 +2445,26 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
     std::vector<uint8_t> c(cp3_bytes(S), 0);
     for (uint64_t g = 0; g < S; ++g) cp3_put(c.data(), g, kDelBit);
     std::vector<uint64_t> key(S, 0);
+    L.fugue = false;
     for (uint32_t d = 0; d < n; ++d) {
         const crdt_hip_oplog_view& v = views[d];
         const uint64_t b = L.doc_slot[d] + 1;
         if (v.n == 0) continue;
         std::memcpy(&par[b], v.parent, v.n * 4ull);
+        if (v.side) {  // Fugue: left children carry kLeftBit / kLeftKey, never the seq flag
+            for (uint32_t i = 0; i < v.n; ++i) {
+                const bool left = v.side[i] != 0;
+                if (v.lamport[i] == 0xFFFFFFFFu) {  // (kMidKey sorts above every right child)
+                    err = "Fugue log with lamport 0xFFFFFFFF";
+                    return CRDT_HIP_EINVAL;
+                }
+                L.fugue |= left;
+                key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i] | (left ? kLeftKey : 0ull);
+                cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
+                                             (left ? kLeftBit : (v.parent[i] == i ? kSeqBit : 0u)));
+            }
+            continue;
+        }
         for (uint32_t i = 0; i < v.n; ++i) {
             key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
             cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
@@ -2409,7 +2483,8 @@ int Engine::ensure_scratch(const Wave& w) {
         dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
-        HIPCHK(dalloc(&jbits_, slots / 32 + 8), "hipMalloc jump bits");
+        // jump bits, then (Fugue) the left-child bits: jbits_words(slots) words each
+        HIPCHK(dalloc(&jbits_, 2 * jbits_words(slots)), "hipMalloc jump bits");
         HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
         HIPCHK(dalloc(&nsqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
@@ -2582,6 +2657,8 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.nsqb = nsqb_;                                                \
     a0.wnib = wnib_;                                                \
     a0.visb = visb_;                                                \
+    a0.lbits = jbits_ + jbits_words(w.nslots);                      \
+    a0.fugue = L.fugue ? 1u : 0u;                                   \
     a0.stile = stile_;                                              \
     a0.plist = plist_;                                              \
     a0.sbytes = sbytes_;                                            \
@@ -2626,7 +2703,8 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
     a0.cap_rmax = cap_rmax;
     const uint32_t ntiles = a0.ntiles;
     const uint32_t nsums = (ntiles + kScanTile - 1) / kScanTile;
-    const uint32_t nq = (uint32_t)((w.nslots / 32 + 4 + 3) / 4);  // jump-bit words, in uint4
+    // jump-bit words (and the left-child bits right after them), in uint4
+    const uint32_t nq = (uint32_t)(jbits_words(w.nslots) / 4) * (L.fugue ? 2u : 1u);
     k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
     MARK(-1);
     k_classify<<<ntiles, kBlock, 0, s>>>(a0);
@@ -2635,7 +2713,10 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
     k_tiles_top<<<1, 1024, 0, s>>>(a0, nsums);
     k_tiles_apply<<<nsums, kBlock, 0, s>>>(a0);
-    k_runs<<<ntiles, kBlock, 0, s>>>(a0);
+    if (L.fugue)
+        k_runs<true><<<ntiles, kBlock, 0, s>>>(a0);
+    else
+        k_runs<false><<<ntiles, kBlock, 0, s>>>(a0);
     k_docmax<<<1, 1024, 0, s>>>(a0);
     MARK(S_RUNS);
     HIPCHK(hipGetLastError(), "level-0 launch");
@@ -2645,7 +2726,10 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_r
 // k_runs alone (run_wave: the run rows did not fit the rows allocated when level 0 ran).
 int Engine::launch_runs(DeviceLogs& L, const Wave& w, bool ord) {
     L0ARGS(a0);
-    k_runs<<<a0.ntiles, kBlock, 0, cur_>>>(a0);
+    if (L.fugue)
+        k_runs<true><<<a0.ntiles, kBlock, 0, cur_>>>(a0);
+    else
+        k_runs<false><<<a0.ntiles, kBlock, 0, cur_>>>(a0);
     HIPCHK(hipGetLastError(), "k_runs launch");
     return CRDT_HIP_OK;
 }
@@ -2808,12 +2892,14 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     const bool ord = mode == ORDER;
     StageClock ck{ev_.data(), 0, {}};
     uint32_t* hctl = host_block(L, wi);
-    // run records are written before the run count is known: runs <= slots
-    if (w.nslots > cap_heads_) {
+    // run records are written before the run count is known: runs <= slots (Fugue: rows <=
+    // 2 slots, a content and a tree row per head with left children)
+    const uint64_t hrows = w.nslots * (L.fugue ? 2ull : 1ull);
+    if (hrows > cap_heads_) {
         dfree(r_head_); dfree(r_pstart_);
-        HIPCHK(dalloc(&r_head_, w.nslots + 64ull), "hipMalloc r_head");
-        HIPCHK(dalloc(&r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
-        cap_heads_ = w.nslots;
+        HIPCHK(dalloc(&r_head_, hrows + 64ull), "hipMalloc r_head");
+        HIPCHK(dalloc(&r_pstart_, hrows + 64ull), "hipMalloc r_pstart");
+        cap_heads_ = hrows;
     }
     // ---- level 0: runs.  Lanes take turns here (an HBM stream): the gate is held from the first
     // level-0 launch to the level-0 sync, so one lane's level 0 overlaps the others' latency-bound
@@ -3003,11 +3089,12 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         if (rc) return rc;
         rc = E.ensure_runs(cr, 0);
         if (rc) return rc;
-        if (w.nslots > E.cap_heads_) {
+        const uint64_t hrows = w.nslots * (L.fugue ? 2ull : 1ull);  // (see run_wave)
+        if (hrows > E.cap_heads_) {
             dfree(E.r_head_); dfree(E.r_pstart_);
-            HIPCHK(dalloc(&E.r_head_, w.nslots + 64ull), "hipMalloc r_head");
-            HIPCHK(dalloc(&E.r_pstart_, w.nslots + 64ull), "hipMalloc r_pstart");
-            E.cap_heads_ = w.nslots;
+            HIPCHK(dalloc(&E.r_head_, hrows + 64ull), "hipMalloc r_head");
+            HIPCHK(dalloc(&E.r_pstart_, hrows + 64ull), "hipMalloc r_pstart");
+            E.cap_heads_ = hrows;
             E.gen_++;
         }
     }
@@ -3250,6 +3337,7 @@ int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t
     docs[0].n = n;
     docs[0].text_cap = n;  // one byte per visible item at most ('a'..'z')
     int rc = plan(R, docs);
+    R.fugue = false;
     if (rc) return rc;
     k_synth_tree<<<grid_for(R.total_slots), kBlock, 0, stream>>>(
         R.parent, R.key, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
@@ -3271,6 +3359,7 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     for (uint32_t b = 0; b < nb; ++b) nmax = std::max(nmax, B.docs[b].n);
     int rc = plan(R, docs);
     if (rc) return rc;
+    R.fugue = B.fugue;
     std::vector<uint32_t> bn(nb);
     for (uint32_t b = 0; b < nb; ++b) bn[b] = B.docs[b].n;
     uint64_t *dbslot = nullptr, *drslot = nullptr;

@@ -63,6 +63,9 @@ struct L1Plan {
 // holds the previous slot; a slot without it has its parent read and classified in full.
 constexpr uint32_t kDelBit = 0x00800000u;
 constexpr uint32_t kSeqBit = 0x00400000u;
+// Fugue: the item is a LEFT child of its parent (bit 21; the previous-slot flag is then never
+// set: a seq item is a right child of the slot before it)
+constexpr uint32_t kLeftBit = 0x00200000u;
 __host__ __device__ inline void cp3_put(uint8_t* b, uint64_t slot, uint32_t v) {
     b[3 * slot] = (uint8_t)v;
     b[3 * slot + 1] = (uint8_t)(v >> 8);
@@ -86,6 +89,8 @@ struct DeviceLogs {
     // device arrays (slot-indexed)
     uint32_t* parent = nullptr;
     uint64_t* key = nullptr;       // the item's id as a sibling key: lamport << 16 | agent
+                                   //   (| 1 << 48 for a Fugue left child)
+    bool fugue = false;            // some document has left children (Fugue logs)
     uint8_t* cp = nullptr;         // 3 bytes per slot: codepoint (bits 0-20) | tombstone (bit 23)
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index

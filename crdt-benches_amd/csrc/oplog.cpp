@@ -168,7 +168,36 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
         }
         at = si + 1;
     }
-    if (k == 1) {  // typing: one item
+    if (fugue) {  // Fugue anchors (see oplog.hpp); every char after the first is a right child
+        if (hasright_.size() < (size_t)first + k) hasright_.resize(std::max<size_t>(first + k, 2 * hasright_.size()), 0);
+        const bool as_left = hasright_[left] != 0;
+        if (as_left && right == NIL) return "resolver index corrupt (Fugue: no right neighbour)";
+        side.resize(side.size() + k, 0);
+        side[first - 1] = as_left ? 1 : 0;
+        if (!as_left) hasright_[left] = 1;
+        for (size_t j = 1; j < k; ++j) hasright_[first + j - 1] = 1;
+        if (k == 1) {
+            parent.push_back(as_left ? right : left);
+            oright.push_back(right);
+            lamport.push_back(++max_lamport);
+            agent.push_back(local_agent);
+            deleted.push_back(0);
+            cp.push_back(cps[0]);
+        } else {
+            const size_t n0 = parent.size();
+            parent.resize(n0 + k);
+            oright.resize(n0 + k, right);
+            lamport.resize(n0 + k);
+            agent.resize(n0 + k, local_agent);
+            deleted.resize(n0 + k, 0);
+            cp.resize(n0 + k);
+            parent[n0] = as_left ? right : left;
+            for (size_t j = 1; j < k; ++j) parent[n0 + j] = first + (uint32_t)j - 1;
+            for (size_t j = 0; j < k; ++j) lamport[n0 + j] = max_lamport + 1 + (uint32_t)j;
+            max_lamport += (uint32_t)k;
+            std::memcpy(cp.data() + n0, cps, k * sizeof(uint32_t));
+        }
+    } else if (k == 1) {  // typing: one item
         parent.push_back(left);
         oright.push_back(right);
         lamport.push_back(++max_lamport);

@@ -27,6 +27,12 @@ public:
     std::vector<uint16_t> agent;
     std::vector<uint8_t> deleted;
     std::vector<uint32_t> del_ops;  // target id of every delete op, in op order
+    // Fugue mode (set on an empty log): side[k] = 1 if item k+1 is a LEFT child of parent[k].
+    // An insert after left neighbour a (full-list successor b) is a right child of a when a has
+    // no right child yet, else a left child of b (the leftmost node of a's right subtree): the
+    // resolver's sequence is then the Fugue in-order at every step.  Empty in RGA mode.
+    std::vector<uint8_t> side;
+    bool fugue = false;
     uint16_t local_agent = 0;
     uint32_t max_lamport = 0;
 
@@ -74,6 +80,7 @@ private:
     mutable std::vector<int64_t> fen_;
     mutable bool fen_dirty_ = false;
     std::vector<uint32_t> cps_;  // scratch for insert_utf8
+    std::vector<uint8_t> hasright_;  // Fugue: item (id) already has a right child
     uint64_t nvis_ = 0;
     // Chunk of the last lookup and the visible items before it.  Edits only change counts at or
     // after the chunk they start in and splits append after it, so the hint stays exact.

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CRDT_HIP_ABI_VERSION 1
+#define CRDT_HIP_ABI_VERSION 2
 
 enum {
     CRDT_HIP_OK = 0,
@@ -71,6 +71,11 @@ typedef struct {
     const uint16_t* agent;
     const uint8_t* deleted;
     const uint32_t* cp;
+    /* optional (NULL: RGA).  Fugue order (SURVEY.md §8(a) s0 "side u8 (Fugue)"): side[k] != 0
+     * makes item k a LEFT child of parent[k]; the document is then the in-order walk (left
+     * children, the item, right children; each side by (lamport, agent) descending).  An RGA
+     * log is the Fugue log without left children.  lamport must stay below 0xFFFFFFFF. */
+    const uint8_t* side;
 } crdt_hip_oplog_view;
 
 /* Per-stage device time of the last merge (HIP events on the context's stream), in ns,
@@ -129,6 +134,10 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 
 /* ---- op log: host-side resolver (positional patch -> anchor op) ---------------------------- */
 int crdt_hip_oplog_new(crdt_hip_oplog** out);
+/* Fugue anchors for every later insert (only on an empty log): an insert after left neighbour a
+ * becomes a right child of a if a has none yet, else a left child of a's full-list successor.
+ * Fugue logs have no update wire format (encode_from / apply_update / replicas refuse them). */
+int crdt_hip_oplog_set_fugue(crdt_hip_oplog* log, int on);
 int crdt_hip_oplog_clone(const crdt_hip_oplog* src, crdt_hip_oplog** out);
 void crdt_hip_oplog_free(crdt_hip_oplog* log);
 /* insert `nbytes` of UTF-8 at codepoint position `pos` (Upstream::insert). */
@@ -166,6 +175,8 @@ int crdt_hip_trace_end_content(const crdt_hip_trace* t, const char** s, size_t* 
 int crdt_hip_trace_chars_to_bytes(crdt_hip_trace* t);
 /* Replay every patch into a fresh op log (the upstream loop body of main.rs:29-34). */
 int crdt_hip_trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out);
+/* The same replay with Fugue anchors (crdt_hip_oplog_set_fugue). */
+int crdt_hip_trace_resolve_fugue(const crdt_hip_trace* t, crdt_hip_oplog** out);
 /* crdt_hip_trace_resolve of n traces on up to `threads` host threads (0: one per trace, capped
  * by the hardware), documents being independent.  out[i] receives trace
  * i's op log; on an error every out[i] is null and the first error is reported. */

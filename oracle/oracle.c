@@ -353,6 +353,134 @@ done:
     return rc;
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* Fugue: resolver with left/right anchors, and the in-order merge.                            */
+/* ------------------------------------------------------------------------------------------ */
+int64_t orc_resolve_fugue(const orc_patches* p, uint32_t* parent, uint8_t* side,
+                          uint32_t* lamport, uint16_t* agent, uint8_t* deleted, uint32_t* cp) {
+    size_t total = p->start_n;
+    for (size_t i = 0; i < p->npatch; ++i) total += p->ins_len[i];
+    rlist L;
+    L.next = (uint32_t*)malloc((total + 1) * 4);
+    L.prev = (uint32_t*)malloc((total + 1) * 4);
+    L.dead = (uint8_t*)calloc(total + 1, 1);
+    uint8_t* hasright = (uint8_t*)calloc(total + 1, 1);
+    L.next[0] = NIL; L.prev[0] = NIL;
+    L.dead[0] = 1;
+    L.cur = 0; L.cnt = 0;
+    uint64_t vis = 0;
+    uint32_t n = 0;
+    int64_t rc = 0;
+    /* one item after `left`: right child of left if left has none yet, else left child of the
+     * item that follows left in the full list */
+#define FUGUE_RUN(POS, SRC, LEN)                                                   \
+    do {                                                                           \
+        if (rl_seek(&L, (POS))) { rc = -1; goto done; }                            \
+        uint32_t left = L.cur;                                                     \
+        for (size_t k = 0; k < (LEN); ++k) {                                       \
+            uint32_t id = ++n, right = L.next[left];                               \
+            if (!hasright[left]) {                                                 \
+                parent[id - 1] = left; side[id - 1] = 0; hasright[left] = 1;       \
+            } else {                                                               \
+                if (right == NIL) { rc = -1; goto done; }                          \
+                parent[id - 1] = right; side[id - 1] = 1;                          \
+            }                                                                      \
+            lamport[id - 1] = id; agent[id - 1] = 0; deleted[id - 1] = 0;          \
+            cp[id - 1] = (SRC)[k];                                                 \
+            L.next[id] = right; L.prev[id] = left;                                 \
+            if (right != NIL) L.prev[right] = id;                                  \
+            L.next[left] = id; L.dead[id] = 0;                                     \
+            left = id;                                                             \
+        }                                                                          \
+        L.cur = left; L.cnt = (POS) + (LEN); vis += (LEN);                         \
+    } while (0)
+    if (p->start_n) FUGUE_RUN(0, p->start_cp, p->start_n);
+    for (size_t i = 0; i < p->npatch; ++i) {
+        uint64_t pos = p->pos[i], del = p->del[i];
+        if (pos > vis || del > vis - pos) { rc = -1; goto done; }
+        if (del) {
+            if (rl_seek(&L, pos + 1)) { rc = -1; goto done; }
+            uint32_t c = L.cur;
+            for (uint64_t k = 0; k < del; ++k) {
+                while (L.dead[c]) c = L.next[c];
+                L.dead[c] = 1; deleted[c - 1] = 1;
+                if (k + 1 < del) c = L.next[c];
+            }
+            L.cur = c; L.cnt = pos; vis -= del;
+        }
+        if (p->ins_len[i]) FUGUE_RUN(pos, p->ins_cp + p->ins_off[i], p->ins_len[i]);
+    }
+    rc = n;
+#undef FUGUE_RUN
+done:
+    free(L.next); free(L.prev); free(L.dead); free(hasright);
+    return rc;
+}
+
+int64_t orc_merge_fugue(uint32_t n, const uint32_t* parent, const uint8_t* side,
+                        const uint32_t* lamport, const uint16_t* agent, const uint8_t* deleted,
+                        const uint32_t* cp, uint8_t* out, size_t cap, uint32_t* order) {
+    keyctx K = {lamport, agent};
+    /* children of v: CSR over groups 2v (left children) and 2v + 1 (right children), each
+     * ascending by timestamp */
+    uint32_t* start = (uint32_t*)calloc(2 * (size_t)n + 3, 4);
+    uint32_t* kids = (uint32_t*)malloc(((size_t)n + 1) * 4);
+    /* the stack holds items to expand and (id | EMIT) markers: at most 2n + 1 entries */
+    uint32_t* stack = (uint32_t*)malloc((2 * (size_t)n + 2) * 4);
+    const uint32_t EMIT = 0x80000000u;
+    int64_t rc = 0;
+    if (n >= EMIT) { rc = -1; goto done; }
+    for (uint32_t i = 1; i <= n; ++i) {
+        uint32_t pr = parent[i - 1];
+        if (pr > n || pr == i || (pr == 0 && side[i - 1])) { rc = -1; goto done; }
+        start[2 * pr + (side[i - 1] ? 0 : 1) + 1]++;
+    }
+    for (uint32_t g = 0; g < 2 * n + 2; ++g) start[g + 1] += start[g];
+    {
+        uint32_t* fill = (uint32_t*)malloc((2 * (size_t)n + 2) * 4);
+        memcpy(fill, start, (2 * (size_t)n + 2) * 4);
+        for (uint32_t i = 1; i <= n; ++i) kids[fill[2 * parent[i - 1] + (side[i - 1] ? 0 : 1)]++] = i;
+        free(fill);
+    }
+    for (uint32_t g = 0; g < 2 * n + 2; ++g) {
+        uint32_t a = start[g], b = start[g + 1];
+        for (uint32_t i = a + 1; i < b; ++i) {
+            uint32_t x = kids[i];
+            uint32_t j = i;
+            while (j > a && ts_greater(&K, kids[j - 1], x)) { kids[j] = kids[j - 1]; --j; }
+            kids[j] = x;
+        }
+    }
+    {
+        size_t sp = 0, k = 0, visited = 0;
+        stack[sp++] = 0;
+        while (sp) {
+            uint32_t e = stack[--sp];
+            if (e & EMIT) {
+                uint32_t v = e & ~EMIT;
+                if (order) order[visited] = v;
+                visited++;
+                if (!deleted[v - 1]) {
+                    if (k + len1(cp[v - 1]) > cap) { rc = -2; goto done; }
+                    k += enc1(cp[v - 1], out + k);
+                }
+                continue;
+            }
+            /* expand e: pushed in reverse of the walk (right children, e itself, left
+             * children, each group ascending), so that the greatest left child pops first,
+             * then e, then the greatest right child */
+            for (uint32_t i = start[2 * e + 1]; i < start[2 * e + 2]; ++i) stack[sp++] = kids[i];
+            if (e) stack[sp++] = e | EMIT;
+            for (uint32_t i = start[2 * e]; i < start[2 * e + 1]; ++i) stack[sp++] = kids[i];
+        }
+        if (visited != n) { rc = -1; goto done; }
+        rc = (int64_t)k;
+    }
+done:
+    free(start); free(kids); free(stack);
+    return rc;
+}
+
 /* Independent O(n^2) integrator (textbook RGA: skip successors with a greater timestamp). */
 static int cmp_lam_idx(const void* a, const void* b, void* ctx) {
     const keyctx* k = (const keyctx*)ctx;

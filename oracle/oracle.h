@@ -73,6 +73,25 @@ int64_t orc_merge_rga(uint32_t n, const uint32_t* parent, const uint32_t* lampor
                       const uint16_t* agent, const uint8_t* deleted, const uint32_t* cp,
                       uint8_t* out, size_t cap, uint32_t* order);
 
+/* Fugue mode (Weidner & Kleppmann, "The Art of the Fugue", 2023), the other document order the
+ * survey names ("side u8 (Fugue)", "in-order (Fugue)").  Every item is
+ * a left (side[i] != 0) or right child of parent[i]; the document is the in-order walk: an
+ * item's left children, the item, its right children, siblings on each side by (lamport, agent)
+ * descending (ties: greater id first), as in the RGA order.  With no left children this is
+ * exactly orc_merge_rga.  Sibling order among concurrent inserts is parity unpinned (diamond-
+ * types' FugueMax tie rules are not available); sequential traces pin it through endContent.
+ * Same return convention as orc_merge_rga; a left child of the document start is malformed. */
+int64_t orc_merge_fugue(uint32_t n, const uint32_t* parent, const uint8_t* side,
+                        const uint32_t* lamport, const uint16_t* agent, const uint8_t* deleted,
+                        const uint32_t* cp, uint8_t* out, size_t cap, uint32_t* order);
+
+/* Resolver with Fugue anchors: an insert after left neighbour `a` (the p-th visible item, or the
+ * start) whose full-list successor is `b` becomes a right child of `a` when `a` has no right
+ * child yet, else a left child of `b` (then the leftmost node of a's right subtree).  Same
+ * arrays as orc_resolve plus side[]. */
+int64_t orc_resolve_fugue(const orc_patches* p, uint32_t* parent, uint8_t* side,
+                          uint32_t* lamport, uint16_t* agent, uint8_t* deleted, uint32_t* cp);
+
 /* Independent O(n^2) RGA integrator: items integrated in (lamport, agent) order into a linked
  * list, each after its parent skipping every following item with a greater timestamp.  For
  * small logs (cross-checks the tree oracle).  Same return convention. */

@@ -113,10 +113,11 @@ class AnchorLog:
         self.agent = np.zeros(max(n, 1), np.uint16)
         self.deleted = np.zeros(max(n, 1), np.uint8)
         self.cp = np.zeros(max(n, 1), np.uint32)
+        self.side = np.zeros(max(n, 1), np.uint8)  # Fugue: 1 = left child of parent
 
     def trimmed(self, n: int) -> "AnchorLog":
         out = AnchorLog(n)
-        for f in ("parent", "oright", "lamport", "agent", "deleted", "cp"):
+        for f in ("parent", "oright", "lamport", "agent", "deleted", "cp", "side"):
             getattr(out, f)[:n] = getattr(self, f)[:n]
         return out
 
@@ -146,6 +147,10 @@ class Oracle:
             getattr(L, fn).argtypes = [C.c_uint32] + [C.c_void_p] * 6 + [C.c_size_t, C.c_void_p]
         L.orc_merge_rga_naive.restype = C.c_int64
         L.orc_merge_rga_naive.argtypes = [C.c_uint32] + [C.c_void_p] * 6 + [C.c_size_t]
+        L.orc_resolve_fugue.restype = C.c_int64
+        L.orc_resolve_fugue.argtypes = [C.POINTER(Patches)] + [C.c_void_p] * 6
+        L.orc_merge_fugue.restype = C.c_int64
+        L.orc_merge_fugue.argtypes = [C.c_uint32] + [C.c_void_p] * 7 + [C.c_size_t, C.c_void_p]
         L.orc_merge_many.restype = C.c_int
         L.orc_merge_many.argtypes = [C.POINTER(OrcLog), C.c_uint32, C.c_int, C.c_void_p,
                                      C.c_void_p]
@@ -191,6 +196,29 @@ class Oracle:
                                  order.ctypes.data if want_order else None)
         if k < 0:
             raise ValueError(f"orc_merge_rga failed ({k})")
+        return (buf.raw[:k], order[: log.n]) if want_order else buf.raw[:k]
+
+    def resolve_fugue(self, t: TraceData) -> AnchorLog:
+        a = AnchorLog(t.n_items)
+        st = t.cstruct()
+        n = self.L.orc_resolve_fugue(C.byref(st), a.parent.ctypes.data, a.side.ctypes.data,
+                                     a.lamport.ctypes.data, a.agent.ctypes.data,
+                                     a.deleted.ctypes.data, a.cp.ctypes.data)
+        if n < 0:
+            raise ValueError("orc_resolve_fugue failed")
+        assert n == t.n_items
+        return a
+
+    def merge_fugue(self, log: AnchorLog, want_order: bool = False):
+        cap = 4 * log.n + 4
+        buf = C.create_string_buffer(cap)
+        order = np.zeros(max(log.n, 1), np.uint32) if want_order else None
+        k = self.L.orc_merge_fugue(log.n, log.parent.ctypes.data, log.side.ctypes.data,
+                                   log.lamport.ctypes.data, log.agent.ctypes.data,
+                                   log.deleted.ctypes.data, log.cp.ctypes.data, buf, cap,
+                                   order.ctypes.data if want_order else None)
+        if k < 0:
+            raise ValueError(f"orc_merge_fugue failed ({k})")
         return (buf.raw[:k], order[: log.n]) if want_order else buf.raw[:k]
 
     def merge_naive(self, log: AnchorLog) -> bytes:

@@ -25,7 +25,7 @@ def test_every_declared_symbol_is_exported():
 
 
 def test_abi_version():
-    assert crdt_hip.lib().crdt_hip_abi_version() == 1
+    assert crdt_hip.lib().crdt_hip_abi_version() == 2
 
 
 def test_library_is_native_gfx950():

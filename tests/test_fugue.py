@@ -1,0 +1,209 @@
+"""Fugue mode ("side u8 (Fugue)", "in-order (Fugue)").
+
+Every item is a left or a right child of its parent; the document is the in-order walk (left
+children, the item, right children; each side by (lamport, agent) descending).  Parity pins:
+  * the four traces resolved with Fugue anchors merge to their endContent (the reference-held
+    fixture), through the oracle and through the device;
+  * the oracle's in-order merge equals a third, recursive Python restatement on random trees
+    (concurrent sibling order is parity unpinned, as for RGA: no reference fixture exercises it);
+  * a log without left children merges exactly as RGA.
+The product resolver's Fugue anchors are checked bit-exact against the oracle's resolver.
+"""
+import sys
+
+import numpy as np
+import pytest
+
+import crdt_hip
+from conftest import TRACES, trace_path
+from oracle_bind import AnchorLog, load_trace
+
+sys.setrecursionlimit(100000)
+
+
+def random_fugue(n, seed, agents=4, p_chain=0.6, p_left=0.4, p_del=0.3, cps=(0x61,)):
+    """A random Fugue tree: item i hangs off i-1 (right) with p_chain, else off a random earlier
+    item on a random side (never left of the document start)."""
+    rng = np.random.default_rng(seed)
+    ids = np.arange(1, n + 1, dtype=np.int64)
+    rnd = rng.integers(0, np.maximum(ids, 1))
+    chain = rng.random(n) < p_chain
+    parent = np.where(chain, ids - 1, rnd).astype(np.uint32)
+    side = ((~chain) & (rng.random(n) < p_left) & (parent > 0)).astype(np.uint8)
+    # ids (lamport, agent) are unique, as every CRDT's are; lamports repeat across agents
+    agent = (ids % agents).astype(np.uint16)
+    lamport = (ids // agents + 1).astype(np.uint32)
+    deleted = (rng.random(n) < p_del).astype(np.uint8)
+    cp = rng.choice(np.asarray(cps, np.uint32), n)
+    return crdt_hip.LogArrays(parent, lamport, agent, deleted, cp, side=side)
+
+
+def to_anchor(arrs) -> AnchorLog:
+    a = AnchorLog(arrs.n)
+    for f in ("parent", "lamport", "agent", "deleted", "cp"):
+        getattr(a, f)[: arrs.n] = getattr(arrs, f)
+    if arrs.side is not None:
+        a.side[: arrs.n] = arrs.side
+    return a
+
+
+def py_fugue_order(arrs):
+    """Recursive restatement: in-order over (left kids desc, item, right kids desc)."""
+    n = arrs.n
+    kids = {}
+    for i in range(1, n + 1):
+        kids.setdefault((int(arrs.parent[i - 1]), int(arrs.side[i - 1])), []).append(i)
+
+    def key(i):
+        return (int(arrs.lamport[i - 1]), int(arrs.agent[i - 1]), i)
+    out = []
+
+    def walk(v):
+        for c in sorted(kids.get((v, 1), []), key=key, reverse=True):
+            walk(c)
+        if v:
+            out.append(v)
+        for c in sorted(kids.get((v, 0), []), key=key, reverse=True):
+            walk(c)
+    walk(0)
+    return out
+
+
+def text_of(arrs, order):
+    return "".join(chr(int(arrs.cp[v - 1])) for v in order if not arrs.deleted[v - 1]).encode()
+
+
+# ---- CPU: oracle and host resolver ------------------------------------------------------------
+@pytest.mark.parametrize("name", TRACES)
+def test_oracle_fugue_resolve_merge_is_end_content(oracle, name):
+    t = load_trace(name)
+    a = oracle.resolve_fugue(t)
+    assert oracle.merge_fugue(a) == t.end_content.encode()
+    assert a.side[: a.n].any()  # the traces do produce left children
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_oracle_fugue_matches_recursive_restatement(oracle, seed):
+    lg = random_fugue(3000, seed, agents=1 + seed)
+    text, order = oracle.merge_fugue(to_anchor(lg), want_order=True)
+    ref = py_fugue_order(lg)
+    assert order.tolist() == ref
+    assert text == text_of(lg, ref)
+
+
+def test_oracle_fugue_without_left_children_is_rga(oracle):
+    lg = random_fugue(5000, 9, p_left=0.0)
+    a = to_anchor(lg)
+    assert oracle.merge_fugue(a) == oracle.merge(a)
+
+
+def test_oracle_fugue_rejects_left_child_of_start(oracle):
+    a = AnchorLog(2)
+    a.parent[:2] = [0, 0]
+    a.side[:2] = [0, 1]
+    a.lamport[:2] = [1, 2]
+    with pytest.raises(ValueError):
+        oracle.merge_fugue(a)
+
+
+@pytest.mark.parametrize("name", TRACES)
+def test_host_fugue_resolver_matches_oracle(oracle, name):
+    lg = crdt_hip.Trace(trace_path(name)).resolve(fugue=True).arrays()
+    ref = oracle.resolve_fugue(load_trace(name))
+    n = lg.n
+    assert n == ref.n
+    for f in ("parent", "lamport", "deleted", "cp", "side"):
+        assert np.array_equal(getattr(lg, f), getattr(ref, f)[:n]), f
+
+
+def test_host_fugue_oplog_api(oracle):
+    log = crdt_hip.OpLog(fugue=True)
+    for pos, text in [(0, "hello"), (0, ">> "), (3, "[x]"), (8, "!"), (2, "~")]:
+        log.insert(pos, text)
+    log.remove(1, 4)
+    lg = log.arrays()
+    assert lg.side is not None and lg.side.any()
+    # the resolver's own sequence is the in-order: replay the same edits positionally
+    s = ""
+    for pos, text in [(0, "hello"), (0, ">> "), (3, "[x]"), (8, "!"), (2, "~")]:
+        s = s[:pos] + text + s[pos:]
+    s = s[:1] + s[4:]
+    assert oracle.merge_fugue(to_anchor(lg)) == s.encode()
+    with pytest.raises(crdt_hip.CrdtHipError):
+        log.encode_from(0)  # Fugue logs have no update wire format
+    rga = crdt_hip.OpLog()
+    rga.insert(0, "a")
+    assert crdt_hip.lib().crdt_hip_oplog_set_fugue(rga._h, 1) != 0  # only on an empty log
+
+
+# ---- GPU: device merge vs oracle --------------------------------------------------------------
+_FUG = {}
+
+
+def fugue_resolved(name):
+    if name not in _FUG:
+        _FUG[name] = crdt_hip.Trace(trace_path(name)).resolve(fugue=True).arrays()
+    return _FUG[name]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", TRACES)
+def test_gpu_fugue_trace_merge_is_end_content(ctx, oracle, golden, name):
+    lg = fugue_resolved(name)
+    text, dig = ctx.merge(lg)
+    assert text == oracle.merge_fugue(to_anchor(lg))
+    assert "%016x" % dig == golden[name]["tree_digest"]
+    order = ctx.merge_order(lg)
+    _, ref = oracle.merge_fugue(to_anchor(lg), want_order=True)
+    assert np.array_equal(order, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("relabel", ["rotate", "shuffle"])
+def test_gpu_fugue_replica_batch(ctx, golden, relabel):
+    bases = [fugue_resolved(n) for n in TRACES] + [crdt_hip.Trace(trace_path(TRACES[0])).resolve().arrays()]
+    b = ctx.batch(bases, replicas=3, relabel=relabel, seed=99)
+    dig, lens, _ = b.merge()
+    for r in range(b.docs):
+        name = TRACES[r % 5] if r % 5 < 4 else TRACES[0]
+        assert "%016x" % dig[r] == golden[name]["tree_digest"], (relabel, r)
+        assert lens[r] == golden[name]["end_bytes"]
+    b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level1", [0, 1])
+def test_gpu_fugue_random_trees_match_oracle(oracle, level1):
+    c = crdt_hip.Context(0)
+    c.set_param("level1", level1)
+    logs = [random_fugue(20000, s, agents=1 + s % 5, p_chain=0.3 + 0.1 * (s % 6),
+                         p_left=0.1 + 0.15 * (s % 5), cps=(0x61, 0xE9, 0x4E2D, 0x1F600))
+            for s in range(10)]
+    logs.append(random_fugue(30000, 77, p_chain=0.0, p_left=0.9, p_del=0.0))  # left-heavy
+    # pasted runs typed backwards: every char a left child of the one typed before it
+    n = 5000
+    logs.append(crdt_hip.LogArrays(np.r_[0, np.arange(1, n)].astype(np.uint32),
+                                   np.arange(1, n + 1), np.zeros(n), np.zeros(n), np.full(n, 0x62),
+                                   side=np.r_[0, np.ones(n - 1)]))
+    logs.append(crdt_hip.Trace(trace_path("sveltecomponent")).resolve().arrays())  # RGA beside
+    dig, lens = c.merge_batch(logs)
+    for i, lg in enumerate(logs):
+        ref = oracle.merge_fugue(to_anchor(lg)) if lg.side is not None else oracle.merge(to_anchor(lg))
+        assert lens[i] == len(ref), i
+        assert dig[i] == oracle.tree_digest(ref), i
+    for i in (0, 3, 10, 11):
+        text, _ = c.merge(logs[i])
+        assert text == oracle.merge_fugue(to_anchor(logs[i])), i
+        order = c.merge_order(logs[i])
+        _, ref = oracle.merge_fugue(to_anchor(logs[i]), want_order=True)
+        assert np.array_equal(order, ref), i
+    c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_fugue_left_child_of_start_is_rejected(ctx):
+    bad = crdt_hip.LogArrays([0, 0], [1, 2], [0, 0], [0, 0], [97, 98], side=[0, 1])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        ctx.merge(bad)
+    assert e.value.code == -5
+    assert ctx.merge(crdt_hip.LogArrays([0, 1], [1, 2], [0, 0], [0, 0], [97, 98], side=[0, 1]))[0] == b"ba"
