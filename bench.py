@@ -228,16 +228,17 @@ def rank_env() -> tuple:
 # ---------------------------------------------------------------------------------------------
 # inputs
 # ---------------------------------------------------------------------------------------------
-def load_bases():
+def load_bases(fugue: bool = False):
     """Resolve the four traces on the host (untimed setup, like the reference's load at
-    main.rs:19): anchor logs + per-trace patches, items, end bytes, golden digest, resolve ms."""
+    main.rs:19): anchor logs + per-trace patches, items, end bytes, golden digest, resolve ms.
+    `fugue`: Fugue anchors (left/right children, in-order document; same endContent)."""
     with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
         golden = json.load(f)
     bases, patches, items, survivors, digests, resolve_ms = [], [], [], [], [], []
     traces = [crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz")) for name in TRACES]
     for name, t in zip(TRACES, traces):
         t0 = time.perf_counter()
-        lg = t.resolve()
+        lg = t.resolve(fugue=fugue)
         resolve_ms.append((time.perf_counter() - t0) * 1e3)
         bases.append(lg.arrays())
         patches.append(len(t))
@@ -445,7 +446,7 @@ def traces_workload(args) -> int:
     ctx = crdt_hip.Context(local)
     comm = Comm(world, rank, ctx)
     t_setup = time.perf_counter()
-    inputs = load_bases()
+    inputs = load_bases(args.order == "fugue")
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
     ctx.set_param("level1", args.level1)
@@ -496,13 +497,14 @@ def traces_workload(args) -> int:
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic replicas of the 4 real josephg traces (resolved on host, "
-                    f"relabel={args.relabel}, resident in HBM)",
+                    f"{args.order} anchors, relabel={args.relabel}, resident in HBM)",
             "config": {
                 "workload": "config 3: 4 traces x %d replicas per GPU" % args.replicas,
                 "docs_per_gpu": batch.docs,
                 "items_per_gpu": items_per_gpu,
                 "patches_per_gpu": patches_per_gpu,
                 "relabel": args.relabel,
+                "order": args.order,
                 "waves": stats[0]["waves"],
                 "lanes": min(args.lanes, stats[0]["waves"]),
                 "parallelism": f"replicas x{world} (no data-path collective)",
@@ -753,6 +755,9 @@ def parse_args(argv=None):
     ap.add_argument("--config1-seconds", type=float, default=4.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--order", default="rga", choices=["rga", "fugue"],
+                    help="document order of the traces workload (fugue: a side line; the CPU "
+                         "baseline and the shuffle companion are RGA-only and are skipped)")
     ap.add_argument("--workload", default="traces",
                     choices=["traces", "seph", "agents64", "big1b", "downstream"],
                     help="traces: config 3 (headline); seph: config 2; agents64: config 4; "
@@ -762,7 +767,11 @@ def parse_args(argv=None):
     ap.add_argument("--p-chain", type=int, default=90,
                     help="config 5: percent of items whose parent is the previous item "
                          "(0 = uniform random parents, the worst case for gathers)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.order == "fugue":  # (the CPU baseline and the companion merge RGA logs)
+        args.no_cpu_baseline = True
+        args.companion_replicas = 0
+    return args
 
 
 def main() -> int:
