@@ -1175,7 +1175,7 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 // ---------------------------------------------------------------------------------------------
 // Level 1 in LDS: the whole run tree of one document per workgroup (k_doctree)
 // ---------------------------------------------------------------------------------------------
-// Documents of the batched configs have at most ~17 k runs, so a document's run tree fits a
+// Documents of the batched configs have at most ~10 k runs, so a document's run tree fits a
 // workgroup's 160 KiB of LDS as four u16 arrays (8 B/run).  The count / scan / place / sort /
 // Euler-tour ranking sequence of the global level-1 path then runs on LDS atomics and LDS
 // gathers inside one 1024-thread workgroup, with barriers between phases, instead of 7+
@@ -1213,7 +1213,14 @@ __device__ __forceinline__ uint32_t lds_ld16(uint16_t* p) { return *(volatile ld
 __device__ __forceinline__ void lds_st16(uint16_t* p, uint32_t v) { *(volatile lds_u16_t*)p = (uint16_t)v; }
 
 constexpr int kDocThreads = 1024;
-constexpr int kDocJ = 20;          // runs per thread: documents of up to 20480 runs
+#ifndef CRDT_DOC_J
+// 12,288 runs per document: the traces need at most 10,113 (seph-blog1) once dead runs are
+// dropped.  Every per-run loop is unrolled kDocJ times (the per-thread arrays live in VGPRs), so
+// kDocJ sets the code size: 20 made k_doctree 60 KB of code, 12 makes it 42 KB and the kernel
+// ~8 % faster (A/B at the headline config; an instruction cache is shared by two CUs).
+#define CRDT_DOC_J 12
+#endif
+constexpr int kDocJ = CRDT_DOC_J;  // runs per thread: documents of up to kDocJ * 1024 runs
 #ifndef CRDT_DOC_LOG2S
 #define CRDT_DOC_LOG2S 2
 #endif
