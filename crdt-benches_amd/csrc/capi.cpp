@@ -195,6 +195,10 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.plan_cache = value == 1;
         return 0;
     }
+    if (k == "fuse_text") {  // 0: k_doctree leaves the text to k_expand (smaller LDS footprint)
+        ctx->eng.fuse_text = value != 0;
+        return 0;
+    }
     if (k == "doctree_lds_max") {  // experiment hook (see Engine::doctree_lds_max)
         ctx->eng.doctree_lds_max = value != 0;
         return 0;

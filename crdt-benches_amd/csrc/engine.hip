@@ -2623,7 +2623,7 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
              dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
     // expansion + digest fused into k_doctree when every document's text fits LDS: text staging
     // + run-start bitvector (tl/8 + tl/16) + one u32 per run
-    p.fuse = p.lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
+    p.fuse = fuse_text && p.lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
     p.dyn_bytes = p.fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
                                dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
                          : dbytes;
@@ -2957,7 +2957,7 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     }
     w.hint_runs = p.R;
     w.hint_rmax = p.rmax;
-    w.hint_lds = p.lds1 && p.fuse && !ord;
+    w.hint_lds = p.lds1 && (p.fuse || !fuse_text) && !ord;
     if (w.hint_lds) learn_shape(w);
     return CRDT_HIP_OK;
 }
@@ -3079,6 +3079,7 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         m.eng[i]->log2m = log2m;
         m.eng[i]->log2m_set = log2m_set;
         m.eng[i]->level1_global = level1_global;
+        m.eng[i]->fuse_text = fuse_text;
         m.eng[i]->l1_split = l1_split;
         m.eng[i]->probe_doc_ = probe_doc_;
     }
@@ -3145,7 +3146,7 @@ int Engine::merge_async_enqueue(DeviceLogs& L, AsyncMerge& m) {
             E.cur_ = E.stream_l1;
         }
         rc = E.launch_lds_level1(L, w, false, m.plans[wi], ck);
-        if (!rc) rc = E.launch_tail(L, w, false, true, ck, E.host_block(L, wi));
+        if (!rc) rc = E.launch_tail(L, w, false, m.plans[wi].fuse, ck, E.host_block(L, wi));
         if (split) {
             E.cur_ = E.stream;
             if (!rc) {
@@ -3275,6 +3276,7 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         eng[i]->log2m = log2m;
         eng[i]->log2m_set = log2m_set;
         eng[i]->level1_global = level1_global;
+        eng[i]->fuse_text = fuse_text;
         eng[i]->probe_doc_ = probe_doc_;
     }
     std::vector<int> rc(K, CRDT_HIP_OK);

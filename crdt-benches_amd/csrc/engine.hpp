@@ -129,6 +129,7 @@ public:
     bool plan_cache = true;
     bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
     bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS
+    bool fuse_text = true;         // k_doctree writes the text when it fits LDS (else k_expand)
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
