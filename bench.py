@@ -456,9 +456,9 @@ def traces_workload(args) -> int:
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
-    if args.l1_split != 1:  # (the engine's default; builds before the parameter lack it)
+    if args.l1_split != 0:  # (the engine's default; builds before the parameter lack it)
         ctx.set_param("l1_split", args.l1_split)
-    if args.tail_wave_div != 4:  # (likewise)
+    if args.tail_wave_div != 0:  # (likewise)
         ctx.set_param("tail_wave_div", args.tail_wave_div)
 
     def make_batch(bases, replicas, relabel, seed):
@@ -745,10 +745,10 @@ def parse_args(argv=None):
     ap.add_argument("--plan-cache", type=int, default=1, choices=[0, 1],
                     help="1: merges after the first enqueue every wave with its learnt launch "
                          "plan and wait once (Engine::merge_async); 0: wait after each level 0")
-    ap.add_argument("--tail-wave-div", type=int, default=4,
+    ap.add_argument("--tail-wave-div", type=int, default=0,
                     help="the last wave of a multi-wave merge holds at most max_wave_slots / this "
                          "(its level 1 overlaps nothing); 0 = plain greedy waves")
-    ap.add_argument("--l1-split", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--l1-split", type=int, default=0, choices=[0, 1],
                     help="1: enqueued waves run level 1 on a low-priority stream of their lane "
                          "(level 0 of the next wave is favoured for the CUs); 0: one stream")
     ap.add_argument("--fuse-text", type=int, default=1, choices=[0, 1],

@@ -113,7 +113,9 @@ public:
     uint32_t log2m = 4;                    // level-1 splitter stride M = 2^log2m
     bool log2m_set = false;                // set by the caller; else chosen per wave from R
     uint64_t max_wave_slots = 1ull << 30;
-    uint32_t tail_wave_div = 4;            // last wave of a multi-wave merge <= max / div (0: off)
+    // last wave of a multi-wave merge <= max / div (0: off; off since the dead-run drop and the
+    // smaller k_doctree: 12.37 -> 12.09 ms at the headline config, tools/sweep_sched.sh)
+    uint32_t tail_wave_div = 0;
     bool level1_global = false;            // never use the per-document LDS level 1
     // Waves merged at once by a multi-wave merge, each on a lane of its own: a helper engine
     // (non-blocking stream + scratch) driven by its own host thread.  The latency-bound level 1
@@ -123,7 +125,9 @@ public:
     // Enqueued waves (merge_async) run level 1 and the tail on stream_l1, created with the lowest
     // stream priority, so that when one wave's latency-bound level 1 and the next wave's HBM-bound
     // level 0 compete for the CUs, the dispatcher favours level 0 (the chain that bounds a merge).
-    bool l1_split = true;
+    // (off by default since the round-2 level-0 work: 12.09 -> 12.05 ms, within noise; the
+    // parameter stays for the A/B)
+    bool l1_split = false;
     // Merges of logs merged before enqueue every wave with its learnt plan and wait once at the
     // end (merge_async) instead of after each wave's level 0.
     bool plan_cache = true;

@@ -207,3 +207,20 @@ def test_gpu_fugue_left_child_of_start_is_rejected(ctx):
         ctx.merge(bad)
     assert e.value.code == -5
     assert ctx.merge(crdt_hip.LogArrays([0, 1], [1, 2], [0, 0], [0, 0], [97, 98], side=[0, 1]))[0] == b"ba"
+
+
+@pytest.mark.gpu
+def test_gpu_fugue_large_log_and_relabelled_replicas(ctx, oracle):
+    """A 3 M-item Fugue log (typing chains, 30 % of the other inserts left children, several
+    agents) against the oracle, then as a resident batch relabelled three ways: every replica
+    must give the same digest (rows, ranks and sides do not depend on the slot order)."""
+    lg = random_fugue(3_000_000, 2024, agents=8, p_chain=0.85, p_left=0.3, p_del=0.5,
+                      cps=(0x61, 0x62, 0xE9, 0x4E2D))
+    ref = oracle.merge_fugue(to_anchor(lg))
+    text, dig = ctx.merge(lg)
+    assert text == ref and dig == oracle.tree_digest(ref)
+    for relabel in ("none", "rotate", "shuffle"):
+        b = ctx.batch([lg], replicas=2, relabel=relabel, seed=5)
+        d2, l2, _ = b.merge()
+        assert all(int(x) == dig for x in d2) and all(int(x) == len(ref) for x in l2), relabel
+        b.close()
