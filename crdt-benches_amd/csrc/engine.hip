@@ -173,7 +173,8 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint32_t lds[kBlock / 64];
     __shared__ uint32_t jl[kScanTile / 32];
     __shared__ uint2 ldoc[kBlock];  // per thread: its document {base slot, items}
-    __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes];
+    // (+64: one sink byte per lane for the branch-free ASCII stores below)
+    __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes + 64];
     const uint32_t tile = blockIdx.x;
     const uint32_t t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
     const bool live = gs < a.nslots;
@@ -223,7 +224,20 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     uint32_t tot;
     const uint32_t ex = block_excl_scan<kBlock / 64>(((uint32_t)__popc(nsq) << 16) | W, lds, tot);
     const uint32_t tw = tot & 0xFFFFu, T = tot >> 16;
-    if (a.mode == 0 && W) {
+    if (a.mode == 0 && W == (uint32_t)__popc(vis)) {
+        // every visible character of the thread is one UTF-8 byte (nearly always on the traces):
+        // 16 unconditional byte stores, a slot without a visible character into the lane's sink
+        // byte, instead of a branch per slot and per byte
+        uint8_t* o = sb + (ex & 0xFFFFu);
+        uint8_t* sink = sb + kTileBytes + (threadIdx.x & 63u);
+        uint32_t pos = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t v = (vis >> k) & 1u;
+            *(v ? o + pos : sink) = (uint8_t)C[k];
+            pos += v;
+        }
+    } else if (a.mode == 0 && W) {
         uint8_t* o = sb + (ex & 0xFFFFu);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
