@@ -60,9 +60,12 @@ MIN_B_PER_TEXT = 1.0
 # Per-kernel algorithmic bytes: each kernel's declared inputs read once +
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
-    "classify": (3.75, 8.0, 1.0),    # 3-byte cp|flags; nsq bits, weight nibbles, jump bits; parents of the nsq items read + listed; tile UTF-8
-    # head/seq bits, nibbles; per run: key + parent slot + rank lookup in, record row out; text move
-    "runs": (0.75, 38.0, 2.0),
+    # 3-byte cp|flags in; nsq + visible bits, weight nibbles, jump bits out; parents of the nsq
+    # items read + listed (counted per run); tile UTF-8
+    "classify": (3.875, 8.0, 1.0),
+    # head stage (k_heads: nsq/visible/jump bits in, head records out) and k_runs: head records,
+    # nibbles; per run: key + parent slot + rank lookup in, record row out; text move
+    "runs": (0.875, 38.0, 2.0),
     "count": (0.0, 8.0, 0.0),
     "scan": (0.0, 8.0, 0.0),
     "place": (0.0, 12.0, 0.0),
