@@ -750,7 +750,9 @@ __global__ __launch_bounds__(kBlock) void k_count(TreeArgs a) {
     const uint32_t p = a.in_parent[g];
     if (p == kNil) return;
     if (p >= a.R || p == g) { atomicOr(&a.ctl[C_ERR], 1u); return; }
-    atomicAdd(&a.deg[p], 1u);
+    // the child's place in its parent's segment comes with the count (roff is free until
+    // k_walk2), so that k_place needs no second atomic
+    a.roff[g] = atomicAdd(&a.deg[p], 1u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n,
@@ -830,9 +832,7 @@ __global__ __launch_bounds__(kBlock) void k_place(TreeArgs a) {
     if (g >= a.R) return;
     const uint32_t p = a.in_parent[g];
     if (p == kNil || p >= a.R || p == g) return;  // flagged by k_count
-    // decrementing restores deg[] to all-zero for the next wave (no memset needed)
-    const uint32_t r = atomicSub(&a.deg[p], 1u) - 1u;
-    a.child[a.cstart[p] + r] = g;
+    a.child[a.cstart[p] + a.roff[g]] = g;  // (the place k_count's atomic handed out)
 }
 
 // Compare-exchange for a descending sort of (key, id) pairs held in registers.
@@ -2810,6 +2810,8 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_);
     k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, R);
     k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_, cstart_);
+    // (the counts are consumed: back to the all-zero state the next wave's k_count expects)
+    HIPCHK(hipMemsetAsync(deg_, 0, R * 4ull, s), "memset deg");
     MARK(S_SCAN);
     k_place<<<gR, kBlock, 0, s>>>(a);
     MARK(S_PLACE);
