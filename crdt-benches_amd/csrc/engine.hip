@@ -150,7 +150,7 @@ constexpr uint64_t kLeftKey = 1ull << 48;
 // words of the jump bitvector of a wave (a multiple of 4: the left-child bits follow it aligned)
 __host__ __device__ constexpr uint64_t jbits_words(uint64_t slots) { return (slots / 32 + 8 + 3) & ~3ull; }
 constexpr uint64_t kMidKey = (1ull << 48) - 1ull;
-constexpr uint32_t kRecContent = 1u << 30, kRecTree = 1u << 31;
+constexpr uint32_t kRecTree = 1u << 31;  // k_runs record of a head with two rows
 
 // k_classify: the characters of 16 slots per thread (3 x 16-byte loads of the codepoint column:
 // codepoint, tombstone, "parent is the previous slot" flag), then the parents of the tile's
@@ -455,17 +455,21 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
 // (tile prefix + hloc + popcount).  Storing the rows from the thread that found each head costs
 // one vector store instruction per head position with lanes scattered over many lines (the
 // address unit, not HBM, bounded that form); one thread per run stores them as contiguous rows.
-// FUGUE: the wave has left children; a tile then holds up to two rows per head (the RGA build
-// keeps its 16 KiB of records and its occupancy).
+// FUGUE: the wave has left children.  A head with left children then numbers two rows; the
+// tile still keeps one record per head (kRecTree marks those heads) and the per-head loop finds
+// each head's first row by a block scan of the rows per head.
 template <bool FUGUE>
 __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     constexpr int NW = kBlock / 64;
     __shared__ uint32_t lsum[NW];
-    __shared__ uint32_t rec[FUGUE ? 2 * kScanTile : kScanTile];
+    __shared__ uint32_t lrow[NW];
+    __shared__ uint32_t rec[kScanTile];
     __shared__ uint16_t lnsq[kBlock];  // nsq bits of every thread's 16 slots
     __shared__ uint2 ldoc[kBlock];     // every thread's document {base slot, items}
     __shared__ uint32_t lsq[NW];
     __shared__ uint16_t lnpf[kBlock];  // non-seq items of the tile before every thread
+    __shared__ uint16_t ldp[FUGUE ? kBlock : 1];  // Fugue: two-row heads before every thread
+    __shared__ uint16_t ldm[FUGUE ? kBlock : 1];  //   and every thread's two-row head bits
     const uint32_t tile = blockIdx.x;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
@@ -496,23 +500,34 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     uint32_t W = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) W += (uint32_t)(nib >> (4 * j)) & 15u;
-    const uint32_t x = ((uint32_t)(__popc(hm) + __popc(dm)) << 16) | W;
+    const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;  // heads (records) << 16 | weight
     const uint32_t inc = wave_incl_scan(x);
     const uint32_t cq = (uint32_t)__popc(nsq), incq = wave_incl_scan(cq);
+    const uint32_t cd = FUGUE ? (uint32_t)__popc(dm) : 0u, incd = FUGUE ? wave_incl_scan(cd) : 0u;
     if (lane == 63u) {
         lsum[wv] = inc;
         lsq[wv] = incq;
+        if (FUGUE) lrow[wv] = incd;
     }
     __syncthreads();
-    uint32_t off = 0, tot = 0, offq = 0;
+    uint32_t off = 0, tot = 0, offq = 0, offd = 0, totd = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
         const uint32_t v = lsum[i];
         off += (i < (int)wv) ? v : 0u;
         offq += (i < (int)wv) ? lsq[i] : 0u;
         tot += v;
+        if (FUGUE) {
+            offd += (i < (int)wv) ? lrow[i] : 0u;
+            totd += lrow[i];
+        }
     }
     lnpf[threadIdx.x] = (uint16_t)(offq + incq - cq);
+    const uint32_t dpre = offd + incd - cd;  // (Fugue) two-row heads of the tile before the thread
+    if (FUGUE) {
+        ldp[threadIdx.x] = (uint16_t)dpre;
+        ldm[threadIdx.x] = (uint16_t)dm;
+    }
     const uint32_t ex = off + inc - x;
     const uint32_t nh = tot >> 16;
     const uint32_t tw_all = tot & 0xFFFFu;
@@ -531,23 +546,18 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             if (hm & (1u << j)) {
-                const uint32_t rv = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p;
-                if (dm & (1u << j)) {  // Fugue: content row, then the run's tree row
-                    rec[r++] = rv | kRecContent;
-                    rec[r++] = rv | kRecTree;
-                } else {
-                    rec[r++] = rv;
-                }
+                rec[r++] = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p |
+                           ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
             }
             p += (uint32_t)(nib >> (4 * j)) & 15u;
         }
     }
     if ((hm & 1u) && (gs & 63u) == 0 && doc.x == gs) {  // document starts are 64-aligned
         const uint32_t d = a.chunk_doc[gs >> a.log2m];
-        a.doc_root[d] = pre.x + (ex >> 16);
+        a.doc_root[d] = pre.x + (ex >> 16) + dpre;  // (rows: heads + two-row heads before)
         a.doc_p0[d] = pre.y + (ex & 0xFFFFu);
     }
-    if (tile + 1u == a.ntiles && threadIdx.x == 0) a.r_pstart[pre.x + nh] = pre.y + tw_all;
+    if (tile + 1u == a.ntiles && threadIdx.x == 0) a.r_pstart[pre.x + nh + totd] = pre.y + tw_all;
     if (a.mode == 0) {
         uint32_t* d32 = reinterpret_cast<uint32_t*>(a.sbytes);
         if (m < hi) d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
@@ -562,12 +572,16 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             for (uint32_t g = max(hi, lo); g < D + tw; ++g) a.sbytes[g] = src[g - D];
     }
     __syncthreads();
-    // one thread per run: every gather of a stage issued before any is used
+    // one thread per head: every gather of a stage issued before any is used
     const uint32_t tbase = tile * kScanTile;
     for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
         const uint32_t rv = rec[i];
-        const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li, rho = pre.x + i;
-        const bool content = (rv & kRecContent) != 0u, treerow = (rv & kRecTree) != 0u;
+        const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
+        const bool two = (rv & kRecTree) != 0u;  // Fugue: a content row, then the tree row
+        // the head's first row: heads before it, plus (Fugue) the two-row heads before it
+        const uint32_t rho = pre.x + i +
+            (FUGUE ? ldp[li >> 4] + (uint32_t)__popc(ldm[li >> 4] & ((1u << (li & 15u)) - 1u)) : 0u);
+        const uint32_t rt = rho + (two ? 1u : 0u);  // the row with the run's parent and key
         const uint2 dc = ldoc[li >> 4];
         const bool root = g == dc.x;
         const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
@@ -578,16 +592,15 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
                          ? a.plist[tbase + lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u))]
                          : 0u;
         a.r_head[rho] = g;
-        // a tree row weighs nothing: its prefix is the next row's (the content row's end)
-        a.r_pstart[rho] = pre.y + (treerow ? (i + 1u < nh ? rec[i + 1u] & 0xFFFFu : tw_all)
-                                           : (rv & 0xFFFFu));
+        a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
+        if (two) {
+            // the tree row weighs nothing: its prefix is the next head's (the content row's end)
+            a.r_head[rt] = g;
+            a.r_pstart[rt] = pre.y + (i + 1u < nh ? rec[i + 1u] & 0xFFFFu : tw_all);
+        }
         uint32_t pr = kNil;
-        if (content) {
-            pr = rho + 1u;  // the run's text, a child of its tree row between the left and the
-                            // right children (kMidKey)
-        } else if (sq) {
-            // the parent is the slot before the head: the previous run's last row
-            pr = rho - (treerow ? 2u : 1u);
+        if (sq) {
+            pr = rho - 1u;  // the parent is the slot before the head: the previous run's last row
         } else if (!root) {
             if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
             const uint32_t ps = dc.x + p;
@@ -604,9 +617,15 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             }
             pr = tp + hl + rows - 1u;
         }
-        if (rho < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
-            a.r_parent[rho] = pr;
-            a.r_key[rho] = root ? 0ull : (content ? kMidKey : key);
+        if (rt < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
+            a.r_parent[rt] = pr;
+            a.r_key[rt] = root ? 0ull : key;
+            if (two) {
+                // the run's text: a child of its tree row between the left and the right
+                // children (kMidKey)
+                a.r_parent[rho] = rt;
+                a.r_key[rho] = kMidKey;
+            }
         }
     }
 }
