@@ -1285,6 +1285,7 @@ struct DocArgs {
     uint32_t ndocs, rcap, scap, chbytes;
     uint32_t probe;  // 1 + document whose phase times are printed (0: none)
     const uint32_t* doc_root;
+    const uint32_t* order;  // workgroup -> document (costliest first)
     const uint32_t* r_parent;
     const uint64_t* r_key;
     uint32_t* roff;
@@ -1422,7 +1423,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     __shared__ uint32_t probe_max, probe_sum;
 #endif
     __shared__ uint32_t bigv[kDocBig], bigw[kDocBig];
-    const uint32_t d = blockIdx.x;
+    const uint32_t d = a.order[blockIdx.x];
     const uint32_t t = threadIdx.x;
     // the plan check and the document's run range in one round of loads (not one after the other)
     const uint32_t base = a.doc_root[d];
@@ -2271,7 +2272,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 // =============================================================================================
 void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
-    dfree(docs_rel); dfree(chunk_doc);
+    dfree(docs_rel); dfree(doc_order); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
 }
@@ -2413,7 +2414,9 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     if (docs.size() > L.cap_docs) {
         L.tab_sig.clear();
         dfree(L.docs_rel);
+        dfree(L.doc_order);
         HIPCHK(dalloc(&L.docs_rel, docs.size()), "hipMalloc logs.docs");
+        HIPCHK(dalloc(&L.doc_order, docs.size()), "hipMalloc logs.doc_order");
         gen_++;
         L.cap_docs = docs.size();
     }
@@ -2442,17 +2445,28 @@ int Engine::upload_tables(DeviceLogs& L) {
     if (sig == L.tab_sig) return CRDT_HIP_OK;
     L.tab_sig.clear();
     std::vector<uint2> rel(nd);
-    std::vector<uint32_t> local(nd);
-    for (const Wave& w : L.waves)
+    std::vector<uint32_t> local(nd), order(nd);
+    for (const Wave& w : L.waves) {
         for (uint32_t k = 0; k < w.ndocs; ++k) {
             const uint32_t d = w.first_doc + k;
             rel[d] = make_uint2((uint32_t)(L.doc_slot[d] - w.slot0), L.docs[d].n);
             local[d] = k;
         }
+        // k_doctree's workgroup order: the costliest documents first (longest-processing-time
+        // order: the last workgroups of a launch are the short ones, so the CUs finish together);
+        // the visible text stands in for the cost
+        uint32_t* o = order.data() + w.first_doc;
+        for (uint32_t k = 0; k < w.ndocs; ++k) o[k] = k;
+        std::stable_sort(o, o + w.ndocs, [&](uint32_t x, uint32_t y) {
+            return L.docs[w.first_doc + x].text_cap > L.docs[w.first_doc + y].text_cap;
+        });
+    }
     // (pageable sources: hipMemcpyAsync has copied them when it returns; the tables are
     // consumed in stream order, so no wait here)
     HIPCHK(hipMemcpyAsync(L.docs_rel, rel.data(), nd * sizeof(uint2), hipMemcpyHostToDevice, stream),
            "upload docs");
+    HIPCHK(hipMemcpyAsync(L.doc_order, order.data(), nd * 4ull, hipMemcpyHostToDevice, stream),
+           "upload doc order");
     const uint64_t nchunks = L.total_slots >> L.log2m;
     if (nd == 1) {  // one document: every chunk is document 0
         HIPCHK(hipMemsetAsync(L.chunk_doc, 0, nchunks * 4, stream), "chunk table");
@@ -2798,6 +2812,7 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.fused = doc_fused_;
     da.lds_bytes = (uint32_t)p.dyn_bytes;
     da.probe = probe_doc_;
+    da.order = L.doc_order + w.first_doc;
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
     MARK(S_DOCTREE);

@@ -93,6 +93,7 @@ struct DeviceLogs {
     bool fugue = false;            // some document has left children (Fugue logs)
     uint8_t* cp = nullptr;         // 3 bytes per slot: codepoint (bits 0-20) | tombstone (bit 23)
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
+    uint32_t* doc_order = nullptr; // per wave: its documents, costliest first (k_doctree order)
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
     uint64_t cap_docs = 0, cap_chunks = 0;
     std::vector<uint64_t> tab_sig;  // the plan docs_rel / chunk_doc were last built for
