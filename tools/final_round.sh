@@ -7,6 +7,8 @@ R=${ROUND:-r02g}
 BENCH=" " bash tools/gpu_round.sh || exit 1
 cp gpurun_out/bench_1.json gpurun_out/${R}_bench_default.json
 ROUND=$R bash tools/profile_round.sh || exit 1
+python3 tools/kt_timed.py gpurun_out/${R}_kt/run_kernel_trace.csv gpurun_out/${R}_bench_4096.json \
+    > gpurun_out/${R}_kernel_timed_4096.txt
 ROUND=${R}_1lane LANES=1 bash tools/kt1.sh || exit 1
 ROUND=$R bash tools/side_lines.sh || exit 1
 timeout -k 10 400 python -u bench.py --order fugue --steps 10 > gpurun_out/${R}_side_fugue.json 2> gpurun_out/${R}_side_fugue.err || exit 1
