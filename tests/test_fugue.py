@@ -224,3 +224,26 @@ def test_gpu_fugue_large_log_and_relabelled_replicas(ctx, oracle):
         d2, l2, _ = b.merge()
         assert all(int(x) == dig for x in d2) and all(int(x) == len(ref) for x in l2), relabel
         b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_gpu_fugue_multi_wave_lanes(golden, lanes):
+    """Fugue and RGA documents in small waves merged on several lanes (learnt plans on the
+    second merge, documents in longest-processing-time order): every replica gives its trace's
+    endContent digest."""
+    c = crdt_hip.Context(0)
+    c.set_param("lanes", lanes)
+    c.set_param("max_wave_slots", 1 << 20)
+    bases = [fugue_resolved(n) for n in TRACES] + [crdt_hip.Trace(trace_path(n)).resolve().arrays()
+                                                   for n in TRACES]
+    b = c.batch(bases, replicas=2, relabel="rotate", seed=11)
+    for _ in range(2):
+        dig, lens, st = b.merge()
+    assert st["waves"] >= 3
+    for r in range(b.docs):
+        name = TRACES[(r % 8) % 4]
+        assert "%016x" % dig[r] == golden[name]["tree_digest"], r
+        assert lens[r] == golden[name]["end_bytes"], r
+    b.close()
+    c.close()
