@@ -337,6 +337,8 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 // the run).  Without its head the dead run's items count as the previous run's, which changes
 // nothing: they weigh nothing, and no parent lookup lands on them.  Nothing else moves: seq heads
 // still follow their parent's run (rho - 1), whose last item is live by its jump bit.
+// Fugue waves: a head with left children numbers two rows (see kRecTree), and hrec .z and the
+// tile totals count rows, not heads.
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
