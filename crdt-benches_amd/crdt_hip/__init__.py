@@ -31,7 +31,7 @@ STAGES = ["classify", "runs", "run_parent", "count", "scan", "place", "link", "w
 EXPORTS = [
     "crdt_hip_abi_version", "crdt_hip_device_count", "crdt_hip_init", "crdt_hip_destroy",
     "crdt_hip_last_error", "crdt_hip_set_param", "crdt_hip_oplog_new", "crdt_hip_oplog_set_fugue",
-    "crdt_hip_oplog_clone", "crdt_hip_trace_resolve_fugue",
+    "crdt_hip_oplog_set_agent", "crdt_hip_oplog_clone", "crdt_hip_trace_resolve_fugue",
     "crdt_hip_oplog_free", "crdt_hip_oplog_insert", "crdt_hip_oplog_remove",
     "crdt_hip_oplog_replace", "crdt_hip_oplog_visible_len", "crdt_hip_oplog_get_view",
     "crdt_hip_oplog_version", "crdt_hip_oplog_encode_from", "crdt_hip_oplog_apply_update",
@@ -117,6 +117,7 @@ def lib() -> C.CDLL:
         "crdt_hip_set_param": (i32, [vp, C.c_char_p, u64]),
         "crdt_hip_oplog_new": (i32, [P(vp)]),
         "crdt_hip_oplog_set_fugue": (i32, [vp, i32]),
+        "crdt_hip_oplog_set_agent": (i32, [vp, C.c_uint16]),
         "crdt_hip_oplog_clone": (i32, [vp, P(vp)]),
         "crdt_hip_oplog_free": (None, [vp]),
         "crdt_hip_oplog_insert": (i32, [vp, sz, C.c_char_p, sz]),
@@ -243,7 +244,7 @@ class LogArrays:
 class OpLog:
     """Host-side resolver (positional patches -> anchor op log), crdt_hip_oplog_*."""
 
-    def __init__(self, handle=None, fugue: bool = False):
+    def __init__(self, handle=None, fugue: bool = False, agent: int = 0):
         if handle is None:
             h = C.c_void_p()
             _check(lib().crdt_hip_oplog_new(C.byref(h)))
@@ -251,6 +252,8 @@ class OpLog:
             if fugue:
                 _check(lib().crdt_hip_oplog_set_fugue(h, 1))
         self._h = handle
+        if agent:
+            _check(lib().crdt_hip_oplog_set_agent(self._h, agent))
 
     def __del__(self):
         if getattr(self, "_h", None) and _LIB is not None:

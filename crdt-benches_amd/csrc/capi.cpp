@@ -226,6 +226,11 @@ int crdt_hip_oplog_set_fugue(crdt_hip_oplog* log, int on) {
     log->log.fugue = on != 0;
     return 0;
 }
+int crdt_hip_oplog_set_agent(crdt_hip_oplog* log, uint16_t agent) {
+    if (!log) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
+    log->log.local_agent = agent;
+    return 0;
+}
 int crdt_hip_oplog_clone(const crdt_hip_oplog* src, crdt_hip_oplog** out) {
     if (!src || !out) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
     return guard(nullptr, [&] { *out = new crdt_hip_oplog(*src); return 0; });
@@ -267,7 +272,9 @@ int crdt_hip_oplog_get_view(const crdt_hip_oplog* log, crdt_hip_oplog_view* out)
     out->agent = L.agent.data();
     out->deleted = L.deleted.data();
     out->cp = L.cp.data();
-    out->side = L.fugue ? L.side.data() : nullptr;
+    // (non-NULL for an empty Fugue log too: a replica made from it is a Fugue replica)
+    static const uint8_t kNoSide = 0;
+    out->side = L.fugue ? (L.side.empty() ? &kNoSide : L.side.data()) : nullptr;
     return 0;
 }
 uint64_t crdt_hip_oplog_version(const crdt_hip_oplog* log) { return log ? log->log.version() : 0; }
@@ -275,7 +282,6 @@ uint64_t crdt_hip_oplog_version(const crdt_hip_oplog* log) { return log ? log->l
 int crdt_hip_oplog_encode_from(const crdt_hip_oplog* log, uint64_t version, uint8_t* buf,
                                size_t cap, size_t* out_len) {
     if (!log || !out_len) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
-    if (log->log.fugue) return set_err(nullptr, CRDT_HIP_EINVAL, "Fugue logs have no update wire format");
     return guard(nullptr, [&] {
         std::vector<uint8_t> u = log->log.encode_from(version);
         *out_len = u.size();
@@ -286,7 +292,6 @@ int crdt_hip_oplog_encode_from(const crdt_hip_oplog* log, uint64_t version, uint
 }
 int crdt_hip_oplog_apply_update(crdt_hip_oplog* log, const uint8_t* buf, size_t len) {
     if (!log || (!buf && len)) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
-    if (log->log.fugue) return set_err(nullptr, CRDT_HIP_EINVAL, "Fugue logs have no update wire format");
     return guard(nullptr, [&] {
         std::string e = log->log.apply_update(buf, len);
         return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EINVAL, e);
@@ -643,8 +648,6 @@ int crdt_hip_replica_new(crdt_hip_ctx* ctx, const crdt_hip_oplog_view* init,
                          crdt_hip_replica** out) {
     if (!ctx || !out) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
     *out = nullptr;
-    if (init && init->side)
-        return set_err(ctx, CRDT_HIP_EINVAL, "Fugue logs have no update wire format (replicas are RGA)");
     if (init) {
         int rc = check_view(ctx, init);
         if (rc) return rc;

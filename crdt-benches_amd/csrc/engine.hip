@@ -146,7 +146,7 @@ constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-by
 // weighted pre-order of the rows is the Fugue in-order (lamport < 0xFFFFFFFF).  The tree row is
 // the last row of its run, so "the run of slot s" (a rank lookup) and "the previous run" of a seq
 // head both land on it.
-constexpr uint64_t kLeftKey = 1ull << 48;
+// (kLeftKey: engine.hpp)
 // words of the jump bitvector of a wave (a multiple of 4: the left-child bits follow it aligned)
 __host__ __device__ constexpr uint64_t jbits_words(uint64_t slots) { return (slots / 32 + 8 + 3) & ~3ull; }
 constexpr uint64_t kMidKey = (1ull << 48) - 1ull;

@@ -66,6 +66,7 @@ constexpr uint32_t kSeqBit = 0x00400000u;
 // Fugue: the item is a LEFT child of its parent (bit 21; the previous-slot flag is then never
 // set: a seq item is a right child of the slot before it)
 constexpr uint32_t kLeftBit = 0x00200000u;
+constexpr uint64_t kLeftKey = 1ull << 48;  // key bit of a left child (see engine.hip)
 __host__ __device__ inline void cp3_put(uint8_t* b, uint64_t slot, uint32_t v) {
     b[3 * slot] = (uint8_t)v;
     b[3 * slot + 1] = (uint8_t)(v >> 8);

@@ -317,7 +317,8 @@ std::string OpLog::remove(uint64_t start, uint64_t end) {
 }
 
 void OpLog::push_item(uint32_t par, uint32_t orr, uint32_t lam, uint16_t ag, uint8_t del,
-                      uint32_t c) {
+                      uint32_t c, uint8_t sd) {
+    if (fugue) side.push_back(sd);
     parent.push_back(par);
     oright.push_back(orr);
     lamport.push_back(lam);
@@ -339,6 +340,7 @@ void OpLog::mark_deleted(uint32_t id) {
 // Rebuild the positional index from the op log itself (RGA document order) after remote
 // items arrived.  Host resolver bookkeeping only: merged documents always come from the device.
 std::string OpLog::rebuild_index() {
+    if (fugue) return rebuild_index_fugue();
     uint32_t n = size();
     std::vector<uint32_t> start(n + 2, 0), kids(n);
     for (uint32_t i = 1; i <= n; ++i) {
@@ -369,23 +371,84 @@ std::string OpLog::rebuild_index() {
         stack.pop_back();
         if (v) {
             ++seen;
-            const bool del = deleted[v - 1] != 0;
-            Chunk* ch = &chunks_.back();
-            Span* last = ch->s.empty() ? nullptr : &ch->s.back();
-            if (last && last->del() == del && last->id + last->len() == v) {
-                last->n++;
-            } else {
-                if (ch->s.size() >= kSpanMax / 2) {
-                    chunks_.push_back(new_chunk());
-                    ch = &chunks_.back();
-                }
-                ch->s.push_back(Span{v, 1u | (del ? 0x80000000u : 0u)});
-            }
-            if (!del) { ch->vis++; nvis_++; }
+            index_append(v);
         }
         uint32_t a = start[v], b = start[v + 1];
         std::sort(kids.begin() + a, kids.begin() + b, [&](uint32_t x, uint32_t y) { return newer(y, x); });
         for (uint32_t j = a; j < b; ++j) stack.push_back(kids[j]);  // oldest pushed first
+    }
+    if (seen != n) return "malformed op log (cycle)";
+    fen_build();
+    stale_ = false;
+    return "";
+}
+
+// Appends item v to the end of the rebuilt sequence.
+void OpLog::index_append(uint32_t v) {
+    const bool del = deleted[v - 1] != 0;
+    Chunk* ch = &chunks_.back();
+    Span* last = ch->s.empty() ? nullptr : &ch->s.back();
+    if (last && last->del() == del && last->id + last->len() == v) {
+        last->n++;
+    } else {
+        if (ch->s.size() >= kSpanMax / 2) {
+            chunks_.push_back(new_chunk());
+            ch = &chunks_.back();
+        }
+        ch->s.push_back(Span{v, 1u | (del ? 0x80000000u : 0u)});
+    }
+    if (!del) { ch->vis++; nvis_++; }
+}
+
+// The Fugue in-order (left children by timestamp descending, the item, then its right children
+// by timestamp descending), as orc_merge_fugue (oracle/oracle.c) walks it; also recomputes
+// hasright_ with the remote right children.
+std::string OpLog::rebuild_index_fugue() {
+    const uint32_t n = size();
+    if (side.size() != n) return "malformed op log (side column)";
+    std::vector<uint32_t> start(2ull * n + 3, 0), kids(n);  // groups 2v (left), 2v + 1 (right)
+    for (uint32_t i = 1; i <= n; ++i) {
+        const uint32_t p = parent[i - 1];
+        if (p > n || p == i || (p == 0 && side[i - 1])) return "malformed op log (parent out of range)";
+        start[2ull * p + (side[i - 1] ? 0 : 1) + 1]++;
+    }
+    for (uint64_t g = 0; g < 2ull * n + 2; ++g) start[g + 1] += start[g];
+    {
+        std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+        for (uint32_t i = 1; i <= n; ++i) kids[fill[2ull * parent[i - 1] + (side[i - 1] ? 0 : 1)]++] = i;
+    }
+    hasright_.assign(std::max<size_t>(hasright_.size(), (size_t)n + 1), 0);
+    for (uint32_t i = 1; i <= n; ++i)
+        if (!side[i - 1]) hasright_[parent[i - 1]] = 1;
+    auto older = [&](uint32_t a, uint32_t b) {  // a has the smaller timestamp
+        if (lamport[a - 1] != lamport[b - 1]) return lamport[a - 1] < lamport[b - 1];
+        return agent[a - 1] < agent[b - 1];
+    };
+    chunks_.clear();
+    chunks_.push_back(new_chunk());
+    nvis_ = 0;
+    hint_c_ = SIZE_MAX;
+    hint_si_ = SIZE_MAX;
+    constexpr uint32_t EMIT = 0x80000000u;
+    std::vector<uint32_t> stack;
+    stack.reserve(2ull * n + 2);
+    stack.push_back(0);
+    size_t seen = 0;
+    while (!stack.empty()) {
+        const uint32_t e = stack.back();
+        stack.pop_back();
+        if (e & EMIT) {
+            ++seen;
+            index_append(e & ~EMIT);
+            continue;
+        }
+        // pushed in reverse of the walk: right children, e, left children (each oldest first)
+        const uint32_t l0 = start[2ull * e], l1 = start[2ull * e + 1], r1 = start[2ull * e + 2];
+        std::sort(kids.begin() + l0, kids.begin() + l1, older);
+        std::sort(kids.begin() + l1, kids.begin() + r1, older);
+        for (uint32_t j = l1; j < r1; ++j) stack.push_back(kids[j]);
+        if (e) stack.push_back(e | EMIT);
+        for (uint32_t j = l0; j < l1; ++j) stack.push_back(kids[j]);
     }
     if (seen != n) return "malformed op log (cycle)";
     fen_build();
@@ -403,7 +466,7 @@ std::vector<uint8_t> OpLog::encode_from(uint64_t ver) const {
     std::vector<uint8_t> b;
     b.reserve(24 + (size_t)n * 18 + 4 + (size_t)m * 4);
     put32(b, kMagic);
-    put32(b, kWireVersion);
+    put32(b, fugue ? kUpdateVersionFugue : kWireVersion);
     put32(b, from_items + 1);
     put32(b, n);
     put32(b, from_dels);
@@ -411,7 +474,11 @@ std::vector<uint8_t> OpLog::encode_from(uint64_t ver) const {
     for (uint32_t k = 0; k < n; ++k) put32(b, parent[from_items + k]);
     for (uint32_t k = 0; k < n; ++k) put32(b, oright[from_items + k]);
     for (uint32_t k = 0; k < n; ++k) put32(b, lamport[from_items + k]);
-    for (uint32_t k = 0; k < n; ++k) put32(b, cp[from_items + k]);
+    if (fugue)
+        for (uint32_t k = 0; k < n; ++k)
+            put32(b, cp[from_items + k] | (side[from_items + k] ? kUpdateSideBit : 0u));
+    else
+        for (uint32_t k = 0; k < n; ++k) put32(b, cp[from_items + k]);
     for (uint32_t k = 0; k < n; ++k) {
         b.push_back((uint8_t)agent[from_items + k]);
         b.push_back((uint8_t)(agent[from_items + k] >> 8));
@@ -423,7 +490,9 @@ std::vector<uint8_t> OpLog::encode_from(uint64_t ver) const {
 
 std::string OpLog::apply_update(const uint8_t* buf, size_t len) {
     if (len < 24 || get32(buf) != kMagic) return "not an update";
-    if (get32(buf + 4) != kWireVersion) return "unsupported update version";
+    const uint32_t ver = get32(buf + 4);
+    if (ver == kUpdateVersionFugue && !fugue) return "Fugue update into an RGA log";
+    if (ver != kWireVersion && ver != kUpdateVersionFugue) return "unsupported update version";
     uint32_t first = get32(buf + 8), n = get32(buf + 12);
     uint32_t first_del = get32(buf + 16), m = get32(buf + 20);
     size_t agent_bytes = ((size_t)n * 2 + 3) / 4 * 4;
@@ -443,6 +512,11 @@ std::string OpLog::apply_update(const uint8_t* buf, size_t len) {
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t id = first + k, par = get32(P + 4 * k);
         if (id > size() && par >= id && par != 0) return "update item references an unknown parent";
+        if (fugue && id > size()) {
+            if (par == 0 && (get32(C + 4 * k) & kUpdateSideBit))
+                return "update item is a left child of the document start";
+            if (get32(L + 4 * k) == 0xFFFFFFFFu) return "Fugue update item with lamport 0xFFFFFFFF";
+        }
     }
     const uint64_t known = std::max<uint64_t>(size(), n ? (uint64_t)first + n - 1 : 0);
     for (uint32_t k = 0; k < m; ++k) {
@@ -452,8 +526,10 @@ std::string OpLog::apply_update(const uint8_t* buf, size_t len) {
     for (uint32_t k = 0; k < n; ++k) {
         uint32_t id = first + k;
         if (id <= size()) continue;  // already known (decode_and_add is idempotent)
+        const uint32_t c = get32(C + 4 * k);
         push_item(get32(P + 4 * k), get32(O + 4 * k), get32(L + 4 * k),
-                  (uint16_t)(A[2 * k] | (A[2 * k + 1] << 8)), 0, get32(C + 4 * k));
+                  (uint16_t)(A[2 * k] | (A[2 * k + 1] << 8)), 0, c & ~kUpdateSideBit,
+                  fugue && (c & kUpdateSideBit) ? 1 : 0);
     }
     for (uint32_t k = 0; k < m; ++k) {
         const uint32_t id = get32(D + 4 * k);

@@ -19,6 +19,10 @@ namespace crdt {
 // Update wire format (OpLog::encode_from / apply_update, decoded on the device by replica.hip).
 constexpr uint32_t kUpdateMagic = 0x55445243u;  // "CRDU"
 constexpr uint32_t kUpdateVersion = 1;
+// A Fugue log's updates: the same layout, with bit 31 of cp[k] = side[k] (1: left child).
+// Only Fugue logs and replicas accept them.
+constexpr uint32_t kUpdateVersionFugue = 2;
+constexpr uint32_t kUpdateSideBit = 0x80000000u;
 
 class OpLog {
 public:
@@ -53,7 +57,7 @@ public:
     // Append a fully-specified item (synthetic generators / decoding); marks the positional
     // index stale.
     void push_item(uint32_t par, uint32_t orr, uint32_t lam, uint16_t ag, uint8_t del,
-                   uint32_t c);
+                   uint32_t c, uint8_t sd = 0);
     void mark_deleted(uint32_t id);
     // For bulk builders that fill the SoA directly.
     void mark_stale() { stale_ = true; }
@@ -99,6 +103,8 @@ private:
     Chunk new_chunk() const;
     bool split_chunk(size_t c);  // true if chunk c was split in two
     std::string rebuild_index();
+    std::string rebuild_index_fugue();
+    void index_append(uint32_t v);
     // p-th visible item (p >= 1): chunk c, span si, offset off inside the span.
     bool find_visible(uint64_t p, size_t& c, size_t& si, uint32_t& off) const;
     uint32_t first_id_from(size_t c, size_t si) const;  // first item at or after (c, si), or NIL

@@ -40,7 +40,8 @@ enum UCtl { U_ERR = 0, U_ITEMS, U_DELS, U_MAXID, U_ADD_CP, U_ADD_B, U_DEL_CP, U_
             U_PLAN,  // replay: the decode's sizes differ from the ones the merge was planned with
             U_N };
 // U_ERR bits
-constexpr uint64_t E_HEADER = 1, E_NOT_READY = 2, E_PARENT = 4, E_DELETE = 8, E_BOUNDS = 16;
+constexpr uint64_t E_HEADER = 1, E_NOT_READY = 2, E_PARENT = 4, E_DELETE = 8, E_BOUNDS = 16,
+                   E_FUGUE = 32;
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 #pragma unroll
@@ -108,6 +109,7 @@ struct UpdArgs {
     uint64_t cap_slots;
     uint32_t* imap;  // per flattened item / delete: its update (found by the check pass, reused
     uint32_t* dmap;  //   by the write pass instead of a second binary search)
+    uint32_t fugue;  // Fugue replica: version-2 updates, cp bit 31 = left child (oplog.hpp)
 };
 
 __global__ __launch_bounds__(kUB) void k_upd_parse(UpdArgs a) {
@@ -122,7 +124,9 @@ __global__ __launch_bounds__(kUB) void k_upd_parse(UpdArgs a) {
             const uint32_t h0 = h[0], h1 = h[1], f = h[2], ni = h[3], mm = h[5];
             const uint64_t need =
                 24ull + 16ull * ni + ((2ull * ni + 3ull) / 4ull) * 4ull + 4ull * mm;
-            bad = h0 != kUpdateMagic || h1 != kUpdateVersion || need > o1 - o0;
+            bad = h0 != kUpdateMagic ||
+                  (h1 != kUpdateVersion && !(h1 == kUpdateVersionFugue && a.fugue)) ||
+                  need > o1 - o0;
             if (!bad) {
                 first = f;
                 nit = ni;
@@ -236,16 +240,22 @@ __global__ __launch_bounds__(kUB) void k_upd_items(UpdArgs a) {
                 err |= E_PARENT;
                 continue;
             }
+            const uint32_t c = a.buf[h.w + 3u * h.y + k], lam = a.buf[h.w + 2u * h.y + k];
+            const bool left = a.fugue && (c & kUpdateSideBit);
+            if (a.fugue && ((left && par == 0u) || lam == 0xFFFFFFFFu)) {
+                err |= E_FUGUE;  // a left child of the document start, or the content-row key
+                continue;
+            }
             if (WRITE) {
                 if ((uint64_t)id >= a.cap_slots) {
                     err |= E_BOUNDS;
                     continue;
                 }
-                const uint32_t c = a.buf[h.w + 3u * h.y + k];
                 a.parent[id] = par;
-                a.key[id] = ((uint64_t)a.buf[h.w + 2u * h.y + k] << 16) |
+                a.key[id] = ((uint64_t)lam << 16) | (left ? kLeftKey : 0ull) |
                             reinterpret_cast<const uint16_t*>(a.buf + h.w + 4u * h.y)[k];
-                cp3_put(a.cp, id, (c & kCpMaskR) | (par == id - 1u ? kSeqBit : 0u));  // live
+                // live; a left child never carries the previous-slot flag
+                cp3_put(a.cp, id, (c & kCpMaskR) | (left ? kLeftBit : (par == id - 1u ? kSeqBit : 0u)));
                 add_cp += 1u;
                 add_b += utf8_len(c & kCpMaskR);
             }
@@ -318,15 +328,17 @@ __global__ __launch_bounds__(kUB) void k_rep_copy(const uint32_t* __restrict__ s
                                                   const uint8_t* __restrict__ sc,
                                                   uint32_t* __restrict__ dp, uint64_t* __restrict__ dk,
                                                   uint8_t* __restrict__ dc, uint64_t n) {
-    const uint64_t nw = cp3_bytes(n) / 4;
+    // (the codepoint column's dwords number about 3/4 of the slots, or more for tiny replicas:
+    // the loop runs over both)
+    const uint64_t nw = cp3_bytes(n) / 4, m = nw > n ? nw : n;
     const uint32_t* sw = reinterpret_cast<const uint32_t*>(sc);
     uint32_t* dw = reinterpret_cast<uint32_t*>(dc);
-    for (uint64_t g = (uint64_t)blockIdx.x * kUB + threadIdx.x; g < nw; g += (uint64_t)gridDim.x * kUB) {
+    for (uint64_t g = (uint64_t)blockIdx.x * kUB + threadIdx.x; g < m; g += (uint64_t)gridDim.x * kUB) {
         if (g < n) {
             dp[g] = sp[g];
             dk[g] = sk[g];
         }
-        dw[g] = sw[g];
+        if (g < nw) dw[g] = sw[g];
     }
 }
 
@@ -431,6 +443,7 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     r.n = n;
     r.vis_cp = r.vis_bytes = 0;
     r.version++;
+    r.logs.fugue = v && v->side;  // a Fugue replica (its merges run the Fugue rows)
     if (!n) return CRDT_HIP_OK;
     DeviceLogs& L = r.logs;
     // on the engine stream, after the padding kernel replica_reserve may have queued there (a
@@ -440,9 +453,14 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     std::vector<uint8_t> c(3ull * n);
     std::vector<uint64_t> key(n);
     for (uint32_t i = 0; i < n; ++i) {
-        key[i] = ((uint64_t)v->lamport[i] << 16) | v->agent[i];
+        const bool left = v->side && v->side[i];
+        if (v->side && (v->lamport[i] == 0xFFFFFFFFu || (left && v->parent[i] == 0))) {
+            E.err = "invalid Fugue log (lamport 0xFFFFFFFF or a left child of the document start)";
+            return CRDT_HIP_EBADLOG;
+        }
+        key[i] = ((uint64_t)v->lamport[i] << 16) | v->agent[i] | (left ? kLeftKey : 0ull);
         cp3_put(c.data(), i, (v->cp[i] & kCpMaskR) | (v->deleted[i] ? kDelBit : 0u) |
-                                 (v->parent[i] == i ? kSeqBit : 0u));
+                                 (left ? kLeftBit : (v->parent[i] == i ? kSeqBit : 0u)));
         if (!v->deleted[i]) {
             r.vis_cp += 1;
             r.vis_bytes += utf8_len_cp(v->cp[i] & kCpMaskR);
@@ -473,6 +491,7 @@ int replica_copy(Engine& E, const Replica& src, Replica& dst) {
         RCHK(hipGetLastError(), "replica copy");
     }
     dst.n = src.n;
+    D.fugue = S.fugue;
     dst.vis_cp = src.vis_cp;
     dst.vis_bytes = src.vis_bytes;
     dst.version++;
@@ -628,6 +647,7 @@ int decode_launch(Engine& E, Replica& r, const uint8_t* buf, uint64_t len,
     a.cap_slots = L.cap_slots;
     a.imap = r.imap;
     a.dmap = r.dmap;
+    a.fugue = L.fugue ? 1u : 0u;
     const uint32_t gi = std::min<uint64_t>(kMaxGrid, grid_for(len / 16 / kItemsPerThread + 1, kUB));
     const uint32_t gd = std::min<uint64_t>(kMaxGrid, grid_for(len / 4 + 1, kUB));
     k_upd_parse<<<nblk, kUB, 0, s>>>(a);
@@ -659,6 +679,7 @@ int replica_settle(Engine& E, Replica& r) {
                 : e & E_NOT_READY ? "update is not causally ready (missing items)"
                 : e & E_PARENT    ? "update item references an unknown parent"
                 : e & E_DELETE    ? "update deletes an unknown item"
+                : e & E_FUGUE     ? "Fugue update item: a left child of the document start or lamport 0xFFFFFFFF"
                                   : "update writes outside the replica";
         return CRDT_HIP_EBADLOG;
     }

@@ -136,8 +136,13 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 int crdt_hip_oplog_new(crdt_hip_oplog** out);
 /* Fugue anchors for every later insert (only on an empty log): an insert after left neighbour a
  * becomes a right child of a if a has none yet, else a left child of a's full-list successor.
- * Fugue logs have no update wire format (encode_from / apply_update / replicas refuse them). */
+ * A Fugue log's updates are wire version 2 (bit 31 of each cp word = left child); only Fugue
+ * logs and Fugue replicas (crdt_hip_replica_new from a Fugue log's view, empty or not) take
+ * them.  Version-1 (RGA) updates apply to either kind. */
 int crdt_hip_oplog_set_fugue(crdt_hip_oplog* log, int on);
+/* The agent id of this log's later local inserts (default 0).  Editors that exchange updates
+ * need distinct agents: (lamport, agent) identifies an item. */
+int crdt_hip_oplog_set_agent(crdt_hip_oplog* log, uint16_t agent);
 int crdt_hip_oplog_clone(const crdt_hip_oplog* src, crdt_hip_oplog** out);
 void crdt_hip_oplog_free(crdt_hip_oplog* log);
 /* insert `nbytes` of UTF-8 at codepoint position `pos` (Upstream::insert). */

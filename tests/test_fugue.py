@@ -9,6 +9,8 @@ children, the item, right children; each side by (lamport, agent) descending).  
   * a log without left children merges exactly as RGA.
 The product resolver's Fugue anchors are checked bit-exact against the oracle's resolver.
 """
+import random
+import struct
 import sys
 
 import numpy as np
@@ -129,11 +131,82 @@ def test_host_fugue_oplog_api(oracle):
         s = s[:pos] + text + s[pos:]
     s = s[:1] + s[4:]
     assert oracle.merge_fugue(to_anchor(lg)) == s.encode()
+    upd = log.encode_from(0)
+    assert struct.unpack_from("<2I", upd) == (0x55445243, 2)  # "CRDU", version 2 (Fugue)
     with pytest.raises(crdt_hip.CrdtHipError):
-        log.encode_from(0)  # Fugue logs have no update wire format
+        crdt_hip.OpLog().apply_update(upd)  # an RGA log takes no Fugue update
     rga = crdt_hip.OpLog()
     rga.insert(0, "a")
     assert crdt_hip.lib().crdt_hip_oplog_set_fugue(rga._h, 1) != 0  # only on an empty log
+
+
+# ---- CPU: the update wire format (version 2: cp bit 31 = left child) --------------------------
+def fugue_updates(name, limit=None):
+    """(sender log, per-patch updates) of a trace replayed on a Fugue log."""
+    t = crdt_hip.Trace(trace_path(name))
+    up = crdt_hip.OpLog(fugue=True)
+    up.insert(0, t.start_content)
+    updates = [up.encode_from(0)]
+    for i in range(len(t) if limit is None else min(limit, len(t))):
+        pos, dele, ins = t.patch(i)
+        v = up.version()
+        up.replace(pos, pos + dele, ins)
+        updates.append(up.encode_from(v))
+    return t, up, updates
+
+
+def same_log(a, b):
+    x, y = a.arrays(), b.arrays()
+    assert x.n == y.n
+    for f in ("parent", "lamport", "agent", "deleted", "cp", "side"):
+        assert np.array_equal(getattr(x, f), getattr(y, f)), f
+
+
+def test_host_fugue_updates_round_trip(oracle):
+    t, up, updates = fugue_updates("sveltecomponent")
+    down = crdt_hip.OpLog(fugue=True)
+    for u in updates:
+        down.apply_update(u)
+    same_log(up, down)
+    assert oracle.merge_fugue(to_anchor(down.arrays())) == t.end_content.encode()
+    # one update from version 0, and every update twice (idempotent)
+    one = crdt_hip.OpLog(fugue=True)
+    one.apply_update(up.encode_from(0))
+    one.apply_update(updates[len(updates) // 2])
+    same_log(up, one)
+
+
+def edit_and_check(oracle, log, rng, k):
+    """k random local edits on a log whose index was rebuilt from remote items: each must land
+    at its position in the oracle's in-order merge of the log."""
+    for _ in range(k):
+        text = oracle.merge_fugue(to_anchor(log.arrays())).decode()
+        if text and rng.random() < 0.3:
+            a = rng.randrange(len(text))
+            b = min(len(text), a + rng.randint(1, 4))
+            log.remove(a, b)
+            want = text[:a] + text[b:]
+        else:
+            p = rng.randint(0, len(text))
+            ins = rng.choice(["x", "yz", "\u00e9", "\U0001f600w", "pq r"])
+            log.insert(p, ins)
+            want = text[:p] + ins + text[p:]
+        assert oracle.merge_fugue(to_anchor(log.arrays())).decode() == want
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode"])
+def test_host_fugue_rebuilt_index_takes_local_edits(oracle, name):
+    """A log that received a whole trace as remote updates rebuilds its positional index as the
+    Fugue in-order (OpLog::rebuild_index_fugue): local edits made on it land where asked."""
+    t, up, updates = fugue_updates(name, limit=20000)
+    down = crdt_hip.OpLog(fugue=True, agent=7)
+    for u in updates:
+        down.apply_update(u)
+    same_log(up, down)
+    assert down.arrays().side.any()
+    edit_and_check(oracle, down, random.Random(5), 60)
+    lg = down.arrays()
+    assert (lg.agent[up.arrays().n:] == 7).all()  # the local agent (crdt_hip_oplog_set_agent)
 
 
 # ---- GPU: device merge vs oracle --------------------------------------------------------------
@@ -247,3 +320,101 @@ def test_gpu_fugue_multi_wave_lanes(golden, lanes):
         assert lens[r] == golden[name]["end_bytes"], r
     b.close()
     c.close()
+
+
+# ---- GPU: Fugue replicas (device decode of version-2 updates) --------------------------------
+_FUPD = {}
+
+
+def fugue_updates_cached(name):
+    if name not in _FUPD:
+        _FUPD[name] = fugue_updates(name)
+    return _FUPD[name]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", TRACES)
+def test_gpu_fugue_replica_decodes_trace(ctx, oracle, golden, name):
+    """Every per-patch update of a trace replayed on a Fugue log, decoded into an (empty) Fugue
+    replica in one batch: the trace's endContent, the sender's log bit for bit."""
+    t, up, updates = fugue_updates_cached(name)
+    r = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
+    r.apply_updates(updates)
+    text, dig = r.merge()
+    assert text == t.end_content.encode()
+    assert "%016x" % dig == golden[name]["tree_digest"]
+    items, vis_cp, vis_b = r.info()
+    assert (items, vis_cp, vis_b) == (up.view().n, len(t.end_content), len(text))
+    assert (text, dig) == ctx.merge(up)
+
+
+@pytest.mark.gpu
+def test_gpu_fugue_replica_random_batches_and_clone(ctx, oracle):
+    """Random-sized batches into a replica made from a partial Fugue log, a device clone taken
+    midway, against the host decoder fed the same updates one at a time."""
+    t, up, updates = fugue_updates_cached("rustcode")
+    at0 = len(updates) // 5
+    host = crdt_hip.OpLog(fugue=True)
+    for u in updates[:at0]:
+        host.apply_update(u)
+    r = crdt_hip.Replica(ctx, host)          # a non-empty Fugue view
+    rng = random.Random(11)
+    i, snap = at0, None
+    while i < len(updates):
+        batch = updates[i: i + rng.choice([1, 3, 50, 700, 4000])]
+        r.apply_updates(batch)
+        for u in batch:
+            host.apply_update(u)
+        i += len(batch)
+        if snap is None and i >= len(updates) // 2:
+            snap = (r.clone(), host.clone(), i)
+    text, _ = r.merge()
+    assert text == t.end_content.encode() == oracle.merge_fugue(to_anchor(host.arrays()))
+    rc, hc, at = snap
+    assert rc.merge()[0] == oracle.merge_fugue(to_anchor(hc.arrays()))
+    rc.apply_updates(updates[at:])
+    assert rc.merge()[0] == text
+
+
+@pytest.mark.gpu
+def test_gpu_fugue_replay_closure(ctx, golden):
+    """crdt_hip_replica_replay (clone + decode + merge as one graph) on a Fugue replica."""
+    name = "sveltecomponent"
+    t, up, updates = fugue_updates_cached(name)
+    init = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
+    init.apply_updates(updates[:1])          # the start content
+    ub = crdt_hip.UpdateBatch(ctx, *crdt_hip.pack_updates(updates[1:]))
+    want = (len(t.end_content), len(t.end_content.encode()), int(golden[name]["tree_digest"], 16))
+    before = init.info()
+    for _ in range(3):
+        assert init.replay(ub) == want
+    assert init.info() == before
+    ub.close()
+    init.close()
+
+
+@pytest.mark.gpu
+def test_gpu_fugue_replica_update_checks(ctx):
+    """An RGA replica rejects a version-2 update; a Fugue replica takes RGA (version-1) updates
+    and rejects a left child of the document start, leaving itself unchanged."""
+    t, up, updates = fugue_updates_cached("sveltecomponent")
+    rga = crdt_hip.Replica(ctx)
+    with pytest.raises(crdt_hip.CrdtHipError):
+        rga.apply_updates(updates[:3])
+    assert rga.info()[0] == 0
+    _, rga_updates = crdt_hip.HipMerge.upstream_updates("", [(0, 0, "abc"), (1, 1, "XY")])
+    f = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
+    f.apply_updates(rga_updates)
+    assert f.merge()[0] == b"aXYc"
+    bad = crdt_hip.OpLog(fugue=True)
+    bad.insert(0, "ab")
+    u = bytearray(bad.encode_from(0))
+    # item 1 (parent 0) marked as a left child: cp words follow 6 header words + 3 columns of 2
+    struct.pack_into("<I", u, 24 + 3 * 8, ord("a") | 0x80000000)
+    with pytest.raises(crdt_hip.CrdtHipError):
+        crdt_hip.OpLog(fugue=True).apply_update(bytes(u))
+    info = f.info()
+    struct.pack_into("<I", u, 8, info[0] + 1)  # new ids for the replica (first id, word 2)
+    with pytest.raises(crdt_hip.CrdtHipError):
+        f.apply_updates([bytes(u)])
+    assert f.info() == info and f.merge()[0] == b"aXYc"

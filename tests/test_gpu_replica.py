@@ -112,6 +112,10 @@ def test_replica_from_initial_log_and_empty(ctx):
     r = crdt_hip.Replica(ctx, log)
     assert r.merge() == ctx.merge(log)
     assert r.info()[0] == log.view().n
+    # a clone of a replica whose capacity is tight (uploaded, never grown) copies every slot
+    # (k_rep_copy once stopped at the codepoint column's dword count, ~3/4 of the slots)
+    c = r.clone()
+    assert c.merge() == ctx.merge(log) and c.info() == r.info()
 
 
 def _set_word(u: bytes, word: int, value: int) -> bytes:
