@@ -652,8 +652,19 @@ def downstream_workload(args) -> int:
     for name in TRACES:
         t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
         patches = [t.patch(i) for i in range(len(t))]
-        up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
-        init = crdt_hip.Replica(ctx, up.log if up.log.view().n else None)
+        if args.order == "fugue":  # a Fugue upstream: version-2 updates into a Fugue replica
+            lg = crdt_hip.OpLog(fugue=True)
+            if t.start_content:
+                lg.insert(0, t.start_content)
+            init = crdt_hip.Replica(ctx, lg)
+            updates = []
+            for pos, dele, ins in patches:
+                v = lg.version()
+                lg.replace(pos, pos + dele, ins)
+                updates.append(lg.encode_from(v))
+        else:
+            up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
+            init = crdt_hip.Replica(ctx, up.log if up.log.view().n else None)
         buf, offs = crdt_hip.pack_updates(updates)
         # the update vector (main.rs:58) resident in HBM, unless the PCIe upload is timed too
         src = (buf, offs) if args.pcie else crdt_hip.UpdateBatch(ctx, buf, offs)
@@ -708,7 +719,7 @@ def downstream_workload(args) -> int:
                                    "device decode, 4 traces one after the other, "
                                    + ("clone / apply / merge_len calls" if args.stepwise or args.pcie
                                       else "one crdt_hip_replica_replay call per closure"),
-                       "updates": total_patches,
+                       "updates": total_patches, "order": args.order,
                        "encoded_bytes": int(sum(w[4] for w in work)),
                        "parallelism": f"replicas x{world} (no data-path collective)"},
             "per_trace": {w[0]: {"ms": per[w[0]] / args.steps * 1e3,
@@ -763,8 +774,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--order", default="rga", choices=["rga", "fugue"],
-                    help="document order of the traces workload (fugue: a side line; the CPU "
-                         "baseline and the shuffle companion are RGA-only and are skipped)")
+                    help="document order of the traces and downstream workloads (fugue: a "
+                         "side line; the CPU baseline and the shuffle companion are RGA-only "
+                         "and are skipped)")
     ap.add_argument("--workload", default="traces",
                     choices=["traces", "seph", "agents64", "big1b", "downstream"],
                     help="traces: config 3 (headline); seph: config 2; agents64: config 4; "

@@ -458,6 +458,7 @@ std::string OpLog::rebuild_index_fugue() {
 
 // Wire format (little-endian): magic, version, first_id, n_items, first_del, n_dels,
 // parent[n], origin_right[n], lamport[n], cp[n] (u32), agent[n] (u16, padded to 4), dels[m].
+// Fugue logs write version 2, with bit 31 of cp[k] = side (1: left child of parent[k]).
 std::vector<uint8_t> OpLog::encode_from(uint64_t ver) const {
     uint32_t from_items = (uint32_t)(ver >> 32), from_dels = (uint32_t)ver;
     if (from_items > size()) from_items = size();
