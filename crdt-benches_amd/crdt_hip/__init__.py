@@ -436,7 +436,8 @@ class LogFile:
             return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
         return LogArrays(arr(v.parent, np.uint32), arr(v.lamport, np.uint32),
                          arr(v.agent, np.uint16), arr(v.deleted, np.uint8),
-                         arr(v.cp, np.uint32), arr(v.origin_right, np.uint32))
+                         arr(v.cp, np.uint32), arr(v.origin_right, np.uint32),
+                         arr(v.side, np.uint8) if v.side else None)
 
 
 def _as_view(log) -> tuple:

@@ -438,7 +438,6 @@ int crdt_hip_trace_save(const crdt_hip_trace* t, const char* path) {
 }
 int crdt_hip_oplog_save(const crdt_hip_oplog* log, const char* path) {
     if (!log || !path) return set_err(nullptr, CRDT_HIP_EINVAL, "null argument");
-    if (log->log.fugue) return set_err(nullptr, CRDT_HIP_EINVAL, "the op-log file format has no side column");
     return guard(nullptr, [&] {
         std::string e = crdt::save_oplog(log->log, path);
         return e.empty() ? 0 : set_err(nullptr, CRDT_HIP_EIO, e);
@@ -475,7 +474,8 @@ int crdt_hip_logfile_open(const char* path, crdt_hip_logfile** out, crdt_hip_opl
         view->agent = f->m.agent;
         view->deleted = f->m.deleted;
         view->cp = f->m.cp;
-        view->side = nullptr;
+        static const uint8_t kNoSide = 0;  // (an empty Fugue file's view is still Fugue)
+        view->side = f->m.fugue ? (f->m.n ? f->m.side : &kNoSide) : nullptr;
         *out = f;
         return 0;
     });

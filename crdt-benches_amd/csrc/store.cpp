@@ -148,9 +148,10 @@ std::string load_trace_bin(const std::string& path, Trace& out) {
 std::string save_oplog(const OpLog& L, const std::string& path) {
     LogHeader h{};
     std::memcpy(h.magic, kLogMagic, 8);
-    h.version = kStoreVersion;
+    h.version = L.fugue ? kLogVersionFugue : kStoreVersion;
     h.n = L.size();
     h.ndels = (uint32_t)L.del_ops.size();
+    if (L.fugue && L.side.size() != L.size()) return "malformed Fugue op log (side column)";
     h.local_agent = L.local_agent;
     h.max_lamport = L.max_lamport;
     const uint64_t n = h.n;
@@ -162,6 +163,8 @@ std::string save_oplog(const OpLog& L, const std::string& path) {
         h.off[i] = at;
         at = align64(at + bytes[i]);
     }
+    const uint64_t side_off = at;  // (Fugue) the side column follows the arrays
+    if (L.fugue) at = align64(at + n);
     h.size = at;
     static const uint8_t zeros[64] = {};
     std::vector<std::pair<const void*, size_t>> parts{{&h, sizeof h}};
@@ -170,6 +173,11 @@ std::string save_oplog(const OpLog& L, const std::string& path) {
         parts.push_back({zeros, (size_t)(h.off[i] - pos)});
         parts.push_back({src[i], (size_t)bytes[i]});
         pos = h.off[i] + bytes[i];
+    }
+    if (L.fugue) {
+        parts.push_back({zeros, (size_t)(side_off - pos)});
+        parts.push_back({L.side.data(), (size_t)n});
+        pos = side_off + n;
     }
     parts.push_back({zeros, (size_t)(h.size - pos)});
     return write_all(path, parts);
@@ -202,13 +210,17 @@ std::string map_oplog(const std::string& path, MappedLog& out) {
         return std::string(what) + path;
     };
     if (std::memcmp(h.magic, kLogMagic, 8) != 0) return fail("not an op-log file: ");
-    if (h.version != kStoreVersion) return fail("unsupported op-log file version in ");
+    if (h.version != kStoreVersion && h.version != kLogVersionFugue)
+        return fail("unsupported op-log file version in ");
     if (h.size != size) return fail("truncated op-log file ");
     const uint64_t n = h.n;
     const uint64_t bytes[7] = {4 * n, 4 * n, 4 * n, 4 * n, 2 * n, n, 4ull * h.ndels};
     for (int i = 0; i < 7; ++i)
         if (h.off[i] % 64 || h.off[i] < sizeof h || h.off[i] > size || bytes[i] > size - h.off[i])
             return fail("corrupt op-log file ");
+    const bool fugue = h.version == kLogVersionFugue;
+    const uint64_t side_off = align64(h.off[6] + bytes[6]);
+    if (fugue && (side_off > size || n > size - side_off)) return fail("corrupt op-log file ");
     const uint8_t* b = static_cast<const uint8_t*>(base);
     if (out.base) munmap(out.base, out.size);
     out.base = base;
@@ -224,6 +236,8 @@ std::string map_oplog(const std::string& path, MappedLog& out) {
     out.agent = reinterpret_cast<const uint16_t*>(b + h.off[4]);
     out.deleted = b + h.off[5];
     out.del_ops = reinterpret_cast<const uint32_t*>(b + h.off[6]);
+    out.fugue = fugue;
+    out.side = fugue ? b + side_off : nullptr;
     return "";
 }
 
@@ -240,6 +254,10 @@ std::string load_oplog(const std::string& path, OpLog& out) {
     L.agent.assign(m.agent, m.agent + m.n);
     L.deleted.assign(m.deleted, m.deleted + m.n);
     L.del_ops.assign(m.del_ops, m.del_ops + m.ndels);
+    if (m.fugue) {
+        L.fugue = true;
+        L.side.assign(m.side, m.side + m.n);
+    }
     uint64_t vis = 0;
     uint32_t ml = 0;
     for (uint32_t i = 0; i < m.n; ++i) {

@@ -17,6 +17,9 @@ namespace crdt {
 constexpr char kTraceMagic[8] = {'C', 'R', 'D', 'T', 'T', 'R', 'C', '1'};
 constexpr char kLogMagic[8] = {'C', 'R', 'D', 'T', 'L', 'O', 'G', '1'};
 constexpr uint32_t kStoreVersion = 1;
+// Op-log files of Fugue logs: version 2, the same header and arrays followed by the side column
+// (n bytes, 64-byte aligned).  Readers take both versions.
+constexpr uint32_t kLogVersionFugue = 2;
 
 bool is_trace_bin(const std::string& path);
 std::string save_trace_bin(const Trace& t, const std::string& path);
@@ -35,6 +38,8 @@ struct MappedLog {
     const uint16_t* agent = nullptr;
     const uint8_t* deleted = nullptr;
     const uint32_t* del_ops = nullptr;
+    const uint8_t* side = nullptr;  // Fugue files (version 2); NULL otherwise
+    bool fugue = false;
     ~MappedLog();
 };
 std::string map_oplog(const std::string& path, MappedLog& out);

@@ -192,7 +192,8 @@ int crdt_hip_trace_resolve_many(const crdt_hip_trace* const* traces, uint32_t n,
  * Trace cache: the parsed trace in one flat file; crdt_hip_trace_load reads either format
  * (recognised by the file's magic), so a cache is a drop-in for the .json.gz path of
  * load_testing_data (main.rs:19,52).  Op-log file: the resolved anchor log as 64-byte-aligned
- * SoA arrays.  Files are written to `path`.tmp and renamed. */
+ * SoA arrays (a Fugue log's file is version 2 and adds its side column; its view has `side`).
+ * Files are written to `path`.tmp and renamed. */
 int crdt_hip_trace_save(const crdt_hip_trace* t, const char* path);
 int crdt_hip_oplog_save(const crdt_hip_oplog* log, const char* path);
 /* An editable op log read from a file (positional edits rebuild the resolver index first). */

@@ -76,6 +76,34 @@ def C_addr(ptr) -> int:
     return ctypes.cast(ptr, ctypes.c_void_p).value or 0
 
 
+@pytest.mark.parametrize("name", ["sveltecomponent", "seph-blog1"])
+def test_fugue_oplog_file_roundtrip(tmp_path, oracle, name):
+    """A Fugue log's file (version 2) keeps the side column: mapped, loaded and edited on."""
+    from test_fugue import to_anchor as fugue_anchor
+    log = crdt_hip.Trace(trace_path(name)).resolve(fugue=True)
+    path = str(tmp_path / f"{name}.fugue.crdtlog")
+    log.save(path)
+    assert open(path, "rb").read()[8:12] == b"\x02\0\0\0"
+    f = crdt_hip.LogFile(path)
+    a, b = f.arrays(), log.arrays()
+    same_arrays(a, b)
+    assert a.side is not None and np.array_equal(a.side, b.side) and a.side.any()
+    assert C_addr(f.view().side) % 64 == 0
+    f.close()
+    back = crdt_hip.OpLog.load(path)
+    assert np.array_equal(back.arrays().side, b.side)
+    for L in (back, log):
+        L.insert(11, "fugue€")
+        L.remove(2, 6)
+    same_arrays(back.arrays(), log.arrays())
+    assert np.array_equal(back.arrays().side, log.arrays().side)
+    assert back.encode_from(0) == log.encode_from(0)
+    assert oracle.merge_fugue(fugue_anchor(back.arrays())) == oracle.merge_fugue(fugue_anchor(log.arrays()))
+    empty = str(tmp_path / "e.fugue.crdtlog")
+    crdt_hip.OpLog(fugue=True).save(empty)
+    assert crdt_hip.LogFile(empty).view().side  # an empty Fugue file is still Fugue
+
+
 def test_empty_log_file(tmp_path):
     path = str(tmp_path / "e.crdtlog")
     crdt_hip.OpLog().save(path)
@@ -126,6 +154,14 @@ def test_mapped_log_merges_on_device(tmp_path, golden):
         text, dig = ctx.merge(f)
         assert len(text) == golden[name]["end_bytes"]
         assert dig == int(golden[name]["tree_digest"], 16)
+    fp = str(tmp_path / "fugue.crdtlog")
+    flog = crdt_hip.Trace(trace_path("rustcode")).resolve(fugue=True)
+    flog.save(fp)
+    ff = crdt_hip.LogFile(fp)
+    assert ctx.merge(ff) == ctx.merge(flog)
+    assert ctx.merge(ff)[1] == int(golden["rustcode"]["tree_digest"], 16)
+    assert crdt_hip.Replica(ctx, ff).merge() == ctx.merge(flog)
+    ff.close()
     b = ctx.batch(files, replicas=3, relabel=2, seed=5)
     digs, lens = b.merge()[:2]
     expect = [int(golden[n]["tree_digest"], 16) for n in TRACES] * 3
