@@ -61,12 +61,14 @@ static std::vector<double> time_iters(int iters, F&& f) {
     return out;
 }
 
+static bool g_fugue = false;  // --order fugue: Fugue logs (left/right anchors, in-order)
+
 // main.rs:17-48 with R = HipMerge
 template <class R>
 static void upstream(const std::string& dir, const char* name, int iters) {
     Loaded L = load(dir, name, R::EDITS_USE_BYTE_OFFSETS);
     auto secs = time_iters(iters, [&] {
-        R rope = R::from_str(L.start);
+        R rope = R::from_str(L.start, g_fugue);
         for (size_t i = 0; i < L.len; ++i) {
             size_t pos, del, il;
             const char* ins;
@@ -92,7 +94,7 @@ static void downstream(const std::string& dir, const char* name, int iters) {
         size_t il;
         crdt_hip_trace_patch(L.t, i, &pos, &del, &p, &il);
         ins = std::string_view(p, il);
-    });
+    }, g_fugue);
     const R& crdt0 = pr.first;
     const auto& updates = pr.second;
     auto secs = time_iters(iters, [&] {
@@ -118,7 +120,8 @@ static void batched(const std::string& dir, int iters, uint32_t replicas, uint32
     for (const char* name : TRACES) {
         Loaded L = load(dir, name, false);
         crdt_hip_oplog* log = nullptr;
-        check(crdt_hip_trace_resolve(L.t, &log), nullptr, "resolve");
+        check(g_fugue ? crdt_hip_trace_resolve_fugue(L.t, &log) : crdt_hip_trace_resolve(L.t, &log),
+              nullptr, "resolve");
         crdt_hip_oplog_view v;
         crdt_hip_oplog_get_view(log, &v);
         logs.push_back(log);
@@ -159,6 +162,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--iters")) iters = std::atoi(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--replicas")) replicas = (uint32_t)std::atoi(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--relabel")) relabel = (uint32_t)std::atoi(argv[i + 1]);
+        else if (!std::strcmp(argv[i], "--order")) g_fugue = !std::strcmp(argv[i + 1], "fugue");
     }
     if (group == "upstream" || group == "all")
         for (const char* t : TRACES) upstream<HipMerge>(dir, t, iters);

@@ -45,9 +45,11 @@ public:
     static constexpr bool EDITS_USE_BYTE_OFFSETS = false;
     using Update = std::vector<uint8_t>;
 
-    // Upstream::from_str (rope.rs:113-121: new op log, one insert of the start content)
-    static HipMerge from_str(std::string_view s) {
+    // Upstream::from_str (rope.rs:113-121: new op log, one insert of the start content);
+    // `fugue`: a Fugue log (left/right anchors, in-order document, version-2 updates)
+    static HipMerge from_str(std::string_view s, bool fugue = false) {
         HipMerge m;
+        if (fugue) check(crdt_hip_oplog_set_fugue(m.log_.get(), 1), nullptr, "set_fugue");
         if (!s.empty()) m.insert(0, s);
         return m;
     }
@@ -108,8 +110,9 @@ public:
     template <class PatchFn>
     static std::pair<HipMerge, std::vector<Update>> upstream_updates(std::string_view start,
                                                                       size_t npatches,
-                                                                      PatchFn&& patch) {
-        HipMerge up = from_str(start);
+                                                                      PatchFn&& patch,
+                                                                      bool fugue = false) {
+        HipMerge up = from_str(start, fugue);
         std::vector<Update> updates;
         updates.reserve(npatches);
         for (size_t i = 0; i < npatches; ++i) {
@@ -125,7 +128,7 @@ public:
                   "encode_from");
             updates.push_back(std::move(u));
         }
-        return {from_str(start), std::move(updates)};
+        return {from_str(start, fugue), std::move(updates)};
     }
     // Downstream::apply_update (rope.rs:222-224)
     void apply_update(const Update& u) {
@@ -160,11 +163,13 @@ public:
     template <class PatchFn>
     static std::pair<HipDownstream, std::vector<Update>> upstream_updates(std::string_view start,
                                                                            size_t npatches,
-                                                                           PatchFn&& patch) {
-        auto pr = HipMerge::upstream_updates(start, npatches, patch);
+                                                                           PatchFn&& patch,
+                                                                           bool fugue = false) {
+        auto pr = HipMerge::upstream_updates(start, npatches, patch, fugue);
         crdt_hip_oplog_view v = pr.first.view();
         HipDownstream d(pr.first.device());
-        check(crdt_hip_replica_new(d.dev_->ctx, v.n ? &v : nullptr, &d.rep_), d.dev_->ctx,
+        // (a Fugue log's view, empty or not, makes a Fugue replica)
+        check(crdt_hip_replica_new(d.dev_->ctx, v.n || v.side ? &v : nullptr, &d.rep_), d.dev_->ctx,
               "replica_new");
         return {std::move(d), std::move(pr.second)};
     }
