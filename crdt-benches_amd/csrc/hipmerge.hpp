@@ -33,9 +33,11 @@ struct Device {
     ~Device() { crdt_hip_destroy(ctx); }
     Device(const Device&) = delete;
     Device& operator=(const Device&) = delete;
+    // The process-wide device, never destroyed: a static destructor would run crdt_hip_destroy
+    // after the HIP runtime's own teardown at exit (the process exit releases the device).
     static std::shared_ptr<Device> shared() {
-        static std::shared_ptr<Device> d = std::make_shared<Device>(0);
-        return d;
+        static std::shared_ptr<Device>* d = new std::shared_ptr<Device>(std::make_shared<Device>(0));
+        return *d;
     }
 };
 
