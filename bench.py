@@ -257,8 +257,10 @@ def load_bases(fugue: bool = False):
 
 
 def host_cpus() -> dict:
-    """CPUs this process may run on (hardware_concurrency honouring the affinity mask) and the
-    cgroup CPU quota, if any."""
+    """CPUs this process can actually use: the affinity mask (what hardware_concurrency honours)
+    capped by the cgroup CPU quota (cpu.max; on the pool's boxes the mask shows the whole
+    machine's 256 CPUs and the quota is 16).  `threads` = min(affinity, floor(quota)): more
+    threads than the quota only time-slice the same CPUs."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     quota = None
     try:
@@ -268,7 +270,8 @@ def host_cpus() -> dict:
                 quota = round(int(q) / int(p), 2)
     except (OSError, ValueError):
         pass
-    return {"threads": n, "cgroup_cpu_quota": quota}
+    eff = n if quota is None else max(1, min(n, int(quota)))
+    return {"threads": eff, "affinity_cpus": n, "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(bases, patches, seconds: float, threads: int) -> dict:
@@ -295,10 +298,10 @@ def cpu_baseline(bases, patches, seconds: float, threads: int) -> dict:
             break
     cpus = host_cpus()
     return {"value": done / el, "unit": "patches/s", "cores": threads, "kind": "port",
-            "cgroup_cpu_quota": cpus["cgroup_cpu_quota"],
+            "affinity_cpus": cpus["affinity_cpus"], "cgroup_cpu_quota": cpus["cgroup_cpu_quota"],
             "sample": f"{rounds} rounds x {len(batch)} documents ({threads} copies of the 4 "
                       f"resolved traces), {el:.1f} s, oracle/oracle.c orc_merge_rga, one "
-                      "document per thread over every CPU of the affinity mask"}
+                      "document per thread, threads = min(affinity mask, cgroup CPU quota)"}
 
 
 def config1(ctx, seconds: float) -> dict:

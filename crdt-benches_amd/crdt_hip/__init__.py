@@ -203,6 +203,9 @@ def tree_digest(data: bytes) -> int:
 
 
 # ------------------------------------------------------------------------------------------------
+_NO_SIDE = (C.c_uint8 * 1)(0)  # the side column of an empty Fugue log (never read)
+
+
 class LogArrays:
     """Anchor op log as numpy SoA (ids 1..n).  Keeps the arrays alive for a View.  `side`
     (optional): 1 = the item is a LEFT child of its parent (Fugue order); None = RGA."""
@@ -230,7 +233,14 @@ class LogArrays:
     def view(self) -> View:
         def p(a, t):
             return a.ctypes.data_as(C.POINTER(t)) if a.size else None
-        side = None if self.side is None else p(self.side, C.c_uint8)
+        # a Fugue log stays a Fugue log when empty: a null side means RGA, so an empty side
+        # column points at a dummy byte (as the C API's kNoSide does, capi.cpp)
+        if self.side is None:
+            side = None
+        elif self.side.size:
+            side = p(self.side, C.c_uint8)
+        else:
+            side = C.cast(_NO_SIDE, C.POINTER(C.c_uint8))
         return View(self.n, p(self.parent, C.c_uint32), p(self.origin_right, C.c_uint32),
                     p(self.lamport, C.c_uint32), p(self.agent, C.c_uint16),
                     p(self.deleted, C.c_uint8), p(self.cp, C.c_uint32), side)

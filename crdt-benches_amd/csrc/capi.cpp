@@ -410,7 +410,13 @@ int crdt_hip_trace_resolve_many(const crdt_hip_trace* const* traces, uint32_t n,
         }
     };
     std::vector<std::thread> pool;
-    for (uint32_t j = 1; j < k; ++j) pool.emplace_back(work);
+    try {
+        pool.reserve(k);
+        for (uint32_t j = 1; j < k; ++j) pool.emplace_back(work);
+    } catch (...) {
+        // no more threads (std::system_error) or no memory: the threads already started and
+        // the calling thread share the work; nothing may cross the C ABI
+    }
     work();
     for (std::thread& th : pool) th.join();
     for (uint32_t i = 0; i < n; ++i)

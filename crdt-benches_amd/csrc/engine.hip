@@ -2511,8 +2511,9 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
             for (uint32_t i = 0; i < v.n; ++i) {
                 const bool left = v.side[i] != 0;
                 if (v.lamport[i] == 0xFFFFFFFFu) {  // (kMidKey sorts above every right child)
-                    err = "Fugue log with lamport 0xFFFFFFFF";
-                    return CRDT_HIP_EINVAL;
+                    // a malformed log, as replica_upload reports it (one code on every path)
+                    err = "invalid Fugue log (lamport 0xFFFFFFFF)";
+                    return CRDT_HIP_EBADLOG;
                 }
                 L.fugue |= left;
                 key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i] | (left ? kLeftKey : 0ull);
@@ -2527,9 +2528,12 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
                                          (v.parent[i] == i ? kSeqBit : 0u));
         }
     }
-    HIPCHK(hipMemcpy(L.parent, par.data(), S * 4, hipMemcpyHostToDevice), "upload parent");
-    HIPCHK(hipMemcpy(L.key, key.data(), S * 8, hipMemcpyHostToDevice), "upload key");
-    HIPCHK(hipMemcpy(L.cp, c.data(), c.size(), hipMemcpyHostToDevice), "upload cp");
+    // on the engine's stream (a null-stream copy does not wait for the non-blocking streams the
+    // kernels run on, nor they for it), then waited for: the host columns are freed on return
+    HIPCHK(hipMemcpyAsync(L.parent, par.data(), S * 4, hipMemcpyHostToDevice, stream), "upload parent");
+    HIPCHK(hipMemcpyAsync(L.key, key.data(), S * 8, hipMemcpyHostToDevice, stream), "upload key");
+    HIPCHK(hipMemcpyAsync(L.cp, c.data(), c.size(), hipMemcpyHostToDevice, stream), "upload cp");
+    HIPCHK(hipStreamSynchronize(stream), "upload sync");
     return CRDT_HIP_OK;
 }
 
@@ -2608,7 +2612,8 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
         HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
         HIPCHK(dalloc(&deg_, r + 16), "hipMalloc deg");
-        HIPCHK(hipMemset(deg_, 0, (r + 16) * 4), "memset deg");
+        // (stream-ordered: k_count adds into it on this engine's streams)
+        HIPCHK(hipMemsetAsync(deg_, 0, (r + 16) * 4, stream), "memset deg");
         HIPCHK(dalloc(&cstart_, r + 16), "hipMalloc cstart");
         HIPCHK(dalloc(&child_, r), "hipMalloc child");
         HIPCHK(dalloc(&defer_, r / 3 + 64), "hipMalloc defer");
@@ -3003,7 +3008,9 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     runs_ += p.R;
     if (!errs && hctl[C_VISITED] != p.R) errs |= 16u;  // unreachable runs: a cycle
     if (errs) {
-        (void)hipMemset(deg_, 0, (cap_runs_ + 16) * 4);  // restore the all-zero invariant
+        // restore the all-zero invariant (stream-ordered, as every use of deg_)
+        (void)hipMemsetAsync(deg_, 0, (cap_runs_ + 16) * 4, stream);
+        (void)hipStreamSynchronize(stream);
         err = "malformed op log detected on device (flags " + std::to_string(errs) + ")";
         return CRDT_HIP_EBADLOG;
     }
@@ -3072,12 +3079,16 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         collect(L, wi, digests, lens, cps, text_bytes);
         if (text_out) {
             std::vector<uint64_t> offs(w.ndocs + 1);
-            HIPCHK(hipMemcpy(offs.data(), toff_, (w.ndocs + 1) * 8ull, hipMemcpyDeviceToHost),
-                   "copy offsets");
+            HIPCHK(hipMemcpyAsync(offs.data(), toff_, (w.ndocs + 1) * 8ull, hipMemcpyDeviceToHost,
+                                  stream), "copy offsets");
+            HIPCHK(hipStreamSynchronize(stream), "copy offsets");
             const uint64_t total = offs[w.ndocs] * (mode == ORDER ? 4 : 1);
             text_out->resize(total);
-            if (total)
-                HIPCHK(hipMemcpy(text_out->data(), text_, total, hipMemcpyDeviceToHost), "copy text");
+            if (total) {
+                HIPCHK(hipMemcpyAsync(text_out->data(), text_, total, hipMemcpyDeviceToHost, stream),
+                       "copy text");
+                HIPCHK(hipStreamSynchronize(stream), "copy text");
+            }
             if (text_offsets) *text_offsets = offs;
         }
     }

@@ -173,7 +173,13 @@ public:
     int merge_async_enqueue(DeviceLogs& L, AsyncMerge& m);
     int merge_async_finish(DeviceLogs& L, AsyncMerge& m, uint64_t* digests, uint64_t* lens,
                            uint64_t* cps, crdt_hip_stats* st);
-    uint64_t generation() const { return gen_; }  // bumped by every (re)allocation of scratch
+    // bumped by every (re)allocation of scratch, this engine's or a lane engine's (a graph that
+    // captured a multi-lane merge holds the lane engines' pointers too)
+    uint64_t generation() const {
+        uint64_t g = gen_;
+        for (const auto& e : lane_eng_) g += e->generation() + 1;
+        return g;
+    }
 
     // One config-5 document generated on the device (synth.cpp synth_tree_item, item by item).
     int synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t del_pct,

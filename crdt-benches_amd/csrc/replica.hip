@@ -511,8 +511,13 @@ int updates_upload(Engine& E, UpdateBatch& ub, const uint8_t* buf, uint64_t len,
     RCHK(hipSetDevice(E.device), "hipSetDevice");
     RCHK(dalloc(&ub.buf, (len + 4) & ~3ull), "hipMalloc update buffer");
     RCHK(dalloc(&ub.off, n + 1ull), "hipMalloc update offsets");
-    if (len) RCHK(hipMemcpy(ub.buf, buf, len, hipMemcpyHostToDevice), "upload updates");
-    if (n) RCHK(hipMemcpy(ub.off, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice), "upload offsets");
+    // on the engine's stream (the decode kernels run there; a null-stream copy would not be
+    // ordered with them), waited for before the caller's buffers may go
+    if (len) RCHK(hipMemcpyAsync(ub.buf, buf, len, hipMemcpyHostToDevice, E.stream), "upload updates");
+    if (n)
+        RCHK(hipMemcpyAsync(ub.off, offsets, (n + 1ull) * 8, hipMemcpyHostToDevice, E.stream),
+             "upload offsets");
+    RCHK(hipStreamSynchronize(E.stream), "upload updates");
     ub.len = len;
     ub.n = n;
     // the largest id the batch carries, from its headers (first id, items at words 2, 3); a

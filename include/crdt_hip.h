@@ -74,7 +74,13 @@ typedef struct {
     /* optional (NULL: RGA).  Fugue order (SURVEY.md §8(a) s0 "side u8 (Fugue)"): side[k] != 0
      * makes item k a LEFT child of parent[k]; the document is then the in-order walk (left
      * children, the item, right children; each side by (lamport, agent) descending).  An RGA
-     * log is the Fugue log without left children.  lamport must stay below 0xFFFFFFFF. */
+     * log is the Fugue log without left children.  lamport must stay below 0xFFFFFFFF (a Fugue
+     * log with lamport 0xFFFFFFFF, or with a left child of the document start, is malformed:
+     * CRDT_HIP_EBADLOG on every path that takes a view).
+     * ABI 2 added this field at the end of the struct: a caller written against ABI 1 must
+     * zero-initialise the whole view (`crdt_hip_oplog_view v = {0};`) and check
+     * crdt_hip_abi_version() == CRDT_HIP_ABI_VERSION, or a garbage `side` makes its log a Fugue
+     * log. */
     const uint8_t* side;
 } crdt_hip_oplog_view;
 
@@ -269,7 +275,13 @@ int crdt_hip_replica_clone(crdt_hip_ctx* ctx, const crdt_hip_replica* src,
                            crdt_hip_replica** out);
 int crdt_hip_replica_free(crdt_hip_replica* r);
 /* Apply updates i = 0..n-1, update i = buf[offsets[i], offsets[i+1]) (n + 1 offsets, each a
- * multiple of 4, offsets[n] <= len < 4 GiB), in order (apply_update, rope.rs:222-224). */
+ * multiple of 4, offsets[n] <= len < 4 GiB), in order (apply_update, rope.rs:222-224).
+ * Same validation as crdt_hip_oplog_apply_update, with one documented difference: the device
+ * replica keeps tombstone bits, not the host log's ordered list of delete ops (which
+ * encode_from re-sends by index), so it does not refuse an update whose first delete index lies
+ * beyond the deletes it has seen ("missing deletes" on the host).  Tombstoning a known item is
+ * order-free, so the documents agree once both have every update
+ * (tests/test_gpu_replica.py::test_gap_in_deletes_host_rejects_device_accepts). */
 int crdt_hip_replica_apply_updates(crdt_hip_ctx* ctx, crdt_hip_replica* r, const uint8_t* buf,
                                    size_t len, const uint64_t* offsets, uint32_t n);
 /* A batch of encoded updates (layout as crdt_hip_replica_apply_updates) uploaded to HBM once:

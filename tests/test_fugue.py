@@ -418,3 +418,26 @@ def test_gpu_fugue_replica_update_checks(ctx):
     with pytest.raises(crdt_hip.CrdtHipError):
         f.apply_updates([bytes(u)])
     assert f.info() == info and f.merge()[0] == b"aXYc"
+
+
+@pytest.mark.gpu
+def test_gpu_fugue_replica_from_empty_fugue_arrays(ctx, golden):
+    """A replica built from the numpy arrays of an EMPTY Fugue log is a Fugue replica: its side
+    column is a zero-length array, which the view passes as a non-null pointer (null = RGA), so
+    version-2 updates apply."""
+    name = "sveltecomponent"
+    t, up, updates = fugue_updates_cached(name)
+    arrs = crdt_hip.OpLog(fugue=True).arrays()
+    assert arrs.side is not None and arrs.side.size == 0
+    r = crdt_hip.Replica(ctx, arrs)
+    r.apply_updates(updates)
+    text, dig = r.merge()
+    assert text == t.end_content.encode()
+    assert "%016x" % dig == golden[name]["tree_digest"]
+
+
+def test_empty_fugue_arrays_view_keeps_side():
+    """CPU half of the above: the view of an empty Fugue log's arrays carries a non-null side."""
+    v = crdt_hip.OpLog(fugue=True).arrays().view()
+    assert v.n == 0 and bool(v.side)
+    assert not bool(crdt_hip.OpLog().arrays().view().side)

@@ -180,6 +180,37 @@ def test_replica_rejects_bad_batches_and_stays_unchanged(ctx):
     assert r.merge() == ref
 
 
+def test_gap_in_deletes_host_rejects_device_accepts(ctx):
+    """A delete-only update that arrives before the delete update preceding it.  The host log
+    keeps the delete ops in order (encode_from re-sends them by index), so it refuses an update
+    whose first delete index lies beyond the ones it holds ("missing deletes").  The device
+    replica keeps no delete-op log, only tombstone bits: tombstoning a known item is state-based
+    and order-free, so it accepts the update.  Once both have every update, the documents agree
+    (documented divergence, crdt_hip.h crdt_hip_replica_apply)."""
+    _, _, updates = trace_updates("sveltecomponent")
+
+    def hdr(u):
+        return struct.unpack_from("<6I", u, 0)
+
+    i = next(i for i in range(1000, len(updates) - 1)
+             if hdr(updates[i])[3] == 0 and hdr(updates[i])[5] > 0
+             and hdr(updates[i + 1])[3] == 0 and hdr(updates[i + 1])[5] > 0)
+    d1, d2 = updates[i], updates[i + 1]
+    host = crdt_hip.OpLog()
+    for x in updates[:i]:
+        host.apply_update(x)
+    with pytest.raises(crdt_hip.CrdtHipError):
+        host.apply_update(d2)                 # first_del beyond the deletes it holds
+    r = crdt_hip.Replica(ctx)
+    r.apply_updates(updates[:i])
+    r.apply_updates([d2])                     # accepted: its targets are known items
+    r.apply_updates([d1])
+    host.apply_update(d1)
+    host.apply_update(d2)
+    assert r.merge() == ctx.merge(host)
+    assert r.info()[1] == host.arrays().deleted.size - int(host.arrays().deleted.sum())
+
+
 def test_downstream_device_bench_loop(golden):
     """The reference's downstream closure (main.rs:63-69) with the device replica:
     clone the initial CRDT, apply every update, len() == endContent length."""

@@ -4,11 +4,18 @@ Config 4 (64-agent concurrent log, 10 M items, seed 0x5EED0001) is compared with
 full size, bytes and pre-order.  Config 5 (one document, 50 % tombstones, seed 0x5EED0002) is
 compared with the oracle at 250 M items (typing chains, p_chain 0.9) and 150 M items (uniform
 random parents, p_chain 0: the worst case for gathers), sizes at which the single-threaded oracle
-finishes in about a minute; at the full 1 G items it is checked through size-independent
-properties: the merged length equals the log's visible items (counted without merging), the
-text is one codepoint per byte, and the digest does not depend on the list-ranking splitter
-stride.  The check being strengthened is the reference's length assert (main.rs:35,68).
+finishes in about a minute; at the full 1 G items the device digest is compared with the
+oracle's, precomputed in the build container by tests/golden/make_config5.c (orc_merge_rga
+over the same generator; 1.5 and 4 minutes single-threaded, ~32 GB) and committed as
+tests/golden/config5.json: an order-sensitive check of all 500 M visible items.  The full-size
+run also checks size-independent properties: the merged length equals the log's visible items
+(counted without merging), the text is one codepoint per byte, and the digest does not depend
+on the list-ranking splitter stride.  The check being strengthened is the reference's length
+assert (main.rs:35,68).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -60,11 +67,21 @@ def test_config5_vs_oracle(ctx, oracle, n, p_chain):
     assert int(dig[0]) == oracle.tree_digest(ref)
 
 
+def config5_golden(n, p_chain):
+    with open(os.path.join(os.path.dirname(__file__), "golden", "config5.json")) as f:
+        for c in json.load(f)["cases"]:
+            if (c["n"], c["p_chain"], c["del_pct"], c["seed"]) == (n, p_chain, 50, SEED5):
+                return c
+    raise KeyError((n, p_chain))
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("p_chain", [90, 0])
 def test_config5_full_size_properties(p_chain):
     n = 1_000_000_000
+    gold = config5_golden(n, p_chain)
     visible = crdt_hip.synth_tree_visible(n, 50, SEED5)
+    assert visible == gold["visible"] == gold["len"]
     digests = []
     for stride in (0, 16, 4096):  # 0: the engine's own choice
         c = crdt_hip.Context(0)
@@ -78,3 +95,5 @@ def test_config5_full_size_properties(p_chain):
         b.close()
         c.close()
     assert len(set(digests)) == 1, digests
+    # order-sensitive: the oracle's digest of the same 1 G-item log (tests/golden/make_config5.c)
+    assert "%016x" % digests[0] == gold["digest"]
