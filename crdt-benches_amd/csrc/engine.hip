@@ -758,6 +758,8 @@ struct TreeArgs {
     uint32_t* gcp;     // per group of a document above 16 MiB: codepoints
     uint4* res;        // per document {UTF-8 bytes, codepoints, digest lo, digest hi}: the wave's
                        // results, after ctl in one block, copied to the host in one transfer
+    const uint32_t* rank;  // per document: its k_doctree workgroup
+    uint4* wg;             // per k_doctree workgroup: its descriptor (DocArgs::wg)
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
@@ -1122,7 +1124,9 @@ __global__ __launch_bounds__(kBlock) void k_wstep(const uint32_t* __restrict__ v
 }
 
 // Single workgroup: per-document length (weight between consecutive document starts), aligned
-// output offsets, leaf offsets.
+// output offsets, leaf offsets; for the LDS level 1 (wg != null) every k_doctree workgroup's
+// descriptor (document, first run, runs, text prefix, text bytes, output offset), so that a
+// k_doctree workgroup finds all of it in one round of loads.
 __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     __shared__ uint64_t st[1024];
     __shared__ uint32_t sl[1024];
@@ -1133,12 +1137,17 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     const uint64_t am = (uint64_t)a.align - 1u;
     for (uint32_t d0 = 0; d0 < a.ndocs; d0 += 1024) {
         const uint32_t d = d0 + threadIdx.x;
-        uint32_t tl = 0;
+        uint32_t tl = 0, p0 = 0, r0 = 0, r1 = 0;
         if (d < a.ndocs) {
             const uint32_t end = d + 1 < a.ndocs ? a.doc_p0[d + 1] : wtotal;
-            tl = end - a.doc_p0[d];
+            p0 = a.doc_p0[d];
+            tl = end - p0;
             a.tlen[d] = tl;
             a.res[d] = make_uint4(tl, 0u, 0u, 0u);
+            if (a.wg) {
+                r0 = a.doc_root[d];
+                r1 = d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL];
+            }
         }
         const uint64_t sz = ((uint64_t)tl + am) & ~am;
         const uint32_t nl = a.align > 1 ? (tl + kLeaf - 1u) / kLeaf : 0u;
@@ -1154,8 +1163,14 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
             __syncthreads();
         }
         if (d < a.ndocs) {
-            a.toff[d] = carry_t + st[threadIdx.x] - sz;
+            const uint64_t to = carry_t + st[threadIdx.x] - sz;
+            a.toff[d] = to;
             a.loff[d] = carry_l + sl[threadIdx.x] - nl;
+            if (a.wg) {
+                const uint32_t k = a.rank[d];
+                a.wg[2u * k] = make_uint4(d, r0, r1 - r0, p0);
+                a.wg[2u * k + 1u] = make_uint4(tl, (uint32_t)to, (uint32_t)(to >> 32), 0u);
+            }
         }
         carry_t += st[1023];
         carry_l += sl[1023];
@@ -1270,8 +1285,12 @@ constexpr int kDocK = (kDocJ + (1 << kDocLog2S) - 1) >> kDocLog2S;
 #ifndef CRDT_DOC_WALK_WAVES
 #define CRDT_DOC_WALK_WAVES 16
 #endif
+// The offset is a Fibonacci hash of the block index (the top bits of the low 16 bits of its
+// product with 2^16 / phi: one full-rate 24-bit multiply), so that the walk tests every node it
+// reaches for being a splitter in three VALU ops.
 __device__ __forceinline__ uint32_t splitter_off(uint32_t b) {
-    return (CRDT_DOC_HASHSPLIT && b) ? (b * 0x9E3779B1u) >> (32u - kDocLog2S) : 0u;
+    if (!CRDT_DOC_HASHSPLIT) return 0u;
+    return (__umul24(b, 0x9E37u) >> (16u - kDocLog2S)) & ((1u << kDocLog2S) - 1u);
 }
 __device__ __forceinline__ uint32_t splitter_run(uint32_t b) {
     return (b << kDocLog2S) | splitter_off(b);
@@ -1279,15 +1298,16 @@ __device__ __forceinline__ uint32_t splitter_run(uint32_t b) {
 constexpr uint32_t kDocLds = 163840 - 1024;  // dynamic LDS budget (static arrays use the rest)
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
-constexpr uint16_t kDead16 = 0xFFFEu;  // nx of a pruned run
 constexpr uint32_t kNil14 = 0x3FFFu;   // no next splitter (splitter records: sum << 14 | next)
-constexpr uint32_t kDocBig = 32;       // runs of >= 0xFFFF bytes per document (LDS side table)
 
 struct DocArgs {
     uint32_t ndocs, rcap, scap, chbytes;
     uint32_t probe;  // 1 + document whose phase times are printed (0: none)
     const uint32_t* doc_root;
-    const uint32_t* order;  // workgroup -> document (costliest first)
+    // per workgroup (costliest document first), written by k_doctotals: {document, first run,
+    // runs, text prefix}, {text bytes, output offset lo, hi, 0}
+    const uint4* wg;
+    uint32_t keyoff;  // LDS byte offset of the sibling keys
     const uint32_t* r_parent;
     const uint64_t* r_key;
     uint32_t* roff;
@@ -1303,9 +1323,10 @@ struct DocArgs {
     uint32_t lds_bytes;   // dynamic LDS of the launch
 };
 
-// LDS bytes of a document with up to rcap - 2 runs: D, nx, ch, w (2 B/run each; together the
-// 8-byte run records later) and the gl region: the work list of sibling groups of two or more
-// (at most one per two runs), later the splitter records (4 B per splitter).
+// LDS bytes of a document with up to rcap - 2 runs: D, nx, ch (2 B/run each), the sibling keys
+// (8 B/run; the 8-byte run records later take D, nx, ch and the front of the keys) and the gl
+// region: the work list of sibling groups of three or more (at most one per three runs), later
+// the splitter records (4 B per splitter).
 __host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t) {
     return (2u * rcap + 15u) & ~15u;
 }
@@ -1315,14 +1336,18 @@ __host__ __device__ constexpr uint32_t doctree_gl_bytes(uint32_t rcap, uint32_t 
     return ((2u * doctree_defer_cap(rcap) > 4u * scap ? 2u * doctree_defer_cap(rcap) : 4u * scap) +
             15u) & ~15u;
 }
+__host__ __device__ constexpr uint32_t doctree_key_off(uint32_t rcap, uint32_t scap) {
+    return (4u * rcap + doctree_ch_bytes(rcap, scap) + 15u) & ~15u;
+}
 __host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap) {
-    return 6ull * rcap + doctree_ch_bytes(rcap, scap) + doctree_gl_bytes(rcap, scap);
+    return (uint64_t)doctree_key_off(rcap, scap) + 8ull * rcap + doctree_gl_bytes(rcap, scap);
 }
 
-// Sort key: (lamport, agent) of the run's head (48 bits) and the local run index (15 bits), so
-// that equal timestamps still order deterministically (greater run first, as the oracle does).
-__device__ __forceinline__ uint64_t doc_key(const DocArgs& a, uint32_t base, uint32_t v) {
-    return (a.r_key[base + v] << 15) | v;
+// Sort key: (lamport, agent) of the run's head (48 bits; Fugue: 49, with the left-child bit) and
+// the local run index (15 bits), so that equal timestamps still order deterministically (greater
+// run first, as the oracle does).  The keys were staged in LDS by the load phase.
+__device__ __forceinline__ uint64_t doc_key(const uint64_t* keys, uint32_t v) {
+    return (keys[v] << 15) | v;
 }
 
 // Phase C of k_doctree: expansion fused, when the document's text and its run-start index fit
@@ -1334,11 +1359,10 @@ __device__ __forceinline__ uint64_t doc_key(const DocArgs& a, uint32_t base, uin
 // per lane (256-byte coalesced stores per wave): byte y belongs to the run of the last set bit
 // at or before y.  Returns false (nothing written) when the document does not fit.
 constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
-__device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t base, uint32_t R,
+__device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t p0, uint64_t toff,
                                          const uint32_t (&ro)[kDocJ], const uint32_t (&ps)[kDocJ],
                                          uint8_t* st, uint32_t* scan_lds, uint64_t* tprobe) {
     const uint32_t t = threadIdx.x;
-    const uint32_t tl = a.tlen[d], p0 = a.doc_p0[d];
     const uint32_t sh = p0 & 15u;
     const uint32_t nq = (sh + tl + 15u) >> 4;  // staged 16-byte pieces
     const uint32_t nw = (tl + 31u) >> 5;       // bitvector words
@@ -1399,18 +1423,22 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
     __syncthreads();
     if (tprobe) *tprobe = wall_clock64();
     // 3) the document in order, 16 bytes per lane per step (one bitvector word covers them)
-    uint4* out = reinterpret_cast<uint4*>(a.text + a.toff[d]);  // 16-aligned
+    uint4* out = reinterpret_cast<uint4*>(a.text + toff);  // 16-aligned
+    // The run of the piece's first byte (the last start at or before it) comes from the bitvector
+    // and its prefix count; every later start inside the piece (bit b of m) moves to the next run
+    // in document order, whose delta is read then (an LDS read only in the lanes that have a
+    // start at b: ~1 in 11 bytes on the traces, instead of one read per byte).
     for (uint32_t i = t; i < (tl + 15u) >> 4; i += kDocThreads) {
         const uint32_t y0 = 16u * i, wd = y0 >> 5, b0 = y0 & 31u;
         const uint32_t bw = bits[wd], pr = pref[wd];
+        const uint32_t m = bw >> b0;  // bit b: a run starts at y0 + b
+        uint32_t r = pr + (uint32_t)__popc(bw & ((2u << b0) - 1u)) - 1u;
+        uint32_t dl = delta[r];
         uint32_t q[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (uint32_t b = 0; b < 16; ++b) {
-            if (y0 + b < tl) {
-                // the run of the last start at or before y (b0 + b = 31: the whole word)
-                const uint32_t r = pr + (uint32_t)__popc(bw & ((2u << (b0 + b)) - 1u)) - 1u;
-                q[b >> 2] |= (uint32_t)st[y0 + b + delta[r]] << (8u * (b & 3u));
-            }
+            if (b && ((m >> b) & 1u)) dl = delta[++r];
+            if (y0 + b < tl) q[b >> 2] |= (uint32_t)st[y0 + b + dl] << (8u * (b & 3u));
         }
         out[i] = make_uint4(q[0], q[1], q[2], q[3]);
     }
@@ -1420,28 +1448,26 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t d, uint32_t 
 __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
-    __shared__ uint32_t npair, nwide, flags, visited_lds, pruned_any, nbig;
+    __shared__ uint32_t nwide, flags, visited_lds;
 #ifdef CRDT_HIP_PROBE
-    __shared__ uint32_t probe_max, probe_sum;
+    __shared__ uint32_t probe_max, probe_sum, probe_wave[48];
 #endif
-    __shared__ uint32_t bigv[kDocBig], bigw[kDocBig];
-    const uint32_t d = a.order[blockIdx.x];
     const uint32_t t = threadIdx.x;
-    // the plan check and the document's run range in one round of loads (not one after the other)
-    const uint32_t base = a.doc_root[d];
-    const uint32_t end = d + 1 < a.ndocs ? a.doc_root[d + 1] : a.ctl[C_RTOTAL];
+    // the plan check and the workgroup's document (written by k_doctotals in LPT order: document,
+    // first run, runs, text offset / length) in one round of loads
+    const uint4 wg = a.wg[2u * blockIdx.x], wg1 = a.wg[2u * blockIdx.x + 1u];
     if (replan(a.ctl)) return;
-    const uint32_t R = end - base;
+    const uint32_t d = wg.x, base = wg.y, R = wg.z;
+    (void)d;
     const uint32_t S = (R + (1u << kDocLog2S) - 1u) >> kDocLog2S;
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
     uint16_t* ch = nx + a.rcap;
-    uint16_t* w = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(ch) + a.chbytes);
-    uint16_t* glist = w + a.rcap;  // sibling-group work list (pairs front, 3..64 back)
+    uint64_t* keys = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(dyn) + a.keyoff);
+    uint16_t* glist = reinterpret_cast<uint16_t*>(keys + a.rcap);  // groups of 3..64
     uint32_t* srec = reinterpret_cast<uint32_t*>(glist);  // splitter records, once gl is dead
-    uint2* rec = reinterpret_cast<uint2*>(dyn);           // run records, once D..w are dead
+    uint2* rec = reinterpret_cast<uint2*>(dyn);           // run records, once D..keys are dead
     uint32_t* rec32 = dyn;
-    const uint32_t gcap = doctree_defer_cap(a.rcap);
     uint32_t* D32 = dyn;
 #ifdef CRDT_HIP_PROBE
     // phase timestamps of one document (probe build, CRDT_HIP_PROBE=<doc>)
@@ -1453,41 +1479,44 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #define PROBE(i) (void)0
 #endif
     if (t == 0) {
-        npair = nwide = 0;
+        nwide = 0;
         flags = 0;
         visited_lds = 0;
-        pruned_any = 0;
 #ifdef CRDT_HIP_PROBE
         probe_max = probe_sum = 0;
 #endif
-        nbig = 0;
     }
     if (R + 2u > a.rcap || S > a.scap || R > (uint32_t)(kDocJ * kDocThreads)) {
         if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);  // host sized rcap/scap from the largest document
         return;
     }
-    // ---- parents and weightless flags (all loads first), cleared counts --------------------
-    uint32_t zw = 0, pruned = 0;  // bit j: run t + 1024 j has no visible bytes / was pruned
+    // ---- parents, weights and sibling keys (all loads first), cleared counts ----------------
+    // (weightless leaves are not pruned here: level 0 dropped 99 % of them, and walking the rest
+    // costs less than a pass that finds them).  The weights stay in registers (wr) until the run
+    // records are built; the keys go to LDS, so that no sibling sort waits for a global gather.
+    uint32_t wr[kDocJ];
     {
         // weights are differences of consecutive weight prefixes: the next run's prefix is the
         // next lane's (lane 63 loads it; v = R - 1 reads the next document's first run or the
         // sentinel)
-        uint32_t gp[kDocJ], gw[kDocJ], gn[kDocJ];
+        uint32_t gp[kDocJ], gn[kDocJ];
+        uint64_t gk[kDocJ];
         const bool l63 = (t & 63u) == 63u;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             gp[j] = v < R ? a.r_parent[base + v] : 0u;
-            gw[j] = v <= R ? a.r_pstart[base + v] : 0u;  // (v = R: the next lane's successor)
+            wr[j] = v <= R ? a.r_pstart[base + v] : 0u;  // (v = R: the next lane's successor)
             gn[j] = (l63 && v < R) ? a.r_pstart[base + v + 1] : 0u;
+            gk[j] = v < R ? a.r_key[base + v] : 0ull;
         }
+        for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            const uint32_t nxt = (uint32_t)__shfl_down((int)gw[j], 1);
-            gw[j] = v < R ? (l63 ? gn[j] : nxt) - gw[j] : 1u;
+            const uint32_t nxt = (uint32_t)__shfl_down((int)wr[j], 1);
+            wr[j] = v < R ? (l63 ? gn[j] : nxt) - wr[j] : 0u;
         }
-        for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
         uint32_t bad = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
@@ -1500,18 +1529,8 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
                     else p = (uint16_t)lp;
                 }
                 nx[v] = p;
-                w[v] = (uint16_t)min(gw[j], 0xFFFFu);
-                if (gw[j] >= 0xFFFFu) {  // a run of 64 KiB or more: the LDS side table
-                    const uint32_t i = atomicAdd(&nbig, 1u);
-                    if (i < kDocBig) {
-                        bigv[i] = v;
-                        bigw[i] = gw[j];
-                    } else {
-                        atomicOr(&flags, 2u);  // that much text: the global path
-                    }
-                }
+                keys[v] = gk[j];
             }
-            zw |= (gw[j] == 0u && v != 0u ? 1u : 0u) << j;
         }
         if (bad) atomicOr(&flags, 1u);
     }
@@ -1527,29 +1546,6 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         }
     }
     __syncthreads();
-    // ---- pruning: a weightless leaf adds nothing to the document and is dropped from its
-    // parent's children; a parent that loses its last child may go in the same pass (the
-    // outcome depends on timing, never the text).  Repeated while it finds anything.
-#ifndef CRDT_DOC_PRUNE_ROUNDS
-#define CRDT_DOC_PRUNE_ROUNDS 1  // (a second round: no measurable change)
-#endif
-    for (int round = 0; round < CRDT_DOC_PRUNE_ROUNDS; ++round) {
-        uint32_t found = 0;
-#pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t v = t + (uint32_t)j * kDocThreads;
-            const uint32_t bit = 1u << j;
-            if ((zw & ~pruned & bit) && D[v] == 0) {
-                const uint16_t p = nx[v];
-                pruned |= bit;
-                found = 1;
-                if (p != kNil16) atomicSub(&D32[p >> 1], 1u << (16u * (p & 1u)));
-            }
-        }
-        if (found) atomicOr(&pruned_any, 1u << round);
-        __syncthreads();
-        if (!((pruned_any >> round) & 1u)) break;
-    }
     PROBE(2);
     // ---- exclusive scan of the counts -> segment starts ------------------------------------
     {
@@ -1573,9 +1569,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         const uint32_t v = t + (uint32_t)j * kDocThreads;
         if (v < R) {
             const uint16_t p = nx[v];
-            if (pruned & (1u << j)) {
-                nx[v] = kDead16;  // never reached by the tour; its splitters are empty
-            } else if (p != kNil16) {
+            if (p != kNil16) {
                 const uint32_t sh = 16u * (p & 1u);
                 const uint32_t old = atomicAdd(&D32[p >> 1], 1u << sh);
                 ch[(old >> sh) & 0xFFFFu] = (uint16_t)v;
@@ -1586,10 +1580,10 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     PROBE(4);
     // ---- sibling order + up-arc successors -------------------------------------------------
     // nx[] is rewritten here: a child's entry is written only by whoever sorts its group.
-    // Single children are linked by their parent's owner; groups of 2 go to the front of an LDS
-    // work list and groups of 3..64 to its back, and the list is sorted in passes whose key
-    // loads are issued together: pairs (kPairs per thread at once), 3..8 (one register network
-    // per thread), 9..64 (one wave per group).  Wider groups hand the wave to the global path.
+    // Single children and pairs (nearly every group on the traces) are linked by their parent's
+    // owner right here, the pair's keys read from LDS; groups of 3..64 go to an LDS work list
+    // and are sorted next: 3..8 by one register network per thread, 9..64 by one wave per group.
+    // Wider groups hand the wave to the global path.
     // fcs[j]: the first child of run t + 1024 j (kNil16: a leaf), or 0x10000 | its segment start
     // while its group is still to be sorted
     uint32_t fcs[kDocJ];
@@ -1603,60 +1597,33 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             if (cnt == 1u) {
                 f = ch[s0];
                 nx[f] = (uint16_t)(p | kUp16);
-            } else if (cnt >= 2u) {
+            } else if (cnt == 2u) {
+                const uint32_t c0 = ch[s0], c1 = ch[s0 + 1u];
+                const bool sw = doc_key(keys, c0) < doc_key(keys, c1);
+                const uint32_t a0 = sw ? c1 : c0, a1 = sw ? c0 : c1;
+                ch[s0] = (uint16_t)a0;
+                ch[s0 + 1u] = (uint16_t)a1;
+                nx[a0] = (uint16_t)a1;
+                nx[a1] = (uint16_t)(p | kUp16);
+                f = a0;
+            } else if (cnt > 2u) {
                 f = 0x10000u | s0;
-                if (cnt == 2u) glist[atomicAdd(&npair, 1u)] = (uint16_t)p;
-                else if (cnt > 64u) atomicOr(&flags, 2u);
-                else glist[gcap - 1u - atomicAdd(&nwide, 1u)] = (uint16_t)p;
+                if (cnt > 64u) atomicOr(&flags, 2u);
+                else glist[atomicAdd(&nwide, 1u)] = (uint16_t)p;
             }
         }
         fcs[j] = f;
     }
     __syncthreads();
     PROBE(12);
-    {
-        constexpr int kPairs = 8;
-        const uint32_t np = npair;
-        for (uint32_t i0 = 0; i0 < np; i0 += kPairs * kDocThreads) {
-            uint32_t s0[kPairs], cc[kPairs], pp[kPairs];
-            uint64_t k0[kPairs], k1[kPairs];
-#pragma unroll
-            for (int e = 0; e < kPairs; ++e) {
-                const uint32_t i = i0 + t + (uint32_t)e * kDocThreads;
-                const uint32_t p = i < np ? glist[i] : 0u;
-                pp[e] = i < np ? p : kNil;
-                s0[e] = p ? D[p - 1] : 0u;
-            }
-#pragma unroll
-            for (int e = 0; e < kPairs; ++e)
-                cc[e] = pp[e] != kNil ? ((uint32_t)ch[s0[e]] | ((uint32_t)ch[s0[e] + 1u] << 16)) : 0u;
-#pragma unroll
-            for (int e = 0; e < kPairs; ++e) {
-                k0[e] = a.r_key[base + (cc[e] & 0xFFFFu)];
-                k1[e] = a.r_key[base + (cc[e] >> 16)];
-            }
-#pragma unroll
-            for (int e = 0; e < kPairs; ++e) {
-                if (pp[e] == kNil) continue;
-                const uint32_t c0 = cc[e] & 0xFFFFu, c1 = cc[e] >> 16;
-                const bool sw = ((k0[e] << 15) | c0) < ((k1[e] << 15) | c1);
-                const uint32_t a0 = sw ? c1 : c0, a1 = sw ? c0 : c1;
-                ch[s0[e]] = (uint16_t)a0;
-                ch[s0[e] + 1u] = (uint16_t)a1;
-                nx[a0] = (uint16_t)a1;
-                nx[a1] = (uint16_t)(pp[e] | kUp16);
-            }
-        }
-    }
 #ifdef CRDT_HIP_PROBE
-    __syncthreads();
     PROBE(11);
 #endif
     // 3..8 children: Batcher's 19-comparator network (padding key 0 sorts last)
     const uint32_t nw = nwide;
     for (uint32_t i0 = 0; i0 < nw; i0 += kDocThreads) {
         const uint32_t i = i0 + t;
-        const uint32_t p = i < nw ? glist[gcap - 1u - i] : 0u;
+        const uint32_t p = i < nw ? glist[i] : 0u;
         const uint32_t b = p ? D[p - 1] : 0u, cnt = i < nw ? D[p] - b : 0u;
         if (cnt < 3u || cnt > 8u) continue;
         uint64_t k[8];
@@ -1664,7 +1631,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) c[q] = (uint32_t)q < cnt ? ch[b + q] : 0u;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) k[q] = (uint32_t)q < cnt ? doc_key(a, base, c[q]) : 0ull;
+        for (int q = 0; q < 8; ++q) k[q] = (uint32_t)q < cnt ? doc_key(keys, c[q]) : 0ull;
         cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
         cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
         cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
@@ -1688,12 +1655,12 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     {
         const uint32_t lane = t & 63u, wv = t >> 6;
         for (uint32_t i = wv; i < nw; i += kDocThreads / 64) {
-            const uint32_t p = glist[gcap - 1u - i];
+            const uint32_t p = glist[i];
             const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
             if (cnt <= 8u) continue;  // wave-uniform
             const bool on = lane < cnt;
             const uint32_t c = on ? ch[s0 + lane] : 0u;
-            const uint64_t k = on ? doc_key(a, base, c) : 0ull;
+            const uint64_t k = on ? doc_key(keys, c) : 0ull;
             uint32_t rank = 0;
             for (uint32_t j = 0; j < cnt; ++j) {
                 const uint64_t kj = ((uint64_t)(uint32_t)__shfl((int)(k >> 32), (int)j) << 32) |
@@ -1722,15 +1689,16 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            uint32_t f = fcs[j], n = 0, ww = 0;
+            uint32_t f = fcs[j], n = 0;
             if (v < R) {
                 if (f & 0x10000u) f = ch[f & 0xFFFFu];
                 n = nx[v];
-                ww = w[v];
-                if ((n & kUp16) && n < kDead16) act |= 1u << j;
+                if ((n & kUp16) && n != kNil16) act |= 1u << j;
             }
             fx[j] = (f & 0xFFFFu) | (n << 16);
-            wx[j] = ww | 0xFFFF0000u;  // spare: "not reached" until walk 1 passes v
+            // the whole weight (below 2^18 on this path); bit 31: "not reached" until walk 1
+            // passes v (then the word is v's sublist and offset, or ~0 for no weight)
+            wx[j] = wr[j] | 0x80000000u;
         }
         __syncthreads();
 #pragma unroll
@@ -1738,6 +1706,9 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             if (v < R) rec[v] = make_uint2(fx[j], wx[j]);
         }
+        // record R: a leaf without weight at the tour's end, where walkers without a sublist
+        // (and the splitter run of a last block beyond R) read and write harmlessly
+        if (t == 0) rec[R] = make_uint2(0xFFFFFFFFu, 0x80000000u);
     }
     __syncthreads();
     PROBE(14);
@@ -1760,7 +1731,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
                 // (the parent is an internal run: never dead)
                 const uint32_t y = lds_ld16(vnx + 4u * (lds_ld16(vnx + 4u * v) & 0x7FFFu));
                 lds_st16(vnx + 4u * v, y);
-                if (!((y & kUp16) && y < kDead16)) act &= ~(1u << j);
+                if (!((y & kUp16) && y != kNil16)) act &= ~(1u << j);
             }
         }
     }
@@ -1770,10 +1741,10 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // A step at v's down arc reads v's record (first child, nx, weight: one 8-byte LDS read):
     // v's weight is added, v's offset inside the sublist and the sublist go to the record's
     // second word, and the walk goes to the first child, or for a leaf to nx (a down arc, or the
-    // end of the tour).  A lane whose sublist ends takes the next splitter of its wave's range
-    // (a wave-uniform cursor advanced by ballot: no LDS atomic in the loop), so the lanes stay
-    // busy until the range runs dry.  The sublist results (sum, next splitter) go to the gl
-    // region, which no walker reads.
+    // end of the tour).  The sublist ends at the next splitter (a node at its block's hashed
+    // offset) or at the tour's end, and the lane takes the next splitter of its wave's range (a
+    // wave-uniform cursor advanced by ballot).  The step is a short VALU chain with selects; a
+    // lane without a splitter walks record R (a weightless leaf) with its stores masked off.
     uint32_t runs = 0;
     uint32_t lane_steps = 0;
     {
@@ -1782,62 +1753,58 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         const uint32_t lo = wv < NWV ? (S * wv) / NWV : S, hi = wv < NWV ? (S * (wv + 1u)) / NWV : S;
         uint32_t cur = lo + 64u;  // the wave's next unassigned splitter (uniform over its lanes)
         uint32_t s = lo + lane < hi ? lo + lane : S;
-        uint32_t V = splitter_run(s), SUM = 0, steps = 0;
+        // (4 S >= R: the splitter run of splitter S, and of a last block beyond R, clamps to R)
+        uint32_t V = min(splitter_run(s), R), SUM = 0, steps = 0;
         const uint32_t step_limit = R + S + 4u;
-        while (s < S) {
-            const uint2 r = rec[V < R ? V : 0u];
-            const uint32_t f = r.x & 0xFFFFu, n = r.x >> 16, ww = r.y & 0xFFFFu;
-            // a pruned run (only ever a splitter's own) ends it, and so does the splitter run of
-            // the last block when it falls beyond the document
-            const bool dn = V < R && n != kDead16;
-            uint32_t wt = ww;
-            if (dn && ww == 0xFFFFu)  // a run of 64 KiB or more: the LDS side table
-                for (uint32_t i = 0; i < nbig; ++i)
-                    if (bigv[i] == V) wt = bigw[i];
-            wt = dn ? wt : 0u;
-            if (dn) {
-                // v's down arc is the last use of its record: the second word now holds v's
-                // offset inside this sublist (18 bits) and the sublist (14 bits)
-                rec32[2u * V + 1u] = wt ? (SUM | (s << 18)) : 0xFFFFFFFFu;
-            }
-            SUM += wt;
-            runs += dn ? 1u : 0u;
-            // the next down arc: the first child, or for a leaf nx (kNil16 at the tour's end)
-            const uint32_t go = !dn ? kNil16 : (f != kNil16 ? f : n);
-            constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
-            // (kNil16 is the tour's end; any other value >= R is an up link a parent cycle left
-            // unresolved: the walk ends there and the runs it misses are reported)
-            const bool end = go >= R;
-            const bool split = !end && (go & mm) == splitter_off(go >> kDocLog2S);  // a splitter's
-            const bool need = end || split;
-            if (need) {
-                srec[s] = (SUM << 14) | (split ? go >> kDocLog2S : kNil14);
-                SUM = 0;
-            } else {
-                V = go;
-            }
-            const uint64_t m = __ballot(need);
-            if (need) {
-                const uint32_t ns = cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                s = ns < hi ? ns : S;
-                V = splitter_run(s);
-            }
-            cur += (uint32_t)__popcll(m);
+        constexpr uint32_t mm = (1u << kDocLog2S) - 1u;
+#ifdef CRDT_HIP_PROBE
+        const uint64_t wc0 = clock64(), ww0 = wall_clock64();
+#endif
+        while (__ballot(s < S)) {  // (steps: wave-uniform, the loop's trip count so far)
             if (++steps > step_limit) {
-                atomicOr(&flags, 4u);
+                if (lane == 0) atomicOr(&flags, 4u);
                 break;
             }
+            const uint2 r = rec[V];
+            const uint32_t f = r.x & 0xFFFFu, n = r.x >> 16, wt = r.y & 0x3FFFFu;
+            const bool act = s < S;
+            // v's down arc is the last use of its record: the second word now holds v's offset
+            // inside this sublist (18 bits) and the sublist (14 bits).  (The stores are exec-
+            // masked, not sent to a dummy address: a wave's idle lanes all storing to one
+            // address serialise on its bank.)
+            const bool own = act & (V < R);
+            if (own) rec32[2u * V + 1u] = wt ? (SUM | (s << 18)) : 0xFFFFFFFFu;
+            SUM += wt;
+            runs += own ? 1u : 0u;
+            // the next down arc: the first child, or for a leaf nx (kNil16 at the tour's end; any
+            // other value >= R is an up link a parent cycle left unresolved: the walk ends there
+            // and the runs it misses are reported)
+            const uint32_t go = f != kNil16 ? f : n;
+            const uint32_t blk = go >> kDocLog2S;
+            const bool end = go >= R;
+            const bool split = ((go & mm) == splitter_off(blk)) & !end;
+            const bool need = act & (end | split);
+            if (need) srec[s] = (SUM << 14) | (split ? blk : kNil14);
+            SUM = need ? 0u : SUM;
+            const uint64_t m = __ballot(need);
+            const uint32_t ns = cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            cur += (uint32_t)__popcll(m);
+            const uint32_t s2 = ns < hi ? ns : S;
+            const uint32_t v2 = min(splitter_run(s2), R);
+            s = need ? s2 : s;
+            V = need ? v2 : min(go, R);
         }
         lane_steps = steps;
+#ifdef CRDT_HIP_PROBE
+        if (lane == 0) {  // per wave: loop cycles, loop wall time (10 ns), iterations
+            probe_wave[3 * (t >> 6)] = (uint32_t)(clock64() - wc0);
+            probe_wave[3 * (t >> 6) + 1] = (uint32_t)(wall_clock64() - ww0);
+            probe_wave[3 * (t >> 6) + 2] = steps;
+        }
+#endif
     }
     (void)lane_steps;
-#ifdef CRDT_HIP_PROBE
-    if (a.probe && d == a.probe - 1u) {
-        atomicMax(&probe_max, lane_steps);
-        atomicAdd(&probe_sum, lane_steps);
-    }
-#endif
     __syncthreads();
     PROBE(7);
     // the slot-order text prefixes of the owned runs, for phase C: loaded now, so that the
@@ -1892,9 +1859,9 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t pk = 0xFFFFFFFFu;
-            if (v < R && !(pruned & (1u << j))) pk = rec32[2u * v + 1u];
+            if (v < R) pk = rec32[2u * v + 1u];
             const uint32_t sid = pk >> 18;
-            // weightless, pruned (or never reached: flagged below)
+            // weightless (or never reached: flagged below)
             ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (srec[sid] >> 14) : kNil;
         }
         if (!a.text) {  // offsets for k_expand
@@ -1903,8 +1870,8 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
                 if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ro[j];
         }
     }
-    const uint32_t wr = wave_sum(runs + (uint32_t)__popc(pruned));  // pruned runs count as reached
-    if ((t & 63u) == 0 && wr) atomicAdd(&visited_lds, wr);
+    const uint32_t wsum = wave_sum(runs);
+    if ((t & 63u) == 0 && wsum) atomicAdd(&visited_lds, wsum);
     __syncthreads();
     PROBE(9);
     if (a.text) {
@@ -1913,13 +1880,14 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 #else
         uint64_t* tprobe = nullptr;
 #endif
-        const bool fused = doc_text(a, d, base, R, ro, ps, reinterpret_cast<uint8_t*>(dyn),
+        const uint64_t toff = ((uint64_t)wg1.z << 32) | wg1.y;
+        const bool fused = doc_text(a, wg1.x, wg.w, toff, ro, ps, reinterpret_cast<uint8_t*>(dyn),
                                     scan_lds, tprobe);
         if (!fused) {
             // the text did not fit LDS: every run copies its bytes from the slot-order text to
             // its document offset (byte stores; only documents above the LDS stage take this)
-            uint8_t* out = a.text + a.toff[d];
-            const uint32_t tl = a.tlen[d];
+            uint8_t* out = a.text + toff;
+            const uint32_t tl = wg1.x;
             bool oob = false;
 #pragma unroll
             for (int j = 0; j < kDocJ; ++j) {
@@ -1949,6 +1917,21 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
                (tp[6] - tp[14]) / 100.0, (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0,
                (tp[9] - tp[8]) / 100.0, (tp[15] - tp[9]) / 100.0, (tp[10] - tp[15]) / 100.0,
                (tp[10] - tp[0]) / 100.0, visited_lds, probe_max, probe_sum);
+    }
+#endif
+#ifdef CRDT_HIP_PROBE
+    if (probe) {
+        uint32_t cmax = 0, wmax = 0, imax = 0, csum = 0, isum = 0;
+        for (int k = 0; k < 16; ++k) {
+            cmax = max(cmax, probe_wave[3 * k]);
+            wmax = max(wmax, probe_wave[3 * k + 1]);
+            imax = max(imax, probe_wave[3 * k + 2]);
+            csum += probe_wave[3 * k];
+            isum += probe_wave[3 * k + 2];
+        }
+        printf("[walk] per wave: cycles max %u mean %u, wall max %.2f us, iterations max %u mean %.1f"
+               " (%.0f cycles per iteration)\n", cmax, csum / 16, wmax / 100.0, imax, isum / 16.0,
+               (double)csum / (isum ? isum : 1));
     }
 #endif
 #undef PROBE
@@ -2274,7 +2257,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 // =============================================================================================
 void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
-    dfree(docs_rel); dfree(doc_order); dfree(chunk_doc);
+    dfree(docs_rel); dfree(doc_rank); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
 }
@@ -2283,7 +2266,7 @@ Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
     dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
-    dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_);
+    dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_); dfree(wgtab_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(out_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
@@ -2416,9 +2399,9 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     if (docs.size() > L.cap_docs) {
         L.tab_sig.clear();
         dfree(L.docs_rel);
-        dfree(L.doc_order);
+        dfree(L.doc_rank);
         HIPCHK(dalloc(&L.docs_rel, docs.size()), "hipMalloc logs.docs");
-        HIPCHK(dalloc(&L.doc_order, docs.size()), "hipMalloc logs.doc_order");
+        HIPCHK(dalloc(&L.doc_rank, docs.size()), "hipMalloc logs.doc_rank");
         gen_++;
         L.cap_docs = docs.size();
     }
@@ -2447,7 +2430,7 @@ int Engine::upload_tables(DeviceLogs& L) {
     if (sig == L.tab_sig) return CRDT_HIP_OK;
     L.tab_sig.clear();
     std::vector<uint2> rel(nd);
-    std::vector<uint32_t> local(nd), order(nd);
+    std::vector<uint32_t> local(nd), order(nd), rank(nd);
     for (const Wave& w : L.waves) {
         for (uint32_t k = 0; k < w.ndocs; ++k) {
             const uint32_t d = w.first_doc + k;
@@ -2462,13 +2445,14 @@ int Engine::upload_tables(DeviceLogs& L) {
         std::stable_sort(o, o + w.ndocs, [&](uint32_t x, uint32_t y) {
             return L.docs[w.first_doc + x].text_cap > L.docs[w.first_doc + y].text_cap;
         });
+        for (uint32_t k = 0; k < w.ndocs; ++k) rank[w.first_doc + o[k]] = k;
     }
     // (pageable sources: hipMemcpyAsync has copied them when it returns; the tables are
     // consumed in stream order, so no wait here)
     HIPCHK(hipMemcpyAsync(L.docs_rel, rel.data(), nd * sizeof(uint2), hipMemcpyHostToDevice, stream),
            "upload docs");
-    HIPCHK(hipMemcpyAsync(L.doc_order, order.data(), nd * 4ull, hipMemcpyHostToDevice, stream),
-           "upload doc order");
+    HIPCHK(hipMemcpyAsync(L.doc_rank, rank.data(), nd * 4ull, hipMemcpyHostToDevice, stream),
+           "upload doc rank");
     const uint64_t nchunks = L.total_slots >> L.log2m;
     if (nd == 1) {  // one document: every chunk is document 0
         HIPCHK(hipMemsetAsync(L.chunk_doc, 0, nchunks * 4, stream), "chunk table");
@@ -2565,7 +2549,7 @@ int Engine::ensure_scratch(const Wave& w) {
     }
     if (w.ndocs + 1 > cap_docs_) {
         dfree(tlen_); dfree(loff_); dfree(toff_); dfree(out_); dfree(doc_root_); dfree(doc_p0_);
-        dfree(doc_fused_);
+        dfree(doc_fused_); dfree(wgtab_);
         const uint64_t nd = w.ndocs + 1;
         HIPCHK(dalloc(&out_, 16 + 4 * nd), "hipMalloc results");  // ctl + one uint4 per document
         ctl_ = out_;
@@ -2576,6 +2560,7 @@ int Engine::ensure_scratch(const Wave& w) {
         HIPCHK(dalloc(&doc_root_, nd), "hipMalloc doc_root");
         HIPCHK(dalloc(&doc_p0_, nd), "hipMalloc doc_p0");
         HIPCHK(dalloc(&doc_fused_, nd), "hipMalloc doc_fused");
+        HIPCHK(dalloc(&wgtab_, 2 * nd), "hipMalloc workgroup descriptors");
         cap_docs_ = nd;
         gen_++;
     }
@@ -2752,6 +2737,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.roff = roff_;                                                                   \
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
     a.leafcp = leafcp_; a.gcp = gcp_; a.res = res_;                                   \
+    a.rank = L.doc_rank + w.first_doc; a.wg = nullptr;                                \
     a.text = text_;                                                                   \
     a.text_cap = ord ? w.order_cap : cap_text_ - 64;                                  \
     a.align = ord ? 1u : 16u
@@ -2819,7 +2805,9 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.fused = doc_fused_;
     da.lds_bytes = (uint32_t)p.dyn_bytes;
     da.probe = probe_doc_;
-    da.order = L.doc_order + w.first_doc;
+    da.wg = wgtab_;
+    da.keyoff = doctree_key_off(p.rcap, p.scap);
+    a.wg = wgtab_;  // (k_doctotals writes the k_doctree workgroup descriptors)
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
     MARK(S_DOCTREE);

@@ -94,7 +94,8 @@ struct DeviceLogs {
     bool fugue = false;            // some document has left children (Fugue logs)
     uint8_t* cp = nullptr;         // 3 bytes per slot: codepoint (bits 0-20) | tombstone (bit 23)
     uint2* docs_rel = nullptr;     // per doc {wave-relative base slot, n}
-    uint32_t* doc_order = nullptr; // per wave: its documents, costliest first (k_doctree order)
+    uint32_t* doc_rank = nullptr;  // per document: its k_doctree workgroup within its wave
+                                   //   (longest-processing-time order: costliest first)
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
     uint64_t cap_docs = 0, cap_chunks = 0;
     std::vector<uint64_t> tab_sig;  // the plan docs_rel / chunk_doc were last built for
@@ -214,6 +215,7 @@ private:
     // digest lo, digest hi}; ctl_ and res_ point into it
     uint32_t* out_ = nullptr;
     uint4* res_ = nullptr;
+    uint4* wgtab_ = nullptr;  // k_doctree workgroup descriptors (two uint4 per document)
     uint8_t* text_ = nullptr;
     uint8_t* doc_fused_ = nullptr;
     // level-1 scratch (per run / per splitter), grown on demand
