@@ -459,6 +459,8 @@ def traces_workload(args) -> int:
     if not args.fuse_text:  # (the engine's default is 1; builds before the parameter lack it)
         ctx.set_param("fuse_text", 0)
     ctx.set_param("lanes", args.lanes)
+    if args.xcd_order != 1:  # (the engine's default; builds before the parameter lack it)
+        ctx.set_param("xcd_order", args.xcd_order)
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
@@ -770,6 +772,8 @@ def parse_args(argv=None):
                          "(level 0 of the next wave is favoured for the CUs); 0: one stream")
     ap.add_argument("--fuse-text", type=int, default=1, choices=[0, 1],
                     help="0: k_doctree leaves the text to k_expand (smaller LDS footprint)")
+    ap.add_argument("--xcd-order", type=int, default=1, choices=[0, 1],
+                    help="1: level-0 tiles in XCD-aware order (each XCD one contiguous range)")
     ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
                     help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

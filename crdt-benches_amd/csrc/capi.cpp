@@ -203,6 +203,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.doctree_lds_max = value != 0;
         return 0;
     }
+    if (k == "xcd_order") {  // 1: XCD-aware tile order in level 0 (engine.hip xcd_block)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "xcd_order must be 0 or 1");
+        ctx->eng.xcd_order = value == 1;
+        return 0;
+    }
     if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)
         ctx->eng.plan_shrink = value != 0;
         return 0;

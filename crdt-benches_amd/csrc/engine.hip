@@ -83,6 +83,18 @@ __global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ ctl, uint4
     for (uint32_t k = i; k < nq; k += gridDim.x * 256) bits[k] = make_uint4(0, 0, 0, 0);
 }
 
+// XCD-aware block order: the dispatcher hands consecutive workgroups to the 8 XCDs in turn, and
+// each XCD has its own L2.  Block b of a grid of G is given item (b % 8) * ceil-share + b / 8, so
+// that every XCD walks one contiguous range of tiles: the tiles of a document then share an L2,
+// and the lookups k_runs makes into the head records of other tiles of the same document (and
+// the jump bits k_classify sets there) stay inside it.  (A bijection for any G.)
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G, uint32_t on) {
+    if (!on) return b;
+    const uint32_t q = G / kXcds, r = G % kXcds, x = b % kXcds, i = b / kXcds;
+    return x < r ? x * (q + 1u) + i : r * (q + 1u) + (x - r) * q + i;
+}
+
 // Every kernel after level 0 starts with this: a wave whose plan was too small does nothing.
 __device__ __forceinline__ bool replan(const uint32_t* ctl) { return ctl[C_REPLAN] != 0u; }
 
@@ -135,6 +147,7 @@ struct L0Args {
     uint32_t* ctl;
     uint32_t cap_runs, cap_rmax;  // capacity of the launch plan (k_docmax flags C_REPLAN above)
     uint32_t cap_rows;            // rows allocated in r_parent / r_key (more runs: not written)
+    uint32_t xcd;                 // 1: XCD-aware tile order in k_classify / k_runs (xcd_block)
 };
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
@@ -175,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint2 ldoc[kBlock];  // per thread: its document {base slot, items}
     // (+64: one sink byte per lane for the branch-free ASCII stores below)
     __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes + 64];
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
     const bool live = gs < a.nslots;
     if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
@@ -472,7 +485,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     __shared__ uint16_t lnpf[kBlock];  // non-seq items of the tile before every thread
     __shared__ uint16_t ldp[FUGUE ? kBlock : 1];  // Fugue: two-row heads before every thread
     __shared__ uint16_t ldm[FUGUE ? kBlock : 1];  //   and every thread's two-row head bits
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
     uint32_t hm = 0, nsq = 0, dm = 0;
@@ -1490,59 +1503,50 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);  // host sized rcap/scap from the largest document
         return;
     }
-    // ---- parents, weights and sibling keys (all loads first), cleared counts ----------------
+    // ---- parents and sibling keys (all loads first), cleared counts --------------------------
     // (weightless leaves are not pruned here: level 0 dropped 99 % of them, and walking the rest
-    // costs less than a pass that finds them).  The weights stay in registers (wr) until the run
-    // records are built; the keys go to LDS, so that no sibling sort waits for a global gather.
-    uint32_t wr[kDocJ];
+    // costs less than a pass that finds them).  The keys go to LDS, so that no sibling sort waits
+    // for a global gather; the weights are loaded later (doc_weights), beside the sorts.
+    // pk[j]: the parent of run t + 1024 j (kNil16: none), then | its place among the parent's
+    // children << 16 (from the count's atomic): the placement needs no second atomic
+    uint32_t pk[kDocJ];
     {
-        // weights are differences of consecutive weight prefixes: the next run's prefix is the
-        // next lane's (lane 63 loads it; v = R - 1 reads the next document's first run or the
-        // sentinel)
-        uint32_t gp[kDocJ], gn[kDocJ];
+        uint32_t gp[kDocJ];
         uint64_t gk[kDocJ];
-        const bool l63 = (t & 63u) == 63u;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             gp[j] = v < R ? a.r_parent[base + v] : 0u;
-            wr[j] = v <= R ? a.r_pstart[base + v] : 0u;  // (v = R: the next lane's successor)
-            gn[j] = (l63 && v < R) ? a.r_pstart[base + v + 1] : 0u;
             gk[j] = v < R ? a.r_key[base + v] : 0ull;
         }
         for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
-#pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
-            const uint32_t v = t + (uint32_t)j * kDocThreads;
-            const uint32_t nxt = (uint32_t)__shfl_down((int)wr[j], 1);
-            wr[j] = v < R ? (l63 ? gn[j] : nxt) - wr[j] : 0u;
-        }
         uint32_t bad = 0;
 #pragma unroll
         for (int j = 0; j < kDocJ; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
+            uint32_t p = kNil16;
             if (v < R) {
-                uint16_t p = kNil16;
                 if (v) {
                     const uint32_t lp = gp[j] - base;
                     if (lp >= R || lp == v) bad = 1;
-                    else p = (uint16_t)lp;
+                    else p = lp;
                 }
-                nx[v] = p;
                 keys[v] = gk[j];
             }
+            pk[j] = p;
         }
         if (bad) atomicOr(&flags, 1u);
     }
     __syncthreads();
     PROBE(1);
-    // ---- child counts (u16 counters, two per LDS dword) ------------------------------------
+    // ---- child counts (u16 counters, two per LDS dword); each child keeps its place ----------
 #pragma unroll
     for (int j = 0; j < kDocJ; ++j) {
-        const uint32_t v = t + (uint32_t)j * kDocThreads;
-        if (v < R) {
-            const uint16_t p = nx[v];
-            if (p != kNil16) atomicAdd(&D32[p >> 1], 1u << (16u * (p & 1u)));
+        const uint32_t p = pk[j];
+        if (p != kNil16) {
+            const uint32_t sh = 16u * (p & 1u);
+            const uint32_t old = atomicAdd(&D32[p >> 1], 1u << sh);
+            pk[j] = p | (((old >> sh) & 0xFFFFu) << 16);
         }
     }
     __syncthreads();
@@ -1560,71 +1564,104 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
             D[v] = (uint16_t)ex;
             ex += c;
         }
+        if (t == 0) D[R] = (uint16_t)total;  // (run p's children: [D[p], D[p + 1]))
     }
     __syncthreads();
     PROBE(3);
-    // ---- placement: D[p] walks from the segment start to the segment end -------------------
+    // ---- placement: segment start + the place the count handed out ---------------------------
 #pragma unroll
     for (int j = 0; j < kDocJ; ++j) {
-        const uint32_t v = t + (uint32_t)j * kDocThreads;
-        if (v < R) {
-            const uint16_t p = nx[v];
-            if (p != kNil16) {
-                const uint32_t sh = 16u * (p & 1u);
-                const uint32_t old = atomicAdd(&D32[p >> 1], 1u << sh);
-                ch[(old >> sh) & 0xFFFFu] = (uint16_t)v;
-            }
-        }
+        const uint32_t p = pk[j] & 0xFFFFu;
+        if (p != kNil16) ch[D[p] + (pk[j] >> 16)] = (uint16_t)(t + (uint32_t)j * kDocThreads);
     }
     __syncthreads();
     PROBE(4);
     // ---- sibling order + up-arc successors -------------------------------------------------
-    // nx[] is rewritten here: a child's entry is written only by whoever sorts its group.
-    // Single children and pairs (nearly every group on the traces) are linked by their parent's
-    // owner right here, the pair's keys read from LDS; groups of 3..64 go to an LDS work list
-    // and are sorted next: 3..8 by one register network per thread, 9..64 by one wave per group.
-    // Wider groups hand the wave to the global path.
-    // fcs[j]: the first child of run t + 1024 j (kNil16: a leaf), or 0x10000 | its segment start
-    // while its group is still to be sorted
+    // nx[] is written here: a child's entry by whoever orders its group.  Single children and
+    // pairs (nearly every group on the traces) order themselves: every child reads its group's
+    // bounds, an only child links up to its parent, a pair member reads its sibling and the
+    // sibling's key and takes its rank (greater key first).  Every owned run is handled at once
+    // (no branch per run), so the LDS round trips of all twelve overlap.  Groups of 3..64 go to
+    // an LDS work list (by their parent's owner) and are sorted next: 3..8 by one register
+    // network per thread, 9..64 by one wave per group; wider groups hand the wave to the global
+    // path.  fcs[j]: 0x10000 | the segment start of run t + 1024 j's children (its first child
+    // once they are ordered), or kNil16 for a leaf.
     uint32_t fcs[kDocJ];
     if (t == 0) nx[0] = kNil16;
+    {
+        // cw[j]: as a child, its group's start | (1 << 14: an only child) | (1 << 15: a pair) |
+        // (the pair's other member << 16)
+        uint32_t cw[kDocJ], pw[kDocJ];
 #pragma unroll
-    for (int j = 0; j < kDocJ; ++j) {
-        const uint32_t p = t + (uint32_t)j * kDocThreads;
-        uint32_t f = kNil16;
-        if (p < R) {
-            const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
-            if (cnt == 1u) {
-                f = ch[s0];
-                nx[f] = (uint16_t)(p | kUp16);
-            } else if (cnt == 2u) {
-                const uint32_t c0 = ch[s0], c1 = ch[s0 + 1u];
-                const bool sw = doc_key(keys, c0) < doc_key(keys, c1);
-                const uint32_t a0 = sw ? c1 : c0, a1 = sw ? c0 : c1;
-                ch[s0] = (uint16_t)a0;
-                ch[s0 + 1u] = (uint16_t)a1;
-                nx[a0] = (uint16_t)a1;
-                nx[a1] = (uint16_t)(p | kUp16);
-                f = a0;
-            } else if (cnt > 2u) {
-                f = 0x10000u | s0;
-                if (cnt > 64u) atomicOr(&flags, 2u);
-                else glist[atomicAdd(&nwide, 1u)] = (uint16_t)p;
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t p = pk[j] & 0xFFFFu, v = t + (uint32_t)j * kDocThreads;
+            const uint32_t q = p != kNil16 ? p : R, u = v < R ? v : R;  // (D[R] .. D[R + 1]: none)
+            cw[j] = (uint32_t)D[q] | ((uint32_t)D[q + 1u] << 16);
+            pw[j] = (uint32_t)D[u] | ((uint32_t)D[u + 1u] << 16);
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            // as a parent
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            const uint32_t b = pw[j] & 0xFFFFu, pc = (pw[j] >> 16) - b;
+            fcs[j] = (v < R && pc) ? (0x10000u | b) : kNil16;
+            if (v < R && pc > 2u) {
+                if (pc > 64u) atomicOr(&flags, 2u);
+                else glist[atomicAdd(&nwide, 1u)] = (uint16_t)v;
+            }
+            // as a child
+            const uint32_t s0 = cw[j] & 0xFFFFu, cnt = (cw[j] >> 16) - s0;
+            const bool child = (pk[j] & 0xFFFFu) != kNil16;
+            const uint32_t o = (child && cnt == 2u) ? ch[s0 + ((pk[j] >> 16) ^ 1u)] : 0u;
+            cw[j] = s0 | (child && cnt == 1u ? 1u << 14 : 0u) | (child && cnt == 2u ? 1u << 15 : 0u) |
+                    (o << 16);
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            const uint32_t up = (pk[j] & 0xFFFFu) | kUp16, s0 = cw[j] & 0x3FFFu;
+            if (cw[j] & (1u << 14)) {
+                nx[v] = (uint16_t)up;
+            } else if (cw[j] & (1u << 15)) {
+                const uint32_t o = cw[j] >> 16;
+                const bool first = doc_key(keys, v) > doc_key(keys, o);
+                ch[s0 + (first ? 0u : 1u)] = (uint16_t)v;
+                nx[v] = (uint16_t)(first ? o : up);
             }
         }
-        fcs[j] = f;
     }
     __syncthreads();
     PROBE(12);
 #ifdef CRDT_HIP_PROBE
     PROBE(11);
 #endif
+    // the weights of the owned runs (for the run records), loaded now so that the sorts of the
+    // wider groups cover their latency: differences of consecutive weight prefixes, the next
+    // run's prefix from the next lane (lane 63 loads it; v = R - 1 reads the next document's
+    // first run or the sentinel)
+    uint32_t wr[kDocJ];
+    {
+        uint32_t gn[kDocJ];
+        const bool l63 = (t & 63u) == 63u;
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            wr[j] = v <= R ? a.r_pstart[base + v] : 0u;  // (v = R: the next lane's successor)
+            gn[j] = (l63 && v < R) ? a.r_pstart[base + v + 1] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kDocJ; ++j) {
+            const uint32_t v = t + (uint32_t)j * kDocThreads;
+            const uint32_t nxt = (uint32_t)__shfl_down((int)wr[j], 1);
+            wr[j] = v < R ? (l63 ? gn[j] : nxt) - wr[j] : 0u;
+        }
+    }
     // 3..8 children: Batcher's 19-comparator network (padding key 0 sorts last)
     const uint32_t nw = nwide;
     for (uint32_t i0 = 0; i0 < nw; i0 += kDocThreads) {
         const uint32_t i = i0 + t;
         const uint32_t p = i < nw ? glist[i] : 0u;
-        const uint32_t b = p ? D[p - 1] : 0u, cnt = i < nw ? D[p] - b : 0u;
+        const uint32_t b = D[p], cnt = i < nw ? D[p + 1u] - b : 0u;
         if (cnt < 3u || cnt > 8u) continue;
         uint64_t k[8];
         uint32_t c[8];
@@ -1656,7 +1693,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         const uint32_t lane = t & 63u, wv = t >> 6;
         for (uint32_t i = wv; i < nw; i += kDocThreads / 64) {
             const uint32_t p = glist[i];
-            const uint32_t s0 = p ? D[p - 1] : 0u, cnt = D[p] - s0;
+            const uint32_t s0 = D[p], cnt = D[p + 1u] - s0;
             if (cnt <= 8u) continue;  // wave-uniform
             const bool on = lane < cnt;
             const uint32_t c = on ? ch[s0 + lane] : 0u;
@@ -2721,7 +2758,8 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.r_key = r_key_;                                              \
     a0.cap_runs = 0xFFFFFFFFu;                                      \
     a0.cap_rmax = 0xFFFFFFFFu;                                      \
-    a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull)
+    a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull);  \
+    a0.xcd = xcd_order ? 1u : 0u
 
 // Tree / digest argument block (run counts come from ctl where the kernels need them).
 #define TREEARGS(a)                                                                   \
@@ -3131,6 +3169,7 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         m.eng[i]->log2m_set = log2m_set;
         m.eng[i]->level1_global = level1_global;
         m.eng[i]->fuse_text = fuse_text;
+        m.eng[i]->xcd_order = xcd_order;
         m.eng[i]->l1_split = l1_split;
         m.eng[i]->probe_doc_ = probe_doc_;
     }
@@ -3328,6 +3367,7 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         eng[i]->log2m_set = log2m_set;
         eng[i]->level1_global = level1_global;
         eng[i]->fuse_text = fuse_text;
+        eng[i]->xcd_order = xcd_order;
         eng[i]->probe_doc_ = probe_doc_;
     }
     std::vector<int> rc(K, CRDT_HIP_OK);

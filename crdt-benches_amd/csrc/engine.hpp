@@ -176,6 +176,7 @@ public:
                            uint64_t* cps, crdt_hip_stats* st);
     // bumped by every (re)allocation of scratch, this engine's or a lane engine's (a graph that
     // captured a multi-lane merge holds the lane engines' pointers too)
+    bool xcd_order = true;  // XCD-aware tile order in k_classify / k_runs (engine.hip xcd_block)
     uint64_t generation() const {
         uint64_t g = gen_;
         for (const auto& e : lane_eng_) g += e->generation() + 1;
