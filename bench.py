@@ -368,7 +368,9 @@ def traces_rank(args, comm, make_batch, inputs) -> dict | None:
     """One rank of the headline: its replica shard (seeded by rank), the timed merges, the counter
     and digest exchange, the whole-job figures.  Returns rank 0's result (None elsewhere)."""
     world, rank = comm.world, comm.rank
+    t_enc = time.perf_counter()
     batch = make_batch(inputs["bases"], args.replicas, args.relabel, shard_seed(rank))
+    enc_s = time.perf_counter() - t_enc  # (synchronous: upload + device encoding of every replica)
     if rank == 0:
         log(f"[bench] rank0: {batch.docs} docs, {batch.items} items, "
             f"{batch.device_bytes / 1e9:.1f} GB resident")
@@ -395,6 +397,7 @@ def traces_rank(args, comm, make_batch, inputs) -> dict | None:
         "value": float(allc[:, 0].sum()) / step_s, "digests_ok": digests_ok,
         "per_rank": [{c: int(allc[r, i]) for i, c in enumerate(COUNTERS)} for r in range(world)],
         "items_per_s": float(allc[:, 1].sum()) / step_s,
+        "encode_s": enc_s,
     }
     return res if rank == 0 else None
 
@@ -461,6 +464,8 @@ def traces_workload(args) -> int:
     ctx.set_param("lanes", args.lanes)
     if args.xcd_order != 1:  # (the engine's default; builds before the parameter lack it)
         ctx.set_param("xcd_order", args.xcd_order)
+    if args.stile_text != 1:  # (likewise)
+        ctx.set_param("stile_text", args.stile_text)
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
@@ -479,20 +484,20 @@ def traces_workload(args) -> int:
     if rank == 0:
         batch, stats = res["batch"], res["stats"]
         items_per_gpu = batch.items
-        rf = roofline_fields(stats, batch, items_per_gpu, res["step_s"])
-        # The stream kernel again with one lane (untimed extra merges after the timed region):
-        # its launches then have the GPU to themselves, as in a one-lane rocprofv3 profile.
-        iso = None
-        if args.lanes > 1 and rf["launches"].get("classify"):
+        # Kernel times for the roofline come from merges with ONE lane (untimed, after the timed
+        # region): with two lanes a wave's level 1 waits for CUs the other lane's level 0 holds,
+        # so its HIP-event interval is not the kernel's own duration (a one-lane rocprofv3
+        # kernel trace agrees with these).  The timed step itself ran with args.lanes lanes.
+        iso_stats = stats
+        if args.lanes > 1:
             ctx.set_param("lanes", 1)
-            st1 = [batch.merge()[2] for _ in range(2)][-1]
+            iso_stats = [batch.merge()[2] for _ in range(3)][1:]
             ctx.set_param("lanes", args.lanes)
-            ns1 = st1["stage_ns"]["classify"] / max(1, st1["stage_launches"]["classify"])
-            b = rf["stream_kernel"]["alg_bytes_per_launch"]
-            iso = {"achieved": b / ns1, "frac": b / ns1 / HBM_PEAK_GBPS, "launch_us": ns1 / 1e3,
-                   "ms_per_step_1_lane": st1["total_ns"] / 1e6,
-                   "kernel_ms_sum_1_lane": sum(st1["stage_ns"].values()) / 1e6}
-            rf["stream_kernel"]["isolated_1_lane"] = iso
+        rf = roofline_fields(iso_stats, batch, items_per_gpu, res["step_s"])
+        rf_lanes = None
+        if args.lanes > 1:
+            rf_lanes = {k: round(float(np.mean([s["stage_ns"][k] for s in stats])) / 1e6, 4)
+                        for k in stats[0]["stage_ns"] if stats[0]["stage_launches"][k]}
         patches_per_gpu = sum(inputs["patches"]) * args.replicas
         out = {
             "metric": METRIC,
@@ -523,9 +528,21 @@ def traces_workload(args) -> int:
             "device_ms_per_step": float(np.mean([s["total_ns"] for s in stats])) / 1e6,
             "runs_per_gpu": stats[0]["runs"],
             "kernels": rf["kernels"],
+            "kernels_source": "one-lane merges after the timed region (uncontended launches)"
+                              if args.lanes > 1 else "the timed merges",
+            "kernels_ms_with_lanes": rf_lanes,
+            "ms_per_step_1_lane": float(np.mean([s["total_ns"] for s in iso_stats])) / 1e6,
             "roofline": rf["roofline"],
             "stream_kernel": rf["stream_kernel"],
             "pipeline": rf["pipeline"],
+            "input_encoding": {
+                "ms": res["encode_s"] * 1e3,
+                "bytes_per_slot": 15,
+                "note": "one-time, untimed: upload of the 4 resolved logs and the device build of "
+                        "every replica's resident op log (relabelled parent u32, key u64 = lamport "
+                        "<< 16 | agent, 3-byte codepoint word with the tombstone and previous-slot "
+                        "flags: O(1) per item); the traffic contract (DESIGN.md section 7) prices "
+                        "the merge over this format"},
             "resolve": {"ms_per_trace": dict(zip(TRACES, inputs["resolve_ms"])),
                         "ms_total_one_core": sum(inputs["resolve_ms"]),
                         "ms_all_parallel": inputs["resolve_parallel_ms"],
@@ -774,6 +791,9 @@ def parse_args(argv=None):
                     help="0: k_doctree leaves the text to k_expand (smaller LDS footprint)")
     ap.add_argument("--xcd-order", type=int, default=1, choices=[0, 1],
                     help="1: level-0 tiles in XCD-aware order (each XCD one contiguous range)")
+    ap.add_argument("--stile-text", type=int, default=1, choices=[0, 1],
+                    help="1: fused level 1 stages text from the tile segments (k_runs skips the "
+                         "slot-order copy)")
     ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
                     help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -208,6 +208,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.xcd_order = value == 1;
         return 0;
     }
+    if (k == "stile_text") {  // 1: fused plans stage text from the tile segments (L1Plan)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "stile_text must be 0 or 1");
+        ctx->eng.stile_text = value == 1;
+        return 0;
+    }
     if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)
         ctx->eng.plan_shrink = value != 0;
         return 0;

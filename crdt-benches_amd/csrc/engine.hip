@@ -148,6 +148,8 @@ struct L0Args {
     uint32_t cap_runs, cap_rmax;  // capacity of the launch plan (k_docmax flags C_REPLAN above)
     uint32_t cap_rows;            // rows allocated in r_parent / r_key (more runs: not written)
     uint32_t xcd;                 // 1: XCD-aware tile order in k_classify / k_runs (xcd_block)
+    uint32_t copy_text;           // k_runs copies the tile text into sbytes (0: k_doctree reads
+                                  //   the tile segments itself, L1Plan::stile_text)
 };
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
@@ -508,7 +510,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     const uint8_t* src = a.stile + (uint64_t)tile * kTileBytes;
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
     uint32_t w0 = 0, w1 = 0;
-    if (a.mode == 0) {
+    const bool copy = a.mode == 0 && a.copy_text;
+    if (copy) {
         w0 = s32[threadIdx.x];
         w1 = s32[threadIdx.x + 1];
     }
@@ -573,7 +576,11 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         a.doc_p0[d] = pre.y + (ex & 0xFFFFu);
     }
     if (tile + 1u == a.ntiles && threadIdx.x == 0) a.r_pstart[pre.x + nh + totd] = pre.y + tw_all;
-    if (a.mode == 0) {
+#ifdef CRDT_EXP_NOTEXT
+    if (false) {
+#else
+    if (copy) {
+#endif
         uint32_t* d32 = reinterpret_cast<uint32_t*>(a.sbytes);
         if (m < hi) d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
         for (m += 4u * kBlock; m < hi; m += 4u * kBlock) {
@@ -600,7 +607,11 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const uint2 dc = ldoc[li >> 4];
         const bool root = g == dc.x;
         const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
+#ifdef CRDT_EXP_NOKEY
+        const uint64_t key = g;  // (timing experiment: no key gather)
+#else
         const uint64_t key = a.in_key[g];
+#endif
         // a non-seq head's parent from the tile's list: its index = the non-seq items before it
         const uint32_t nw = lnsq[li >> 4];
         uint32_t p = (!sq && !root)
@@ -631,6 +642,9 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
                 rows += (uint32_t)__popcll(hb & lw & mask);
             }
             pr = tp + hl + rows - 1u;
+#ifdef CRDT_EXP_NOHREC
+            pr = rho - 1u;  // (timing experiment: a valid chain, no head-record gathers)
+#endif
         }
         if (rt < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
             a.r_parent[rt] = pr;
@@ -773,6 +787,7 @@ struct TreeArgs {
                        // results, after ctl in one block, copied to the host in one transfer
     const uint32_t* rank;  // per document: its k_doctree workgroup
     uint4* wg;             // per k_doctree workgroup: its descriptor (DocArgs::wg)
+    const uint2* docs;     // per document {wave-relative base slot, items}
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
@@ -1181,8 +1196,11 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
             a.loff[d] = carry_l + sl[threadIdx.x] - nl;
             if (a.wg) {
                 const uint32_t k = a.rank[d];
+                const uint2 dr = a.docs[d];
+                const uint32_t t0 = dr.x / kScanTile, t1 = (dr.x + dr.y) / kScanTile;
                 a.wg[2u * k] = make_uint4(d, r0, r1 - r0, p0);
-                a.wg[2u * k + 1u] = make_uint4(tl, (uint32_t)to, (uint32_t)(to >> 32), 0u);
+                a.wg[2u * k + 1u] = make_uint4(tl, (uint32_t)to, (uint32_t)(to >> 32),
+                                               t0 | (min(t1 - t0, 0xFFFu) << 20));
             }
         }
         carry_t += st[1023];
@@ -1312,14 +1330,23 @@ constexpr uint32_t kDocLds = 163840 - 1024;  // dynamic LDS budget (static array
 constexpr uint16_t kNil16 = 0xFFFFu;
 constexpr uint16_t kUp16 = 0x8000u;
 constexpr uint32_t kNil14 = 0x3FFFu;   // no next splitter (splitter records: sum << 14 | next)
+// Documents staged from the per-tile text segments span at most this many tiles (a tile prefix
+// table of kDocTiles + 1 entries in LDS): documents of up to ~4 M slots
+constexpr uint32_t kDocTiles = 1024;
 
 struct DocArgs {
     uint32_t ndocs, rcap, scap, chbytes;
     uint32_t probe;  // 1 + document whose phase times are printed (0: none)
     const uint32_t* doc_root;
     // per workgroup (costliest document first), written by k_doctotals: {document, first run,
-    // runs, text prefix}, {text bytes, output offset lo, hi, 0}
+    // runs, text prefix}, {text bytes, output offset lo, hi, first tile | (tiles - 1) << 20}
     const uint4* wg;
+    // stile_text: the slot-order text is read from the tiles' segments (k_classify's stile, one
+    // kTileBytes segment per tile, tile_hw .y = the tile's weight prefix after the scan) instead
+    // of sbytes, which k_runs then does not write
+    uint32_t stile_text, ntiles;
+    const uint8_t* stile;
+    const uint2* tile_hw;
     uint32_t keyoff;  // LDS byte offset of the sibling keys
     const uint32_t* r_parent;
     const uint64_t* r_key;
@@ -1372,7 +1399,105 @@ __device__ __forceinline__ uint64_t doc_key(const uint64_t* keys, uint32_t v) {
 // per lane (256-byte coalesced stores per wave): byte y belongs to the run of the last set bit
 // at or before y.  Returns false (nothing written) when the document does not fit.
 constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
+// Staging from the tiles' text segments (DocArgs::stile_text): the document's text is the part
+// [p0, p0 + tl) of the weight range of tiles t0 .. t0 + nt, each tile's share contiguous in its
+// kTileBytes segment, staged at offset (weight position - p0 + sh).  tpx = the tiles' weight
+// prefixes (the first nt + 2 lanes hold one each).  Work items are the 16-byte staging chunks each
+// tile's share overlaps (a block scan of the per-tile counts, then a 10-step binary search per
+// item over the table in LDS).  A chunk wholly inside one share is two aligned 16-byte loads from
+// the segment, a funnel shift and one 16-byte LDS store; a chunk a share only partly covers (at
+// most two per tile) stores its bytes one by one (the neighbouring tile stores the rest).
+__device__ __forceinline__ uint32_t funnel_byte(uint32_t lo, uint32_t hi, uint32_t b) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * b));
+}
+__device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, uint32_t tl,
+                                                 uint32_t sh, uint32_t t0, uint32_t nt,
+                                                 uint32_t tpx_reg, uint8_t* st, uint32_t* tab,
+                                                 uint32_t* scan_lds) {
+    const uint32_t t = threadIdx.x;
+    uint32_t* tpx = tab;               // nt + 2 weight prefixes
+    uint32_t* itp = tab + (nt + 2u);   // nt + 2 item prefixes
+    if (t <= nt + 1u) tpx[t] = tpx_reg;
+    __syncthreads();
+    const uint32_t base = p0 - sh;  // weight position of staging byte 0
+    uint32_t cnt = 0;
+    if (t <= nt) {
+        const uint32_t lo = max(tpx[t], p0), hi = min(tpx[t + 1u], p0 + tl);
+        cnt = hi > lo ? ((hi - base + 15u) >> 4) - ((lo - base) >> 4) : 0u;
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan<kDocThreads / 64>(cnt, scan_lds, total);
+    if (t <= nt) itp[t] = ex;
+    __syncthreads();
+    constexpr int kE = 2;  // items per thread and round (registers: ro / ps are live here)
+    for (uint32_t i0 = 0; i0 < total; i0 += kE * kDocThreads) {
+        uint32_t kk[kE], ii[kE];
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+            ii[e] = i0 + t + (uint32_t)e * kDocThreads;
+            kk[e] = 0;
+        }
+        // the last tile whose first item is at or before the item (10 steps: nt + 1 <= 1024)
+#pragma unroll
+        for (uint32_t step = 512; step; step >>= 1) {
+#pragma unroll
+            for (int e = 0; e < kE; ++e) {
+                const uint32_t c = kk[e] + step;
+                if (c <= nt && itp[c] <= ii[e]) kk[e] = c;
+            }
+        }
+        uint4 q0[kE], q1[kE];
+        uint32_t cb[kE], slo[kE], shi[kE], u[kE];
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+            const uint32_t x0 = tpx[kk[e]];
+            const uint32_t lo = max(x0, p0) - base, hi = min(tpx[kk[e] + 1u], p0 + tl) - base;
+            cb[e] = ((lo >> 4) + (ii[e] - itp[kk[e]])) << 4;  // the chunk (staging offset)
+            slo[e] = lo;                                       // the share, in staging offsets
+            shi[e] = ii[e] < total ? hi : 0u;
+            // the chunk's first byte in the tile's segment, and the aligned pair covering it
+            u[e] = cb[e] + base - x0;
+            const uint4* src = reinterpret_cast<const uint4*>(
+                a.stile + (uint64_t)(t0 + kk[e]) * kTileBytes + (u[e] & ~15u));
+            q0[e] = make_uint4(0, 0, 0, 0);
+            q1[e] = make_uint4(0, 0, 0, 0);
+            if (ii[e] < total && cb[e] >= slo[e] && cb[e] + 16u <= shi[e]) {
+                q0[e] = src[0];
+                q1[e] = src[1];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+            if (ii[e] >= total) continue;
+            if (cb[e] >= slo[e] && cb[e] + 16u <= shi[e]) {
+                // wholly inside the share: 16 bytes from the aligned pair, shifted
+                const uint32_t w[8] = {q0[e].x, q0[e].y, q0[e].z, q0[e].w,
+                                       q1[e].x, q1[e].y, q1[e].z, q1[e].w};
+                const uint32_t dw = (u[e] >> 2) & 3u, b = u[e] & 3u;
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    // w[dw + k] and w[dw + k + 1] by selects (dw is per lane)
+                    uint32_t lo = w[k], hi = w[k + 1];
+#pragma unroll
+                    for (uint32_t s2 = 1; s2 < 4; ++s2)
+                        if (dw == s2) { lo = w[k + s2]; hi = w[k + s2 + 1]; }
+                    o[k] = funnel_byte(lo, hi, b);
+                }
+                *reinterpret_cast<uint4*>(st + cb[e]) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+                // partly covered: the covered bytes one by one, from the segment directly
+                const uint8_t* seg = a.stile + (uint64_t)(t0 + kk[e]) * kTileBytes;
+                const uint32_t x0 = tpx[kk[e]];
+                for (uint32_t j = max(cb[e], slo[e]); j < min(cb[e] + 16u, shi[e]); ++j)
+                    st[j] = seg[j + base - x0];
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t p0, uint64_t toff,
+                                         uint32_t tiles, uint32_t tpx_reg,
                                          const uint32_t (&ro)[kDocJ], const uint32_t (&ps)[kDocJ],
                                          uint8_t* st, uint32_t* scan_lds, uint64_t* tprobe) {
     const uint32_t t = threadIdx.x;
@@ -1381,30 +1506,41 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     const uint32_t nw = (tl + 31u) >> 5;       // bitvector words
     const uint32_t o_bits = 16u * nq + 16u, o_pref = o_bits + 4u * nw;
     const uint32_t o_delta = (o_pref + 2u * nw + 15u) & ~15u;
+    const uint32_t t0 = tiles & 0xFFFFFu, nt = tiles >> 20;
     uint32_t mine = 0;
 #pragma unroll
     for (int j = 0; j < kDocJ; ++j) mine += ro[j] != kNil ? 1u : 0u;
     uint32_t Rw;
     (void)block_excl_scan<kDocThreads / 64>(mine, scan_lds, Rw);
-    if (o_delta + 4u * Rw > a.lds_bytes || nq > (uint32_t)(kDocQ * kDocThreads)) return false;
+    const uint32_t o_tab = (o_delta + 4u * Rw + 15u) & ~15u;
+    if (o_tab + (a.stile_text ? 8u * (nt + 2u) : 0u) > a.lds_bytes ||
+        nq > (uint32_t)(kDocQ * kDocThreads))
+        return false;
     uint32_t* bits = reinterpret_cast<uint32_t*>(st + o_bits);
     uint16_t* pref = reinterpret_cast<uint16_t*>(st + o_pref);
     uint32_t* delta = reinterpret_cast<uint32_t*>(st + o_delta);
     // 1) staging (every load first; the run prefixes ps were loaded before the offsets)
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.sbytes + (p0 - sh));
-        uint4 q[kDocQ];
-#pragma unroll
-        for (int k = 0; k < kDocQ; ++k) {
-            const uint32_t i = t + (uint32_t)k * kDocThreads;
-            q[k] = i < nq ? src[i] : make_uint4(0, 0, 0, 0);
-        }
+    if (a.stile_text) {
         for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
-        uint4* stq = reinterpret_cast<uint4*>(st);
+        stage_from_tiles(a, p0, tl, sh, t0, nt, tpx_reg, st,
+                         reinterpret_cast<uint32_t*>(st + o_tab), scan_lds);
+    }
+    {
+        if (!a.stile_text) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.sbytes + (p0 - sh));
+            uint4 q[kDocQ];
 #pragma unroll
-        for (int k = 0; k < kDocQ; ++k) {
-            const uint32_t i = t + (uint32_t)k * kDocThreads;
-            if (i < nq) stq[i] = q[k];
+            for (int k = 0; k < kDocQ; ++k) {
+                const uint32_t i = t + (uint32_t)k * kDocThreads;
+                q[k] = i < nq ? src[i] : make_uint4(0, 0, 0, 0);
+            }
+            for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
+            uint4* stq = reinterpret_cast<uint4*>(st);
+#pragma unroll
+            for (int k = 0; k < kDocQ; ++k) {
+                const uint32_t i = t + (uint32_t)k * kDocThreads;
+                if (i < nq) stq[i] = q[k];
+            }
         }
         __syncthreads();
         // 2) run starts -> ranks in document order -> staging offset minus document offset
@@ -1510,6 +1646,12 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     // pk[j]: the parent of run t + 1024 j (kNil16: none), then | its place among the parent's
     // children << 16 (from the count's atomic): the placement needs no second atomic
     uint32_t pk[kDocJ];
+    // (stile_text) this lane's entry of the document's tile prefix table, used by phase C
+    uint32_t tpx_reg = 0;
+    if (a.stile_text) {
+        const uint32_t t0 = wg1.w & 0xFFFFFu, nt = wg1.w >> 20;
+        if (t <= nt + 1u) tpx_reg = t0 + t < a.ntiles ? a.tile_hw[t0 + t].y : a.ctl[C_WTOTAL];
+    }
     {
         uint32_t gp[kDocJ];
         uint64_t gk[kDocJ];
@@ -1918,9 +2060,13 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         uint64_t* tprobe = nullptr;
 #endif
         const uint64_t toff = ((uint64_t)wg1.z << 32) | wg1.y;
-        const bool fused = doc_text(a, wg1.x, wg.w, toff, ro, ps, reinterpret_cast<uint8_t*>(dyn),
-                                    scan_lds, tprobe);
-        if (!fused) {
+        const bool fused = doc_text(a, wg1.x, wg.w, toff, wg1.w, tpx_reg, ro, ps,
+                                    reinterpret_cast<uint8_t*>(dyn), scan_lds, tprobe);
+        if (!fused && a.stile_text) {
+            // no slot-order text to copy from (k_runs skipped it): the host merges the wave
+            // again on its synchronous path, which writes it
+            if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);
+        } else if (!fused) {
             // the text did not fit LDS: every run copies its bytes from the slot-order text to
             // its document offset (byte stores; only documents above the LDS stage take this)
             uint8_t* out = a.text + toff;
@@ -2408,6 +2554,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         w.max_splitters_per_doc = std::max<uint32_t>(w.max_splitters_per_doc, (uint32_t)(2 * ds / M));
         w.text_cap += dt;
         w.max_doc_text = std::max<uint64_t>(w.max_doc_text, docs[d].text_cap);
+        w.max_doc_slots = std::max<uint64_t>(w.max_doc_slots, ds);
         w.leaf_cap += (docs[d].text_cap + kLeaf - 1) / kLeaf;
         w.order_cap += docs[d].n;
         L.items += docs[d].n;
@@ -2700,6 +2847,8 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     // expansion + digest fused into k_doctree when every document's text fits LDS: text staging
     // + run-start bitvector (tl/8 + tl/16) + one u32 per run
     p.fuse = fuse_text && p.lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
+    // (a document spans at most max_doc_slots / 4096 + 2 tiles)
+    p.stile_text = p.fuse && stile_text && w.max_doc_slots / kScanTile + 2u <= kDocTiles;
     p.dyn_bytes = p.fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
                                dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
                          : dbytes;
@@ -2759,7 +2908,8 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.cap_runs = 0xFFFFFFFFu;                                      \
     a0.cap_rmax = 0xFFFFFFFFu;                                      \
     a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull);  \
-    a0.xcd = xcd_order ? 1u : 0u
+    a0.xcd = xcd_order ? 1u : 0u;                                  \
+    a0.copy_text = 1u
 
 // Tree / digest argument block (run counts come from ctl where the kernels need them).
 #define TREEARGS(a)                                                                   \
@@ -2776,14 +2926,16 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
     a.leafcp = leafcp_; a.gcp = gcp_; a.res = res_;                                   \
     a.rank = L.doc_rank + w.first_doc; a.wg = nullptr;                                \
+    a.docs = L.docs_rel + w.first_doc;                                                \
     a.text = text_;                                                                   \
     a.text_cap = ord ? w.order_cap : cap_text_ - 64;                                  \
     a.align = ord ? 1u : 16u
 
-int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs,
-                          uint32_t cap_rmax, StageClock& ck) {
+int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text,
+                          uint32_t cap_runs, uint32_t cap_rmax, StageClock& ck) {
     hipStream_t s = cur_;
     L0ARGS(a0);
+    a0.copy_text = copy_text ? 1u : 0u;
     a0.cap_runs = cap_runs;
     a0.cap_rmax = cap_rmax;
     const uint32_t ntiles = a0.ntiles;
@@ -2821,7 +2973,7 @@ int Engine::launch_runs(DeviceLogs& L, const Wave& w, bool ord) {
 
 // k_doctotals, k_doctree (k_expand for documents whose text did not fit runs in the tail).
 int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
-                              StageClock& ck) {
+                              bool stile, StageClock& ck) {
     hipStream_t s = cur_;
     TREEARGS(a);
     DocArgs da{};
@@ -2845,6 +2997,10 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.probe = probe_doc_;
     da.wg = wgtab_;
     da.keyoff = doctree_key_off(p.rcap, p.scap);
+    da.stile_text = stile ? 1u : 0u;
+    da.ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
+    da.stile = stile_;
+    da.tile_hw = tile_hw_;
     a.wg = wgtab_;  // (k_doctotals writes the k_doctree workgroup descriptors)
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
@@ -2996,7 +3152,8 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     // level 1.
     std::unique_lock<std::mutex> gate;
     if (l0_gate_) gate = std::unique_lock<std::mutex>(*l0_gate_);
-    int rc = launch_level0(L, w, ord, 0xFFFFFFFFu, 0xFFFFFFFFu, ck);
+    // (the plan is not known yet: k_runs writes the slot-order text)
+    int rc = launch_level0(L, w, ord, true, 0xFFFFFFFFu, 0xFFFFFFFFu, ck);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(hctl, ctl_, 64, hipMemcpyDeviceToHost, s), "copy ctl");
     HIPCHK(hipStreamSynchronize(s), "level-0 sync");
@@ -3019,7 +3176,9 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     }
     if ((rc = clock_mark(ck, 0xFF))) return rc;  // the host wait above is no stage's time
     uint32_t rounds = 0;
-    rc = p.lds1 ? launch_lds_level1(L, w, ord, p, ck) : launch_global_level1(L, w, ord, p, ck, rounds);
+    // (k_runs wrote the slot-order text here: the plan was not known when level 0 ran)
+    rc = p.lds1 ? launch_lds_level1(L, w, ord, p, false, ck)
+                : launch_global_level1(L, w, ord, p, ck, rounds);
     if (rc) return rc;
     rc = launch_tail(L, w, ord, p.fuse, ck, hctl);
     if (rc) return rc;
@@ -3170,6 +3329,7 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         m.eng[i]->level1_global = level1_global;
         m.eng[i]->fuse_text = fuse_text;
         m.eng[i]->xcd_order = xcd_order;
+        m.eng[i]->stile_text = stile_text;
         m.eng[i]->l1_split = l1_split;
         m.eng[i]->probe_doc_ = probe_doc_;
     }
@@ -3227,7 +3387,8 @@ int Engine::merge_async_enqueue(DeviceLogs& L, AsyncMerge& m) {
         // level 0 overwrites the lane's scratch: after the lane's previous level 1
         if (E.l1_pending_) HIPCHK(hipStreamWaitEvent(E.stream, E.ev_l1_, 0), "stream wait");
         E.cur_ = E.stream;
-        int rc = E.launch_level0(L, w, false, m.plans[wi].R, m.plans[wi].rmax, ck);
+        int rc = E.launch_level0(L, w, false, !m.plans[wi].stile_text, m.plans[wi].R,
+                                 m.plans[wi].rmax, ck);
         if (rc) return rc;
         prev_l0 = ck.ev ? ck.ev[ck.n - 1] : nullptr;  // the end of level 0
         if (split) {
@@ -3235,7 +3396,7 @@ int Engine::merge_async_enqueue(DeviceLogs& L, AsyncMerge& m) {
             HIPCHK(hipStreamWaitEvent(E.stream_l1, E.ev_l0_, 0), "stream wait");
             E.cur_ = E.stream_l1;
         }
-        rc = E.launch_lds_level1(L, w, false, m.plans[wi], ck);
+        rc = E.launch_lds_level1(L, w, false, m.plans[wi], m.plans[wi].stile_text, ck);
         if (!rc) rc = E.launch_tail(L, w, false, m.plans[wi].fuse, ck, E.host_block(L, wi));
         if (split) {
             E.cur_ = E.stream;
@@ -3368,6 +3529,7 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         eng[i]->level1_global = level1_global;
         eng[i]->fuse_text = fuse_text;
         eng[i]->xcd_order = xcd_order;
+        eng[i]->stile_text = stile_text;
         eng[i]->probe_doc_ = probe_doc_;
     }
     std::vector<int> rc(K, CRDT_HIP_OK);

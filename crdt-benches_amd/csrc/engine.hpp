@@ -32,6 +32,7 @@ struct Wave {
     uint64_t leaf_cap;   // 4 KiB leaves
     uint64_t order_cap;  // u32 entries for ORDER mode
     uint64_t max_doc_text;  // largest document text bound of the wave
+    uint64_t max_doc_slots = 0;  // largest document of the wave, in slots
     // Launch plan of the wave's level 1, learnt by a merge that waited for level 0 (run count,
     // runs of the largest document); valid until the logs are planned again.  A merge that
     // enqueues the wave with it does not wait for level 0: the device checks the plan (k_docmax
@@ -52,6 +53,10 @@ struct StageClock {
 struct L1Plan {
     uint32_t R = 0, rmax = 0;
     bool lds1 = false, fuse = false;
+    // k_doctree stages each document's text from the per-tile segments k_classify wrote (stile),
+    // so k_runs does not copy them into the slot-order text (sbytes): fused plans whose
+    // documents span at most kDocTiles tiles
+    bool stile_text = false;
     uint32_t rcap = 0, scap = 0;
     uint64_t dyn_bytes = 0;
 };
@@ -177,6 +182,7 @@ public:
     // bumped by every (re)allocation of scratch, this engine's or a lane engine's (a graph that
     // captured a multi-lane merge holds the lane engines' pointers too)
     bool xcd_order = true;  // XCD-aware tile order in k_classify / k_runs (engine.hip xcd_block)
+    bool stile_text = true;  // fused plans stage text from the tile segments (L1Plan::stile_text)
     uint64_t generation() const {
         uint64_t g = gen_;
         for (const auto& e : lane_eng_) g += e->generation() + 1;
@@ -278,9 +284,12 @@ private:
     int clock_mark(StageClock& c, int stage);
     // The launches of one wave, in stream order.
     int launch_runs(DeviceLogs& L, const Wave& w, bool ord);
-    int launch_level0(DeviceLogs& L, const Wave& w, bool ord, uint32_t cap_runs, uint32_t cap_rmax,
+    int launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text, uint32_t cap_runs,
+                      uint32_t cap_rmax,
                       StageClock& ck);
-    int launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p, StageClock& ck);
+    // stile: k_doctree stages the text from the tile segments (k_runs did not copy it)
+    int launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p, bool stile,
+                          StageClock& ck);
     int launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Plan& p,
                              StageClock& ck, uint32_t& rounds);
     int launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, StageClock& ck,
