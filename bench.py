@@ -753,6 +753,91 @@ def downstream_workload(args) -> int:
     return 0 if ok else 1
 
 
+def upstream_inc_workload(args) -> int:
+    """the upstream loop (main.rs:28-36) with len() every K patches instead of
+    once at the end.  The reference's len() (rope.rs:135, checkout_tip) materialises the whole
+    document each time.  Per checkpoint the step applies the chunk's updates (encoded on the host
+    beforehand, as upstream_updates does, rope.rs:196-220, resident in HBM) to a device replica
+    and asks for the length, once with the incremental merge (crdt_hip_replica_merge_inc: only
+    the appended items are ranked) and, in a second timed pass, with a full merge per checkpoint
+    (crdt_hip_replica_merge_len).  Every checkpoint's codepoints are checked against the host
+    log's visible length after the same patches.  value = patches/s of the incremental loop."""
+    world, rank, local = rank_env()
+    ctx = crdt_hip.Context(local)
+    comm = Comm(world, rank, ctx)
+    name, K = args.inc_trace, args.every
+    t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
+    patches = [t.patch(i) for i in range(len(t))]
+    up = crdt_hip.HipMerge.from_str(t.start_content)
+    chunks, expect = [], []
+    for i in range(0, len(patches), K):
+        v = up.log.version()
+        for pos, dele, ins in patches[i:i + K]:
+            up.replace(pos, pos + dele, ins)
+        buf, offs = crdt_hip.pack_updates([up.log.encode_from(v)])
+        chunks.append(crdt_hip.UpdateBatch(ctx, buf, offs))
+        expect.append(up.log.visible_len())
+    init = crdt_hip.HipMerge.from_str(t.start_content).log
+
+    def loop(incremental, per_ck):
+        r = crdt_hip.Replica(ctx, init if init.view().n else None)
+        ok, paths = True, 0
+        for c, ub in enumerate(chunks):
+            r.apply_resident(ub)
+            t0 = time.perf_counter()
+            if incremental:
+                cps, nb, path, _ = r.merge_inc()
+                paths += path
+            else:
+                cps, nb, _ = r.merge_len()
+            per_ck.append(time.perf_counter() - t0)
+            ok &= cps == expect[c]
+        r.close()
+        return ok, paths
+
+    res = {}
+    for mode in ("incremental", "incremental_3_launches", "full"):
+        ctx.set_param("inc_coop", 0 if mode == "incremental_3_launches" else 1)
+        for _ in range(args.warmup):
+            loop(mode != "full", [])
+        comm.barrier()
+        per_ck: list = []
+        t0 = time.perf_counter()
+        ok, paths = True, 0
+        for _ in range(args.steps):
+            o, p = loop(mode != "full", per_ck)
+            ok &= o
+            paths += p
+        comm.barrier()
+        el = time.perf_counter() - t0
+        res[mode] = {"ms_per_step": el / args.steps * 1e3, "ok": bool(ok),
+                     "len_ms_mean": float(np.mean(per_ck)) * 1e3,
+                     "len_ms_median": float(np.median(per_ck)) * 1e3,
+                     "incremental_calls": paths // max(1, args.steps)}
+    ctx.set_param("inc_coop", 1)
+    inc, full = res["incremental"], res["full"]
+    ok = inc["ok"] and full["ok"] and res["incremental_3_launches"]["ok"]
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": len(patches) / (inc["ms_per_step"] / 1e3),
+            "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": inc["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "trace",
+            "config": {"workload": f"upstream (main.rs:28-36) with len() every {K} patches: "
+                                   "apply the chunk's updates to a device replica + len()",
+                       "trace": name, "patches": len(patches), "checkpoints": len(chunks),
+                       "updates_resident": True},
+            "incremental": inc, "incremental_3_launches": res["incremental_3_launches"],
+            "full": full,
+            "len_speedup_mean": full["len_ms_mean"] / inc["len_ms_mean"],
+            "len_speedup_median": full["len_ms_median"] / inc["len_ms_median"],
+            "lens_ok": bool(ok),
+        }
+        print(json.dumps(out), flush=True)
+    comm.close()
+    return 0 if ok else 1
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -805,11 +890,14 @@ def parse_args(argv=None):
                          "side line; the CPU baseline and the shuffle companion are RGA-only "
                          "and are skipped)")
     ap.add_argument("--workload", default="traces",
-                    choices=["traces", "seph", "agents64", "big1b", "downstream"],
+                    choices=["traces", "seph", "agents64", "big1b", "downstream", "upstream_inc"],
                     help="traces: config 3 (headline); seph: config 2; agents64: config 4; "
                          "big1b: config 5 (SURVEY.md §8(d)); downstream: the reference's "
                          "downstream group with device-side update decode (§8(f) row 2)")
     ap.add_argument("--items", type=int, default=0, help="items of the synthetic workloads")
+    ap.add_argument("--every", type=int, default=1000,
+                    help="upstream_inc: len() every this many patches")
+    ap.add_argument("--inc-trace", default="automerge-paper", help="upstream_inc: the trace")
     ap.add_argument("--p-chain", type=int, default=90,
                     help="config 5: percent of items whose parent is the previous item "
                          "(0 = uniform random parents, the worst case for gathers)")
@@ -835,6 +923,8 @@ def main() -> int:
     crdt_hip = _engine
     if args.workload == "downstream":
         return downstream_workload(args)
+    if args.workload == "upstream_inc":
+        return upstream_inc_workload(args)
     if args.workload != "traces":
         return side_workload(args)
     return traces_workload(args)

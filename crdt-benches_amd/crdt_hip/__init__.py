@@ -32,6 +32,7 @@ EXPORTS = [
     "crdt_hip_abi_version", "crdt_hip_device_count", "crdt_hip_init", "crdt_hip_destroy",
     "crdt_hip_last_error", "crdt_hip_set_param", "crdt_hip_oplog_new", "crdt_hip_oplog_set_fugue",
     "crdt_hip_oplog_set_agent", "crdt_hip_oplog_clone", "crdt_hip_trace_resolve_fugue",
+    "crdt_hip_replica_merge_inc",
     "crdt_hip_oplog_free", "crdt_hip_oplog_insert", "crdt_hip_oplog_remove",
     "crdt_hip_oplog_replace", "crdt_hip_oplog_visible_len", "crdt_hip_oplog_get_view",
     "crdt_hip_oplog_version", "crdt_hip_oplog_encode_from", "crdt_hip_oplog_apply_update",
@@ -165,6 +166,7 @@ def lib() -> C.CDLL:
         "crdt_hip_replica_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_replica_merge": (i32, [vp, vp, vp, sz, P(sz), P(u64)]),
         "crdt_hip_replica_merge_len": (i32, [vp, vp, P(u64), P(u64), P(u64)]),
+        "crdt_hip_replica_merge_inc": (i32, [vp, vp, vp, sz, P(sz), P(u64), P(u32)]),
         "crdt_hip_replica_replay": (i32, [vp, vp, vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_merge_len": (i32, [vp, P(View), P(u64), P(u64), P(u64)]),
         "crdt_hip_comm_unique_id": (i32, [vp]),
@@ -708,6 +710,17 @@ class Replica:
         _check(lib().crdt_hip_replica_merge(self.ctx._h, self._h, None, 0, C.byref(n),
                                             C.byref(dig)), self.ctx._h)
         return int(n.value), int(dig.value)
+
+    def merge_inc(self, text: bool = False) -> tuple:
+        """Incremental len() (crdt_hip_replica_merge_inc): (codepoints, UTF-8 bytes, path, text or
+        None); path 1 = only the items appended since the previous call were ranked, 0 = a full
+        merge (first call, concurrent update, > 4096 new items, Fugue)."""
+        cap = self.info()[2] + 16 if text else 0
+        buf = C.create_string_buffer(cap) if text else None
+        n, c, p = C.c_size_t(), C.c_uint64(), C.c_uint32()
+        _check(lib().crdt_hip_replica_merge_inc(self.ctx._h, self._h, buf, cap, C.byref(n),
+                                                C.byref(c), C.byref(p)), self.ctx._h)
+        return int(c.value), int(n.value), int(p.value), (buf.raw[: n.value] if text else None)
 
     def replay(self, batch: "UpdateBatch") -> tuple:
         """The downstream closure (main.rs:63-69) in one device call: a copy of this replica

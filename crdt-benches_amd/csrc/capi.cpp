@@ -213,6 +213,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.stile_text = value == 1;
         return 0;
     }
+    if (k == "inc_coop") {  // 1: incremental merges in one cooperative launch (incr.hip)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "inc_coop must be 0 or 1");
+        ctx->eng.inc_coop = value == 1;
+        return 0;
+    }
     if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)
         ctx->eng.plan_shrink = value != 0;
         return 0;
@@ -811,6 +816,27 @@ int crdt_hip_replica_merge_len(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint64_t*
         if (codepoints) *codepoints = cps;
         if (bytes) *bytes = len;
         if (digest) *digest = dig;
+        return 0;
+    });
+}
+
+int crdt_hip_replica_merge_inc(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out, size_t cap,
+                               size_t* out_len, uint64_t* codepoints, uint32_t* path) {
+    if (!ctx || !r) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (r->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "replica belongs to another context");
+    return guard(ctx, [&] {
+        std::vector<uint8_t> text;
+        uint64_t len = 0, cps = 0;
+        uint32_t p = 0;
+        int rc = crdt::replica_merge_inc(ctx->eng, r->r, out ? &text : nullptr, &len, &cps, &p);
+        if (rc) return from_engine(ctx, rc);
+        if (out_len) *out_len = (size_t)len;
+        if (codepoints) *codepoints = cps;
+        if (path) *path = p;
+        if (out) {
+            if (cap < len) return set_err(ctx, CRDT_HIP_ESPACE, "output buffer too small");
+            if (len) std::memcpy(out, text.data(), (size_t)len);
+        }
         return 0;
     });
 }

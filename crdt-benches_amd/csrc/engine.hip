@@ -357,7 +357,7 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
-    uint64_t hw = 0, lv = 0, lb = 0;
+    uint64_t hw = 0, lv = 0, lb = 0, vs = 0;
     if (gs < a.nslots) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         const uint32_t l0 = gs - doc.x, n = doc.y;
@@ -374,9 +374,11 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
             hw = root | (item & (nsq | prevj));
             lv = root | vis | (item & jw);
+            vs = vis;
             if (a.fugue) lb = *reinterpret_cast<const uint64_t*>(a.lbits + (gs >> 5));
         }
     }
+    const uint64_t hw0 = hw;  // the run boundaries (before the dead-run drop)
     {
         // the next word's live slots before its first head keep this word's last run
         const uint64_t hn = (uint64_t)__shfl_down((long long)hw, 1);
@@ -391,6 +393,26 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             pm &= pm >> k;
         }
         hw &= z;
+    }
+    if (a.fugue) {
+        // Fugue: a head with left children numbers two rows only if its run holds visible text;
+        // a weightless content row is a leaf that adds nothing, so such a run keeps its tree row
+        // alone (its left children, then the last item's right children).  The same segmented
+        // OR over the visible bits alone (a run that goes on past the wave's words: kept), and
+        // the left-child bits become the two-row bits k_runs reads.
+        const uint64_t hn = (uint64_t)__shfl_down((long long)hw0, 1);
+        const uint64_t vn = (uint64_t)__shfl_down((long long)vs, 1);
+        const bool carry = (threadIdx.x & 63u) == 63u || hn == 0ull ||
+                           (vn & low_mask64((uint32_t)__builtin_ctzll(hn))) != 0ull;
+        uint64_t z = vs | (carry ? (1ull << 63) : 0ull);
+        uint64_t pm = ~(hw0 >> 1);
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            z |= (z >> k) & pm;
+            pm &= pm >> k;
+        }
+        lb &= z;
+        if (gs < a.nslots) *reinterpret_cast<uint64_t*>(a.lbits + (gs >> 5)) = lb;
     }
     // Fugue: a head with left children numbers two run rows (k_runs)
     const uint32_t c = (uint32_t)__popcll(hw) + (uint32_t)__popcll(hw & lb);

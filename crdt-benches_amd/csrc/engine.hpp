@@ -142,6 +142,9 @@ public:
     bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
     bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS
     bool fuse_text = true;         // k_doctree writes the text when it fits LDS (else k_expand)
+    // incremental merges (incr.hip): the three phases in one cooperative launch with grid-wide
+    // barriers (else three launches)
+    bool inc_coop = true;
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).

@@ -440,6 +440,7 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
     const uint32_t n = v ? v->n : 0u;
     int rc = replica_reserve(E, r, n);
     if (rc) return rc;
+    r.inc.valid = false;
     r.n = n;
     r.vis_cp = r.vis_bytes = 0;
     r.version++;
@@ -474,6 +475,7 @@ int replica_upload(Engine& E, Replica& r, const crdt_hip_oplog_view* v) {
 
 int replica_copy(Engine& E, const Replica& src, Replica& dst) {
     RCHK(hipSetDevice(E.device), "hipSetDevice");
+    dst.inc.valid = false;
     if (src.pending) {
         E.err = "replica has an unsettled decode";
         return CRDT_HIP_EINVAL;
@@ -744,6 +746,7 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
         rc = replica_reserve(E, w, cap ? cap - 1 : 0);
         if (rc) return rc;
         w.n = init.n;  // the copy below
+        w.inc.valid = false;
         rc = decode_prepare(E, w, ub.len, ub.n, true, ub.max_id);
         if (rc) return rc;
         // (test hook: with plan_shrink the planned sizes are off by one, forcing the fallback)

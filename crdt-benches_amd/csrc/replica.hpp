@@ -15,6 +15,34 @@
 
 namespace crdt {
 
+// Incremental merge state of a replica (incr.hip, crdt_hip_replica_merge_inc): the document
+// order of the items 0..n it covers (tombstones included; rank 0 = the document start), its
+// inverse, and the merged text.
+constexpr uint32_t kIncMax = 4096;  // most items a fast-path merge appends
+struct IncState {
+    bool valid = false;
+    uint32_t n = 0;                  // items the order covers
+    uint64_t cap = 0;                // entries of seq[0], seq[1], rank
+    uint32_t* seq[2] = {nullptr, nullptr};  // rank -> slot (ping-pong: seq[cur] is current)
+    int cur = 0;
+    uint32_t* rank = nullptr;        // slot -> rank
+    uint32_t* ins = nullptr;         // new items in order: kIncMax slots, then kIncMax anchors
+    uint64_t ins_cap = 0;
+    uint4* bsum = nullptr;           // per splice block
+    uint64_t bsum_cap = 0;
+    uint8_t* text = nullptr;
+    uint64_t text_cap = 0;
+    uint64_t* ctl = nullptr;         // device counters (incr.hip ICtl)
+    uint64_t* hres = nullptr;        // host-mapped result block (written by the last phase)
+    uint64_t* dres = nullptr;        //   (its device address)
+    uint64_t calls = 0;              // calls made (stamps the result block)
+    std::vector<uint32_t> hseq;      // (rebuild staging)
+    IncState() = default;
+    IncState(const IncState&) = delete;
+    IncState& operator=(const IncState&) = delete;
+    ~IncState();
+};
+
 struct Replica {
     DeviceLogs logs;          // one document: slot 0 = document start, slot k = item k
     uint32_t n = 0;           // items present (ids 1..n)
@@ -38,6 +66,7 @@ struct Replica {
     uint64_t gen = 0;          // bumped by every (re)allocation of the replica's device arrays
     uint64_t version = 0;      // bumped by every change of the contents
     std::vector<void*> graveyard;  // arrays replaced by a regrow, freed at the next wait
+    IncState inc;              // incremental merge state (invalid until the first merge_inc)
 
     Replica() = default;
     Replica(const Replica&) = delete;
@@ -118,5 +147,11 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
 // the merged text, counted on the device).
 int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* len,
                   uint64_t* digest, crdt_hip_stats* st, uint64_t* cps = nullptr);
+
+// Incremental merge (incr.hip): the merged text (may be null), its UTF-8 bytes and codepoints;
+// *path = 1 when only the items appended since the previous merge_inc were ranked, 0 for a
+// full merge (the first call, a concurrent update, more than kIncMax new items, Fugue).
+int replica_merge_inc(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* bytes,
+                      uint64_t* cps, uint32_t* path);
 
 }  // namespace crdt

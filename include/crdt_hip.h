@@ -315,6 +315,17 @@ int crdt_hip_replica_replay(crdt_hip_ctx* ctx, const crdt_hip_replica* init,
 int crdt_hip_replica_merge_len(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint64_t* codepoints,
                                uint64_t* bytes, uint64_t* digest);
 
+/* Incremental len(): the replica keeps its document order and text between
+ * calls, and the items appended since the previous call are ranked alone when every one of them
+ * with an old parent has a key (lamport, agent) above every older item's (local edits; updates
+ * that race no older op), at most 4096 of them; deletes only re-weigh.  Anything else merges in
+ * full (engine ORDER mode) and rebuilds the state.  Returns the merged text (out may be NULL),
+ * its UTF-8 bytes and codepoints; *path = 1 for the incremental path, 0 for a full merge.
+ * Replaces the from-scratch checkout_tip of Dt::len (rope.rs:135) for a caller that asks for the
+ * length every K patches (main.rs:35 / :68 with len() inside the loop). */
+int crdt_hip_replica_merge_inc(crdt_hip_ctx* ctx, crdt_hip_replica* r, uint8_t* out, size_t cap,
+                               size_t* out_len, uint64_t* codepoints, uint32_t* path);
+
 /* ---- multi-GPU (RCCL over xGMI): digest/counter exchange only ----------------------------- */
 int crdt_hip_comm_unique_id(uint8_t id[128]);
 int crdt_hip_comm_init(crdt_hip_ctx* ctx, int nranks, int rank, const uint8_t id[128]);

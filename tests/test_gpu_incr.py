@@ -1,0 +1,151 @@
+"""GPU parity tests of the incremental len() (crdt_hip_replica_merge_inc, csrc/incr.hip).
+
+SURVEY §8(f) row 3: the reference's len() (Dt::len -> checkout_tip, /root/reference/src/rope.rs:135)
+re-materialises the whole document each call; the upstream loop (/root/reference/src/main.rs:28-36)
+with a len() every K patches pays a full merge per call.  The replica keeps its order and text
+and ranks only the items appended since the previous call.  Every checkpoint is compared with
+the CPU oracle's merge of the same log (oracle/oracle.c orc_merge_rga) and with the replica's own
+counters; the path taken (1 = incremental, 0 = full) is asserted where it is determined.
+"""
+import pytest
+
+import crdt_hip
+from conftest import trace_path
+from test_gpu_merge import to_anchor
+from test_gpu_replica import trace_updates
+
+pytestmark = pytest.mark.gpu
+
+
+def _checkpoints(ctx, oracle, name, K, every_oracle=1):
+    t, patches, updates = trace_updates(name)
+    r = crdt_hip.Replica(ctx)
+    host = crdt_hip.OpLog()
+    paths = []
+    for c, i in enumerate(range(0, len(updates), K)):
+        batch = updates[i:i + K]
+        n_before = r.info()[0]
+        r.apply_updates(batch)
+        for u in batch:
+            host.apply_update(u)
+        cps, nb, path, text = r.merge_inc(text=True)
+        # (local edits: the fast path applies unless the batch appended more than 4096 items)
+        paths.append(path if r.info()[0] - n_before <= 4096 else "big")
+        items, vis_cp, vis_b = r.info()
+        assert (cps, nb) == (vis_cp, vis_b) == (len(text.decode()), len(text))
+        if c % every_oracle == 0 or i + K >= len(updates):
+            assert text == oracle.merge(to_anchor(host.arrays())), f"checkpoint {c} ({i + K} patches)"
+    assert text.decode() == t.end_content
+    return paths
+
+
+@pytest.mark.parametrize("coop", [1, 0])
+def test_incremental_len_every_1000_patches_sveltecomponent(ctx, oracle, coop):
+    """coop 1: the three phases in one cooperative launch; 0: three launches."""
+    ctx.set_param("inc_coop", coop)
+    try:
+        paths = _checkpoints(ctx, oracle, "sveltecomponent", 1000)
+    finally:
+        ctx.set_param("inc_coop", 1)
+    # the first call builds the state; every later one is a local edit batch (keys increase)
+    assert paths[0] in (0, "big") and all(p in (1, "big") for p in paths[1:]), paths
+    assert paths.count(1) >= len(paths) // 2, paths
+
+
+def test_incremental_len_every_1000_patches_automerge_paper(ctx, oracle):
+    """The verdict's case: automerge-paper, len() every 1000 patches, oracle at every checkpoint."""
+    paths = _checkpoints(ctx, oracle, "automerge-paper", 1000)
+    assert paths[0] in (0, "big") and all(p in (1, "big") for p in paths[1:]), paths
+    assert paths.count(1) >= len(paths) - 10, paths
+
+
+@pytest.mark.parametrize("K", [1, 7, 4096])
+def test_incremental_len_small_and_large_steps(ctx, oracle, K):
+    """One patch per call, an odd step, and steps large enough that some batches carry more than
+    4096 items (then the full path runs and rebuilds the state)."""
+    t, patches, updates = trace_updates("sveltecomponent")
+    n = 3000 if K < 100 else len(updates)
+    r = crdt_hip.Replica(ctx)
+    host = crdt_hip.OpLog()
+    for i in range(0, n, K):
+        batch = updates[i:i + K]
+        r.apply_updates(batch)
+        for u in batch:
+            host.apply_update(u)
+        if K == 1 and i % 97 and i + 1 < n:
+            continue  # (len() at every 97th patch: the others accumulate)
+        cps, nb, path, text = r.merge_inc(text=True)
+        assert text == oracle.merge(to_anchor(host.arrays()))
+
+
+def test_concurrent_update_falls_back_to_full_merge(ctx, oracle):
+    """Agent 2 edits without having seen agent 1's latest items: its items' keys are below the
+    replica's largest key, so the fast path refuses them and the full merge runs."""
+    a = crdt_hip.OpLog(agent=1)
+    b = crdt_hip.OpLog(agent=2)
+    a.insert(0, "hello")
+    b.apply_update(a.encode_from(0))
+    r = crdt_hip.Replica(ctx)
+    r.apply_updates([a.encode_from(0)])
+    assert r.merge_inc(text=True)[3] == b"hello"
+    va, vb = a.version(), b.version()
+    a.insert(5, " world, again")                 # lamports 6.. (agent 1)
+    r.apply_updates([a.encode_from(va)])
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == b"hello world, again"
+    b.insert(0, "X")                             # lamport 6 (agent 2): older than agent 1's 18
+    b.insert(3, "Y")
+    r.apply_updates([b.encode_from(vb)])
+    a.apply_update(b.encode_from(vb))
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 0
+    assert text == oracle.merge(to_anchor(a.arrays()))
+    # the state was rebuilt: a later local edit goes the fast way again
+    va = a.version()
+    a.insert(2, "--")
+    r.apply_updates([a.encode_from(va)])
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == oracle.merge(to_anchor(a.arrays()))
+
+
+def test_deletes_only_and_many_roots(ctx, oracle):
+    """A batch of deletes only (no new items: the order is kept, the text re-weighed), and a batch
+    whose items hang off many different old parents (roots ordered by anchor)."""
+    log = crdt_hip.OpLog()
+    log.insert(0, "abcdefghijklmnopqrstuvwxyz" * 40)
+    r = crdt_hip.Replica(ctx)
+    r.apply_updates([log.encode_from(0)])
+    r.merge_inc()
+    v = log.version()
+    for k in range(0, 900, 37):
+        log.remove(k, k + 3)
+    r.apply_updates([log.encode_from(v)])
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == oracle.merge(to_anchor(log.arrays()))
+    v = log.version()
+    for k in range(0, 800, 13):
+        log.insert(k, "é中😀"[k % 3])
+    r.apply_updates([log.encode_from(v)])
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == oracle.merge(to_anchor(log.arrays()))
+    assert cps == len(text.decode())
+
+
+def test_incremental_state_survives_clone_and_fugue_takes_the_full_path(ctx, oracle):
+    t, patches, updates = trace_updates("sveltecomponent")
+    r = crdt_hip.Replica(ctx)
+    r.apply_updates(updates[:5000])
+    r.merge_inc()
+    c = r.clone()                 # a clone starts without state: its first call is a full merge
+    c.apply_updates(updates[5000:5200])
+    assert c.merge_inc()[2] == 0
+    r.apply_updates(updates[5000:5200])
+    assert r.merge_inc()[2] == 1
+    assert r.merge_inc(text=True)[3] == c.merge_inc(text=True)[3]
+    # Fugue replicas always merge in full (the fast path orders RGA trees only)
+    up = crdt_hip.OpLog(fugue=True)
+    up.insert(0, "fugue text")
+    f = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
+    f.apply_updates([up.encode_from(0)])
+    cps, nb, path, text = f.merge_inc(text=True)
+    assert path == 0 and text == b"fugue text"
