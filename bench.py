@@ -466,6 +466,8 @@ def traces_workload(args) -> int:
         ctx.set_param("xcd_order", args.xcd_order)
     if args.stile_text != 1:  # (likewise)
         ctx.set_param("stile_text", args.stile_text)
+    if args.nsq_list != 1:  # (likewise)
+        ctx.set_param("nsq_list", args.nsq_list)
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
@@ -796,8 +798,8 @@ def upstream_inc_workload(args) -> int:
         return ok, paths
 
     res = {}
-    for mode in ("incremental", "incremental_3_launches", "full"):
-        ctx.set_param("inc_coop", 0 if mode == "incremental_3_launches" else 1)
+    for mode in ("incremental", "incremental_coop", "full"):
+        ctx.set_param("inc_coop", 1 if mode == "incremental_coop" else 0)
         for _ in range(args.warmup):
             loop(mode != "full", [])
         comm.barrier()
@@ -814,9 +816,9 @@ def upstream_inc_workload(args) -> int:
                      "len_ms_mean": float(np.mean(per_ck)) * 1e3,
                      "len_ms_median": float(np.median(per_ck)) * 1e3,
                      "incremental_calls": paths // max(1, args.steps)}
-    ctx.set_param("inc_coop", 1)
+    ctx.set_param("inc_coop", 0)
     inc, full = res["incremental"], res["full"]
-    ok = inc["ok"] and full["ok"] and res["incremental_3_launches"]["ok"]
+    ok = inc["ok"] and full["ok"] and res["incremental_coop"]["ok"]
     if rank == 0:
         out = {
             "metric": METRIC, "value": len(patches) / (inc["ms_per_step"] / 1e3),
@@ -827,7 +829,7 @@ def upstream_inc_workload(args) -> int:
                                    "apply the chunk's updates to a device replica + len()",
                        "trace": name, "patches": len(patches), "checkpoints": len(chunks),
                        "updates_resident": True},
-            "incremental": inc, "incremental_3_launches": res["incremental_3_launches"],
+            "incremental": inc, "incremental_coop": res["incremental_coop"],
             "full": full,
             "len_speedup_mean": full["len_ms_mean"] / inc["len_ms_mean"],
             "len_speedup_median": full["len_ms_median"] / inc["len_ms_median"],
@@ -879,6 +881,9 @@ def parse_args(argv=None):
     ap.add_argument("--stile-text", type=int, default=1, choices=[0, 1],
                     help="1: fused level 1 stages text from the tile segments (k_runs skips the "
                          "slot-order copy)")
+    ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1],
+                    help="1: resident batches carry the compact list of the non-seq items' parents "
+                         "(input encoding; k_classify streams it); 0: k_classify gathers them")
     ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
                     help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -213,6 +213,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.stile_text = value == 1;
         return 0;
     }
+    if (k == "nsq_list") {  // 1: batches get the compact nsq parent list (Engine::build_nsq)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0 or 1");
+        ctx->eng.nsq_list = value == 1;
+        return 0;
+    }
     if (k == "inc_coop") {  // 1: incremental merges in one cooperative launch (incr.hip)
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "inc_coop must be 0 or 1");
         ctx->eng.inc_coop = value == 1;

@@ -150,6 +150,10 @@ struct L0Args {
     uint32_t xcd;                 // 1: XCD-aware tile order in k_classify / k_runs (xcd_block)
     uint32_t copy_text;           // k_runs copies the tile text into sbytes (0: k_doctree reads
                                   //   the tile segments itself, L1Plan::stile_text)
+    // resident batches (Engine::build_nsq): the parents of the nsq items in slot order and their
+    // prefix count per 64 slots (offset to the wave's first chunk); null: gather in_parent
+    const uint32_t* nsq_par;
+    const uint32_t* nsq_pre;
 };
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
@@ -194,6 +198,15 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     const uint32_t t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
     const bool live = gs < a.nslots;
     if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
+    // (resident batches) the tile's range of the compact nsq parent list, first: the loads of its
+    // first entries are issued as soon as it arrives, behind the codepoint column, instead of a
+    // gather round trip at the end of the block
+    const bool cl = a.nsq_par != nullptr;
+    uint32_t nlo = 0, nhi = 0;
+    if (cl) {
+        nlo = a.nsq_pre[t0 >> 6];
+        nhi = a.nsq_pre[min(t0 + kScanTile, a.nslots) >> 6];
+    }
     // the codepoint column first (its address does not wait for the document lookup); padding
     // slots hold junk and are masked below
     uint4 cq[3] = {};
@@ -203,6 +216,14 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) cq[q] = cv[q];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+    }
+    uint32_t ppre[4] = {0u, 0u, 0u, 0u};  // list entries threadIdx.x + j kBlock of the tile
+    if (cl) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t q = nlo + threadIdx.x + (uint32_t)j * kBlock;
+            ppre[j] = q < nhi ? a.nsq_par[q] : 0u;
+        }
     }
     const uint32_t n = doc.y, l0 = gs - doc.x;
     ldoc[threadIdx.x] = doc;
@@ -275,6 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         const uint4* src = reinterpret_cast<const uint4*>(sb);
         for (uint32_t i = threadIdx.x; i < (tw + 15u) / 16u; i += kBlock) dst[i] = src[i];
     }
+    if (cl && T != nhi - nlo && threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 1u);  // list != flags
     if (T == 0) {  // (block-uniform) no nsq item: no jump bit from this tile
         if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = 0u;
         return;
@@ -297,12 +319,19 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
             o[j] = q < T ? lst[q] : 0xFFFFu;
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] = o[j] != 0xFFFFu ? a.in_parent[t0 + (o[j] & 0x7FFFu)] : 0u;
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t q = t + (uint32_t)j * kBlock;
+            p[j] = o[j] == 0xFFFFu             ? 0u
+                   : !cl                       ? a.in_parent[t0 + (o[j] & 0x7FFFu)]
+                   : t == threadIdx.x          ? ppre[j]
+                   : nlo + q < nhi             ? a.nsq_par[nlo + q]
+                                               : 0u;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (o[j] == 0xFFFFu) continue;
             const uint32_t oi = o[j] & 0x7FFFu;
-            pl[t + (uint32_t)j * kBlock] = p[j];
+            if (!cl) pl[t + (uint32_t)j * kBlock] = p[j];
             const uint2 d = ldoc[oi / kScanItems];
             const bool left = (o[j] >> 15) != 0u;
             if (p[j] > d.y || p[j] == t0 + oi - d.x || (left && p[j] == 0u)) {
@@ -516,6 +545,10 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     uint64_t nib = 0;
     uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
+    // the parents of the tile's nsq items: the compact list of a resident batch, else the tile's
+    // plist segment k_classify wrote
+    const uint32_t* pls = a.nsq_par ? a.nsq_par + a.nsq_pre[tile * (kScanTile / 64)]
+                                    : a.plist + (uint64_t)tile * kScanTile;
     if (gs < a.nslots) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
@@ -637,7 +670,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         // a non-seq head's parent from the tile's list: its index = the non-seq items before it
         const uint32_t nw = lnsq[li >> 4];
         uint32_t p = (!sq && !root)
-                         ? a.plist[tbase + lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u))]
+                         ? pls[lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u))]
                          : 0u;
         a.r_head[rho] = g;
         a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
@@ -2395,6 +2428,44 @@ __device__ __forceinline__ Perm replica_perm(uint32_t kind, uint32_t n, uint64_t
 // Every replica of a batch in one launch: blockIdx.y strides over the replica documents,
 // blockIdx.x x 256 threads over a document's items.  Replica r is a relabelled copy of base
 // r % nb: item k goes to slot perm(k) and its parent is relabelled the same way.
+// ---- the compact nsq parent list of a resident batch (Engine::build_nsq) ---------------------------
+// One thread per 64-slot chunk of a wave: the chunk's nsq items (items without the previous-slot
+// flag), the same classification as k_classify's.
+__device__ __forceinline__ uint64_t chunk_nsq_bits(const L0Args& a, uint32_t gs) {
+    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+    const uint32_t l0 = gs - doc.x, n = doc.y;
+    const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 192 B, 16-aligned
+    uint64_t bits = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const uint4 q0 = cv[3 * g], q1 = cv[3 * g + 1], q2 = cv[3 * g + 2];
+        const uint32_t CW[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                 q2.x, q2.y, q2.z, q2.w, 0u};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
+            const uint32_t lo = CW[wd] >> sh, hi = sh > 8 ? CW[wd + 1] << (32 - sh) : 0u;
+            const uint32_t c = (lo | hi) & 0x00FFFFFFu;
+            const uint32_t slot = 16u * (uint32_t)g + (uint32_t)k;
+            const bool it = (l0 + slot - 1u) < n;
+            bits |= (uint64_t)(it && !(c & kSeqBit) ? 1u : 0u) << slot;
+        }
+    }
+    return bits;
+}
+__global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c * 64ull >= a.nslots) return;
+    cnt[c] = (uint32_t)__popcll(chunk_nsq_bits(a, c * 64u));
+}
+__global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t* pre, uint32_t* out) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c * 64ull >= a.nslots) return;
+    uint32_t o = pre[c];
+    for (uint64_t b = chunk_nsq_bits(a, c * 64u); b; b &= b - 1ull)
+        out[o++] = a.in_parent[c * 64u + (uint32_t)__builtin_ctzll(b)];
+}
+
 __global__ __launch_bounds__(kBlock) void k_replicate(
     const uint32_t* __restrict__ bp, const uint64_t* __restrict__ bk,
     const uint8_t* __restrict__ bc,
@@ -2462,6 +2533,8 @@ inline uint32_t ceil_log2(uint64_t x) {
 // =============================================================================================
 void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
+    dfree(nsq_par); dfree(nsq_pre);
+    nsq_items = 0;
     dfree(docs_rel); dfree(doc_rank); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
@@ -2532,6 +2605,13 @@ std::string Engine::init(int dev) {
 
 int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
+    // (a new slot layout: the compact nsq list, if any, no longer matches it)
+    if (L.nsq_par || L.nsq_pre) {
+        (void)hipStreamSynchronize(stream);
+        dfree(L.nsq_par);
+        dfree(L.nsq_pre);
+        L.nsq_items = 0;
+    }
     L.log2m = kDocAlignLog2;
     L.docs = docs;
     L.doc_slot.resize(docs.size());
@@ -2931,6 +3011,8 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.cap_rmax = 0xFFFFFFFFu;                                      \
     a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull);  \
     a0.xcd = xcd_order ? 1u : 0u;                                  \
+    a0.nsq_par = L.nsq_par;                                         \
+    a0.nsq_pre = L.nsq_pre ? L.nsq_pre + (w.slot0 >> 6) : nullptr;  \
     a0.copy_text = 1u
 
 // Tree / digest argument block (run counts come from ctl where the kernels need them).
@@ -3125,7 +3207,6 @@ int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, Stag
     return CRDT_HIP_OK;
 }
 #undef MARK
-#undef L0ARGS
 #undef TREEARGS
 
 int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t rounds,
@@ -3627,7 +3708,7 @@ int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t
         R.parent, R.key, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
     HIPCHK(hipGetLastError(), "synth launch");
     HIPCHK(hipStreamSynchronize(stream), "synth");
-    return CRDT_HIP_OK;
+    return build_nsq(R);
 }
 
 int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,
@@ -3670,7 +3751,50 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     dfree(dbn);
     dfree(drslot);
     if (e != hipSuccess) return fail("replicate", e);
+    return build_nsq(R);
+}
+
+// The compact nsq parent list of resident logs (input encoding, once per batch): count the nsq
+// items per 64-slot chunk, scan, scatter their parents in slot order.  k_classify then streams
+// each tile's range of it (4 bytes per nsq item) instead of gathering the parent column (a 64-byte
+// sector per nsq item), and k_runs reads the parents of its nsq heads there.
+int Engine::build_nsq(DeviceLogs& L) {
+    HIPCHK(hipStreamSynchronize(stream), "nsq list");
+    dfree(L.nsq_par);
+    dfree(L.nsq_pre);
+    L.nsq_items = 0;
+    if (!L.total_slots || !nsq_list) return CRDT_HIP_OK;
+    const bool ord = false;  // (L0ARGS)
+    const uint64_t nch = L.total_slots / 64 + 64;  // (a last tile's range ends within)
+    if (nch >= (1ull << 32)) return CRDT_HIP_OK;
+    HIPCHK(dalloc(&L.nsq_pre, nch + 1), "hipMalloc nsq prefix");
+    HIPCHK(hipMemsetAsync(L.nsq_pre, 0, (nch + 1) * 4, stream), "nsq prefix");
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_nsq_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6));
+    }
+    const uint32_t n = (uint32_t)nch, nb = (n + kScanTile - 1) / kScanTile;
+    uint32_t* sums = nullptr;
+    HIPCHK(dalloc(&sums, nb), "hipMalloc nsq scan");
+    k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, sums);
+    k_scan_top<<<1, 1024, 0, stream>>>(sums, nb, L.nsq_pre, n);
+    k_scan_apply<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, sums, L.nsq_pre);
+    uint32_t total = 0;
+    hipError_t e = hipMemcpyAsync(&total, L.nsq_pre + n, 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    dfree(sums);
+    if (e != hipSuccess) return fail("nsq scan", e);
+    HIPCHK(dalloc(&L.nsq_par, (uint64_t)total + 1), "hipMalloc nsq list");
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_nsq_scatter<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(
+            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par);
+    }
+    HIPCHK(hipGetLastError(), "nsq list launch");
+    HIPCHK(hipStreamSynchronize(stream), "nsq list");
+    L.nsq_items = total;
     return CRDT_HIP_OK;
 }
+#undef L0ARGS
 
 }  // namespace crdt

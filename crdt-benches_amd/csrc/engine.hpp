@@ -104,6 +104,13 @@ struct DeviceLogs {
     uint32_t* chunk_doc = nullptr; // per M-chunk of the whole slot space: wave-local doc index
     uint64_t cap_docs = 0, cap_chunks = 0;
     std::vector<uint64_t> tab_sig;  // the plan docs_rel / chunk_doc were last built for
+    // Resident batches (Engine::build_nsq, part of the input encoding): the parents of the items
+    // without the previous-slot flag, in slot order, and their prefix count per 64 slots
+    // (nsq_pre[c] = such items in slots < 64 c).  k_classify streams a tile's range of it instead
+    // of gathering the parent column.  Null for logs that change (uploads, replicas).
+    uint32_t* nsq_par = nullptr;
+    uint32_t* nsq_pre = nullptr;
+    uint64_t nsq_items = 0;
 
     void release();
     ~DeviceLogs() { release(); }
@@ -143,8 +150,12 @@ public:
     bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS
     bool fuse_text = true;         // k_doctree writes the text when it fits LDS (else k_expand)
     // incremental merges (incr.hip): the three phases in one cooperative launch with grid-wide
-    // barriers (else three launches)
-    bool inc_coop = true;
+    // barriers, else three launches (the default: 44 vs 56 us per len() on automerge-paper, the
+    // grid barriers cost more than the launches)
+    bool inc_coop = false;
+    // resident batches get the compact list of the non-seq items' parents (build_nsq); 0: the
+    // level-0 kernels gather the parent column instead (A/B)
+    bool nsq_list = true;
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -195,6 +206,9 @@ public:
     // One config-5 document generated on the device (synth.cpp synth_tree_item, item by item).
     int synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t del_pct,
                    uint64_t seed);
+
+    // The compact nsq parent list of L (after its last plan; see DeviceLogs::nsq_par).
+    int build_nsq(DeviceLogs& L);
 
     // Materialise `replicas` relabelled copies of `bases` (already uploaded in B) into R.
     int replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,

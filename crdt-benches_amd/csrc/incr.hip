@@ -26,6 +26,9 @@
 #include <hip/hip_cooperative_groups.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "engine.hpp"
@@ -40,6 +43,7 @@ constexpr uint32_t kIncThreads = 1024;
 constexpr uint32_t kSpliceRanks = 4;                                // old ranks per thread
 constexpr uint32_t kSpliceTile = kIncThreads * kSpliceRanks;        // old ranks per tile
 constexpr uint32_t kIncGroupMax = 1024;  // largest sibling group ranked in k_inc_forest
+constexpr uint32_t kIncThinGroup = 32;   // more roots than this: ranked one wave per root
 constexpr uint32_t kCpMaskI = 0x001FFFFFu;
 constexpr uint32_t kDelBitI = 0x00800000u;
 
@@ -64,8 +68,13 @@ struct IncArgs {
     uint64_t text_cap;
     uint64_t* ctl;
     uint64_t* hres;             // host-mapped result {flag, bytes, codepoints, call number}
+    uint64_t* tsp;              // (CRDT_INC_PROFILE) phase timestamps of the forest, or null
     uint64_t call;              // this call's number (a stale result block is detected)
 };
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32i_t;
+__device__ __forceinline__ uint32_t lds_ld(uint32_t* p) { return *(volatile lds_u32i_t*)p; }
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) { *(volatile lds_u32i_t*)p = v; }
 
 __device__ __forceinline__ uint32_t cp_word(const uint8_t* cp, uint32_t s) {
     return (uint32_t)cp[3ull * s] | ((uint32_t)cp[3ull * s + 1] << 8) |
@@ -99,9 +108,12 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
            + 8u * mmax               // keys (u64), later the output pairs
            + 4u * mmax               // A: anchor rank of a root (u32)
            + 4u * (2u * mmax + 4u)   // tour successor (u16) and suffix sum (u16), packed u32
+           + 2u * mmax               // vrk: ranks among many roots (u16)
            + 64u;
 }
 
+#define INC_TS(i) \
+    if (a.tsp && threadIdx.x == 0) a.tsp[i] = wall_clock64()
 __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint32_t* red,
                                            uint32_t& flag) {
     constexpr uint32_t Q = kIncMax / kIncThreads;  // items per thread
@@ -112,7 +124,9 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     uint32_t* tour = start + (kIncMax + 2u);                // 2 kIncMax + 4: succ | sum << 16
     uint16_t* lp = reinterpret_cast<uint16_t*>(tour + (2u * kIncMax + 4u));  // kIncMax + 2
     uint16_t* ch = lp + (kIncMax + 2u);                     // kIncMax + 2
+    uint16_t* vrk = ch + (kIncMax + 2u);                    // kIncMax: ranks among the roots
     if (t == 0) flag = 0;
+    INC_TS(0);
     const uint64_t maxkey0 = a.ctl[I_MAXKEY];
     // ---- load: parents, keys, anchors; counts cleared ----
     uint32_t plc[Q];
@@ -147,6 +161,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         }
         if (bad) atomicOr(&flag, bad);
     }
+    INC_TS(1);
     __syncthreads();
     // ---- child counts; each child keeps its place among its parent's children ----
 #pragma unroll
@@ -154,6 +169,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         const uint32_t i = t + (uint32_t)q * kIncThreads;
         plc[q] = i < m ? atomicAdd(&start[lp[i]], 1u) : 0u;
     }
+    INC_TS(2);
     __syncthreads();
     // ---- segment starts: exclusive scan over nodes 0..m (m + 1 <= kIncMax + 1 counts) ----
     {
@@ -170,21 +186,49 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         }
         if (t == 0) start[m + 1u] = tot;  // (= m)
     }
+    INC_TS(3);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t i = t + (uint32_t)q * kIncThreads;
         if (i < m) ch[start[lp[i]] + plc[q]] = (uint16_t)i;
     }
+    INC_TS(4);
     __syncthreads();
     // ---- rank among siblings: roots by (anchor asc, key desc), other groups by key desc (the
     // anchors of non-roots are all 0); ties by the greater index, as the full merge does ----
     uint32_t rk[Q];
+    // the roots (children of V) when there are many of them: one wave per root, its lanes over
+    // the other roots (a thread walking all of them alone is an r-long chain of LDS reads)
+    const uint32_t v0 = start[m], nv = start[m + 1u] - v0;
+    const bool wide_v = nv > kIncThinGroup;
+    if (wide_v) {
+        const uint32_t lane = t & 63u;
+        for (uint32_t idx = t >> 6; idx < nv; idx += kIncThreads / 64) {
+            const uint32_t i = ch[v0 + idx];
+            const uint32_t ai = A[i];
+            const uint64_t ki = keys[i];
+            uint32_t r = 0;
+            for (uint32_t s = lane; s < nv; s += 64) {
+                const uint32_t j = ch[v0 + s];
+                const uint32_t aj = A[j];
+                const uint64_t kj = keys[j];
+                r += (aj < ai || (aj == ai && (kj > ki || (kj == ki && j > i)))) ? 1u : 0u;
+            }
+            r = wave_sum(r);
+            if (lane == 0) vrk[i] = (uint16_t)r;
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t i = t + (uint32_t)q * kIncThreads;
         rk[q] = 0;
         if (i >= m) continue;
+        if (wide_v && lp[i] == m) {
+            rk[q] = vrk[i];
+            continue;
+        }
         const uint32_t g0 = start[lp[i]], g1 = start[lp[i] + 1u];
         if (g1 - g0 > kIncGroupMax) {
             atomicOr(&flag, (uint32_t)F_GROUP);
@@ -201,12 +245,14 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         }
         rk[q] = r;
     }
+    INC_TS(5);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t i = t + (uint32_t)q * kIncThreads;
         if (i < m) ch[start[lp[i]] + rk[q]] = (uint16_t)i;
     }
+    INC_TS(6);
     __syncthreads();
     if (flag) {  // (block-uniform after the barrier)
         if (t == 0) a.ctl[I_FLAG] = flag;
@@ -233,34 +279,40 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         tour[2u * V + 1u] = E;
         tour[E] = E;
     }
+    INC_TS(7);
     __syncthreads();
-    // ---- pointer jumping: (succ, sum to the end) until every successor is the end ----
+    // ---- pointer jumping without barriers: a record (succ | weight of [arc, succ) << 16) is a
+    // valid stretch of the tour at all times, so joining it with an old or a new record of its
+    // successor is equally right; each thread jumps its own arcs until they reach the end (every
+    // pass at least doubles... or extends a record by one arc: E passes bound it) ----
     {
-        uint32_t rounds = 0;
-        for (uint32_t len = 1; len < E + 1u; len <<= 1) ++rounds;
-        for (uint32_t r = 0; r < rounds; ++r) {
-            uint32_t nv[(2u * kIncMax + 4u + kIncThreads - 1u) / kIncThreads];
-            constexpr int NA = (int)((2u * kIncMax + 4u + kIncThreads - 1u) / kIncThreads);
+        constexpr int NA = (int)((2u * kIncMax + 4u + kIncThreads - 1u) / kIncThreads);
+        uint32_t live = 0;
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            const uint32_t arc = t + (uint32_t)q * kIncThreads;
+            live |= (arc < E ? 1u : 0u) << q;
+        }
+        for (uint32_t pass = 0; live && pass <= E; ++pass) {
 #pragma unroll
             for (int q = 0; q < NA; ++q) {
+                if (!((live >> q) & 1u)) continue;
                 const uint32_t arc = t + (uint32_t)q * kIncThreads;
-                nv[q] = 0;
-                if (arc > E) continue;
-                const uint32_t x = tour[arc];
+                const uint32_t x = lds_ld(tour + arc);
                 const uint32_t s = x & 0xFFFFu;
-                const uint32_t y = tour[s];
-                // sums: the arc's own plus the successor's (the end contributes nothing)
-                nv[q] = (s == E) ? x : ((y & 0xFFFFu) | (((x >> 16) + (y >> 16)) << 16));
+                if (s == E) {
+                    live &= ~(1u << q);
+                    continue;
+                }
+                const uint32_t y = lds_ld(tour + s);
+                const uint32_t nx = (y & 0xFFFFu) | (((x >> 16) + (y >> 16)) << 16);
+                lds_st(tour + arc, nx);
+                if ((y & 0xFFFFu) == E) live &= ~(1u << q);
             }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < NA; ++q) {
-                const uint32_t arc = t + (uint32_t)q * kIncThreads;
-                if (arc <= E) tour[arc] = nv[q];
-            }
-            __syncthreads();
         }
     }
+    INC_TS(8);
+    __syncthreads();
     // ---- every item's place among the new items; its root's anchor by a max-scan ----
     uint32_t* os = reinterpret_cast<uint32_t*>(keys);  // (keys are dead) slot by place
     uint32_t* oa = os + kIncMax;                       // a root's anchor by place, else 0
@@ -308,6 +360,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     }
     // the largest key now held (the next merge's check)
     __syncthreads();  // (red is reused)
+    INC_TS(9);
     {
         const uint32_t hi32 = block_max_u32((uint32_t)(kmax >> 32), red);
         const uint32_t lo32 = block_max_u32((uint32_t)(kmax >> 32) == hi32 ? (uint32_t)kmax : 0u, red);
@@ -316,7 +369,9 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             if (km > maxkey0) a.ctl[I_MAXKEY] = km;
         }
     }
+    INC_TS(10);
 }
+#undef INC_TS
 
 // Number of new items anchored before old rank k (ins_a is non-decreasing).
 __device__ __forceinline__ uint32_t anchored_before(const uint32_t* ins_a, uint32_t m, uint32_t k) {
@@ -336,22 +391,28 @@ __device__ __forceinline__ uint64_t ld_flag(const uint64_t* p) {
 // ---- splice: the new order of one tile; rank rewritten; the tile's text sums -------------------
 // Tile b takes old ranks [k0, k1) and the new items anchored in [k0, k1): its outputs are the
 // places [k0 + c(k0), k1 + c(k1)), c(k) = new items anchored before k.
+// la: the anchors (ins_a) copied to LDS by inc_load_anchors (searched there, not in HBM: ins_a
+// was written by one workgroup, and a dependent chain of loads from another XCD's L2 is slow).
+__device__ __forceinline__ void inc_load_anchors(const IncArgs& a, uint32_t* la) {
+    for (uint32_t j = threadIdx.x; j < a.m; j += kIncThreads) la[j] = a.ins_a[j];
+    __syncthreads();
+}
 __device__ __forceinline__ void inc_splice_tile(const IncArgs& a, uint32_t b, uint32_t* red,
-                                                uint32_t* cb) {
+                                                uint32_t* cb, const uint32_t* la) {
     const uint32_t N0 = a.n0 + 1u, m = a.m;
     const uint32_t k0 = b * kSpliceTile, k1 = min(N0, k0 + kSpliceTile);
-    if (threadIdx.x < 2u) cb[threadIdx.x] = m ? anchored_before(a.ins_a, m, threadIdx.x ? k1 : k0) : 0u;
+    if (threadIdx.x < 2u) cb[threadIdx.x] = m ? anchored_before(la, m, threadIdx.x ? k1 : k0) : 0u;
     const uint32_t kb = k0 + threadIdx.x * kSpliceRanks;
     uint32_t sl[kSpliceRanks];
 #pragma unroll
     for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = kb + q < k1 ? a.seq[kb + q] : 0u;
-    uint32_t c = (m && kb < k1) ? anchored_before(a.ins_a, m, kb) : 0u;
     uint32_t bytes = 0, cps = 0;
 #pragma unroll
     for (int q = 0; q < (int)kSpliceRanks; ++q) {
         const uint32_t k = kb + q;
         if (k >= k1) break;
-        while (c < m && a.ins_a[c] < k) ++c;
+        // (a search per rank: a whole subtree of new items shares one anchor)
+        const uint32_t c = m ? anchored_before(la, m, k) : 0u;
         const uint32_t np = k + c;
         a.seq2[np] = sl[q];
         a.rank[sl[q]] = np;
@@ -362,7 +423,7 @@ __device__ __forceinline__ void inc_splice_tile(const IncArgs& a, uint32_t b, ui
     __syncthreads();
     const uint32_t c0 = cb[0], c1 = cb[1];
     for (uint32_t j = c0 + threadIdx.x; j < c1; j += kIncThreads) {
-        const uint32_t s = a.ins_s[j], np = a.ins_a[j] + 1u + j;
+        const uint32_t s = a.ins_s[j], np = la[j] + 1u + j;
         a.seq2[np] = s;
         a.rank[s] = np;
         const uint32_t w = slot_bytes(a.cp, s);
@@ -377,22 +438,31 @@ __device__ __forceinline__ void inc_splice_tile(const IncArgs& a, uint32_t b, ui
 
 // ---- text: the UTF-8 of one tile's outputs, at the bytes of the tiles before it ----------------
 __device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint32_t b, uint32_t* red) {
+    // the tile's range and the bytes of the tiles before it, and the first chunk's items and
+    // codepoint words, all loaded before the first wait
+    const uint4 me = a.bsum[b];
     uint32_t p = 0;
     for (uint32_t i = threadIdx.x; i < b; i += kIncThreads) p += a.bsum[i].x;
+    uint32_t cw[kSpliceRanks];
+    auto load = [&](uint32_t o0) {
+        const uint32_t ob = o0 + threadIdx.x * kSpliceRanks;
+        uint32_t sl[kSpliceRanks];
+#pragma unroll
+        for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = ob + q < me.w ? a.seq2[ob + q] : 0u;
+#pragma unroll
+        for (int q = 0; q < (int)kSpliceRanks; ++q) cw[q] = sl[q] ? cp_word(a.cp, sl[q]) : kDelBitI;
+    };
+    load(me.z);
     uint32_t ptot;
     (void)block_excl_scan<kIncThreads / 64>(p, red, ptot);
-    const uint4 me = a.bsum[b];
     uint64_t base = ptot;
     if (base + me.x > a.text_cap) return;  // (flagged from the totals)
     for (uint32_t o0 = me.z; o0 < me.w; o0 += kSpliceTile) {
-        const uint32_t ob = o0 + threadIdx.x * kSpliceRanks;
-        uint32_t cw[kSpliceRanks], L[kSpliceRanks];
+        if (o0 != me.z) load(o0);
+        uint32_t L[kSpliceRanks];
         uint32_t tot = 0;
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) {
-            const uint32_t o = ob + q;
-            const uint32_t s = o < me.w ? a.seq2[o] : 0u;
-            cw[q] = s ? cp_word(a.cp, s) : kDelBitI;
             L[q] = (cw[q] & kDelBitI) ? 0u : utf8_len(cw[q] & kCpMaskI);
             tot += L[q];
         }
@@ -450,8 +520,10 @@ __global__ __launch_bounds__(kIncThreads) void k_inc_forest(IncArgs a) {
 __global__ __launch_bounds__(kIncThreads) void k_inc_splice(IncArgs a) {
     __shared__ uint32_t red[kIncThreads / 64];
     __shared__ uint32_t cb[2];
+    __shared__ uint32_t la[kIncMax];
     if (ld_flag(&a.ctl[I_FLAG])) return;
-    inc_splice_tile(a, blockIdx.x, red, cb);
+    inc_load_anchors(a, la);
+    inc_splice_tile(a, blockIdx.x, red, cb, la);
 }
 __global__ __launch_bounds__(kIncThreads) void k_inc_text(IncArgs a) {
     __shared__ uint32_t red[kIncThreads / 64];
@@ -477,11 +549,14 @@ __global__ __launch_bounds__(kIncThreads) void k_inc_all(IncArgs a) {
     }
     grid.sync();
     const bool go = ld_flag(&a.ctl[I_FLAG]) == 0;
-    if (go)
+    if (go && blockIdx.x < a.nblk) {
+        uint32_t* la = reinterpret_cast<uint32_t*>(lds);
+        inc_load_anchors(a, la);
         for (uint32_t b = blockIdx.x; b < a.nblk; b += gridDim.x) {
-            inc_splice_tile(a, b, red, cb);
+            inc_splice_tile(a, b, red, cb, la);
             __syncthreads();
         }
+    }
     grid.sync();
     if (go)
         for (uint32_t b = blockIdx.x; b < a.nblk; b += gridDim.x) {
@@ -630,25 +705,67 @@ IncArgs make_args(Replica& r, IncState& s, uint32_t n0, uint32_t m) {
     return a;
 }
 
+// CRDT_INC_PROFILE=1: per call, device times of the phases (events) and host times, to stderr
+bool inc_profile() {
+    static const bool on = [] {
+        const char* e = std::getenv("CRDT_INC_PROFILE");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 // The three phases (one cooperative launch, or three launches), then a wait for the result.
 int inc_run(Engine& E, IncState& s, IncArgs& a) {
     hipStream_t st = E.stream;
     const IncLaunch& li = inc_launch_info(E.device);
     ICHK(li.err, "incremental merge setup");
     const uint32_t lds = inc_forest_lds(kIncMax);
+    const bool prof = inc_profile();
+    static hipEvent_t ev[4] = {};
+    static uint64_t* tsp = nullptr;
+    if (prof && !ev[0]) {
+        for (auto& e : ev) ICHK(hipEventCreate(&e), "event");
+        ICHK(dalloc(&tsp, 16), "timestamps");
+    }
+    a.tsp = prof ? tsp : nullptr;
+    const auto h0 = std::chrono::steady_clock::now();
+    if (prof) ICHK(hipEventRecord(ev[0], st), "event");
     if (E.inc_coop && li.coop_grid) {
         const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(li.coop_grid, a.nblk));
         void* args[] = {&a};
         ICHK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_inc_all), dim3(grid),
                                         dim3(kIncThreads), args, lds, st),
              "k_inc_all launch");
+        if (prof)
+            for (int k = 1; k < 4; ++k) ICHK(hipEventRecord(ev[k], st), "event");
     } else {
         k_inc_forest<<<1, kIncThreads, a.m ? lds : 0, st>>>(a);
+        if (prof) ICHK(hipEventRecord(ev[1], st), "event");
         k_inc_splice<<<a.nblk, kIncThreads, 0, st>>>(a);
+        if (prof) ICHK(hipEventRecord(ev[2], st), "event");
         k_inc_text<<<a.nblk + 1u, kIncThreads, 0, st>>>(a);
+        if (prof) ICHK(hipEventRecord(ev[3], st), "event");
         ICHK(hipGetLastError(), "incremental merge launch");
     }
+    const auto h1 = std::chrono::steady_clock::now();
     ICHK(hipStreamSynchronize(st), "incremental merge sync");
+    if (prof && a.tsp && a.m) {
+        uint64_t ts[11] = {};
+        ICHK(hipMemcpy(ts, a.tsp, sizeof(ts), hipMemcpyDeviceToHost), "timestamps");
+        std::fprintf(stderr, "[inc-forest] us:");
+        for (int k = 1; k < 11; ++k) std::fprintf(stderr, " %.1f", (ts[k] - ts[k - 1]) / 100.0);
+        std::fprintf(stderr, " | total %.1f\n", (ts[10] - ts[0]) / 100.0);
+    }
+    if (prof) {
+        const auto h2 = std::chrono::steady_clock::now();
+        float t[3] = {};
+        for (int k = 0; k < 3; ++k) (void)hipEventElapsedTime(&t[k], ev[k], ev[k + 1]);
+        std::fprintf(stderr, "[inc] m %u n0 %u coop %d | device forest %.1f splice %.1f text %.1f us"
+                     " | host enqueue %.1f wait %.1f us\n", a.m, a.n0, (int)(E.inc_coop && li.coop_grid),
+                     1e3 * t[0], 1e3 * t[1], 1e3 * t[2],
+                     std::chrono::duration<double, std::micro>(h1 - h0).count(),
+                     std::chrono::duration<double, std::micro>(h2 - h1).count());
+    }
     if (s.hres[3] != a.call) {
         E.err = "incremental merge: no result from the device";
         return CRDT_HIP_EDEVICE;

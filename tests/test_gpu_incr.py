@@ -7,6 +7,8 @@ and ranks only the items appended since the previous call.  Every checkpoint is 
 the CPU oracle's merge of the same log (oracle/oracle.c orc_merge_rga) and with the replica's own
 counters; the path taken (1 = incremental, 0 = full) is asserted where it is determined.
 """
+import struct
+
 import pytest
 
 import crdt_hip
@@ -41,12 +43,12 @@ def _checkpoints(ctx, oracle, name, K, every_oracle=1):
 
 @pytest.mark.parametrize("coop", [1, 0])
 def test_incremental_len_every_1000_patches_sveltecomponent(ctx, oracle, coop):
-    """coop 1: the three phases in one cooperative launch; 0: three launches."""
+    """coop 1: the three phases in one cooperative launch; 0: three launches (the default)."""
     ctx.set_param("inc_coop", coop)
     try:
         paths = _checkpoints(ctx, oracle, "sveltecomponent", 1000)
     finally:
-        ctx.set_param("inc_coop", 1)
+        ctx.set_param("inc_coop", 0)
     # the first call builds the state; every later one is a local edit batch (keys increase)
     assert paths[0] in (0, "big") and all(p in (1, "big") for p in paths[1:]), paths
     assert paths.count(1) >= len(paths) // 2, paths
@@ -78,34 +80,49 @@ def test_incremental_len_small_and_large_steps(ctx, oracle, K):
         assert text == oracle.merge(to_anchor(host.arrays()))
 
 
+def _with_item_id(u: bytes, k: int, lamport: int, agent: int) -> bytes:
+    """Update u (OpLog.encode_from's wire layout: 24-byte header, then parent, origin-right,
+    lamport and codepoint words, then u16 agents) with item k's (lamport, agent) replaced."""
+    n = struct.unpack_from("<I", u, 12)[0]
+    b = bytearray(u)
+    struct.pack_into("<I", b, 24 + 8 * n + 4 * k, lamport)
+    struct.pack_into("<H", b, 24 + 16 * n + 2 * k, agent)
+    return bytes(b)
+
+
 def test_concurrent_update_falls_back_to_full_merge(ctx, oracle):
-    """Agent 2 edits without having seen agent 1's latest items: its items' keys are below the
-    replica's largest key, so the fast path refuses them and the full merge runs."""
+    """An update whose item sorts below an older sibling (a concurrent insert that lost the
+    race: its key is below the replica's largest key) cannot go the fast way: the full merge runs
+    and puts it after the older sibling's subtree, as the oracle does."""
     a = crdt_hip.OpLog(agent=1)
-    b = crdt_hip.OpLog(agent=2)
-    a.insert(0, "hello")
-    b.apply_update(a.encode_from(0))
+    h = crdt_hip.OpLog(agent=1)  # the host log fed the same (patched) updates
     r = crdt_hip.Replica(ctx)
-    r.apply_updates([a.encode_from(0)])
+
+    def ship(u):
+        r.apply_updates([u])
+        h.apply_update(u)
+
+    a.insert(0, "hello")
+    ship(a.encode_from(0))
     assert r.merge_inc(text=True)[3] == b"hello"
-    va, vb = a.version(), b.version()
-    a.insert(5, " world, again")                 # lamports 6.. (agent 1)
-    r.apply_updates([a.encode_from(va)])
+    v = a.version()
+    a.insert(5, " world")
+    ship(a.encode_from(v))
     cps, nb, path, text = r.merge_inc(text=True)
-    assert path == 1 and text == b"hello world, again"
-    b.insert(0, "X")                             # lamport 6 (agent 2): older than agent 1's 18
-    b.insert(3, "Y")
-    r.apply_updates([b.encode_from(vb)])
-    a.apply_update(b.encode_from(vb))
+    assert path == 1 and text == b"hello world"
+    v = a.version()
+    a.insert(0, "XY")                            # X: a new child of the document start
+    u = _with_item_id(a.encode_from(v), 0, 1, 0)  # X's key (1, agent 0) < 'h' (1, agent 1)
+    ship(u)
     cps, nb, path, text = r.merge_inc(text=True)
     assert path == 0
-    assert text == oracle.merge(to_anchor(a.arrays()))
+    assert text == oracle.merge(to_anchor(h.arrays())) == b"hello worldXY"
     # the state was rebuilt: a later local edit goes the fast way again
-    va = a.version()
+    v = a.version()
     a.insert(2, "--")
-    r.apply_updates([a.encode_from(va)])
+    ship(a.encode_from(v))
     cps, nb, path, text = r.merge_inc(text=True)
-    assert path == 1 and text == oracle.merge(to_anchor(a.arrays()))
+    assert path == 1 and text == oracle.merge(to_anchor(h.arrays()))
 
 
 def test_deletes_only_and_many_roots(ctx, oracle):
