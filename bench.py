@@ -468,6 +468,8 @@ def traces_workload(args) -> int:
         ctx.set_param("stile_text", args.stile_text)
     if args.nsq_list != 1:  # (likewise)
         ctx.set_param("nsq_list", args.nsq_list)
+    if args.cp2 != 0:  # (likewise)
+        ctx.set_param("cp2", args.cp2)
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
@@ -543,8 +545,10 @@ def traces_workload(args) -> int:
                 "note": "one-time, untimed: upload of the 4 resolved logs and the device build of "
                         "every replica's resident op log (relabelled parent u32, key u64 = lamport "
                         "<< 16 | agent, 3-byte codepoint word with the tombstone and previous-slot "
-                        "flags: O(1) per item); the traffic contract (DESIGN.md section 7) prices "
-                        "the merge over this format"},
+                        "flags: O(1) per item) and of the compact list of the parents of the items "
+                        "without the previous-slot flag (u32 each, slot order, a prefix count per "
+                        "64 slots; Engine::build_nsq); the traffic contract (DESIGN.md section 7) "
+                        "prices the merge over this format"},
             "resolve": {"ms_per_trace": dict(zip(TRACES, inputs["resolve_ms"])),
                         "ms_total_one_core": sum(inputs["resolve_ms"]),
                         "ms_all_parallel": inputs["resolve_parallel_ms"],
@@ -798,8 +802,7 @@ def upstream_inc_workload(args) -> int:
         return ok, paths
 
     res = {}
-    for mode in ("incremental", "incremental_coop", "full"):
-        ctx.set_param("inc_coop", 1 if mode == "incremental_coop" else 0)
+    for mode in ("incremental", "full"):
         for _ in range(args.warmup):
             loop(mode != "full", [])
         comm.barrier()
@@ -816,9 +819,8 @@ def upstream_inc_workload(args) -> int:
                      "len_ms_mean": float(np.mean(per_ck)) * 1e3,
                      "len_ms_median": float(np.median(per_ck)) * 1e3,
                      "incremental_calls": paths // max(1, args.steps)}
-    ctx.set_param("inc_coop", 0)
     inc, full = res["incremental"], res["full"]
-    ok = inc["ok"] and full["ok"] and res["incremental_coop"]["ok"]
+    ok = inc["ok"] and full["ok"]
     if rank == 0:
         out = {
             "metric": METRIC, "value": len(patches) / (inc["ms_per_step"] / 1e3),
@@ -829,8 +831,7 @@ def upstream_inc_workload(args) -> int:
                                    "apply the chunk's updates to a device replica + len()",
                        "trace": name, "patches": len(patches), "checkpoints": len(chunks),
                        "updates_resident": True},
-            "incremental": inc, "incremental_coop": res["incremental_coop"],
-            "full": full,
+            "incremental": inc, "full": full,
             "len_speedup_mean": full["len_ms_mean"] / inc["len_ms_mean"],
             "len_speedup_median": full["len_ms_median"] / inc["len_ms_median"],
             "lens_ok": bool(ok),
@@ -881,6 +882,10 @@ def parse_args(argv=None):
     ap.add_argument("--stile-text", type=int, default=1, choices=[0, 1],
                     help="1: fused level 1 stages text from the tile segments (k_runs skips the "
                          "slot-order copy)")
+    ap.add_argument("--cp2", type=int, default=0, choices=[0, 1],
+                    help="1: resident batches carry the 2-byte character column (input encoding; "
+                         "escaped codepoints in a side table); 0: the 3-byte column (default: "
+                         "faster, DESIGN.md section 4)")
     ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1],
                     help="1: resident batches carry the compact list of the non-seq items' parents "
                          "(input encoding; k_classify streams it); 0: k_classify gathers them")

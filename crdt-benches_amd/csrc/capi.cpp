@@ -213,14 +213,14 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.stile_text = value == 1;
         return 0;
     }
+    if (k == "cp2") {  // 1: batches get the 2-byte character column (Engine::build_cp2)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "cp2 must be 0 or 1");
+        ctx->eng.cp2_column = value == 1;
+        return 0;
+    }
     if (k == "nsq_list") {  // 1: batches get the compact nsq parent list (Engine::build_nsq)
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0 or 1");
         ctx->eng.nsq_list = value == 1;
-        return 0;
-    }
-    if (k == "inc_coop") {  // 1: incremental merges in one cooperative launch (incr.hip)
-        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "inc_coop must be 0 or 1");
-        ctx->eng.inc_coop = value == 1;
         return 0;
     }
     if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)

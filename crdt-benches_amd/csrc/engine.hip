@@ -154,7 +154,22 @@ struct L0Args {
     // prefix count per 64 slots (offset to the wave's first chunk); null: gather in_parent
     const uint32_t* nsq_par;
     const uint32_t* nsq_pre;
+    // resident batches (Engine::build_cp2): the 2-byte character column (an ASCII character, or
+    // an escape to xcp, and the three flags), the escaped codepoints in slot order with their
+    // prefix count per 64 slots (offset to the wave), and one bit per 16 slots with an escape
+    // (global group index = xgrp_off + wave-relative group).  sparse_nib: the weight nibbles are
+    // written only for 16-slot groups with an escape (k_runs takes the visible bits elsewhere)
+    const uint16_t* in_cp2;
+    const uint32_t* xcp;
+    const uint32_t* xpre;
+    const uint32_t* xgrp;
+    uint64_t xgrp_off;
+    uint32_t sparse_nib;
 };
+// the 2-byte character word: ASCII character (bits 0-6), escape (bit 7: the codepoint is the
+// slot's entry in xcp), left child (13), previous-slot flag (14), tombstone (15)
+constexpr uint32_t kCp2Esc = 0x80u;
+__host__ __device__ constexpr uint32_t cp2_flags_to_word(uint32_t v) { return ((v >> 13) & 7u) << 21; }
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 // Fugue (left children).  A run whose head has left children is numbered as two rows: a content
@@ -188,6 +203,7 @@ constexpr uint32_t kRecTree = 1u << 31;  // k_runs record of a head with two row
 //    head, and k_runs reads its parent there (coalesced) instead of gathering it.
 // The stream part reads 3 bytes per slot and waits for one round trip; the parent part is one
 // more round trip at the end of the block, hidden behind the other blocks' streams.
+template <bool CP2>
 __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint32_t lds[kBlock / 64];
     __shared__ uint32_t jl[kScanTile / 32];
@@ -211,31 +227,63 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     // slots hold junk and are masked below
     uint4 cq[3] = {};
     uint2 doc = make_uint2(0, 0);
+    uint32_t xp = 0;  // (CP2) escapes before the thread's 64-slot chunk
     if (live) {
-        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B, 16-aligned
+        if (CP2) {
+            const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp2 + gs);  // 32 B, 16-aligned
+            cq[0] = cv[0];
+            cq[1] = cv[1];
+#ifndef CRDT_CP2_XPRE_LATE
+            xp = a.xpre[gs >> 6];
+#endif
+        } else {
+            const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B
 #pragma unroll
-        for (int q = 0; q < 3; ++q) cq[q] = cv[q];
+            for (int q = 0; q < 3; ++q) cq[q] = cv[q];
+        }
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
     }
-    uint32_t ppre[4] = {0u, 0u, 0u, 0u};  // list entries threadIdx.x + j kBlock of the tile
-    if (cl) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t q = nlo + threadIdx.x + (uint32_t)j * kBlock;
-            ppre[j] = q < nhi ? a.nsq_par[q] : 0u;
-        }
-    }
+
     const uint32_t n = doc.y, l0 = gs - doc.x;
     ldoc[threadIdx.x] = doc;
-    // the 16 three-byte values from 12 dwords (constant shifts: value k at byte 3k)
-    const uint32_t CW[13] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z,
-                             cq[1].w, cq[2].x, cq[2].y, cq[2].z, cq[2].w, 0u};
     uint32_t C[16];
+    uint32_t escm = 0;  // (CP2) slots whose codepoint is in xcp
+    if (CP2) {
+        // the 16 two-byte words from 8 dwords; flags moved to the three-byte word's positions
+        const uint32_t CW[8] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z, cq[1].w};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
-        const uint32_t lo = CW[wd] >> sh, hi = sh > 8 ? CW[wd + 1] << (32 - sh) : 0u;
-        C[k] = (lo | hi) & 0x00FFFFFFu;
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t v = (CW[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+            C[k] = (v & 0x7Fu) | cp2_flags_to_word(v);
+            escm |= ((v & kCp2Esc) ? 1u : 0u) << k;
+        }
+        // escaped codepoints (not on the traces' hot path: a wave-uniform branch): the entry of
+        // the chunk's first escape, plus the escapes of the chunk's groups before this one (the
+        // chunk's four groups are lanes 4c..4c+3)
+        if (__ballot(escm != 0u)) {
+#ifdef CRDT_CP2_XPRE_LATE
+            if (live) xp = a.xpre[gs >> 6];
+#endif
+            const uint32_t cnt = (uint32_t)__popc(escm), l4 = threadIdx.x & ~3u;
+            const uint32_t e0 = (uint32_t)__shfl((int)cnt, (int)(l4 & 63u));
+            const uint32_t e1 = (uint32_t)__shfl((int)cnt, (int)((l4 + 1u) & 63u));
+            const uint32_t e2 = (uint32_t)__shfl((int)cnt, (int)((l4 + 2u) & 63u));
+            const uint32_t g = threadIdx.x & 3u;
+            uint32_t idx = xp + (g > 0 ? e0 : 0u) + (g > 1 ? e1 : 0u) + (g > 2 ? e2 : 0u);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if ((escm >> k) & 1u) C[k] |= a.xcp[idx++];
+        }
+    } else {
+        // the 16 three-byte values from 12 dwords (constant shifts: value k at byte 3k)
+        const uint32_t CW[13] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z,
+                                 cq[1].w, cq[2].x, cq[2].y, cq[2].z, cq[2].w, 0u};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
+            const uint32_t lo = CW[wd] >> sh, hi = sh > 8 ? CW[wd + 1] << (32 - sh) : 0u;
+            C[k] = (lo | hi) & 0x00FFFFFFu;
+        }
     }
     // branch-free classification of the 16 slots; weights straight into their nibbles
     uint32_t nsq = 0, W = 0, vis = 0, lm = 0;
@@ -253,7 +301,9 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     }
     if (live) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
-        a.wnib[gs >> 4] = nib;
+        // (sparse: only the groups with an escaped codepoint can weigh more than one byte per
+        // visible slot; k_runs reads the nibbles of exactly those, by the same escape bits)
+        if (!CP2 || !a.sparse_nib || escm) a.wnib[gs >> 4] = nib;
         a.visb[gs >> 4] = (uint16_t)vis;
     }
     // one scan for both: nsq items << 16 | weight (a tile holds at most 4096 and 16,384)
@@ -290,6 +340,16 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         }
     }
     __syncthreads();
+    // (compact list) the tile's first list entries, loaded now that the slot words are dead: they
+    // arrive while the text is copied out and the nsq items are listed
+    uint32_t ppre[4] = {0u, 0u, 0u, 0u};  // list entries threadIdx.x + j kBlock of the tile
+    if (cl) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t q = nlo + threadIdx.x + (uint32_t)j * kBlock;
+            ppre[j] = q < nhi ? a.nsq_par[q] : 0u;
+        }
+    }
     if (threadIdx.x == 0) a.tile_hw[tile].y = tw;
     if (a.mode == 0) {
         uint4* dst = reinterpret_cast<uint4*>(a.stile + (uint64_t)tile * kTileBytes);
@@ -553,7 +613,22 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
         if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
-        nib = a.wnib[gs >> 4];
+        if (a.sparse_nib) {
+            // one weight per visible slot unless the group holds an escaped codepoint (then
+            // k_classify wrote its nibbles); the visible bits are loaded with the escape word,
+            // not behind it
+            const uint64_t gb = a.xgrp_off + (gs >> 4);
+            const uint32_t xg = a.xgrp[gb >> 5];
+            const uint32_t v = a.visb[gs >> 4];
+            if ((xg >> (gb & 31u)) & 1u) {
+                nib = a.wnib[gs >> 4];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) nib |= (uint64_t)((v >> j) & 1u) << (4 * j);
+            }
+        } else {
+            nib = a.wnib[gs >> 4];
+        }
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         nsq = a.nsqb[gs >> 4];
         lnsq[threadIdx.x] = (uint16_t)nsq;
@@ -2466,6 +2541,52 @@ __global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t
         out[o++] = a.in_parent[c * 64u + (uint32_t)__builtin_ctzll(b)];
 }
 
+// ---- the 2-byte character column of a resident batch (Engine::build_cp2) ---------------------
+// One thread per 64-slot chunk of a wave.  Escapes: items whose codepoint is not ASCII.
+__global__ __launch_bounds__(kBlock) void k_cp2_count(L0Args a, uint32_t* cnt) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c * 64ull >= a.nslots) return;
+    const uint32_t gs = c * 64u;
+    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+    const uint32_t l0 = gs - doc.x, n = doc.y;
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < 64; ++j) {
+        const bool it = (l0 + j - 1u) < n;
+        k += (it && (cp3_get(a.in_cp, gs + j) & kCpMask) >= 0x80u) ? 1u : 0u;
+    }
+    cnt[c] = k;
+}
+__global__ __launch_bounds__(kBlock) void k_cp2_fill(L0Args a, const uint32_t* pre, uint16_t* cp2,
+                                                     uint32_t* xcp, uint32_t* xgrp) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c * 64ull >= a.nslots) return;
+    const uint32_t gs = c * 64u;
+    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+    const uint32_t l0 = gs - doc.x, n = doc.y;
+    uint32_t o = pre[c], gbits = 0;
+    for (uint32_t j = 0; j < 64; ++j) {
+        const bool it = (l0 + j - 1u) < n;
+        const uint32_t v = cp3_get(a.in_cp, gs + j), cp = v & kCpMask;
+        uint32_t w = 0;
+        if (it) {
+            w = ((v >> 21) & 7u) << 13;
+            if (cp >= 0x80u) {
+                w |= kCp2Esc;
+                xcp[o++] = cp;
+                gbits |= 1u << (j >> 4);
+            } else {
+                w |= cp;
+            }
+        }
+        cp2[gs + j] = (uint16_t)w;
+    }
+    for (uint32_t g = 0; g < 4; ++g)
+        if ((gbits >> g) & 1u) {
+            const uint64_t gi = a.xgrp_off + 4ull * c + g;
+            atomicOr(&xgrp[gi >> 5], 1u << (gi & 31u));
+        }
+}
+
 __global__ __launch_bounds__(kBlock) void k_replicate(
     const uint32_t* __restrict__ bp, const uint64_t* __restrict__ bk,
     const uint8_t* __restrict__ bc,
@@ -2535,6 +2656,8 @@ void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
     dfree(nsq_par); dfree(nsq_pre);
     nsq_items = 0;
+    dfree(cp2); dfree(xcp); dfree(xpre); dfree(xgrp);
+    nesc = 0;
     dfree(docs_rel); dfree(doc_rank); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
@@ -2606,11 +2729,13 @@ std::string Engine::init(int dev) {
 int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
     // (a new slot layout: the compact nsq list, if any, no longer matches it)
-    if (L.nsq_par || L.nsq_pre) {
+    if (L.nsq_par || L.nsq_pre || L.cp2) {
         (void)hipStreamSynchronize(stream);
         dfree(L.nsq_par);
         dfree(L.nsq_pre);
         L.nsq_items = 0;
+        dfree(L.cp2); dfree(L.xcp); dfree(L.xpre); dfree(L.xgrp);
+        L.nesc = 0;
     }
     L.log2m = kDocAlignLog2;
     L.docs = docs;
@@ -3012,6 +3137,12 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull);  \
     a0.xcd = xcd_order ? 1u : 0u;                                  \
     a0.nsq_par = L.nsq_par;                                         \
+    a0.in_cp2 = L.cp2 ? L.cp2 + w.slot0 : nullptr;                  \
+    a0.xcp = L.xcp;                                                 \
+    a0.xpre = L.xpre ? L.xpre + (w.slot0 >> 6) : nullptr;           \
+    a0.xgrp = L.xgrp;                                               \
+    a0.xgrp_off = w.slot0 >> 4;                                     \
+    a0.sparse_nib = (L.cp2 && !ord) ? 1u : 0u;                      \
     a0.nsq_pre = L.nsq_pre ? L.nsq_pre + (w.slot0 >> 6) : nullptr;  \
     a0.copy_text = 1u
 
@@ -3048,7 +3179,10 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text
     const uint32_t nq = (uint32_t)(jbits_words(w.nslots) / 4) * (L.fugue ? 2u : 1u);
     k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
     MARK(-1);
-    k_classify<<<ntiles, kBlock, 0, s>>>(a0);
+    if (a0.in_cp2)
+        k_classify<true><<<ntiles, kBlock, 0, s>>>(a0);
+    else
+        k_classify<false><<<ntiles, kBlock, 0, s>>>(a0);
     MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
@@ -3708,7 +3842,8 @@ int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t
         R.parent, R.key, R.cp, n, R.total_slots, p_chain_pct, del_pct, seed);
     HIPCHK(hipGetLastError(), "synth launch");
     HIPCHK(hipStreamSynchronize(stream), "synth");
-    return build_nsq(R);
+    const int rc2 = build_nsq(R);
+    return rc2 ? rc2 : build_cp2(R);
 }
 
 int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,
@@ -3751,7 +3886,8 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     dfree(dbn);
     dfree(drslot);
     if (e != hipSuccess) return fail("replicate", e);
-    return build_nsq(R);
+    const int rc2 = build_nsq(R);
+    return rc2 ? rc2 : build_cp2(R);
 }
 
 // The compact nsq parent list of resident logs (input encoding, once per batch): count the nsq
@@ -3793,6 +3929,52 @@ int Engine::build_nsq(DeviceLogs& L) {
     HIPCHK(hipGetLastError(), "nsq list launch");
     HIPCHK(hipStreamSynchronize(stream), "nsq list");
     L.nsq_items = total;
+    return CRDT_HIP_OK;
+}
+
+// The 2-byte character column of resident logs (input encoding, once per batch): every slot's
+// character as one ASCII byte or an escape, with the three flags; the escaped codepoints in slot
+// order (xcp) with a prefix count per 64 slots (xpre); one bit per 16 slots holding an escape
+// (xgrp).  k_classify then reads 2 bytes per slot instead of 3, and writes the weight nibbles only
+// for groups with an escape (k_runs weighs the other groups by their visible bits).
+int Engine::build_cp2(DeviceLogs& L) {
+    HIPCHK(hipStreamSynchronize(stream), "character column");
+    dfree(L.cp2); dfree(L.xcp); dfree(L.xpre); dfree(L.xgrp);
+    L.nesc = 0;
+    if (!L.total_slots || !cp2_column) return CRDT_HIP_OK;
+    const bool ord = false;  // (L0ARGS)
+    const uint64_t nch = L.total_slots / 64 + 64;
+    if (nch >= (1ull << 32)) return CRDT_HIP_OK;
+    const uint64_t ngw = L.total_slots / 16 / 32 + 2;
+    HIPCHK(dalloc(&L.xpre, nch + 1), "hipMalloc escape prefix");
+    HIPCHK(dalloc(&L.xgrp, ngw), "hipMalloc escape groups");
+    HIPCHK(dalloc(&L.cp2, L.total_slots), "hipMalloc character column");
+    HIPCHK(hipMemsetAsync(L.xpre, 0, (nch + 1) * 4, stream), "escape prefix");
+    HIPCHK(hipMemsetAsync(L.xgrp, 0, ngw * 4, stream), "escape groups");
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_cp2_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.xpre + (w.slot0 >> 6));
+    }
+    const uint32_t n = (uint32_t)nch, nb = (n + kScanTile - 1) / kScanTile;
+    uint32_t* sums = nullptr;
+    HIPCHK(dalloc(&sums, nb), "hipMalloc escape scan");
+    k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.xpre, n, sums);
+    k_scan_top<<<1, 1024, 0, stream>>>(sums, nb, L.xpre, n);
+    k_scan_apply<<<nb, kBlock, 0, stream>>>(L.xpre, n, sums, L.xpre);
+    uint32_t total = 0;
+    hipError_t e = hipMemcpyAsync(&total, L.xpre + n, 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    dfree(sums);
+    if (e != hipSuccess) return fail("escape scan", e);
+    HIPCHK(dalloc(&L.xcp, (uint64_t)total + 1), "hipMalloc escaped codepoints");
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_cp2_fill<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(
+            a0, L.xpre + (w.slot0 >> 6), L.cp2 + w.slot0, L.xcp, L.xgrp);
+    }
+    HIPCHK(hipGetLastError(), "character column launch");
+    HIPCHK(hipStreamSynchronize(stream), "character column");
+    L.nesc = total;
     return CRDT_HIP_OK;
 }
 #undef L0ARGS

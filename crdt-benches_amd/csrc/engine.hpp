@@ -111,6 +111,14 @@ struct DeviceLogs {
     uint32_t* nsq_par = nullptr;
     uint32_t* nsq_pre = nullptr;
     uint64_t nsq_items = 0;
+    // Resident batches (Engine::build_cp2): the 2-byte character column (ASCII byte or escape,
+    // plus the flags), the escaped codepoints in slot order and their prefix count per 64 slots,
+    // and one bit per 16 slots that hold an escape.  Null: k_classify reads the 3-byte column.
+    uint16_t* cp2 = nullptr;
+    uint32_t* xcp = nullptr;
+    uint32_t* xpre = nullptr;
+    uint32_t* xgrp = nullptr;
+    uint64_t nesc = 0;
 
     void release();
     ~DeviceLogs() { release(); }
@@ -149,13 +157,14 @@ public:
     bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
     bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS
     bool fuse_text = true;         // k_doctree writes the text when it fits LDS (else k_expand)
-    // incremental merges (incr.hip): the three phases in one cooperative launch with grid-wide
-    // barriers, else three launches (the default: 44 vs 56 us per len() on automerge-paper, the
-    // grid barriers cost more than the launches)
-    bool inc_coop = false;
     // resident batches get the compact list of the non-seq items' parents (build_nsq); 0: the
     // level-0 kernels gather the parent column instead (A/B)
     bool nsq_list = true;
+    // resident batches get the 2-byte character column (build_cp2); off by default: same-box A/B
+    // at the headline config, k_classify 3.79 -> 3.97 ms and k_runs 3.55 -> 3.72 ms per step with
+    // it (one byte per slot less is not what bounds them; the decode and the sparse weights cost
+    // more), so the 3-byte column stays the default
+    bool cp2_column = false;
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -209,6 +218,8 @@ public:
 
     // The compact nsq parent list of L (after its last plan; see DeviceLogs::nsq_par).
     int build_nsq(DeviceLogs& L);
+    // The 2-byte character column of L (after its last plan; see DeviceLogs::cp2).
+    int build_cp2(DeviceLogs& L);
 
     // Materialise `replicas` relabelled copies of `bases` (already uploaded in B) into R.
     int replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,

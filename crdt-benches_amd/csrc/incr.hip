@@ -11,21 +11,23 @@
 //   new items with an old parent p (the roots of the new forest) go right after p, ahead of p's
 //   old children, when their sibling key (lamport, agent) is above every old item's key — the
 //   case of every local edit (the resolver's lamport = max + 1) and of any update that does not
-//   race an older one.  The new forest (at most kIncMax items) is ordered in one workgroup
-//   (k_inc_forest): children grouped by parent and ranked among their siblings (roots by
-//   (anchor rank asc, key desc), other groups by key desc), then an Euler tour of the forest
-//   ranked by pointer jumping in LDS gives every new item its place.  k_inc_splice merges the old
-//   order with the new items (an old rank k moves to k + #new items anchored before it) and
-//   rewrites `rank`; k_inc_text writes the text of the new order.  Deletes change no order: the
-//   tombstone bits the decode set make those items weigh nothing in k_inc_text.
+//   race an older one.  One launch (k_inc), one workgroup per tile of 4096 old ranks:
+//   - every workgroup orders the new forest (at most kIncMax items) in LDS (inc_forest): children
+//     grouped by parent and ranked among their siblings (roots by (anchor rank asc, key desc),
+//     other groups by key desc), an Euler tour of the forest ranked by barrier-free pointer
+//     jumping, every item's place and the old rank its subtree follows;
+//   - it splices its tile (an old rank k moves to k + #new items anchored before it, the new items
+//     anchored inside the tile go in between) and rewrites `rank`;
+//   - it takes its text offset from the tiles before it by decoupled look-back and writes its
+//     text.  Deletes change no order: the tombstone bits the decode set make those items weigh
+//     nothing.
 //
 // Anything else — a root whose key is not above every old key (a concurrent update), more than
 // kIncMax new items, a Fugue replica — falls back to a full merge (engine ORDER mode), which also
 // rebuilds the state.  Every fast-path merge is checked against the decode's counters (bytes and
 // codepoints of the visible text) by the host.
-#include <hip/hip_cooperative_groups.h>
-
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -39,17 +41,24 @@
 namespace crdt {
 namespace {
 
-constexpr uint32_t kIncThreads = 1024;
+#ifndef CRDT_INC_THREADS
+#define CRDT_INC_THREADS 1024
+#endif
+constexpr uint32_t kIncThreads = CRDT_INC_THREADS;
 constexpr uint32_t kSpliceRanks = 4;                                // old ranks per thread
 constexpr uint32_t kSpliceTile = kIncThreads * kSpliceRanks;        // old ranks per tile
-constexpr uint32_t kIncGroupMax = 1024;  // largest sibling group ranked in k_inc_forest
+constexpr uint32_t kIncGroupMax = 1024;  // largest sibling group ranked in inc_forest
 constexpr uint32_t kIncThinGroup = 32;   // more roots than this: ranked one wave per root
+#ifndef CRDT_INC_RUNS
+#define CRDT_INC_RUNS 1
+#endif
+constexpr bool kIncRuns = CRDT_INC_RUNS;  // contract runs of new items before the tour
 constexpr uint32_t kCpMaskI = 0x001FFFFFu;
 constexpr uint32_t kDelBitI = 0x00800000u;
 
 // device counters (u64)
-enum ICtl { I_FLAG = 0, I_MAXKEY, I_BYTES, I_CPS, I_N };
-// I_FLAG bits: the fast path does not apply (the host merges in full)
+enum ICtl { I_MAXKEY = 0, I_MAXKEY_B, I_N };  // the largest key, two slots (calls alternate)
+// flag bits (the result block): the fast path does not apply (the host merges in full)
 constexpr uint64_t F_KEY = 1, F_ORDER = 2, F_GROUP = 4, F_TEXT = 8;
 
 struct IncArgs {
@@ -60,9 +69,9 @@ struct IncArgs {
     uint32_t* rank;             // slot -> rank
     const uint32_t* seq;        // rank -> slot (n0 + 1 entries)
     uint32_t* seq2;             // the new order (n0 + 1 + m entries)
-    uint32_t* ins_s;            // the new items in their order: slot
-    uint32_t* ins_a;            //   and the old rank they follow (non-decreasing)
-    uint4* bsum;                // per splice block: {bytes, codepoints, first output, end}
+    uint32_t* lb_flag;          // per tile: look-back status (call epoch << 2 | state)
+    uint64_t* lb_agg;           //   its aggregate and its inclusive prefix {bytes | cps << 32}
+    uint64_t* lb_inc;
     uint32_t nblk;
     uint8_t* text;
     uint64_t text_cap;
@@ -80,25 +89,17 @@ __device__ __forceinline__ uint32_t cp_word(const uint8_t* cp, uint32_t s) {
     return (uint32_t)cp[3ull * s] | ((uint32_t)cp[3ull * s + 1] << 8) |
            ((uint32_t)cp[3ull * s + 2] << 16);
 }
-// UTF-8 bytes of slot s in the text (0: the document start or a tombstone)
-__device__ __forceinline__ uint32_t slot_bytes(const uint8_t* cp, uint32_t s) {
-    if (s == 0) return 0;
-    const uint32_t c = cp_word(cp, s);
+// The codepoint word of slot s (the document start: a tombstone, it has no text)
+__device__ __forceinline__ uint32_t slot_word(const uint8_t* cp, uint32_t s) {
+    return s ? cp_word(cp, s) : kDelBitI;
+}
+// UTF-8 bytes of a codepoint word in the text (0: a tombstone)
+__device__ __forceinline__ uint32_t word_bytes(uint32_t c) {
     return (c & kDelBitI) ? 0u : utf8_len(c & kCpMaskI);
 }
 
-__device__ __forceinline__ uint32_t block_max_u32(uint32_t x, uint32_t* lds) {
-#pragma unroll
-    for (int o = 32; o; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
-    if ((threadIdx.x & 63u) == 0) lds[threadIdx.x >> 6] = x;
-    __syncthreads();
-    uint32_t t = 0;
-    for (uint32_t i = 0; i < blockDim.x / 64; ++i) t = max(t, lds[i]);
-    __syncthreads();
-    return t;
-}
 
-// ---- k_inc_forest: the order of the appended items (one workgroup) -----------------------------
+// ---- inc_forest: the order of the appended items (in each workgroup) ---------------------------
 // Items i = 0..m-1 are slots n0 + 1 + i.  Local node m is a virtual root V whose children are
 // the items with an old parent.  LDS (dynamic): see the carve-up below.
 __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
@@ -108,7 +109,8 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
            + 8u * mmax               // keys (u64), later the output pairs
            + 4u * mmax               // A: anchor rank of a root (u32)
            + 4u * (2u * mmax + 4u)   // tour successor (u16) and suffix sum (u16), packed u32
-           + 2u * mmax               // vrk: ranks among many roots (u16)
+           + 2u * mmax               // vrk: ranks among many roots, then run heads (u16)
+           + 2u * mmax               // rend: the last item of each run (u16)
            + 64u;
 }
 
@@ -125,9 +127,10 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     uint16_t* lp = reinterpret_cast<uint16_t*>(tour + (2u * kIncMax + 4u));  // kIncMax + 2
     uint16_t* ch = lp + (kIncMax + 2u);                     // kIncMax + 2
     uint16_t* vrk = ch + (kIncMax + 2u);                    // kIncMax: ranks among the roots
+    uint16_t* rend = vrk + kIncMax;                         // kIncMax: the last item of a run
     if (t == 0) flag = 0;
     INC_TS(0);
-    const uint64_t maxkey0 = a.ctl[I_MAXKEY];
+    const uint64_t maxkey0 = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
     // ---- load: parents, keys, anchors; counts cleared ----
     uint32_t plc[Q];
     uint64_t kmax = 0;
@@ -254,23 +257,62 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     }
     INC_TS(6);
     __syncthreads();
-    if (flag) {  // (block-uniform after the barrier)
-        if (t == 0) a.ctl[I_FLAG] = flag;
-        return;
+    if (flag) return;  // (block-uniform after the barrier)
+    // ---- runs: item i continues i - 1 when i - 1 is its parent and i its only child (typing),
+    // so a run is a range of consecutive items whose places are consecutive; only run heads
+    // enter the tour (run i's weight = its length).  hd[i] = the head of i's run (a max-scan in
+    // item order, four consecutive items per thread), rend[h] = the last item of run h ----
+    uint16_t* hd = vrk;  // (the root ranks are dead)
+    {
+        const uint32_t i0 = Q * t;
+        uint32_t h[Q], mx = 0;
+#pragma unroll
+        for (int k = 0; k < (int)Q; ++k) {
+            const uint32_t i = i0 + (uint32_t)k;
+            const bool cont = kIncRuns && i < m && i > 0 && lp[i] == i - 1u &&
+                              start[i] - start[i - 1u] == 1u;
+            h[k] = (i < m && !cont) ? i : 0u;
+            mx = max(mx, h[k]);
+        }
+        uint32_t inc = mx;
+        const uint32_t lane = t & 63u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= (uint32_t)o) inc = max(inc, y);
+        }
+        if (lane == 63u) red[t >> 6] = inc;
+        __syncthreads();
+        uint32_t run = 0;
+        for (uint32_t w = 0; w < (t >> 6); ++w) run = max(run, red[w]);
+        const uint32_t prev = (uint32_t)__shfl_up((int)inc, 1);
+        run = max(run, lane ? prev : 0u);
+#pragma unroll
+        for (int k = 0; k < (int)Q; ++k) {
+            const uint32_t i = i0 + (uint32_t)k;
+            run = max(run, h[k]);
+            if (i >= m) continue;
+            hd[i] = (uint16_t)run;
+            const bool next_cont = kIncRuns && i + 1u < m && lp[i + 1u] == i &&
+                                   start[i + 1u] - start[i] == 1u;
+            if (!next_cont) rend[run] = (uint16_t)i;
+        }
     }
-    if (t == 0) a.ctl[I_FLAG] = 0;
-    // ---- Euler tour of the forest: down(x) = 2x, up(x) = 2x + 1 (x = 0..m, V = m), end E ----
-    // succ in the low 16 bits, the arc's weight (1 for an item's down arc) in the high 16
+    __syncthreads();
+    // ---- Euler tour of the run forest: down(h) = 2h, up(h) = 2h + 1 (h a run head or V = m),
+    // end E; succ in the low 16 bits, the arc's weight (a run's length on its down arc) high ----
     const uint32_t E = 2u * m + 2u, V = m;
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t x = t + (uint32_t)q * kIncThreads;
-        if (x >= m) continue;
-        const uint32_t c0 = start[x], c1 = start[x + 1u];
+        if (x >= m || hd[x] != x) continue;
+        const uint32_t e = rend[x];
+        const uint32_t c0 = start[e], c1 = start[e + 1u];
         const uint32_t sd = c1 > c0 ? 2u * ch[c0] : 2u * x + 1u;
         const uint32_t p = lp[x], pos = start[p] + rk[q];
-        const uint32_t su = pos + 1u < start[p + 1u] ? 2u * ch[pos + 1u] : 2u * p + 1u;
-        tour[2u * x] = sd | (1u << 16);
+        const uint32_t pr = p == V ? V : hd[p];  // (a parent is always the last item of its run)
+        const uint32_t su = pos + 1u < start[p + 1u] ? 2u * ch[pos + 1u] : 2u * pr + 1u;
+        tour[2u * x] = sd | ((e - x + 1u) << 16);
         tour[2u * x + 1u] = su;
     }
     if (t == 0) {
@@ -283,15 +325,16 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     __syncthreads();
     // ---- pointer jumping without barriers: a record (succ | weight of [arc, succ) << 16) is a
     // valid stretch of the tour at all times, so joining it with an old or a new record of its
-    // successor is equally right; each thread jumps its own arcs until they reach the end (every
-    // pass at least doubles... or extends a record by one arc: E passes bound it) ----
+    // successor is equally right; each thread jumps its own arcs (those of run heads and V) until
+    // they reach the end (every pass extends a record by at least one arc: E passes bound it) ----
     {
         constexpr int NA = (int)((2u * kIncMax + 4u + kIncThreads - 1u) / kIncThreads);
+        static_assert(NA <= 32, "arcs per thread");
         uint32_t live = 0;
 #pragma unroll
         for (int q = 0; q < NA; ++q) {
-            const uint32_t arc = t + (uint32_t)q * kIncThreads;
-            live |= (arc < E ? 1u : 0u) << q;
+            const uint32_t arc = t + (uint32_t)q * kIncThreads, x = arc >> 1;
+            live |= (arc < E && (x == V || hd[x] == x) ? 1u : 0u) << q;
         }
         for (uint32_t pass = 0; live && pass <= E; ++pass) {
 #pragma unroll
@@ -313,23 +356,18 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     }
     INC_TS(8);
     __syncthreads();
-    // ---- every item's place among the new items; its root's anchor by a max-scan ----
-    uint32_t* os = reinterpret_cast<uint32_t*>(keys);  // (keys are dead) slot by place
-    uint32_t* oa = os + kIncMax;                       // a root's anchor by place, else 0
-    uint32_t pa[Q], px[Q];
-#pragma unroll
-    for (int q = 0; q < (int)Q; ++q) {
-        const uint32_t x = t + (uint32_t)q * kIncThreads;
-        px[q] = x < m ? m - (tour[2u * x] >> 16) : 0u;
-        pa[q] = (x < m && lp[x] == V) ? A[x] : 0u;
-    }
-    __syncthreads();
+    // ---- every item's place among the new items; its root's anchor by a max-scan.  The result
+    // stays in LDS for the splice: os[place] = slot, oa[place] = the old rank it follows ----
+    uint32_t* os = reinterpret_cast<uint32_t*>(keys);  // (the keys are dead since the ranking)
+    uint32_t* oa = os + kIncMax;
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t x = t + (uint32_t)q * kIncThreads;
         if (x < m) {
-            os[px[q]] = n0 + 1u + x;
-            oa[px[q]] = pa[q];
+            const uint32_t h = hd[x];
+            const uint32_t px = m - (tour[2u * h] >> 16) + (x - h);
+            os[px] = n0 + 1u + x;
+            oa[px] = lp[x] == V ? A[x] : 0u;  // (a root's anchor; inside a subtree 0)
         }
     }
     __syncthreads();
@@ -338,7 +376,6 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         const uint32_t lo = min(m, t * Q), hi = min(m, lo + Q);
         uint32_t mx = 0;
         for (uint32_t i = lo; i < hi; ++i) mx = max(mx, oa[i]);
-        // exclusive max over the threads before this one
         uint32_t inc = mx;
         const uint32_t lane = t & 63u;
 #pragma unroll
@@ -354,116 +391,164 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         run = max(run, lane ? prev : 0u);
         for (uint32_t i = lo; i < hi; ++i) {
             run = max(run, oa[i]);
-            a.ins_s[i] = os[i];
-            a.ins_a[i] = run;
+            oa[i] = run;
         }
     }
-    // the largest key now held (the next merge's check)
-    __syncthreads();  // (red is reused)
     INC_TS(9);
-    {
-        const uint32_t hi32 = block_max_u32((uint32_t)(kmax >> 32), red);
-        const uint32_t lo32 = block_max_u32((uint32_t)(kmax >> 32) == hi32 ? (uint32_t)kmax : 0u, red);
-        if (t == 0) {
-            const uint64_t km = ((uint64_t)hi32 << 32) | lo32;
-            if (km > maxkey0) a.ctl[I_MAXKEY] = km;
+    // the largest key now held, for the next call's check (workgroup 0; the slot this call
+    // writes is not the one any workgroup of it reads)
+    if (blockIdx.x == 0) {
+        uint64_t km = max(kmax, maxkey0);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(km >> 32), o) << 32) |
+                           (uint32_t)__shfl_xor((int)(uint32_t)km, o);
+            km = max(km, y);
         }
+        if ((t & 63u) == 0)
+            atomicMax(reinterpret_cast<unsigned long long*>(&a.ctl[I_MAXKEY + (a.call & 1u)]),
+                      (unsigned long long)km);
     }
+    __syncthreads();
     INC_TS(10);
 }
 #undef INC_TS
 
-// Number of new items anchored before old rank k (ins_a is non-decreasing).
-__device__ __forceinline__ uint32_t anchored_before(const uint32_t* ins_a, uint32_t m, uint32_t k) {
+// Number of new items anchored before old rank k (la is non-decreasing).
+__device__ __forceinline__ uint32_t anchored_before(const uint32_t* la, uint32_t m, uint32_t k) {
     uint32_t lo = 0, hi = m;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (ins_a[mid] < k) lo = mid + 1u;
+        if (la[mid] < k) lo = mid + 1u;
         else hi = mid;
     }
     return lo;
 }
 
-__device__ __forceinline__ uint64_t ld_flag(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ---- splice: the new order of one tile; rank rewritten; the tile's text sums -------------------
-// Tile b takes old ranks [k0, k1) and the new items anchored in [k0, k1): its outputs are the
-// places [k0 + c(k0), k1 + c(k1)), c(k) = new items anchored before k.
-// la: the anchors (ins_a) copied to LDS by inc_load_anchors (searched there, not in HBM: ins_a
-// was written by one workgroup, and a dependent chain of loads from another XCD's L2 is slow).
-__device__ __forceinline__ void inc_load_anchors(const IncArgs& a, uint32_t* la) {
-    for (uint32_t j = threadIdx.x; j < a.m; j += kIncThreads) la[j] = a.ins_a[j];
-    __syncthreads();
-}
-__device__ __forceinline__ void inc_splice_tile(const IncArgs& a, uint32_t b, uint32_t* red,
-                                                uint32_t* cb, const uint32_t* la) {
+// ---- splice: the new order of one tile; rank rewritten; the tile's text totals ----------------
+// Tile b takes old ranks [k0, k1) and the new items anchored in [k0, k1) (os / la: the new items
+// by place, in LDS): its outputs are the places [k0 + c(k0), k1 + c(k1)), c(k) = new items
+// anchored before k.  Returns {bytes, codepoints} of its outputs; range = its output places.
+__device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, uint32_t* red,
+                                                 uint32_t* cb, const uint32_t* os,
+                                                 const uint32_t* la, uint32_t* cwl,
+                                                 const uint32_t (&sl)[kSpliceRanks], uint2& range) {
     const uint32_t N0 = a.n0 + 1u, m = a.m;
     const uint32_t k0 = b * kSpliceTile, k1 = min(N0, k0 + kSpliceTile);
+    // the tile's first output place (every thread finds it: the words go to LDS at place - o0)
+    const uint32_t o0 = k0 + (m ? anchored_before(la, m, k0) : 0u);
     if (threadIdx.x < 2u) cb[threadIdx.x] = m ? anchored_before(la, m, threadIdx.x ? k1 : k0) : 0u;
     const uint32_t kb = k0 + threadIdx.x * kSpliceRanks;
-    uint32_t sl[kSpliceRanks];
+    uint32_t cwq[kSpliceRanks];
 #pragma unroll
-    for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = kb + q < k1 ? a.seq[kb + q] : 0u;
+    for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = kb + q < k1 ? slot_word(a.cp, sl[q]) : kDelBitI;
     uint32_t bytes = 0, cps = 0;
+    // c(k) for the thread's first rank by binary search; the next ranks search again only past
+    // an anchor (a whole subtree of new items shares one anchor, so no linear walk over them)
+    uint32_t c = (m && kb < k1) ? anchored_before(la, m, kb) : 0u;
 #pragma unroll
     for (int q = 0; q < (int)kSpliceRanks; ++q) {
         const uint32_t k = kb + q;
         if (k >= k1) break;
-        // (a search per rank: a whole subtree of new items shares one anchor)
-        const uint32_t c = m ? anchored_before(la, m, k) : 0u;
+        if (q && c < m && la[c] < k) c = anchored_before(la, m, k);
         const uint32_t np = k + c;
         a.seq2[np] = sl[q];
+        cwl[np - o0] = cwq[q];
         a.rank[sl[q]] = np;
-        const uint32_t w = slot_bytes(a.cp, sl[q]);
+        const uint32_t w = word_bytes(cwq[q]);
         bytes += w;
         cps += w ? 1u : 0u;
     }
     __syncthreads();
     const uint32_t c0 = cb[0], c1 = cb[1];
     for (uint32_t j = c0 + threadIdx.x; j < c1; j += kIncThreads) {
-        const uint32_t s = a.ins_s[j], np = la[j] + 1u + j;
-        a.seq2[np] = s;
-        a.rank[s] = np;
-        const uint32_t w = slot_bytes(a.cp, s);
+        const uint32_t sj = os[j], np = la[j] + 1u + j;
+        const uint32_t cwj = slot_word(a.cp, sj);
+        a.seq2[np] = sj;
+        cwl[np - o0] = cwj;
+        a.rank[sj] = np;
+        const uint32_t w = word_bytes(cwj);
         bytes += w;
         cps += w ? 1u : 0u;
     }
     uint32_t tb, tc;
     (void)block_excl_scan<kIncThreads / 64>(bytes, red, tb);
     (void)block_excl_scan<kIncThreads / 64>(cps, red, tc);
-    if (threadIdx.x == 0) a.bsum[b] = make_uint4(tb, tc, k0 + c0, k1 + c1);
+    range = make_uint2(k0 + c0, k1 + c1);
+    return make_uint2(tb, tc);
 }
 
-// ---- text: the UTF-8 of one tile's outputs, at the bytes of the tiles before it ----------------
-__device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint32_t b, uint32_t* red) {
-    // the tile's range and the bytes of the tiles before it, and the first chunk's items and
-    // codepoint words, all loaded before the first wait
-    const uint4 me = a.bsum[b];
-    uint32_t p = 0;
-    for (uint32_t i = threadIdx.x; i < b; i += kIncThreads) p += a.bsum[i].x;
-    uint32_t cw[kSpliceRanks];
-    auto load = [&](uint32_t o0) {
+// ---- decoupled look-back over the tiles: the bytes / codepoints of the tiles before tile b ------
+// Per tile a status word (call epoch << 2 | 1: aggregate published, | 2: inclusive prefix
+// published) and two values; a workgroup publishes its aggregate, then its first wave reads up to
+// 64 predecessors at once (nearest first) until it meets an inclusive prefix, spinning on those
+// not yet published.  Workgroups are dispatched in index order, so every predecessor runs.
+__device__ __forceinline__ uint32_t lb_state(const uint32_t* f, uint32_t epoch) {
+    const uint32_t v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    return (v >> 2) == epoch ? (v & 3u) : 0u;
+}
+__device__ __forceinline__ void lb_publish(const IncArgs& a, uint32_t b, uint64_t v, uint32_t st,
+                                           uint32_t epoch) {
+    (st == 2u ? a.lb_inc : a.lb_agg)[b] = v;
+    __hip_atomic_store(&a.lb_flag[b], (epoch << 2) | st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t inc_lookback(const IncArgs& a, uint32_t b, uint64_t agg,
+                                                 uint64_t* excl_lds) {
+    const uint32_t epoch = (uint32_t)(a.call & 0x3FFFFFFFu);
+    if (threadIdx.x == 0) lb_publish(a, b, agg, b == 0 ? 2u : 1u, epoch);
+    if (b == 0) return 0;
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        uint64_t excl = 0;
+        int64_t j0 = (int64_t)b - 1;
+        for (;;) {
+            const int64_t j = j0 - (int64_t)lane;
+            uint32_t st = j >= 0 ? lb_state(a.lb_flag + j, epoch) : 2u;
+            const uint64_t inc2 = __ballot(st == 2u);
+            // lanes up to (and including) the nearest inclusive prefix must all be published
+            const uint32_t p = inc2 ? (uint32_t)__builtin_ctzll(inc2) : 64u;
+            const uint64_t need = p >= 63u ? ~0ull : ((2ull << p) - 1ull);
+            if (__ballot(st == 0u) & need) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;  // (re-read the window)
+            }
+            uint64_t v = 0;
+            if (lane <= p && j >= 0) v = (lane == p) ? a.lb_inc[j] : a.lb_agg[j];
+            // (64-bit sum over the wave: bytes in the low half, codepoints in the high half)
+#pragma unroll
+            for (int o = 32; o; o >>= 1) {
+                const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), o) << 32) |
+                                   (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+                v += y;
+            }
+            excl += v;
+            if (p < 64u) break;
+            j0 -= 64;
+        }
+        if (lane == 0) {
+            lb_publish(a, b, excl + agg, 2u, epoch);
+            *excl_lds = excl;
+        }
+    }
+    __syncthreads();
+    return *excl_lds;
+}
+
+// ---- text: the UTF-8 of one tile's output places at byte offset `base` --------------------------
+// (the places were written by this workgroup's splice: no other workgroup's writes are read)
+__device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint2 range, uint64_t base,
+                                              const uint32_t* cwl, uint32_t* red) {
+    for (uint32_t o0 = range.x; o0 < range.y; o0 += kSpliceTile) {
         const uint32_t ob = o0 + threadIdx.x * kSpliceRanks;
-        uint32_t sl[kSpliceRanks];
+        uint32_t cw[kSpliceRanks], L[kSpliceRanks];
+        // (the codepoint words the splice staged in LDS by place)
 #pragma unroll
-        for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = ob + q < me.w ? a.seq2[ob + q] : 0u;
-#pragma unroll
-        for (int q = 0; q < (int)kSpliceRanks; ++q) cw[q] = sl[q] ? cp_word(a.cp, sl[q]) : kDelBitI;
-    };
-    load(me.z);
-    uint32_t ptot;
-    (void)block_excl_scan<kIncThreads / 64>(p, red, ptot);
-    uint64_t base = ptot;
-    if (base + me.x > a.text_cap) return;  // (flagged from the totals)
-    for (uint32_t o0 = me.z; o0 < me.w; o0 += kSpliceTile) {
-        if (o0 != me.z) load(o0);
-        uint32_t L[kSpliceRanks];
+        for (int q = 0; q < (int)kSpliceRanks; ++q)
+            cw[q] = ob + q < range.y ? cwl[ob + q - range.x] : kDelBitI;
         uint32_t tot = 0;
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) {
-            L[q] = (cw[q] & kDelBitI) ? 0u : utf8_len(cw[q] & kCpMaskI);
+            L[q] = word_bytes(cw[q]);
             tot += L[q];
         }
         uint32_t all;
@@ -485,89 +570,63 @@ __device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint32_t b, uint
     }
 }
 
-// The totals (one workgroup): the flag, bytes and codepoints of every tile, to the host-mapped
-// result block, stamped with the call number.
-__device__ __forceinline__ void inc_totals(const IncArgs& a, uint32_t ntiles, uint32_t* red) {
-    uint32_t b = 0, c = 0;
-    for (uint32_t i = threadIdx.x; i < ntiles; i += kIncThreads) {
-        const uint4 v = a.bsum[i];
-        b += v.x;
-        c += v.y;
+// ---- the whole incremental merge in one launch: one workgroup per tile of old ranks ------------
+// Every workgroup orders the new items itself (the forest is small: the same result in each, no
+// grid-wide barrier), splices its tile, takes its byte offset by look-back and writes its text.
+// The last tile's workgroup reports the totals to the host-mapped result block.
+__global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ uint32_t red[kIncThreads / 64];
+    __shared__ uint32_t cb[2];
+    __shared__ uint32_t flag;
+    __shared__ uint64_t excl_lds;
+    const uint32_t b = blockIdx.x;
+    // the tile's old order, loaded before the forest so that the round trip overlaps it
+    uint32_t sl[kSpliceRanks];
+    {
+        const uint32_t k0 = b * kSpliceTile, k1 = min(a.n0 + 1u, k0 + kSpliceTile);
+        const uint32_t kb = k0 + threadIdx.x * kSpliceRanks;
+#pragma unroll
+        for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = kb + q < k1 ? a.seq[kb + q] : 0u;
     }
-    uint32_t tb, tc;
-    (void)block_excl_scan<kIncThreads / 64>(b, red, tb);
-    (void)block_excl_scan<kIncThreads / 64>(c, red, tc);
-    if (threadIdx.x == 0) {
-        const uint64_t f = ld_flag(&a.ctl[I_FLAG]) | (tb > a.text_cap ? F_TEXT : 0u);
-        a.ctl[I_BYTES] = tb;
-        a.ctl[I_CPS] = tc;
-        a.hres[0] = f;
-        a.hres[1] = tb;
-        a.hres[2] = tc;
+    if (a.m) {
+        inc_forest(a, lds, red, flag);
+    } else if (threadIdx.x == 0) {
+        flag = 0;
+        if (blockIdx.x == 0) {  // (carry the largest key over to this call's slot)
+            const uint64_t km = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
+            atomicMax(reinterpret_cast<unsigned long long*>(&a.ctl[I_MAXKEY + (a.call & 1u)]),
+                      (unsigned long long)km);
+        }
+    }
+    __syncthreads();
+    const uint32_t f = flag;
+    uint64_t tot = 0;
+    if (f == 0) {
+        const uint32_t* os = reinterpret_cast<const uint32_t*>(lds);
+        const uint32_t* la = os + kIncMax;
+        // the tile's codepoint words by place, in the forest's tour region (dead by now)
+        uint32_t* cwl = reinterpret_cast<uint32_t*>(lds + 12u * kIncMax + 4u * (kIncMax + 2u));
+        uint2 range;
+        const uint2 agg = inc_splice_tile(a, b, red, cb, os, la, cwl, sl, range);
+        const uint64_t agg64 = ((uint64_t)agg.y << 32) | agg.x;
+        const uint64_t excl = inc_lookback(a, b, agg64, &excl_lds);
+        const uint64_t base = (uint32_t)excl;
+        if (base + agg.x <= a.text_cap) inc_text_tile(a, range, base, cwl, red);
+        tot = excl + agg64;
+    }
+    if (b + 1u == gridDim.x && threadIdx.x == 0) {
+        const uint64_t bytes = (uint32_t)tot, cps = tot >> 32;
+        a.hres[0] = f ? f : (bytes > a.text_cap ? F_TEXT : 0u);
+        a.hres[1] = bytes;
+        a.hres[2] = cps;
         __threadfence_system();
         a.hres[3] = a.call;
     }
 }
 
-// ---- the three phases as kernels (stream order between them) ------------------------------------
-__global__ __launch_bounds__(kIncThreads) void k_inc_forest(IncArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t red[kIncThreads / 64];
-    __shared__ uint32_t flag;
-    if (a.m) inc_forest(a, lds, red, flag);
-    else if (threadIdx.x == 0) a.ctl[I_FLAG] = 0;
-}
-__global__ __launch_bounds__(kIncThreads) void k_inc_splice(IncArgs a) {
-    __shared__ uint32_t red[kIncThreads / 64];
-    __shared__ uint32_t cb[2];
-    __shared__ uint32_t la[kIncMax];
-    if (ld_flag(&a.ctl[I_FLAG])) return;
-    inc_load_anchors(a, la);
-    inc_splice_tile(a, blockIdx.x, red, cb, la);
-}
-__global__ __launch_bounds__(kIncThreads) void k_inc_text(IncArgs a) {
-    __shared__ uint32_t red[kIncThreads / 64];
-    if (blockIdx.x == gridDim.x - 1u) {  // (the last workgroup also reports)
-        inc_totals(a, gridDim.x - 1u, red);
-        return;
-    }
-    if (ld_flag(&a.ctl[I_FLAG])) return;
-    inc_text_tile(a, blockIdx.x, red);
-}
-
-// ---- all three in one cooperative launch (grid-wide barriers between the phases) -----------------
-__global__ __launch_bounds__(kIncThreads) void k_inc_all(IncArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t red[kIncThreads / 64];
-    __shared__ uint32_t cb[2];
-    __shared__ uint32_t flag;
-    namespace cg = cooperative_groups;
-    cg::grid_group grid = cg::this_grid();
-    if (blockIdx.x == 0) {
-        if (a.m) inc_forest(a, lds, red, flag);
-        else if (threadIdx.x == 0) a.ctl[I_FLAG] = 0;
-    }
-    grid.sync();
-    const bool go = ld_flag(&a.ctl[I_FLAG]) == 0;
-    if (go && blockIdx.x < a.nblk) {
-        uint32_t* la = reinterpret_cast<uint32_t*>(lds);
-        inc_load_anchors(a, la);
-        for (uint32_t b = blockIdx.x; b < a.nblk; b += gridDim.x) {
-            inc_splice_tile(a, b, red, cb, la);
-            __syncthreads();
-        }
-    }
-    grid.sync();
-    if (go)
-        for (uint32_t b = blockIdx.x; b < a.nblk; b += gridDim.x) {
-            inc_text_tile(a, b, red);
-            __syncthreads();
-        }
-    if (blockIdx.x == gridDim.x - 1u) inc_totals(a, go ? a.nblk : 0u, red);
-}
-
-// The largest sibling key of items 1..n (state rebuild).
-__global__ __launch_bounds__(256) void k_inc_maxkey(const uint64_t* key, uint32_t n, uint64_t* ctl) {
+// The largest sibling key of items 1..n (state rebuild) into ctl[slot].
+__global__ __launch_bounds__(256) void k_inc_maxkey(const uint64_t* key, uint32_t n, uint64_t* dst) {
     uint64_t mx = 0;
     for (uint64_t s = 1 + blockIdx.x * 256ull + threadIdx.x; s <= n; s += 256ull * gridDim.x)
         mx = max(mx, key[s]);
@@ -578,7 +637,7 @@ __global__ __launch_bounds__(256) void k_inc_maxkey(const uint64_t* key, uint32_
         mx = max(mx, y);
     }
     if ((threadIdx.x & 63u) == 0 && mx)
-        atomicMax(reinterpret_cast<unsigned long long*>(&ctl[I_MAXKEY]), (unsigned long long)mx);
+        atomicMax(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)mx);
 }
 
 int ifail(Engine& E, const char* what, hipError_t e) {
@@ -592,32 +651,11 @@ int ifail(Engine& E, const char* what, hipError_t e) {
         if (_e != hipSuccess) return ifail(E, what, _e); \
     } while (0)
 
-// Dynamic LDS of the forest kernels, and the cooperative grid (workgroups that fit at once).
-struct IncLaunch {
-    hipError_t err = hipSuccess;
-    uint32_t coop_grid = 0;
-};
-const IncLaunch& inc_launch_info(int device) {
-    static IncLaunch info = [device] {
-        IncLaunch li;
-        const int lds = (int)inc_forest_lds(kIncMax);
-        li.err = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inc_forest),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (li.err == hipSuccess)
-            li.err = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inc_all),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        int per_cu = 0, cus = 0, coop = 0;
-        if (li.err == hipSuccess)
-            li.err = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, reinterpret_cast<const void*>(&k_inc_all), kIncThreads, lds);
-        if (li.err == hipSuccess)
-            li.err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (li.err == hipSuccess)
-            li.err = hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device);
-        if (li.err == hipSuccess && coop) li.coop_grid = (uint32_t)std::max(0, per_cu * cus);
-        return li;
-    }();
-    return info;
+hipError_t inc_setup() {
+    static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inc),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)inc_forest_lds(kIncMax));
+    return e;
 }
 
 template <class T>
@@ -630,8 +668,7 @@ hipError_t igrow(T** p, uint64_t& cap, uint64_t need) {
     return e;
 }
 
-// Room for an order of `items` items and a text of `bytes` bytes.  Growing the order arrays
-// drops the state (the next merge rebuilds it).
+// Room for an order of `items` items and a text of `bytes` bytes.
 int inc_reserve(Engine& E, IncState& s, uint64_t items, uint64_t bytes) {
     const uint64_t need = items + 1 + kIncMax;  // (room for the next call's new items)
     if (need > s.cap) {
@@ -663,9 +700,18 @@ int inc_reserve(Engine& E, IncState& s, uint64_t items, uint64_t bytes) {
         s.cur = 0;
         s.cap = cap;
     }
-    const uint64_t nblk = (s.cap + kSpliceTile - 1) / kSpliceTile + 1;
-    ICHK(igrow(&s.bsum, s.bsum_cap, nblk), "hipMalloc tile sums");
-    ICHK(igrow(&s.ins, s.ins_cap, 2ull * kIncMax), "hipMalloc new-item order");
+    const uint64_t ntiles = (s.cap + kSpliceTile - 1) / kSpliceTile + 1;
+    if (ntiles > s.lb_cap) {
+        dfree(s.lb_flag);
+        dfree(s.lb_agg);
+        dfree(s.lb_inc);
+        s.lb_cap = 0;
+        ICHK(dalloc(&s.lb_flag, ntiles), "hipMalloc look-back");
+        ICHK(dalloc(&s.lb_agg, ntiles), "hipMalloc look-back");
+        ICHK(dalloc(&s.lb_inc, ntiles), "hipMalloc look-back");
+        ICHK(hipMemsetAsync(s.lb_flag, 0, ntiles * 4, E.stream), "clear look-back");
+        s.lb_cap = ntiles;
+    }
     const uint64_t tcap = bytes + 64;
     if (tcap > s.text_cap)
         ICHK(igrow(&s.text, s.text_cap, std::max<uint64_t>(tcap, 2 * s.text_cap)), "hipMalloc text");
@@ -693,9 +739,9 @@ IncArgs make_args(Replica& r, IncState& s, uint32_t n0, uint32_t m) {
     a.rank = s.rank;
     a.seq = s.seq[s.cur];
     a.seq2 = s.seq[s.cur ^ 1];
-    a.ins_s = s.ins;
-    a.ins_a = s.ins + kIncMax;
-    a.bsum = s.bsum;
+    a.lb_flag = s.lb_flag;
+    a.lb_agg = s.lb_agg;
+    a.lb_inc = s.lb_inc;
     a.nblk = (uint32_t)((n0 + 1ull + kSpliceTile - 1) / kSpliceTile);
     a.text = s.text;
     a.text_cap = s.text_cap;
@@ -705,7 +751,8 @@ IncArgs make_args(Replica& r, IncState& s, uint32_t n0, uint32_t m) {
     return a;
 }
 
-// CRDT_INC_PROFILE=1: per call, device times of the phases (events) and host times, to stderr
+// CRDT_INC_PROFILE=1: per call, the kernel's device time (events), the forest's phases and the
+// host times, to stderr
 bool inc_profile() {
     static const bool on = [] {
         const char* e = std::getenv("CRDT_INC_PROFILE");
@@ -714,14 +761,12 @@ bool inc_profile() {
     return on;
 }
 
-// The three phases (one cooperative launch, or three launches), then a wait for the result.
-int inc_run(Engine& E, IncState& s, IncArgs& a) {
+// One launch, then a wait for the result block (sync: for the whole stream).
+int inc_run(Engine& E, IncState& s, IncArgs& a, bool sync) {
     hipStream_t st = E.stream;
-    const IncLaunch& li = inc_launch_info(E.device);
-    ICHK(li.err, "incremental merge setup");
-    const uint32_t lds = inc_forest_lds(kIncMax);
+    ICHK(inc_setup(), "incremental merge setup");
     const bool prof = inc_profile();
-    static hipEvent_t ev[4] = {};
+    static hipEvent_t ev[2] = {};
     static uint64_t* tsp = nullptr;
     if (prof && !ev[0]) {
         for (auto& e : ev) ICHK(hipEventCreate(&e), "event");
@@ -730,39 +775,42 @@ int inc_run(Engine& E, IncState& s, IncArgs& a) {
     a.tsp = prof ? tsp : nullptr;
     const auto h0 = std::chrono::steady_clock::now();
     if (prof) ICHK(hipEventRecord(ev[0], st), "event");
-    if (E.inc_coop && li.coop_grid) {
-        const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(li.coop_grid, a.nblk));
-        void* args[] = {&a};
-        ICHK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_inc_all), dim3(grid),
-                                        dim3(kIncThreads), args, lds, st),
-             "k_inc_all launch");
-        if (prof)
-            for (int k = 1; k < 4; ++k) ICHK(hipEventRecord(ev[k], st), "event");
-    } else {
-        k_inc_forest<<<1, kIncThreads, a.m ? lds : 0, st>>>(a);
-        if (prof) ICHK(hipEventRecord(ev[1], st), "event");
-        k_inc_splice<<<a.nblk, kIncThreads, 0, st>>>(a);
-        if (prof) ICHK(hipEventRecord(ev[2], st), "event");
-        k_inc_text<<<a.nblk + 1u, kIncThreads, 0, st>>>(a);
-        if (prof) ICHK(hipEventRecord(ev[3], st), "event");
-        ICHK(hipGetLastError(), "incremental merge launch");
-    }
+    k_inc<<<std::max<uint32_t>(1, a.nblk), kIncThreads, inc_forest_lds(kIncMax), st>>>(a);
+    ICHK(hipGetLastError(), "incremental merge launch");
+    if (prof) ICHK(hipEventRecord(ev[1], st), "event");
     const auto h1 = std::chrono::steady_clock::now();
-    ICHK(hipStreamSynchronize(st), "incremental merge sync");
-    if (prof && a.tsp && a.m) {
-        uint64_t ts[11] = {};
-        ICHK(hipMemcpy(ts, a.tsp, sizeof(ts), hipMemcpyDeviceToHost), "timestamps");
-        std::fprintf(stderr, "[inc-forest] us:");
-        for (int k = 1; k < 11; ++k) std::fprintf(stderr, " %.1f", (ts[k] - ts[k - 1]) / 100.0);
-        std::fprintf(stderr, " | total %.1f\n", (ts[10] - ts[0]) / 100.0);
+    // The result block is written last, after a system-scope fence, so the host can take it as
+    // soon as it lands instead of waiting for the stream to report completion (a blocking wait
+    // costs ~10 us of wake-up on top of the kernel).  Later work on the stream is ordered behind
+    // the kernel anyway; a caller that copies the text waits for the stream (sync = true).  A
+    // result that does not arrive within a bound falls back to the stream wait, which reports
+    // any device error.
+    bool landed = false;
+    if (!sync && !prof) {
+        const auto t0 = std::chrono::steady_clock::now();
+        volatile const uint64_t* stamp = s.hres + 3;
+        for (uint32_t spin = 0;; ++spin) {
+            if (*stamp == a.call) {
+                landed = true;
+                break;
+            }
+            if ((spin & 1023u) == 1023u &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+                break;
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
     }
+    if (!landed) ICHK(hipStreamSynchronize(st), "incremental merge sync");
     if (prof) {
         const auto h2 = std::chrono::steady_clock::now();
-        float t[3] = {};
-        for (int k = 0; k < 3; ++k) (void)hipEventElapsedTime(&t[k], ev[k], ev[k + 1]);
-        std::fprintf(stderr, "[inc] m %u n0 %u coop %d | device forest %.1f splice %.1f text %.1f us"
-                     " | host enqueue %.1f wait %.1f us\n", a.m, a.n0, (int)(E.inc_coop && li.coop_grid),
-                     1e3 * t[0], 1e3 * t[1], 1e3 * t[2],
+        float t = 0;
+        (void)hipEventElapsedTime(&t, ev[0], ev[1]);
+        uint64_t ts[11] = {};
+        if (a.m) ICHK(hipMemcpy(ts, tsp, sizeof(ts), hipMemcpyDeviceToHost), "timestamps");
+        std::fprintf(stderr, "[inc] m %u n0 %u tiles %u | kernel %.1f us | forest", a.m, a.n0,
+                     a.nblk, 1e3 * t);
+        for (int k = 1; k < 11; ++k) std::fprintf(stderr, " %.1f", (ts[k] - ts[k - 1]) / 100.0);
+        std::fprintf(stderr, " | host enqueue %.1f wait %.1f us\n",
                      std::chrono::duration<double, std::micro>(h1 - h0).count(),
                      std::chrono::duration<double, std::micro>(h2 - h1).count());
     }
@@ -796,11 +844,13 @@ int inc_rebuild(Engine& E, Replica& r, IncState& s) {
     if (r.n) std::memcpy(s.hseq.data() + 1, raw.data(), raw.size());
     ICHK(hipMemcpyAsync(s.seq[s.cur], s.hseq.data(), (r.n + 1ull) * 4, hipMemcpyHostToDevice, st),
          "upload order");
+    // the largest key, into the slot the next call reads (that call copies it forward)
     ICHK(hipMemsetAsync(s.ctl, 0, I_N * 8, st), "clear counters");
+    const uint64_t next = s.calls + 1;
     k_inc_maxkey<<<std::max<uint32_t>(1, std::min<uint32_t>(grid_for(r.n, 256), 1024)), 256, 0, st>>>(
-        r.logs.key, r.n, s.ctl);
+        r.logs.key, r.n, s.ctl + I_MAXKEY + ((next & 1u) ^ 1u));
     IncArgs a = make_args(r, s, r.n, 0);  // m = 0: the splice copies the order and sets the ranks
-    rc = inc_run(E, s, a);
+    rc = inc_run(E, s, a, true);
     if (rc) return rc;
     if (s.hres[0] || s.hres[1] != r.vis_bytes || s.hres[2] != r.vis_cp) {
         E.err = "incremental merge state: rebuilt text disagrees with the replica's counters";
@@ -818,8 +868,9 @@ IncState::~IncState() {
     dfree(seq[0]);
     dfree(seq[1]);
     dfree(rank);
-    dfree(ins);
-    dfree(bsum);
+    dfree(lb_flag);
+    dfree(lb_agg);
+    dfree(lb_inc);
     dfree(text);
     dfree(ctl);
     if (hres) (void)hipHostFree(hres);
@@ -850,7 +901,7 @@ int replica_merge_inc(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_
     }
     if (fast) {
         IncArgs a = make_args(r, s, s.n, r.n - s.n);
-        rc = inc_run(E, s, a);
+        rc = inc_run(E, s, a, text != nullptr);
         if (rc) return rc;
         if (s.hres[0] == 0) {
             if (s.hres[1] != r.vis_bytes || s.hres[2] != r.vis_cp) {

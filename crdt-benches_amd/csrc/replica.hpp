@@ -26,10 +26,10 @@ struct IncState {
     uint32_t* seq[2] = {nullptr, nullptr};  // rank -> slot (ping-pong: seq[cur] is current)
     int cur = 0;
     uint32_t* rank = nullptr;        // slot -> rank
-    uint32_t* ins = nullptr;         // new items in order: kIncMax slots, then kIncMax anchors
-    uint64_t ins_cap = 0;
-    uint4* bsum = nullptr;           // per splice block
-    uint64_t bsum_cap = 0;
+    uint32_t* lb_flag = nullptr;     // per tile of the order: look-back status, aggregate and
+    uint64_t* lb_agg = nullptr;      //   inclusive prefix of the text (incr.hip inc_lookback)
+    uint64_t* lb_inc = nullptr;
+    uint64_t lb_cap = 0;
     uint8_t* text = nullptr;
     uint64_t text_cap = 0;
     uint64_t* ctl = nullptr;         // device counters (incr.hip ICtl)

@@ -41,14 +41,8 @@ def _checkpoints(ctx, oracle, name, K, every_oracle=1):
     return paths
 
 
-@pytest.mark.parametrize("coop", [1, 0])
-def test_incremental_len_every_1000_patches_sveltecomponent(ctx, oracle, coop):
-    """coop 1: the three phases in one cooperative launch; 0: three launches (the default)."""
-    ctx.set_param("inc_coop", coop)
-    try:
-        paths = _checkpoints(ctx, oracle, "sveltecomponent", 1000)
-    finally:
-        ctx.set_param("inc_coop", 0)
+def test_incremental_len_every_1000_patches_sveltecomponent(ctx, oracle):
+    paths = _checkpoints(ctx, oracle, "sveltecomponent", 1000)
     # the first call builds the state; every later one is a local edit batch (keys increase)
     assert paths[0] in (0, "big") and all(p in (1, "big") for p in paths[1:]), paths
     assert paths.count(1) >= len(paths) // 2, paths

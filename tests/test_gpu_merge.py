@@ -482,3 +482,37 @@ def test_rccl_single_rank_allgather(ctx):
     big = np.arange(16384, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
     assert np.array_equal(c.allgather_u64(big, 1), big)
     c.close()
+
+
+@pytest.mark.parametrize("relabel", ["rotate", "shuffle"])
+def test_batch_mixed_ascii_and_escaped_codepoints(ctx, oracle, relabel):
+    """Resident batches can read the 2-byte character column (Engine::build_cp2, param cp2):
+    ASCII characters inline, every other codepoint an escape into a side table.  Documents with a few escaped
+    codepoints scattered among ASCII (2-, 3- and 4-byte UTF-8, some deleted), relabelled, against
+    the oracle; and the same batch with the 3-byte column (cp2 off) gives the same digests."""
+    rng = np.random.default_rng(11)
+    logs = []
+    for n, p_esc in ((30_000, 0.02), (5_000, 0.3), (20_000, 0.0005)):
+        ids = np.arange(1, n + 1, dtype=np.uint32)
+        parent = np.where(rng.random(n) < 0.9, ids - 1, rng.integers(0, ids, dtype=np.uint32))
+        deleted = (rng.random(n) < 0.1).astype(np.uint8)
+        cp = rng.integers(0x20, 0x7F, n, dtype=np.uint32)
+        esc = rng.random(n) < p_esc
+        cp[esc] = rng.choice([0xE9, 0x4E2D, 0x1F600, 0x7FF, 0x800, 0xFFFF, 0x10000],
+                             int(esc.sum())).astype(np.uint32)
+        logs.append(crdt_hip.LogArrays(parent, ids, np.zeros(n, np.uint16), deleted, cp))
+    refs = [oracle.merge(to_anchor(lg)) for lg in logs]
+    want = [oracle.tree_digest(r) for r in refs]
+    digests = {}
+    for cp2 in (1, 0):
+        ctx.set_param("cp2", cp2)
+        try:
+            b = ctx.batch(logs, replicas=3, relabel=relabel, seed=21)
+            d, l, _ = b.merge()
+            b.close()
+        finally:
+            ctx.set_param("cp2", 0)
+        for i, (x, y) in enumerate(zip(d, l)):
+            assert int(x) == want[i % 3] and int(y) == len(refs[i % 3]), (cp2, i)
+        digests[cp2] = list(map(int, d))
+    assert digests[0] == digests[1]
