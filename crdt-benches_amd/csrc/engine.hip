@@ -34,6 +34,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -1724,7 +1725,8 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     return true;
 }
 
-__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
+// One document (workgroup descriptor widx); the kernel below runs it once per descriptor.
+__device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
     __shared__ uint32_t nwide, flags, visited_lds;
@@ -1734,7 +1736,7 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     const uint32_t t = threadIdx.x;
     // the plan check and the workgroup's document (written by k_doctotals in LPT order: document,
     // first run, runs, text offset / length) in one round of loads
-    const uint4 wg = a.wg[2u * blockIdx.x], wg1 = a.wg[2u * blockIdx.x + 1u];
+    const uint4 wg = a.wg[2u * widx], wg1 = a.wg[2u * widx + 1u];
     if (replan(a.ctl)) return;
     const uint32_t d = wg.x, base = wg.y, R = wg.z;
     (void)d;
@@ -2253,6 +2255,10 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
         if (flags & 4u) atomicOr(&a.ctl[C_ERR], 2u);
     }
 }
+
+// Level 1 in LDS: one workgroup per document descriptor (LPT order).  (A persistent form that
+// walks several descriptors per workgroup spilled 34 VGPRs: not used.)
+__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) { doctree_doc(a, blockIdx.x); }
 // ---------------------------------------------------------------------------------------------
 // digest: xxh64 of 4 KiB leaves, then xxh64 of the leaf digests seeded with the length
 // ---------------------------------------------------------------------------------------------
@@ -2710,8 +2716,20 @@ std::string Engine::init(int dev) {
         return hipGetErrorString(e);
     if ((e = hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_hi)) != hipSuccess)
         return hipGetErrorString(e);
-    if ((e = hipStreamCreateWithPriority(&stream_l1, hipStreamNonBlocking, prio_lo)) != hipSuccess)
+    // (experiment, CRDT_L1_CU_KEEP=k in 1..7: the level-1 stream of l1_split runs on k of every 8
+    // CUs, leaving the rest to another lane's level 0)
+    const char* keep = std::getenv("CRDT_L1_CU_KEEP");
+    const int k = keep ? std::atoi(keep) : 0;
+    if (k >= 1 && k <= 7) {
+        uint32_t mask[16] = {};
+        for (int cu = 0; cu < 512; ++cu)
+            if (cu % 8 < k) mask[cu / 32] |= 1u << (cu % 32);
+        if ((e = hipExtStreamCreateWithCUMask(&stream_l1, 16, mask)) != hipSuccess)
+            return hipGetErrorString(e);
+    } else if ((e = hipStreamCreateWithPriority(&stream_l1, hipStreamNonBlocking, prio_lo)) !=
+               hipSuccess) {
         return hipGetErrorString(e);
+    }
     if ((e = hipEventCreateWithFlags(&ev_l0_, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ev_l1_, hipEventDisableTiming)) != hipSuccess)
         return hipGetErrorString(e);
