@@ -155,6 +155,8 @@ struct L0Args {
     // prefix count per 64 slots (offset to the wave's first chunk); null: gather in_parent
     const uint32_t* nsq_par;
     const uint32_t* nsq_pre;
+    const uint64_t* nsq_key;    // (beside nsq_par) the keys of the nsq items: every nsq item that
+                                //   survives is a run head, whose key k_runs then need not gather
     // resident batches (Engine::build_cp2): the 2-byte character column (an ASCII character, or
     // an escape to xcp, and the three flags), the escaped codepoints in slot order with their
     // prefix count per 64 slots (offset to the wave), and one bit per 16 slots with an escape
@@ -608,8 +610,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     const uint2 pre = a.tile_hw[tile];
     // the parents of the tile's nsq items: the compact list of a resident batch, else the tile's
     // plist segment k_classify wrote
-    const uint32_t* pls = a.nsq_par ? a.nsq_par + a.nsq_pre[tile * (kScanTile / 64)]
-                                    : a.plist + (uint64_t)tile * kScanTile;
+    const uint32_t nlo = a.nsq_par ? a.nsq_pre[tile * (kScanTile / 64)] : 0u;
+    const uint32_t* pls = a.nsq_par ? a.nsq_par + nlo : a.plist + (uint64_t)tile * kScanTile;
     if (gs < a.nslots) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
@@ -738,16 +740,20 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const uint2 dc = ldoc[li >> 4];
         const bool root = g == dc.x;
         const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
+        // a non-seq head's parent from the tile's list: its index = the non-seq items before it;
+        // (resident batches) its key from the same index of the key list, a seq head's gathered
+        const uint32_t nw = lnsq[li >> 4];
+        const uint32_t lix = lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u));
 #ifdef CRDT_EXP_NOKEY
         const uint64_t key = g;  // (timing experiment: no key gather)
 #else
-        const uint64_t key = a.in_key[g];
+#ifndef CRDT_NO_NSQ_KEY
+        const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
+#else
+        const uint64_t key = a.in_key[g];  // (A/B build: every head's key gathered)
 #endif
-        // a non-seq head's parent from the tile's list: its index = the non-seq items before it
-        const uint32_t nw = lnsq[li >> 4];
-        uint32_t p = (!sq && !root)
-                         ? pls[lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u))]
-                         : 0u;
+#endif
+        uint32_t p = (!sq && !root) ? pls[lix] : 0u;
         a.r_head[rho] = g;
         a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
         if (two) {
@@ -2539,12 +2545,16 @@ __global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt) {
     if (c * 64ull >= a.nslots) return;
     cnt[c] = (uint32_t)__popcll(chunk_nsq_bits(a, c * 64u));
 }
-__global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t* pre, uint32_t* out) {
+__global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t* pre, uint32_t* out,
+                                                        uint64_t* kout) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c * 64ull >= a.nslots) return;
     uint32_t o = pre[c];
-    for (uint64_t b = chunk_nsq_bits(a, c * 64u); b; b &= b - 1ull)
-        out[o++] = a.in_parent[c * 64u + (uint32_t)__builtin_ctzll(b)];
+    for (uint64_t b = chunk_nsq_bits(a, c * 64u); b; b &= b - 1ull) {
+        const uint32_t g = c * 64u + (uint32_t)__builtin_ctzll(b);
+        out[o] = a.in_parent[g];
+        kout[o++] = a.in_key[g];
+    }
 }
 
 // ---- the 2-byte character column of a resident batch (Engine::build_cp2) ---------------------
@@ -2660,7 +2670,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 // =============================================================================================
 void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
-    dfree(nsq_par); dfree(nsq_pre);
+    dfree(nsq_par); dfree(nsq_pre); dfree(nsq_key);
     nsq_items = 0;
     dfree(cp2); dfree(xcp); dfree(xpre); dfree(xgrp);
     nesc = 0;
@@ -2716,20 +2726,8 @@ std::string Engine::init(int dev) {
         return hipGetErrorString(e);
     if ((e = hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_hi)) != hipSuccess)
         return hipGetErrorString(e);
-    // (experiment, CRDT_L1_CU_KEEP=k in 1..7: the level-1 stream of l1_split runs on k of every 8
-    // CUs, leaving the rest to another lane's level 0)
-    const char* keep = std::getenv("CRDT_L1_CU_KEEP");
-    const int k = keep ? std::atoi(keep) : 0;
-    if (k >= 1 && k <= 7) {
-        uint32_t mask[16] = {};
-        for (int cu = 0; cu < 512; ++cu)
-            if (cu % 8 < k) mask[cu / 32] |= 1u << (cu % 32);
-        if ((e = hipExtStreamCreateWithCUMask(&stream_l1, 16, mask)) != hipSuccess)
-            return hipGetErrorString(e);
-    } else if ((e = hipStreamCreateWithPriority(&stream_l1, hipStreamNonBlocking, prio_lo)) !=
-               hipSuccess) {
+    if ((e = hipStreamCreateWithPriority(&stream_l1, hipStreamNonBlocking, prio_lo)) != hipSuccess)
         return hipGetErrorString(e);
-    }
     if ((e = hipEventCreateWithFlags(&ev_l0_, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ev_l1_, hipEventDisableTiming)) != hipSuccess)
         return hipGetErrorString(e);
@@ -2747,10 +2745,11 @@ std::string Engine::init(int dev) {
 int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
     // (a new slot layout: the compact nsq list, if any, no longer matches it)
-    if (L.nsq_par || L.nsq_pre || L.cp2) {
+    if (L.nsq_par || L.nsq_pre || L.nsq_key || L.cp2) {
         (void)hipStreamSynchronize(stream);
         dfree(L.nsq_par);
         dfree(L.nsq_pre);
+        dfree(L.nsq_key);
         L.nsq_items = 0;
         dfree(L.cp2); dfree(L.xcp); dfree(L.xpre); dfree(L.xgrp);
         L.nesc = 0;
@@ -3155,6 +3154,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull);  \
     a0.xcd = xcd_order ? 1u : 0u;                                  \
     a0.nsq_par = L.nsq_par;                                         \
+    a0.nsq_key = L.nsq_key;                                         \
     a0.in_cp2 = L.cp2 ? L.cp2 + w.slot0 : nullptr;                  \
     a0.xcp = L.xcp;                                                 \
     a0.xpre = L.xpre ? L.xpre + (w.slot0 >> 6) : nullptr;           \
@@ -3916,6 +3916,7 @@ int Engine::build_nsq(DeviceLogs& L) {
     HIPCHK(hipStreamSynchronize(stream), "nsq list");
     dfree(L.nsq_par);
     dfree(L.nsq_pre);
+    dfree(L.nsq_key);
     L.nsq_items = 0;
     if (!L.total_slots || !nsq_list) return CRDT_HIP_OK;
     const bool ord = false;  // (L0ARGS)
@@ -3939,10 +3940,11 @@ int Engine::build_nsq(DeviceLogs& L) {
     dfree(sums);
     if (e != hipSuccess) return fail("nsq scan", e);
     HIPCHK(dalloc(&L.nsq_par, (uint64_t)total + 1), "hipMalloc nsq list");
+    HIPCHK(dalloc(&L.nsq_key, (uint64_t)total + 1), "hipMalloc nsq keys");
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
         k_nsq_scatter<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(
-            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par);
+            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par, L.nsq_key);
     }
     HIPCHK(hipGetLastError(), "nsq list launch");
     HIPCHK(hipStreamSynchronize(stream), "nsq list");

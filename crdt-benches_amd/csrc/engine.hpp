@@ -110,6 +110,8 @@ struct DeviceLogs {
     // of gathering the parent column.  Null for logs that change (uploads, replicas).
     uint32_t* nsq_par = nullptr;
     uint32_t* nsq_pre = nullptr;
+    uint64_t* nsq_key = nullptr;   // beside nsq_par: the items' keys (k_runs reads a non-seq
+                                   //   head's key there instead of gathering it)
     uint64_t nsq_items = 0;
     // Resident batches (Engine::build_cp2): the 2-byte character column (ASCII byte or escape,
     // plus the flags), the escaped codepoints in slot order and their prefix count per 64 slots,

@@ -116,8 +116,11 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
 
 #define INC_TS(i) \
     if (a.tsp && threadIdx.x == 0) a.tsp[i] = wall_clock64()
+// (sl / cwq: the splice's old order of this tile and its codepoint words, gathered here beside
+// the forest's own dependent loads so that the splice does not wait for them)
 __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint32_t* red,
-                                           uint32_t& flag) {
+                                           uint32_t& flag, const uint32_t (&sl)[kSpliceRanks],
+                                           uint32_t (&cwq)[kSpliceRanks]) {
     constexpr uint32_t Q = kIncMax / kIncThreads;  // items per thread
     const uint32_t t = threadIdx.x, m = a.m, n0 = a.n0;
     uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
@@ -145,6 +148,8 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             kk[q] = i < m ? a.key[n0 + 1u + i] : 0ull;
         }
         uint32_t bad = 0;
+#pragma unroll
+        for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);
 #pragma unroll
         for (int q = 0; q < (int)Q; ++q) {
             const uint32_t i = t + (uint32_t)q * kIncThreads;
@@ -432,16 +437,14 @@ __device__ __forceinline__ uint32_t anchored_before(const uint32_t* la, uint32_t
 __device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, uint32_t* red,
                                                  uint32_t* cb, const uint32_t* os,
                                                  const uint32_t* la, uint32_t* cwl,
-                                                 const uint32_t (&sl)[kSpliceRanks], uint2& range) {
+                                                 const uint32_t (&sl)[kSpliceRanks],
+                                                 const uint32_t (&cwq)[kSpliceRanks], uint2& range) {
     const uint32_t N0 = a.n0 + 1u, m = a.m;
     const uint32_t k0 = b * kSpliceTile, k1 = min(N0, k0 + kSpliceTile);
     // the tile's first output place (every thread finds it: the words go to LDS at place - o0)
     const uint32_t o0 = k0 + (m ? anchored_before(la, m, k0) : 0u);
     if (threadIdx.x < 2u) cb[threadIdx.x] = m ? anchored_before(la, m, threadIdx.x ? k1 : k0) : 0u;
     const uint32_t kb = k0 + threadIdx.x * kSpliceRanks;
-    uint32_t cwq[kSpliceRanks];
-#pragma unroll
-    for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = kb + q < k1 ? slot_word(a.cp, sl[q]) : kDelBitI;
     uint32_t bytes = 0, cps = 0;
     // c(k) for the thread's first rank by binary search; the next ranks search again only past
     // an anchor (a whole subtree of new items shares one anchor, so no linear walk over them)
@@ -589,9 +592,14 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = kb + q < k1 ? a.seq[kb + q] : 0u;
     }
+    uint32_t cwq[kSpliceRanks];
     if (a.m) {
-        inc_forest(a, lds, red, flag);
-    } else if (threadIdx.x == 0) {
+        inc_forest(a, lds, red, flag, sl, cwq);
+    } else {
+#pragma unroll
+        for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);
+    }
+    if (!a.m && threadIdx.x == 0) {
         flag = 0;
         if (blockIdx.x == 0) {  // (carry the largest key over to this call's slot)
             const uint64_t km = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
@@ -608,7 +616,7 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
         // the tile's codepoint words by place, in the forest's tour region (dead by now)
         uint32_t* cwl = reinterpret_cast<uint32_t*>(lds + 12u * kIncMax + 4u * (kIncMax + 2u));
         uint2 range;
-        const uint2 agg = inc_splice_tile(a, b, red, cb, os, la, cwl, sl, range);
+        const uint2 agg = inc_splice_tile(a, b, red, cb, os, la, cwl, sl, cwq, range);
         const uint64_t agg64 = ((uint64_t)agg.y << 32) | agg.x;
         const uint64_t excl = inc_lookback(a, b, agg64, &excl_lds);
         const uint64_t base = (uint32_t)excl;
