@@ -545,10 +545,10 @@ def traces_workload(args) -> int:
                 "note": "one-time, untimed: upload of the 4 resolved logs and the device build of "
                         "every replica's resident op log (relabelled parent u32, key u64 = lamport "
                         "<< 16 | agent, 3-byte codepoint word with the tombstone and previous-slot "
-                        "flags: O(1) per item) and of the compact list of the parents of the items "
-                        "without the previous-slot flag (u32 each, slot order, a prefix count per "
-                        "64 slots; Engine::build_nsq); the traffic contract (DESIGN.md section 7) "
-                        "prices the merge over this format"},
+                        "flags: O(1) per item) and of the compact list of the items without the "
+                        "previous-slot flag (parent u32 and key u64 each, slot order, a prefix "
+                        "count per 64 slots; Engine::build_nsq); the traffic contract (DESIGN.md "
+                        "section 7) prices the merge over this format"},
             "resolve": {"ms_per_trace": dict(zip(TRACES, inputs["resolve_ms"])),
                         "ms_total_one_core": sum(inputs["resolve_ms"]),
                         "ms_all_parallel": inputs["resolve_parallel_ms"],
