@@ -111,6 +111,7 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
            + 4u * (2u * mmax + 4u)   // tour successor (u16) and suffix sum (u16), packed u32
            + 2u * mmax               // vrk: ranks among many roots, then run heads (u16)
            + 2u * mmax               // rend: the last item of each run (u16)
+           + 2u * (mmax + 2u)        // cs: children by segment, sorted (u16)
            + 64u;
 }
 
@@ -131,13 +132,14 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     uint16_t* ch = lp + (kIncMax + 2u);                     // kIncMax + 2
     uint16_t* vrk = ch + (kIncMax + 2u);                    // kIncMax: ranks among the roots
     uint16_t* rend = vrk + kIncMax;                         // kIncMax: the last item of a run
+    uint16_t* cs = rend + kIncMax;                          // kIncMax + 2: ch sorted
     if (t == 0) flag = 0;
     INC_TS(0);
     const uint64_t maxkey0 = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
-    // ---- load: parents, keys, anchors; counts cleared ----
+    // ---- load: parents, keys, anchors; child counts (each child keeps its place among its
+    // parent's children).  The counts are cleared while the loads are in flight ----
     uint32_t plc[Q];
     uint64_t kmax = 0;
-    for (uint32_t x = t; x <= m + 1u; x += kIncThreads) start[x] = 0;
     {
         uint32_t pp[Q];
         uint64_t kk[Q];
@@ -150,33 +152,32 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         uint32_t bad = 0;
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);
+        for (uint32_t x = t; x <= m + 1u; x += kIncThreads) start[x] = 0;
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < (int)Q; ++q) {
             const uint32_t i = t + (uint32_t)q * kIncThreads;
+            plc[q] = 0;
             if (i >= m) continue;
             keys[i] = kk[q];
             kmax = max(kmax, kk[q]);
+            uint32_t li;
             if (pp[q] <= n0) {  // a root: after its old parent, ahead of the parent's old children
-                lp[i] = (uint16_t)m;
+                li = m;
                 A[i] = a.rank[pp[q]];
                 if (kk[q] <= maxkey0) bad |= (uint32_t)F_KEY;
             } else {
                 const uint32_t l = pp[q] - (n0 + 1u);
                 if (l >= i) bad |= (uint32_t)F_ORDER;  // (parents precede their children)
-                lp[i] = (uint16_t)(l < i ? l : m);
+                li = l < i ? l : m;
                 A[i] = 0;
             }
+            lp[i] = (uint16_t)li;
+            plc[q] = atomicAdd(&start[li], 1u);
         }
         if (bad) atomicOr(&flag, bad);
     }
     INC_TS(1);
-    __syncthreads();
-    // ---- child counts; each child keeps its place among its parent's children ----
-#pragma unroll
-    for (int q = 0; q < (int)Q; ++q) {
-        const uint32_t i = t + (uint32_t)q * kIncThreads;
-        plc[q] = i < m ? atomicAdd(&start[lp[i]], 1u) : 0u;
-    }
     INC_TS(2);
     __syncthreads();
     // ---- segment starts: exclusive scan over nodes 0..m (m + 1 <= kIncMax + 1 counts) ----
@@ -253,13 +254,13 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         }
         rk[q] = r;
     }
-    INC_TS(5);
-    __syncthreads();
+    // (sorted into a second array: ch is still being read by other threads)
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t i = t + (uint32_t)q * kIncThreads;
-        if (i < m) ch[start[lp[i]] + rk[q]] = (uint16_t)i;
+        if (i < m) cs[start[lp[i]] + rk[q]] = (uint16_t)i;
     }
+    INC_TS(5);
     INC_TS(6);
     __syncthreads();
     if (flag) return;  // (block-uniform after the barrier)
@@ -313,16 +314,16 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         if (x >= m || hd[x] != x) continue;
         const uint32_t e = rend[x];
         const uint32_t c0 = start[e], c1 = start[e + 1u];
-        const uint32_t sd = c1 > c0 ? 2u * ch[c0] : 2u * x + 1u;
+        const uint32_t sd = c1 > c0 ? 2u * cs[c0] : 2u * x + 1u;
         const uint32_t p = lp[x], pos = start[p] + rk[q];
         const uint32_t pr = p == V ? V : hd[p];  // (a parent is always the last item of its run)
-        const uint32_t su = pos + 1u < start[p + 1u] ? 2u * ch[pos + 1u] : 2u * pr + 1u;
+        const uint32_t su = pos + 1u < start[p + 1u] ? 2u * cs[pos + 1u] : 2u * pr + 1u;
         tour[2u * x] = sd | ((e - x + 1u) << 16);
         tour[2u * x + 1u] = su;
     }
     if (t == 0) {
         const uint32_t c0 = start[V], c1 = start[V + 1u];
-        tour[2u * V] = c1 > c0 ? 2u * ch[c0] : 2u * V + 1u;
+        tour[2u * V] = c1 > c0 ? 2u * cs[c0] : 2u * V + 1u;
         tour[2u * V + 1u] = E;
         tour[E] = E;
     }
@@ -434,7 +435,7 @@ __device__ __forceinline__ uint32_t anchored_before(const uint32_t* la, uint32_t
 // Tile b takes old ranks [k0, k1) and the new items anchored in [k0, k1) (os / la: the new items
 // by place, in LDS): its outputs are the places [k0 + c(k0), k1 + c(k1)), c(k) = new items
 // anchored before k.  Returns {bytes, codepoints} of its outputs; range = its output places.
-__device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, uint32_t* red,
+__device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, uint32_t* rsum,
                                                  uint32_t* cb, const uint32_t* os,
                                                  const uint32_t* la, uint32_t* cwl,
                                                  const uint32_t (&sl)[kSpliceRanks],
@@ -474,9 +475,21 @@ __device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, u
         bytes += w;
         cps += w ? 1u : 0u;
     }
-    uint32_t tb, tc;
-    (void)block_excl_scan<kIncThreads / 64>(bytes, red, tb);
-    (void)block_excl_scan<kIncThreads / 64>(cps, red, tc);
+    // the tile's totals (one barrier; rsum is used for nothing else, so no trailing barrier)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    bytes = wave_incl_scan(bytes);
+    cps = wave_incl_scan(cps);
+    if (lane == 63u) {
+        rsum[wv] = bytes;
+        rsum[kIncThreads / 64 + wv] = cps;
+    }
+    __syncthreads();
+    uint32_t tb = 0, tc = 0;
+#pragma unroll
+    for (int i = 0; i < (int)(kIncThreads / 64); ++i) {
+        tb += rsum[i];
+        tc += rsum[kIncThreads / 64 + i];
+    }
     range = make_uint2(k0 + c0, k1 + c1);
     return make_uint2(tb, tc);
 }
@@ -580,6 +593,7 @@ __device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint2 range, uin
 __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t red[kIncThreads / 64];
+    __shared__ uint32_t rsum[2 * (kIncThreads / 64)];
     __shared__ uint32_t cb[2];
     __shared__ uint32_t flag;
     __shared__ uint64_t excl_lds;
@@ -616,7 +630,7 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
         // the tile's codepoint words by place, in the forest's tour region (dead by now)
         uint32_t* cwl = reinterpret_cast<uint32_t*>(lds + 12u * kIncMax + 4u * (kIncMax + 2u));
         uint2 range;
-        const uint2 agg = inc_splice_tile(a, b, red, cb, os, la, cwl, sl, cwq, range);
+        const uint2 agg = inc_splice_tile(a, b, rsum, cb, os, la, cwl, sl, cwq, range);
         const uint64_t agg64 = ((uint64_t)agg.y << 32) | agg.x;
         const uint64_t excl = inc_lookback(a, b, agg64, &excl_lds);
         const uint64_t base = (uint32_t)excl;
