@@ -47,6 +47,10 @@ import numpy as np  # noqa: E402
 crdt_hip = None  # the engine binding, imported once this process knows it is a rank
 
 TRACES = ["automerge-paper", "rustcode", "sveltecomponent", "seph-blog1"]
+# (experiments only: CRDT_BENCH_TRACES=a,b restricts the batch to those traces; bench lines
+# use all four)
+if os.environ.get("CRDT_BENCH_TRACES"):
+    TRACES = [t for t in TRACES if t in os.environ["CRDT_BENCH_TRACES"].split(",")]
 METRIC = "merged CRDT ops/sec (whole node) + achieved HBM GB/s, batched trace merge"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Minimum HBM traffic of the design (the §8(d) contract restated for the
@@ -381,7 +385,7 @@ def traces_rank(args, comm, make_batch, inputs) -> dict | None:
 
     dig, lens, stats, elapsed = merge_steps(batch, comm, args.warmup, args.steps, on_warmup)
     expect = expected_digests(inputs["digests"], batch.docs)
-    surv = np.array([inputs["survivors"][d % 4] for d in range(batch.docs)], np.uint64)
+    surv = np.array([inputs["survivors"][d % len(TRACES)] for d in range(batch.docs)], np.uint64)
     ok_local = bool(np.array_equal(dig, expect)) and bool(np.array_equal(lens, surv))
     patches_rank = sum(inputs["patches"]) * args.replicas
     cnt = np.array([patches_rank, batch.items, stats[0]["runs"], stats[0]["text_bytes"],
