@@ -1444,9 +1444,8 @@ constexpr int kDocJ = CRDT_DOC_J;  // runs per thread: documents of up to kDocJ 
 #endif
 // splitters: one run per block of 2^kDocLog2S consecutive runs, at a hashed position inside the
 // block (block 0: the document start), so that no chain of the tour whose run indices share a
-// residue can miss every splitter; splitter b = block b; kDocK per thread
+// residue can miss every splitter; splitter b = block b; (J + S - 1) / S per thread
 constexpr uint32_t kDocLog2S = CRDT_DOC_LOG2S;
-constexpr int kDocK = (kDocJ + (1 << kDocLog2S) - 1) >> kDocLog2S;
 #ifndef CRDT_DOC_HASHSPLIT
 #define CRDT_DOC_HASHSPLIT 1
 #endif
@@ -1633,9 +1632,10 @@ __device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, 
     }
 }
 
+template <int J>
 __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t p0, uint64_t toff,
                                          uint32_t tiles, uint32_t tpx_reg,
-                                         const uint32_t (&ro)[kDocJ], const uint32_t (&ps)[kDocJ],
+                                         const uint32_t (&ro)[J], const uint32_t (&ps)[J],
                                          uint8_t* st, uint32_t* scan_lds, uint64_t* tprobe) {
     const uint32_t t = threadIdx.x;
     const uint32_t sh = p0 & 15u;
@@ -1646,7 +1646,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     const uint32_t t0 = tiles & 0xFFFFFu, nt = tiles >> 20;
     uint32_t mine = 0;
 #pragma unroll
-    for (int j = 0; j < kDocJ; ++j) mine += ro[j] != kNil ? 1u : 0u;
+    for (int j = 0; j < J; ++j) mine += ro[j] != kNil ? 1u : 0u;
     uint32_t Rw;
     (void)block_excl_scan<kDocThreads / 64>(mine, scan_lds, Rw);
     const uint32_t o_tab = (o_delta + 4u * Rw + 15u) & ~15u;
@@ -1682,7 +1682,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
         __syncthreads();
         // 2) run starts -> ranks in document order -> staging offset minus document offset
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j)
+        for (int j = 0; j < J; ++j)
             if (ro[j] != kNil) atomicOr(&bits[ro[j] >> 5], 1u << (ro[j] & 31u));
         __syncthreads();
         {
@@ -1699,7 +1699,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             if (ro[j] == kNil) continue;
             const uint32_t wd = ro[j] >> 5;
             const uint32_t rank = pref[wd] + (uint32_t)__popc(bits[wd] & ((1u << (ro[j] & 31u)) - 1u));
@@ -1732,7 +1732,9 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
 }
 
 // One document (workgroup descriptor widx); the kernel below runs it once per descriptor.
+template <int J>
 __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
+    constexpr int KK = (J + (1 << kDocLog2S) - 1) >> kDocLog2S;
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     __shared__ uint32_t scan_lds[kDocThreads / 64];
     __shared__ uint32_t nwide, flags, visited_lds;
@@ -1773,7 +1775,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         probe_max = probe_sum = 0;
 #endif
     }
-    if (R + 2u > a.rcap || S > a.scap || R > (uint32_t)(kDocJ * kDocThreads)) {
+    if (R + 2u > a.rcap || S > a.scap || R > (uint32_t)(J * kDocThreads)) {
         if (t == 0) atomicOr(&a.ctl[C_ERR], 32u);  // host sized rcap/scap from the largest document
         return;
     }
@@ -1783,7 +1785,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     // for a global gather; the weights are loaded later (doc_weights), beside the sorts.
     // pk[j]: the parent of run t + 1024 j (kNil16: none), then | its place among the parent's
     // children << 16 (from the count's atomic): the placement needs no second atomic
-    uint32_t pk[kDocJ];
+    uint32_t pk[J];
     // (stile_text) this lane's entry of the document's tile prefix table, used by phase C
     uint32_t tpx_reg = 0;
     if (a.stile_text) {
@@ -1791,10 +1793,10 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         if (t <= nt + 1u) tpx_reg = t0 + t < a.ntiles ? a.tile_hw[t0 + t].y : a.ctl[C_WTOTAL];
     }
     {
-        uint32_t gp[kDocJ];
-        uint64_t gk[kDocJ];
+        uint32_t gp[J];
+        uint64_t gk[J];
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             gp[j] = v < R ? a.r_parent[base + v] : 0u;
             gk[j] = v < R ? a.r_key[base + v] : 0ull;
@@ -1802,7 +1804,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
         uint32_t bad = 0;
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t p = kNil16;
             if (v < R) {
@@ -1821,7 +1823,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     PROBE(1);
     // ---- child counts (u16 counters, two per LDS dword); each child keeps its place ----------
 #pragma unroll
-    for (int j = 0; j < kDocJ; ++j) {
+    for (int j = 0; j < J; ++j) {
         const uint32_t p = pk[j];
         if (p != kNil16) {
             const uint32_t sh = 16u * (p & 1u);
@@ -1850,7 +1852,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     PROBE(3);
     // ---- placement: segment start + the place the count handed out ---------------------------
 #pragma unroll
-    for (int j = 0; j < kDocJ; ++j) {
+    for (int j = 0; j < J; ++j) {
         const uint32_t p = pk[j] & 0xFFFFu;
         if (p != kNil16) ch[D[p] + (pk[j] >> 16)] = (uint16_t)(t + (uint32_t)j * kDocThreads);
     }
@@ -1866,21 +1868,21 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     // network per thread, 9..64 by one wave per group; wider groups hand the wave to the global
     // path.  fcs[j]: 0x10000 | the segment start of run t + 1024 j's children (its first child
     // once they are ordered), or kNil16 for a leaf.
-    uint32_t fcs[kDocJ];
+    uint32_t fcs[J];
     if (t == 0) nx[0] = kNil16;
     {
         // cw[j]: as a child, its group's start | (1 << 14: an only child) | (1 << 15: a pair) |
         // (the pair's other member << 16)
-        uint32_t cw[kDocJ], pw[kDocJ];
+        uint32_t cw[J], pw[J];
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t p = pk[j] & 0xFFFFu, v = t + (uint32_t)j * kDocThreads;
             const uint32_t q = p != kNil16 ? p : R, u = v < R ? v : R;  // (D[R] .. D[R + 1]: none)
             cw[j] = (uint32_t)D[q] | ((uint32_t)D[q + 1u] << 16);
             pw[j] = (uint32_t)D[u] | ((uint32_t)D[u + 1u] << 16);
         }
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             // as a parent
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             const uint32_t b = pw[j] & 0xFFFFu, pc = (pw[j] >> 16) - b;
@@ -1897,7 +1899,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
                     (o << 16);
         }
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             const uint32_t up = (pk[j] & 0xFFFFu) | kUp16, s0 = cw[j] & 0x3FFFu;
             if (cw[j] & (1u << 14)) {
@@ -1919,18 +1921,18 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     // wider groups cover their latency: differences of consecutive weight prefixes, the next
     // run's prefix from the next lane (lane 63 loads it; v = R - 1 reads the next document's
     // first run or the sentinel)
-    uint32_t wr[kDocJ];
+    uint32_t wr[J];
     {
-        uint32_t gn[kDocJ];
+        uint32_t gn[J];
         const bool l63 = (t & 63u) == 63u;
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             wr[j] = v <= R ? a.r_pstart[base + v] : 0u;  // (v = R: the next lane's successor)
             gn[j] = (l63 && v < R) ? a.r_pstart[base + v + 1] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             const uint32_t nxt = (uint32_t)__shfl_down((int)wr[j], 1);
             wr[j] = v < R ? (l63 ? gn[j] : nxt) - wr[j] : 0u;
@@ -2002,9 +2004,9 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     // ---- first children of the sorted groups; the run records --------------------------------
     uint32_t act = 0;  // bit j: run t + 1024 j still has an up link (see below)
     {
-        uint32_t fx[kDocJ], wx[kDocJ];
+        uint32_t fx[J], wx[J];
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t f = fcs[j], n = 0;
             if (v < R) {
@@ -2019,7 +2021,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             if (v < R) rec[v] = make_uint2(fx[j], wx[j]);
         }
@@ -2126,9 +2128,9 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     PROBE(7);
     // the slot-order text prefixes of the owned runs, for phase C: loaded now, so that the
     // pointer jumping and the offsets cover their latency
-    uint32_t ps[kDocJ];
+    uint32_t ps[J];
 #pragma unroll
-    for (int j = 0; j < kDocJ; ++j) {
+    for (int j = 0; j < J; ++j) {
         const uint32_t v = t + (uint32_t)j * kDocThreads;
         ps[j] = (a.text && v < R) ? a.r_pstart[base + v] : 0u;
     }
@@ -2138,9 +2140,9 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     // equally right: the jumping runs without barriers, each thread until its own records reach
     // the end (every pass advances a record by at least one splitter: S passes bound it).
     {
-        uint32_t x[kDocK], live = 0;
+        uint32_t x[KK], live = 0;
 #pragma unroll
-        for (int k = 0; k < kDocK; ++k) {
+        for (int k = 0; k < KK; ++k) {
             const uint32_t s = t + (uint32_t)k * kDocThreads;
             x[k] = s < S ? srec[s] : kNil14;
             live |= ((x[k] & kNil14) != kNil14 ? 1u : 0u) << k;
@@ -2150,11 +2152,11 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
                 atomicOr(&flags, 4u);
                 break;
             }
-            uint32_t y[kDocK];
+            uint32_t y[KK];
 #pragma unroll
-            for (int k = 0; k < kDocK; ++k) y[k] = ((live >> k) & 1u) ? lds_ld32(srec + (x[k] & kNil14)) : 0u;
+            for (int k = 0; k < KK; ++k) y[k] = ((live >> k) & 1u) ? lds_ld32(srec + (x[k] & kNil14)) : 0u;
 #pragma unroll
-            for (int k = 0; k < kDocK; ++k) {
+            for (int k = 0; k < KK; ++k) {
                 if (!((live >> k) & 1u)) continue;
                 x[k] = (x[k] & ~kNil14) + y[k];  // sums add, the link jumps
                 lds_st32(srec + t + (uint32_t)k * kDocThreads, x[k]);
@@ -2169,11 +2171,11 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         return;
     }
     // ---- run offsets: sublist offset (total - suffix of its splitter) + offset inside ------
-    uint32_t ro[kDocJ];  // document offset of every owned run with visible bytes, else kNil
+    uint32_t ro[J];  // document offset of every owned run with visible bytes, else kNil
     {
         const uint32_t total = srec[0] >> 14;
 #pragma unroll
-        for (int j = 0; j < kDocJ; ++j) {
+        for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t pk = 0xFFFFFFFFu;
             if (v < R) pk = rec32[2u * v + 1u];
@@ -2183,7 +2185,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         }
         if (!a.text) {  // offsets for k_expand
 #pragma unroll
-            for (int j = 0; j < kDocJ; ++j)
+            for (int j = 0; j < J; ++j)
                 if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ro[j];
         }
     }
@@ -2211,7 +2213,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             const uint32_t tl = wg1.x;
             bool oob = false;
 #pragma unroll
-            for (int j = 0; j < kDocJ; ++j) {
+            for (int j = 0; j < J; ++j) {
                 const uint32_t v = t + (uint32_t)j * kDocThreads;
                 if (ro[j] == kNil) continue;
                 const uint32_t wv = a.r_pstart[base + v + 1] - ps[j];
@@ -2264,7 +2266,31 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 
 // Level 1 in LDS: one workgroup per document descriptor (LPT order).  (A persistent form that
 // walks several descriptors per workgroup spilled 34 VGPRs: not used.)
-__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) { doctree_doc(a, blockIdx.x); }
+// The document's run count picks the instance: every per-run loop is unrolled J times, so a
+// document of at most 4096 / 8192 runs skips the empty slots of the 12-run instance.
+#ifndef CRDT_DOC_JSET
+#define CRDT_DOC_JSET 1
+#endif
+template <int J>
+__device__ __forceinline__ bool doctree_try(const DocArgs& a, uint32_t R) {
+    if (J > kDocJ || R > (uint32_t)J * kDocThreads) return false;
+    doctree_doc<(J > kDocJ ? kDocJ : J)>(a, blockIdx.x);
+    return true;
+}
+__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
+    const uint32_t R = a.wg[2u * blockIdx.x].z;
+    (void)R;
+#if CRDT_DOC_JSET == 1
+    if (doctree_try<4>(a, R) || doctree_try<8>(a, R)) return;
+#elif CRDT_DOC_JSET == 2
+    if (doctree_try<3>(a, R) || doctree_try<7>(a, R) || doctree_try<8>(a, R) ||
+        doctree_try<10>(a, R))
+        return;
+#elif CRDT_DOC_JSET == 3
+    if (doctree_try<4>(a, R) || doctree_try<8>(a, R) || doctree_try<10>(a, R)) return;
+#endif
+    doctree_doc<kDocJ>(a, blockIdx.x);
+}
 // ---------------------------------------------------------------------------------------------
 // digest: xxh64 of 4 KiB leaves, then xxh64 of the leaf digests seeded with the length
 // ---------------------------------------------------------------------------------------------
