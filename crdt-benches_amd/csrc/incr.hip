@@ -119,10 +119,13 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
     if (a.tsp && threadIdx.x == 0) a.tsp[i] = wall_clock64()
 // (sl / cwq: the splice's old order of this tile and its codepoint words, gathered here beside
 // the forest's own dependent loads so that the splice does not wait for them)
+// Q: items per thread (m <= Q * kIncThreads); the caller picks the smallest instance that holds
+// the batch, so that no per-item loop runs over empty slots
+template <uint32_t Q>
 __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint32_t* red,
                                            uint32_t& flag, const uint32_t (&sl)[kSpliceRanks],
                                            uint32_t (&cwq)[kSpliceRanks]) {
-    constexpr uint32_t Q = kIncMax / kIncThreads;  // items per thread
+    static_assert(Q * kIncThreads <= kIncMax, "items per thread");
     const uint32_t t = threadIdx.x, m = a.m, n0 = a.n0;
     uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
     uint32_t* A = reinterpret_cast<uint32_t*>(keys + kIncMax);
@@ -182,7 +185,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     __syncthreads();
     // ---- segment starts: exclusive scan over nodes 0..m (m + 1 <= kIncMax + 1 counts) ----
     {
-        constexpr uint32_t P = (kIncMax + 1u + kIncThreads - 1u) / kIncThreads + 1u;
+        constexpr uint32_t P = (Q * kIncThreads + 1u + kIncThreads - 1u) / kIncThreads + 1u;
         const uint32_t lo = min(m + 1u, t * P), hi = min(m + 1u, lo + P);
         uint32_t s = 0;
         for (uint32_t x = lo; x < hi; ++x) s += start[x];
@@ -334,7 +337,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     // successor is equally right; each thread jumps its own arcs (those of run heads and V) until
     // they reach the end (every pass extends a record by at least one arc: E passes bound it) ----
     {
-        constexpr int NA = (int)((2u * kIncMax + 4u + kIncThreads - 1u) / kIncThreads);
+        constexpr int NA = (int)((2u * Q * kIncThreads + 4u + kIncThreads - 1u) / kIncThreads);
         static_assert(NA <= 32, "arcs per thread");
         uint32_t live = 0;
 #pragma unroll
@@ -608,7 +611,12 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     }
     uint32_t cwq[kSpliceRanks];
     if (a.m) {
-        inc_forest(a, lds, red, flag, sl, cwq);
+        if (a.m <= kIncThreads)
+            inc_forest<1>(a, lds, red, flag, sl, cwq);
+        else if (a.m <= 2u * kIncThreads)
+            inc_forest<2>(a, lds, red, flag, sl, cwq);
+        else
+            inc_forest<kIncMax / kIncThreads>(a, lds, red, flag, sl, cwq);
     } else {
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);
