@@ -288,19 +288,51 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
             C[k] = (lo | hi) & 0x00FFFFFFu;
         }
     }
-    // branch-free classification of the 16 slots; weights straight into their nibbles
-    uint32_t nsq = 0, W = 0, vis = 0, lm = 0;
-    uint64_t nib = 0;
+    // classification of the 16 slots as bit masks.  The items are a contiguous range of them
+    // (slot k is an item iff 0 <= l0 + k - 1 < n); the flags are gathered into masks, and a
+    // thread whose codepoints are all ASCII (nearly every thread on the traces) weighs each
+    // visible item 1 byte: its nibbles are its visible bits spread out.  Otherwise (or in ORDER
+    // mode, where every item weighs 1) the weights are taken per slot.
+    uint32_t itm = 0;
+    if (live && l0 <= n) {
+        const uint32_t k0 = l0 == 0u ? 1u : 0u, k1 = min(16u, n + 1u - l0);
+        itm = k1 > k0 ? (((1u << k1) - 1u) & ~((1u << k0) - 1u)) : 0u;
+    }
+    uint32_t dm = 0, sm = 0, lfm = 0, hi = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const bool it = live && (l0 + k - 1u) < n;  // an item (not the document start / padding)
-        const bool del = (C[k] & kDelBit) != 0u;
-        const uint32_t w = it ? (a.mode ? 1u : (del ? 0u : utf8_len(C[k] & kCpMask))) : 0u;
-        W += w;
-        nib |= (uint64_t)w << (4 * k);
-        nsq |= (it && !(C[k] & kSeqBit) ? 1u : 0u) << k;
-        vis |= (w ? 1u : 0u) << k;
-        lm |= (it && (C[k] & kLeftBit) ? 1u : 0u) << k;
+        dm |= ((C[k] >> 23) & 1u) << k;
+        sm |= ((C[k] >> 22) & 1u) << k;
+        lfm |= ((C[k] >> 21) & 1u) << k;
+        hi |= C[k] & (kCpMask & ~0x7Fu);
+    }
+    const uint32_t nsq0 = itm & ~sm, lm = itm & lfm;
+    uint32_t nsq = nsq0, W, vis;
+    uint64_t nib;
+    if (a.mode || hi == 0u) {
+        vis = a.mode ? itm : (itm & ~dm);
+        W = (uint32_t)__popc(vis);
+        // 16 bits -> 16 nibbles (bit k to bit 4k), each half by three shift-or-mask steps
+        uint32_t l8 = vis & 0xFFu, h8 = vis >> 8;
+        l8 = (l8 | (l8 << 12)) & 0x000F000Fu;
+        h8 = (h8 | (h8 << 12)) & 0x000F000Fu;
+        l8 = (l8 | (l8 << 6)) & 0x03030303u;
+        h8 = (h8 | (h8 << 6)) & 0x03030303u;
+        l8 = (l8 | (l8 << 3)) & 0x11111111u;
+        h8 = (h8 | (h8 << 3)) & 0x11111111u;
+        nib = ((uint64_t)h8 << 32) | l8;
+    } else {
+        W = 0;
+        vis = 0;
+        nib = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const bool it = (itm >> k) & 1u;
+            const uint32_t w = it && !((dm >> k) & 1u) ? utf8_len(C[k] & kCpMask) : 0u;
+            W += w;
+            nib |= (uint64_t)w << (4 * k);
+            vis |= (w ? 1u : 0u) << k;
+        }
     }
     if (live) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
