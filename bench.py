@@ -70,10 +70,15 @@ KERNEL_BYTES = {
     # head stage (k_heads: nsq/visible/jump bits in, head records out) and k_runs: head records,
     # nibbles; per run: key + parent slot + rank lookup in, record row out; text move
     "runs": (0.875, 38.0, 2.0),
-    "count": (0.0, 8.0, 0.0),
-    "scan": (0.0, 8.0, 0.0),
-    "place": (0.0, 12.0, 0.0),
+    # global level 1 (radix): histograms (parent in); per pass 16 B element in + out; order pass
+    # (element in, pair + first child out); sort B per pass 8 B in + out (last: 4 B out), records
+    # (first child, next sibling, parent, weight prefix in; 16 B out) -- per pass counts in
+    # stage_launches, priced per run in alg_bytes below
+    "count": (0.0, 4.0, 0.0),
+    "scan": (0.0, 0.0, 0.0),
+    "place": (0.0, 32.0, 0.0),
     "link": (0.0, 28.0, 0.0),
+    "sortb": (0.0, 16.0, 0.0),
     "walk1": (0.0, 16.0, 0.0),
     "rank": (0.0, 0.5, 0.0),
     "walk2": (0.0, 20.0, 0.0),
@@ -90,8 +95,14 @@ PMC_FILE = "profiles/pmc_per_item.json"
 COUNTERS = ["patches", "items", "runs", "text_bytes", "docs", "elapsed_ns", "device_ns", "ok"]
 
 
-# kernels whose PMC traffic makes up a stage's (the stage clock times them together)
-STAGE_PMC_KERNELS = {"classify": ["k_clear", "k_classify"]}
+# kernels whose PMC traffic makes up a stage's (the stage clock times them together, and the
+# stage's algorithmic bytes in KERNEL_BYTES cover all of them)
+STAGE_PMC_KERNELS = {
+    "classify": ["k_clear", "k_classify"],
+    "runs": ["k_heads", "k_tiles_reduce", "k_tiles_top", "k_tiles_apply", "k_runs", "k_docmax"],
+    "doctree": ["k_doctotals", "k_doctree"],
+    "digest": ["k_leafhash", "k_docdigest"],
+}
 
 
 def measured_traffic(stage: str, items_per_launch: float):
@@ -442,6 +453,15 @@ def roofline_fields(stats, batch, items_per_gpu, step_s) -> dict:
     dom = max(timed, key=lambda k: stage_ns[k])
     out = roof(dom)
     out["traffic_source"] = PMC_FILE if out["traffic"] is not None else None
+    out["choice"] = "the stage with the most device time per step (one-lane HIP events)"
+    # every stage's roofline (the dominant one can change from box to box when two stages are
+    # within a few percent), and the batched-merge kernels together (north star: >= 50 %)
+    rooflines = {k: roof(k) for k in timed}
+    tot_b = sum(alg_bytes(k) for k in timed)
+    tot_ns = sum(stage_ns[k] for k in timed)
+    merge_all = {"bound": "hbm", "achieved": tot_b / tot_ns, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                 "frac": tot_b / tot_ns / HBM_PEAK_GBPS, "alg_bytes_per_step": tot_b,
+                 "device_ms_per_step": tot_ns / 1e6, "stages": timed}
     min_bytes = MIN_B_PER_SLOT * slots + MIN_B_PER_RUN * runs + MIN_B_PER_TEXT * text_bytes
     pipeline = {"min_bytes_per_step": min_bytes,
                 "contract_b_per_item": min_bytes / items_per_gpu,
@@ -450,6 +470,7 @@ def roofline_fields(stats, batch, items_per_gpu, step_s) -> dict:
                         "previous-slot flags) + 6 B/run head (lamport, agent) + 1 B/merged byte, "
                         "over the wall time of a step"}
     return {"kernels": per_kernel, "roofline": out, "pipeline": pipeline,
+            "rooflines": rooflines, "batched_merge": merge_all,
             "stream_kernel": roof("classify") if launches.get("classify") else None,
             "stage_ns": stage_ns, "launches": launches}
 
@@ -541,6 +562,8 @@ def traces_workload(args) -> int:
             "kernels_ms_with_lanes": rf_lanes,
             "ms_per_step_1_lane": float(np.mean([s["total_ns"] for s in iso_stats])) / 1e6,
             "roofline": rf["roofline"],
+            "rooflines": rf["rooflines"],
+            "batched_merge": rf["batched_merge"],
             "stream_kernel": rf["stream_kernel"],
             "pipeline": rf["pipeline"],
             "input_encoding": {

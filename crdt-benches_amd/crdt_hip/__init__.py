@@ -24,7 +24,7 @@ ERRORS = {
     -1: "EINVAL", -2: "ERANGE", -3: "ENOMEM", -4: "EDEVICE", -5: "EBADLOG", -6: "ESPACE",
     -7: "EIO", -8: "ECOMM",
 }
-STAGES = ["classify", "runs", "run_parent", "count", "scan", "place", "link", "walk1", "rank",
+STAGES = ["classify", "runs", "sortb", "count", "scan", "place", "link", "walk1", "rank",
           "walk2", "expand", "digest", "doctree"]
 
 # Every symbol include/crdt_hip.h declares (checked by tests/test_abi.py).

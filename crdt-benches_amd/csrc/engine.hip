@@ -20,9 +20,11 @@
 //    k_runs        run records (head slot, weight prefix, key, parent run by rank lookup),
 //                  slot-order UTF-8
 //  Level 1 merges the tree of runs:
-//    k_count / k_scan_* / k_place        children grouped by parent run
-//    k_link / k_sortmid / k_sortbig      sibling order -> first-child / next-sibling
-//    k_walk1 / k_pred / k_winit / k_wstep / k_walk2
+//    k_rs_hist / k_rs_scan / k_rs_pass   LDS-staged LSD radix sort of (parent run, run id, key)
+//                                        by parent run: sibling groups contiguous and keyed
+//    k_rs_order / k_rs_big               sibling order: {run, next sibling} pairs, first children
+//    k_rs_pass (sort B) / k_rs_records   the pairs by run id; the run records in run order
+//    k_walk1 / k_sup1 / k_sup_step / k_sup2 / k_walk2
 //                                        Euler-tour list ranking (sublists from splitters
 //                                        run id % M == 0, pointer jumping over the splitter
 //                                        lists); weighted so the rank is each run's byte offset
@@ -55,15 +57,13 @@ constexpr int kScanTile = kBlock * kScanItems;
 constexpr uint32_t kDocAlignLog2 = 6;  // slot-level document alignment (chunk table: 1/64)
 constexpr uint32_t kLeaf = 4096;
 constexpr uint64_t kMaxWaveText = (1ull << 32) - (1ull << 20);  // weight prefixes are u32
-constexpr int kMidGrid = 16384;
-constexpr int kBigGrid = 256;
+constexpr int kBigGrid = 256;   // k_rs_big workgroups
 constexpr int kBigThreads = 1024;
-constexpr int kBigLds = 4096;
 
 // ctl words (device, zeroed per wave)
 enum Ctl {
-    C_NDEFER = 0,   // deferred sibling segments (9..64 children)
-    C_NBIG = 1,     // sibling segments with > 64 children
+    C_RSV0 = 0,     // (unused)
+    C_RSV1 = 1,     // (unused)
     C_ERR = 2,      // error bits: 1 bad parent, 2 walk overrun, 4 text overflow, 8 write out
                     //   of range, 16 unreachable runs (cycle)
     C_RTOTAL = 3,   // runs of the wave
@@ -100,7 +100,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G, uint32_t o
 __device__ __forceinline__ bool replan(const uint32_t* ctl) { return ctl[C_REPLAN] != 0u; }
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
-enum Stage { S_CLASSIFY, S_RUNS, S_RPARENT, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
+enum Stage { S_CLASSIFY, S_RUNS, S_SORTB, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
              S_WALK2, S_EXPAND, S_DIGEST, S_DOCTREE, S_N };
 
 
@@ -935,15 +935,9 @@ struct TreeArgs {
     const uint32_t* pstart;      // weight prefix per run (+ sentinel): weight = [g + 1] - [g]
     const uint32_t* doc_root;    // per document: its document-start run
     const uint32_t* doc_p0;      // per document: weight prefix at its start
-    uint32_t* deg;
-    uint32_t* cstart;
-    uint32_t* child;
     uint4* rec;  // per run {first_child, weight, next_sibling, parent}
-    uint32_t* defer;
-    uint32_t* bigl;
     uint32_t* ctl;
-    uint32_t* sw;
-    uint32_t* snext;
+    uint2* swn;        // per splitter {sublist weight, next splitter}
     uint32_t* roff;
     uint32_t* tlen;
     uint64_t* toff;
@@ -961,19 +955,6 @@ struct TreeArgs {
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
 };
-
-__device__ __forceinline__ uint64_t sib_key(const TreeArgs& a, uint32_t c) { return a.key[c]; }
-
-__global__ __launch_bounds__(kBlock) void k_count(TreeArgs a) {
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.R) return;
-    const uint32_t p = a.in_parent[g];
-    if (p == kNil) return;
-    if (p >= a.R || p == g) { atomicOr(&a.ctl[C_ERR], 1u); return; }
-    // the child's place in its parent's segment comes with the count (roff is free until
-    // k_walk2), so that k_place needs no second atomic
-    a.roff[g] = atomicAdd(&a.deg[p], 1u);
-}
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n,
                                                          uint32_t* __restrict__ sums) {
@@ -1047,15 +1028,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* __restric
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_place(TreeArgs a) {
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.R) return;
-    const uint32_t p = a.in_parent[g];
-    if (p == kNil || p >= a.R || p == g) return;  // flagged by k_count
-    a.child[a.cstart[p] + a.roff[g]] = g;  // (the place k_count's atomic handed out)
-}
-
-// Compare-exchange for a descending sort of (key, id) pairs held in registers.
+// Compare-exchange for a descending sort of (key, id) pairs held in registers (k_doctree).
 __device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uint32_t& ib) {
     if (ka < kb) {
         const uint64_t tk = ka; ka = kb; kb = tk;
@@ -1063,172 +1036,385 @@ __device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uin
     }
 }
 
-// Run records: {first_child, weight} written by the run itself, {next_sibling, parent} by
-// whoever sorted its sibling group; one 16-byte load per arc in the walks.
-__device__ __forceinline__ void set_dn(const TreeArgs& a, uint32_t g, uint32_t fc, uint32_t w) {
-    reinterpret_cast<uint2*>(a.rec + g)[0] = make_uint2(fc, w);
-}
-__device__ __forceinline__ void set_up(const TreeArgs& a, uint32_t c, uint32_t ns, uint32_t p) {
-    reinterpret_cast<uint2*>(a.rec + c)[1] = make_uint2(ns, p);
-}
-__device__ __forceinline__ void set_fc(const TreeArgs& a, uint32_t p, uint32_t c) {
-    reinterpret_cast<uint32_t*>(a.rec + p)[0] = c;
+// ---------------------------------------------------------------------------------------------
+// Level 1, grid-wide: the run records by two LDS-staged LSD radix sorts
+// ---------------------------------------------------------------------------------------------
+// The Euler-tour walks read one record per run: {first child, weight, next sibling, parent}.
+// Children of a parent, ordered by sibling key, are found by sorting:
+//  A. every run as a 16-byte element {parent run, run id, key lo, key hi} (a document start's
+//     parent is R: those sort last and are nobody's child), by parent run, 8-bit digits, least
+//     significant first, each pass stable.  A sibling group leaves it contiguous, in run-id
+//     order, carrying its keys, so one streaming pass (k_rs_order) orders each group in
+//     registers and emits, per run, the pair {run, next sibling}, and the first child of each
+//     parent (parents ascend along the sorted array: those writes are monotone, not random);
+//  B. the pairs by run id (a permutation of 0..R-1: its digit counts are known in closed form),
+//     whose last pass writes the next siblings in run order.
+// Both sorts replace random per-run accesses (a child-count atomic, a placement scatter, a key
+// gather per child, a record scatter per child) with passes that read and write whole stretches.
+// One launch per pass ("onesweep"): a workgroup claims the next tile from a counter, ranks its
+// elements per wave and digit (ballot matching: stable within the wave), publishes the tile's
+// digit counts, takes the counts of every earlier tile by decoupled look-back (one thread per
+// digit), reorders the tile by digit in LDS and writes each digit's stretch contiguously.
+constexpr uint32_t kRsThreads = 512;
+constexpr uint32_t kRsWaves = kRsThreads / 64;
+constexpr uint32_t kRsItemsA = 8;                        // sort A: 4096 x 16 B per tile
+constexpr uint32_t kRsItemsB = 16;                       // sort B: 8192 x 8 B per tile
+constexpr uint32_t kRsTileA = kRsThreads * kRsItemsA;
+constexpr uint32_t kRsTileB = kRsThreads * kRsItemsB;
+constexpr uint32_t kRsBins = 256;
+constexpr uint32_t kRsMaxPass = 4;
+constexpr uint32_t kRsAgg = 0x80000000u;  // look-back word: a tile's digit count (else prefix + 1)
+constexpr uint32_t kRsLook = 16;          // look-back words read per round trip
+// rs_small_: bucket starts of sort A [pass][bin], of sort B, then counters: tile counters of the
+// passes of A (4) and B (4), the lengths of the deferred and the long group lists
+constexpr uint32_t kRsHistB = kRsMaxPass * kRsBins;
+constexpr uint32_t kRsCtl = 2 * kRsMaxPass * kRsBins;
+constexpr uint32_t kRsBig = 8;
+constexpr uint32_t kRsSmall = kRsCtl + 16;
+constexpr uint32_t kRsBigLds = 8192;  // groups of up to this many children sort in LDS
+
+struct RsArgs {
+    uint32_t R, pass, npass;
+    const void* in;      // the previous pass's output (or the order pass's pairs)
+    void* out;
+    uint32_t* hist;      // this sort's [pass][256] bucket starts
+    uint32_t* tctr;      // this sort's tile counter per pass
+    uint32_t* rctl;      // the counters block
+    uint32_t* status;    // [tiles][256] look-back words (zeroed before every pass)
+    uint2* bigl;         // {start, children} of each group of more than 64 children
+    uint2* B;            // per element of A: {run, next sibling}
+    uint32_t* fc;        // per run: its first child (kNil: a leaf)
+};
+
+// The parent run of run g in sort A (document starts and malformed parents: R).
+__device__ __forceinline__ uint32_t rs_parent(const TreeArgs& a, uint32_t g, bool& bad) {
+    const uint32_t p = a.in_parent[g];
+    bad = p != kNil && (p >= a.R || p == g);
+    return (p == kNil || bad) ? a.R : p;
 }
 
-// Up to 8 siblings: Batcher's 19-comparator odd-even merge network (verified on all 0-1
-// inputs), padding key 0 sorts last (every child key has lamport >= 1).
-__device__ __forceinline__ uint32_t link_small(const TreeArgs& a, uint32_t g, uint32_t s0,
-                                               uint32_t cnt) {
-    uint64_t k[8];
-    uint32_t c[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] = (uint32_t)i < cnt ? a.child[s0 + i] : kNil;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = (uint32_t)i < cnt ? a.key[c[i]] : 0ull;
-    cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
-    cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
-    cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
-    cx(k[4], c[4], k[6], c[6]); cx(k[5], c[5], k[7], c[7]);
-    cx(k[1], c[1], k[2], c[2]); cx(k[5], c[5], k[6], c[6]);
-    cx(k[0], c[0], k[4], c[4]); cx(k[1], c[1], k[5], c[5]);
-    cx(k[2], c[2], k[6], c[6]); cx(k[3], c[3], k[7], c[7]);
-    cx(k[2], c[2], k[4], c[4]); cx(k[3], c[3], k[5], c[5]);
-    cx(k[1], c[1], k[2], c[2]); cx(k[3], c[3], k[4], c[4]); cx(k[5], c[5], k[6], c[6]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        if ((uint32_t)i < cnt) set_up(a, c[i], (uint32_t)i + 1 < cnt ? c[i + 1 < 8 ? i + 1 : 7] : kNil, g);
-    return c[0];
-}
-
-__global__ __launch_bounds__(kBlock) void k_link(TreeArgs a) {
-    __shared__ uint32_t nblk, bbase;
-    if (threadIdx.x == 0) nblk = 0;
+// Digit histograms of every pass of sort A (LDS, then one global add per bin and block).
+__global__ __launch_bounds__(kBlock) void k_rs_hist(TreeArgs a, RsArgs r) {
+    __shared__ uint32_t h[kRsMaxPass * kRsBins];
+    for (uint32_t i = threadIdx.x; i < r.npass * kRsBins; i += kBlock) h[i] = 0;
     __syncthreads();
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    bool defer = false;
-    if (g < a.R) {
-        const uint32_t w = a.pstart[g + 1] - a.pstart[g];
-        if (a.in_parent[g] == kNil) set_up(a, g, kNil, kNil);  // no sibling, no parent
-        const uint32_t s0 = a.cstart[g], cnt = a.cstart[g + 1] - s0;
-        uint32_t fc = kNil;
-        if (cnt == 1) {
-            const uint32_t c0 = a.child[s0];
-            fc = c0;
-            set_up(a, c0, kNil, g);
-        } else if (cnt == 2) {
-            uint32_t c0 = a.child[s0], c1 = a.child[s0 + 1];
-            if (sib_key(a, c0) < sib_key(a, c1)) { uint32_t t = c0; c0 = c1; c1 = t; }
-            fc = c0;
-            set_up(a, c0, c1, g);
-            set_up(a, c1, kNil, g);
-        } else if (cnt <= 8) {
-            if (cnt) fc = link_small(a, g, s0, cnt);
-        } else {
-            defer = true;  // first_child written by the sort kernels
-        }
-        set_dn(a, g, fc, w);
+    uint32_t bad_any = 0;
+    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < a.R; g += gridDim.x * kBlock) {
+        bool bad;
+        const uint32_t pv = rs_parent(a, g, bad);
+        bad_any |= bad ? 1u : 0u;
+        for (uint32_t k = 0; k < r.npass; ++k) atomicAdd(&h[k * kRsBins + ((pv >> (8u * k)) & 255u)], 1u);
     }
-    // deferred segments: one global atomic per block
-    uint32_t slot = 0;
-    if (defer) slot = atomicAdd(&nblk, 1u);
+    if (bad_any) atomicOr(&a.ctl[C_ERR], 1u);
     __syncthreads();
-    if (threadIdx.x == 0 && nblk) bbase = atomicAdd(&a.ctl[C_NDEFER], nblk);
-    __syncthreads();
-    if (defer) a.defer[bbase + slot] = g;
+    for (uint32_t i = threadIdx.x; i < r.npass * kRsBins; i += kBlock)
+        if (h[i]) atomicAdd(&r.hist[i], h[i]);
 }
 
-// One wave per deferred segment of 9..64 children: rank = #siblings with a greater key, then
-// ds_permute scatters ids into rank order and shuffles hand each lane its successor.
-__global__ __launch_bounds__(kBlock) void k_sortmid(TreeArgs a) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nw = (gridDim.x * kBlock) >> 6;
-    const uint32_t nd = a.ctl[C_NDEFER];
-    for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6; i < nd; i += nw) {
-        const uint32_t p = a.defer[i];
-        const uint32_t s0 = a.cstart[p], cnt = a.cstart[p + 1] - s0;
-        if (cnt > 64) {
-            if (lane == 0) a.bigl[atomicAdd(&a.ctl[C_NBIG], 1u)] = p;
-            continue;
-        }
-        const bool on = lane < cnt;
-        const uint32_t c = on ? a.child[s0 + lane] : 0u;
-        const uint64_t k = on ? sib_key(a, c) : 0ull;
-        const uint32_t khi = (uint32_t)(k >> 32), klo = (uint32_t)k;
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const uint32_t hj = (uint32_t)__shfl((int)khi, (int)j);
-            const uint32_t lj = (uint32_t)__shfl((int)klo, (int)j);
-            rank += (hj > khi) || (hj == khi && lj > klo);
-        }
-        // lane r <- id of rank r
-        const uint32_t sorted =
-            (uint32_t)__builtin_amdgcn_ds_permute((int)((on ? rank : lane) << 2), (int)c);
-        const uint32_t succ = (uint32_t)__shfl((int)sorted, (int)((lane + 1) & 63));
-        const uint32_t ns_of_rank = (lane + 1 < cnt) ? succ : kNil;
-        const uint32_t ns = (uint32_t)__shfl((int)ns_of_rank, (int)(on ? rank : 0));
-        if (on) {
-            set_up(a, c, ns, p);
-            if (rank == 0) set_fc(a, p, c);
-        }
+// Single workgroup: bucket starts of every pass of both sorts.  Sort B sorts a permutation of
+// 0..R-1: digit d of pass k is held by full * 256^k values of each complete cycle of 256^(k+1)
+// and by the part of the last cycle's block of d.
+__global__ __launch_bounds__(kRsBins) void k_rs_scan(RsArgs r) {
+    __shared__ uint32_t lds[kRsBins / 64];
+    const uint32_t d = threadIdx.x;
+    for (uint32_t k = 0; k < r.npass; ++k) {
+        uint32_t tot;
+        const uint32_t v = r.hist[k * kRsBins + d];
+        r.hist[k * kRsBins + d] = block_excl_scan<kRsBins / 64>(v, lds, tot);
+        const uint64_t P = 1ull << (8u * k), Q = P << 8;
+        const uint64_t rem = r.R % Q, lo = (uint64_t)d * P;
+        const uint64_t cnt = (r.R / Q) * P + (rem > lo ? std::min<uint64_t>(rem - lo, P) : 0ull);
+        r.hist[kRsHistB + k * kRsBins + d] = block_excl_scan<kRsBins / 64>((uint32_t)cnt, lds, tot);
     }
 }
 
-// Bitonic sort (descending by key) of one sibling segment with the "flip" formulation: every
-// compare-exchange has the same direction, so the virtual -inf padding up to a power of two
-// never has to be stored.
-__global__ __launch_bounds__(kBigThreads) void k_sortbig(TreeArgs a) {
-    __shared__ uint64_t skey[kBigLds];
-    __shared__ uint32_t sid[kBigLds];
-    const uint32_t nb = a.ctl[C_NBIG];
+__device__ __forceinline__ uint32_t rs_lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// One pass.  T: uint4 (sort A) or uint2 (sort B), the sort key in .x.  MODE 0: the first pass of
+// A (elements built from r_parent / r_key); 1: elements from r.in to r.out; 2: the last pass of
+// B (r.out[position] = .y, the next sibling: a permutation lands in run order).
+template <class T, int MODE, int ITEMS>
+__global__ __launch_bounds__(kRsThreads) void k_rs_pass(TreeArgs a, RsArgs r) {
+    constexpr uint32_t TILE = kRsThreads * ITEMS;
+    __shared__ T buf[TILE];
+    __shared__ uint32_t wc[kRsWaves][kRsBins + 1];  // per wave and digit (+1: invalid elements)
+    __shared__ uint32_t dst[kRsBins];               // the tile's digit starts
+    __shared__ uint32_t gof[kRsBins];               // bucket position of the tile's digit start
+    __shared__ uint32_t red[kRsWaves];
+    __shared__ uint32_t tsh;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    if (t == 0) tsh = atomicAdd(&r.tctr[r.pass], 1u);
+    for (uint32_t i = t; i < kRsWaves * (kRsBins + 1); i += kRsThreads) (&wc[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t tile = tsh, R = r.R, sh = 8u * r.pass;
+    // wave wv takes elements [base, base + 64 ITEMS) of the tile, lane-striped
+    const uint32_t base = tile * TILE + wv * (64u * ITEMS);
+    T e[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t i = base + (uint32_t)j * 64u + lane;
+        e[j] = T{};
+        if (i < R) {
+            if constexpr (MODE == 0) {
+                bool bad;
+                const uint64_t k = a.key[i];
+                e[j] = make_uint4(rs_parent(a, i, bad), i, (uint32_t)k, (uint32_t)(k >> 32));
+            } else {
+                e[j] = reinterpret_cast<const T*>(r.in)[i];
+            }
+        }
+    }
+    // stable ranks per wave and digit: the lanes holding the same digit (8 ballots), the rank
+    // among them, and the wave's running count of the digit in LDS (its leader adds them)
+    uint32_t pos[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t i = base + (uint32_t)j * 64u + lane;
+        const bool valid = i < R;
+        const uint32_t d = valid ? (e[j].x >> sh) & 255u : kRsBins;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t rk = rs_lanes_below(peers);
+        const uint32_t old = wc[wv][d];
+        if (valid && rk == 0u) wc[wv][d] = old + (uint32_t)__popcll(peers);
+        pos[j] = (d << 16) | (old + rk);
+    }
+    __syncthreads();
+    // per digit: the waves' counts -> exclusive prefixes over the waves, the tile's count
+    uint32_t c = 0;
+    if (t < kRsBins) {
+#pragma unroll
+        for (int w = 0; w < (int)kRsWaves; ++w) {
+            const uint32_t x = wc[w][t];
+            wc[w][t] = c;
+            c += x;
+        }
+        // published at once (look-backs of later tiles wait for it); tile 0 is its own prefix
+        __hip_atomic_store(&r.status[(uint64_t)tile * kRsBins + t], tile == 0 ? c + 1u : (kRsAgg | c),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint32_t nval;
+    const uint32_t ds = block_excl_scan<kRsWaves>(c, red, nval);
+    if (t < kRsBins) {
+        dst[t] = ds;
+        uint32_t ex = 0;
+        if (tile > 0) {
+            // decoupled look-back: earlier tiles' counts of this digit, nearest first, until one
+            // that has published its inclusive prefix (tile 0 always has); kRsLook words per
+            // round trip, consumed in order up to the first inclusive one or the first not yet
+            // published (then read again from there)
+            for (uint32_t j = tile - 1u;;) {
+                uint32_t w[kRsLook];
+#pragma unroll
+                for (int q = 0; q < (int)kRsLook; ++q)
+                    w[q] = (int)j - q >= 0 ? __hip_atomic_load(&r.status[(uint64_t)(j - q) * kRsBins + t],
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : 1u;
+                uint32_t used = 0;
+                bool done = false, stall = false;
+#pragma unroll
+                for (int q = 0; q < (int)kRsLook; ++q) {
+                    if (done || stall) continue;
+                    if (w[q] == 0u) {
+                        stall = true;
+                    } else if (w[q] & kRsAgg) {
+                        ex += w[q] & ~kRsAgg;
+                        ++used;
+                    } else {
+                        ex += w[q] - 1u;
+                        done = true;
+                    }
+                }
+                if (done) break;
+                j -= used;
+                if (stall) __builtin_amdgcn_s_sleep(1);
+            }
+            __hip_atomic_store(&r.status[(uint64_t)tile * kRsBins + t], ex + c + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        gof[t] = r.hist[r.pass * kRsBins + t] + ex - ds;  // (+ the element's tile position)
+    }
+    __syncthreads();
+    // the tile in digit order in LDS
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t i = base + (uint32_t)j * 64u + lane;
+        if (i < R) {
+            const uint32_t d = pos[j] >> 16;
+            buf[dst[d] + wc[wv][d] + (pos[j] & 0xFFFFu)] = e[j];
+        }
+    }
+    __syncthreads();
+    // out: each digit's stretch lands contiguously at its bucket position
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t i = (uint32_t)k * kRsThreads + t;
+        if (i < nval) {
+            const T x = buf[i];
+            const uint32_t o = gof[(x.x >> sh) & 255u] + i;
+            if constexpr (MODE == 2)
+                reinterpret_cast<uint32_t*>(r.out)[o] = x.y;
+            else
+                reinterpret_cast<T*>(r.out)[o] = x;
+        }
+    }
+}
+
+// Sibling order descending by (key, run id).
+__device__ __forceinline__ bool rs_before(uint64_t ka, uint32_t ca, uint64_t kb, uint32_t cb) {
+    return ka > kb || (ka == kb && ca > cb);
+}
+
+// One sibling group held by lanes [gs, ge] of a wave (lane l: child c, key k, element position
+// j; on: the lane is in a group this wave orders): each child's rank among its siblings, the
+// children by rank (ds_permute), next siblings by shuffle; the pair {c, next sibling} to B[j],
+// and the group's first child to fc[p].
+__device__ __forceinline__ void rs_order_lanes(const RsArgs& r, bool on, uint32_t gs, uint32_t ge,
+                                               uint32_t p, uint32_t c, uint64_t k, uint32_t j,
+                                               uint32_t maxlen) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t rank = 0;
+    const uint32_t khi = (uint32_t)(k >> 32), klo = (uint32_t)k;
+    for (uint32_t q = 0; q < maxlen; ++q) {
+        const uint32_t l = min(gs + q, 63u);
+        const uint32_t hj = (uint32_t)__shfl((int)khi, (int)l);
+        const uint32_t lj = (uint32_t)__shfl((int)klo, (int)l);
+        const uint32_t cj = (uint32_t)__shfl((int)c, (int)l);
+        if (on && gs + q <= ge)
+            rank += rs_before(((uint64_t)hj << 32) | lj, cj, k, c) ? 1u : 0u;
+    }
+    const uint32_t tgt = on ? gs + rank : lane;
+    const uint32_t sorted = (uint32_t)__builtin_amdgcn_ds_permute((int)(tgt << 2), (int)c);
+    const uint32_t nx = (uint32_t)__shfl((int)sorted, (int)min(tgt + 1u, 63u));
+    if (on) {
+        r.B[j] = make_uint2(c, tgt + 1u <= ge ? nx : kNil);
+        if (rank == 0) r.fc[p] = c;
+    }
+}
+
+// Streaming pass over sort A's output: one wave per 64 consecutive elements.  Groups wholly
+// inside the window are ordered here; a group that starts in the window and runs past its end is
+// ordered by the same wave from a second load at its start (up to 64 children; a longer one is
+// listed for k_rs_big).  A group that started in an earlier window belongs to that window's
+// wave.  Document starts have no sibling.
+__global__ __launch_bounds__(kBlock) void k_rs_order(TreeArgs a, RsArgs r, const uint4* __restrict__ E) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t R = a.R;
+    const bool valid = i < R;
+    const uint4 e = valid ? E[i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+    const uint32_t p = e.x;
+    if (valid && p == R) r.B[i] = make_uint2(e.y, kNil);
+    uint32_t pl = (uint32_t)__shfl_up((int)p, 1), pr = (uint32_t)__shfl_down((int)p, 1);
+    if (lane == 0) pl = (valid && i > 0) ? E[i - 1].x : 0xFFFFFFFEu;
+    if (lane == 63u) pr = (i + 1u < R) ? E[i + 1].x : 0xFFFFFFFDu;
+    const bool st = valid && pl != p, en = valid && pr != p;
+    const uint64_t SB = __ballot(st), EB = __ballot(en);
+    const uint64_t below = SB & (lane == 63u ? ~0ull : ((2ull << lane) - 1ull));
+    const uint64_t above = EB & ~((1ull << lane) - 1ull);
+    const uint32_t gs = below ? 63u - (uint32_t)__clzll(below) : 64u;
+    const uint32_t ge = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+    const bool on = valid && p != R && gs < 64u && ge < 64u;
+    // the group that crosses the window's end (at most one): its start lane, if in this window
+    const uint64_t cross = __ballot(valid && st && p != R && ge == 64u);
+    uint32_t len = on ? ge - gs + 1u : 0u;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) len = max(len, (uint32_t)__shfl_xor((int)len, o));
+    if (len) rs_order_lanes(r, on, gs, ge, p, e.y, ((uint64_t)e.w << 32) | e.z, i, len);
+    if (!cross) return;  // (wave-uniform)
+    const uint32_t cl = (uint32_t)__builtin_ctzll(cross);
+    const uint32_t s0 = (uint32_t)__shfl((int)i, (int)cl), cp = (uint32_t)__shfl((int)p, (int)cl);
+    const uint32_t k = s0 + lane;
+    const uint4 f = k < R ? E[k] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+    const uint64_t in = __ballot(f.x == cp);
+    const uint32_t n = in == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~in);
+    if (n == 64u && s0 + 64u < R && E[s0 + 64u].x == cp) {
+        // more than 64 children: the group's length, then k_rs_big
+        uint32_t m = 64;
+        for (;;) {
+            const uint32_t q = s0 + m + lane;
+            const uint64_t b = __ballot(q < R && E[q].x == cp);
+            if (b == ~0ull) {
+                m += 64u;
+                continue;
+            }
+            m += (uint32_t)__builtin_ctzll(~b);
+            break;
+        }
+        if (lane == 0) r.bigl[atomicAdd(&r.rctl[kRsBig], 1u)] = make_uint2(s0, m);
+        return;
+    }
+    rs_order_lanes(r, lane < n, 0u, n - 1u, cp, f.y, ((uint64_t)f.w << 32) | f.z, k, n);
+}
+
+// One workgroup per group of more than 64 children: bitonic sort (descending by key, run id;
+// the "flip" formulation, so the padding to a power of two is never stored) in LDS, or in place
+// in the element array beyond kRsBigLds children; then the pairs and the first child.
+__global__ __launch_bounds__(kBigThreads) void k_rs_big(TreeArgs a, RsArgs r, uint4* __restrict__ E) {
+    __shared__ uint64_t sk[kRsBigLds];
+    __shared__ uint32_t sc[kRsBigLds];
+    const uint32_t nb = r.rctl[kRsBig];
     for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
-        const uint32_t p = a.bigl[bi];
-        const uint32_t s0 = a.cstart[p], cnt = a.cstart[p + 1] - s0;
+        const uint2 g = r.bigl[bi];
+        const uint32_t s0 = g.x, cnt = g.y, p = E[s0].x;
         uint32_t P = 1;
         while (P < cnt) P <<= 1;
-        uint32_t* seg = a.child + s0;
-        if (P <= (uint32_t)kBigLds) {
+        const bool lds = P <= kRsBigLds;
+        if (lds) {
             for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) {
-                sid[i] = seg[i];
-                skey[i] = sib_key(a, seg[i]);
+                const uint4 e = E[s0 + i];
+                sk[i] = ((uint64_t)e.w << 32) | e.z;
+                sc[i] = e.y;
             }
             __syncthreads();
-            for (uint32_t k = 2; k <= P; k <<= 1) {
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t t = threadIdx.x; t < P / 2; t += kBigThreads) {
-                        const uint32_t i = (t / j) * 2 * j + (t % j);
-                        const uint32_t l = (j == (k >> 1)) ? (i ^ (k - 1)) : (i ^ j);
-                        if (l < cnt && skey[i] < skey[l]) {
-                            uint64_t tk = skey[i]; skey[i] = skey[l]; skey[l] = tk;
-                            uint32_t ti = sid[i]; sid[i] = sid[l]; sid[l] = ti;
+        }
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < P / 2; t += kBigThreads) {
+                    const uint32_t i = (t / j) * 2 * j + (t % j);
+                    const uint32_t l = (j == (k >> 1)) ? (i ^ (k - 1)) : (i ^ j);
+                    if (l >= cnt) continue;
+                    if (lds) {
+                        if (rs_before(sk[l], sc[l], sk[i], sc[i])) {
+                            const uint64_t tk = sk[i]; sk[i] = sk[l]; sk[l] = tk;
+                            const uint32_t tc = sc[i]; sc[i] = sc[l]; sc[l] = tc;
+                        }
+                    } else {
+                        const uint4 ei = E[s0 + i], el = E[s0 + l];
+                        if (rs_before(((uint64_t)el.w << 32) | el.z, el.y, ((uint64_t)ei.w << 32) | ei.z, ei.y)) {
+                            E[s0 + i] = el;
+                            E[s0 + l] = ei;
                         }
                     }
-                    __syncthreads();
                 }
-            }
-            for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) seg[i] = sid[i];
-            __syncthreads();
-        } else {
-            for (uint32_t k = 2; k <= P; k <<= 1) {
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t t = threadIdx.x; t < P / 2; t += kBigThreads) {
-                        const uint32_t i = (t / j) * 2 * j + (t % j);
-                        const uint32_t l = (j == (k >> 1)) ? (i ^ (k - 1)) : (i ^ j);
-                        if (l < cnt) {
-                            const uint32_t ci = seg[i], cl = seg[l];
-                            if (sib_key(a, ci) < sib_key(a, cl)) { seg[i] = cl; seg[l] = ci; }
-                        }
-                    }
-                    __syncthreads();
-                }
+                __syncthreads();
             }
         }
         for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) {
-            const uint32_t c = seg[i];
-            set_up(a, c, i + 1 < cnt ? seg[i + 1] : kNil, p);
+            const uint32_t c = lds ? sc[i] : E[s0 + i].y;
+            const uint32_t nx = i + 1 < cnt ? (lds ? sc[i + 1] : E[s0 + i + 1].y) : kNil;
+            r.B[s0 + i] = make_uint2(c, nx);
+            if (i == 0) r.fc[p] = c;
         }
-        if (threadIdx.x == 0) set_fc(a, p, seg[0]);
         __syncthreads();
     }
+}
+
+// The run records in run order, every input coalesced: {first child, weight, next sibling,
+// parent} (a document start, or a run with a malformed parent: no parent, no sibling).
+__global__ __launch_bounds__(kBlock) void k_rs_records(TreeArgs a, const uint32_t* __restrict__ fc,
+                                                       const uint32_t* __restrict__ ns) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.R) return;
+    bool bad;
+    const uint32_t p = rs_parent(a, g, bad);
+    a.rec[g] = make_uint4(fc[g], a.pstart[g + 1] - a.pstart[g], ns[g], p == a.R ? kNil : p);
 }
 
 // Euler-tour walks (sublist list ranking).  Regular splitters: both arcs of every run that is
@@ -1281,43 +1467,83 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
             if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
         }
     }
-    a.sw[s] = sum;
-    a.snext[s] = nxt;
+    a.swn[s] = make_uint2(sum, nxt);
 }
 
-// pred[] <- reverse links of the splitter lists (pred pre-filled with kNil).
-__global__ __launch_bounds__(kBlock) void k_pred(const uint32_t* __restrict__ snext, uint32_t S,
-                                                  uint32_t* __restrict__ pred) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= S) return;
-    const uint32_t nx = snext[s];
-    if (nx != kNil) pred[nx] = s;
+// Ranking of the splitter lists (exclusive prefix of the sublist weights along each document's
+// list), by sublists once more: every list head (a document start's splitter, s >= Sreg) and every
+// regular splitter s = 0 mod kSup is a super-splitter; the supers' own lists are ranked by
+// pointer jumping (kSup times fewer entries than the splitters), then every super walks its stretch
+// of the splitter list once more writing the prefixes.  Two dependent gathers per splitter plus a
+// few rounds over the supers, instead of log2(list length) rounds over all splitters.
+constexpr uint32_t kSupLog2 = 6, kSup = 1u << kSupLog2;
+__device__ __forceinline__ bool is_super(uint32_t s, uint32_t Sreg) { return s >= Sreg || (s & (kSup - 1u)) == 0u; }
+// compact index of a super: regular ones first, then one per document
+__device__ __forceinline__ uint32_t super_idx(uint32_t s, uint32_t Sreg) {
+    return s >= Sreg ? ((Sreg + kSup - 1u) >> kSupLog2) + (s - Sreg) : s >> kSupLog2;
 }
-__global__ __launch_bounds__(kBlock) void k_winit(const uint32_t* __restrict__ sw,
-                                                   const uint32_t* __restrict__ pred, uint32_t S,
-                                                   uint32_t* __restrict__ val,
-                                                   uint32_t* __restrict__ ptr) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= S) return;
-    const uint32_t p = pred[s];
-    val[s] = p != kNil ? sw[p] : 0u;
-    ptr[s] = p;
+__device__ __forceinline__ uint32_t super_of(uint32_t c, uint32_t Sreg) {
+    const uint32_t nr = (Sreg + kSup - 1u) >> kSupLog2;
+    return c >= nr ? Sreg + (c - nr) : c << kSupLog2;
 }
-// One pointer-jumping round: val = exclusive prefix over the splitter list so far.
-__global__ __launch_bounds__(kBlock) void k_wstep(const uint32_t* __restrict__ vin,
-                                                   const uint32_t* __restrict__ pin, uint32_t S,
-                                                   uint32_t* __restrict__ vout,
-                                                   uint32_t* __restrict__ pout) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= S) return;
-    const uint32_t p = pin[s];
-    uint32_t v = vin[s], q = kNil;
-    if (p != kNil) {
-        v += vin[p];
-        q = pin[p];
+struct SupArgs {
+    uint32_t S, Sreg, Sc, step_limit;
+    const uint2* swn;    // per splitter {weight, next}
+    uint2* sup;          // per super {stretch weight, next super (compact, kNil: end)}
+    uint32_t* pred;      // per super: its predecessor (kNil: a list head or unused)
+    uint2* vp[2];        // pointer jumping {exclusive prefix, predecessor}
+    uint32_t* spref;     // per splitter: its exclusive prefix along its list
+    uint32_t* ctl;
+};
+__global__ __launch_bounds__(kBlock) void k_sup1(SupArgs a) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= a.Sc) return;
+    uint32_t x = super_of(c, a.Sreg), sum = 0, nx = kNil, steps = 0;
+    if (x < a.S) {
+        for (;;) {
+            const uint2 w = a.swn[x];
+            sum += w.x;
+            if (w.y == kNil) break;
+            if (is_super(w.y, a.Sreg)) { nx = super_idx(w.y, a.Sreg); break; }
+            x = w.y;
+            if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
+        }
     }
-    vout[s] = v;
-    pout[s] = q;
+    a.sup[c] = make_uint2(sum, nx);
+    if (nx != kNil) a.pred[nx] = c;  // (pred pre-filled with kNil)
+}
+__global__ __launch_bounds__(kBlock) void k_sup_init(SupArgs a) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= a.Sc) return;
+    const uint32_t p = a.pred[c];
+    a.vp[0][c] = make_uint2(p != kNil ? a.sup[p].x : 0u, p);
+}
+// One pointer-jumping round over the supers: {prefix so far, predecessor} packed, one gather.
+__global__ __launch_bounds__(kBlock) void k_sup_step(const uint2* __restrict__ in, uint32_t n,
+                                                     uint2* __restrict__ out) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= n) return;
+    uint2 v = in[c];
+    if (v.y != kNil) {
+        const uint2 q = in[v.y];
+        v = make_uint2(v.x + q.x, q.y);
+    }
+    out[c] = v;
+}
+__global__ __launch_bounds__(kBlock) void k_sup2(SupArgs a, const uint2* __restrict__ vp) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= a.Sc) return;
+    uint32_t x = super_of(c, a.Sreg), steps = 0;
+    if (x >= a.S) return;
+    uint32_t pref = vp[c].x;
+    for (;;) {
+        const uint2 w = a.swn[x];
+        a.spref[x] = pref;
+        pref += w.x;
+        if (w.y == kNil || is_super(w.y, a.Sreg)) break;
+        x = w.y;
+        if (++steps > a.step_limit) break;
+    }
 }
 
 // Single workgroup: per-document length (weight between consecutive document starts), aligned
@@ -2743,9 +2969,10 @@ Engine::~Engine() {
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_); dfree(wgtab_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
-    dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
-    dfree(out_); dfree(rec_); dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_);
-    dfree(v1_); dfree(p0_); dfree(p1_); dfree(tlen_); dfree(loff_); dfree(toff_);
+    dfree(rs_elem_[0]); dfree(rs_elem_[1]); dfree(rs_status_); dfree(rs_bigl_);
+    dfree(rs_small_);
+    dfree(out_); dfree(rec_); dfree(swn_); dfree(spref_); dfree(sup_); dfree(spred_);
+    dfree(svp_[0]); dfree(svp_[1]); dfree(tlen_); dfree(loff_); dfree(toff_);
     dfree(leafh_); dfree(ghash_); dfree(text_);
     dfree(leafcp_); dfree(gcp_); dfree(tab_slot_); dfree(tab_local_);
     if (host_out_) (void)hipHostFree(host_out_);
@@ -3075,35 +3302,49 @@ int Engine::ensure_scratch(const Wave& w) {
 // Level-1 scratch, sized by the runs of the wave (known after level 0).
 int Engine::ensure_runs(uint64_t R, uint64_t S) {
     if (R > cap_runs_) {
-        dfree(r_parent_); dfree(roff_); dfree(r_key_);
-        dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_);
-        dfree(scan_sums_); dfree(rec_);
+        dfree(r_parent_); dfree(roff_); dfree(r_key_); dfree(rec_);
         const uint64_t r = R + (R >> 3) + 4096;  // headroom against regrowth
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
         HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
-        HIPCHK(dalloc(&deg_, r + 16), "hipMalloc deg");
-        // (stream-ordered: k_count adds into it on this engine's streams)
-        HIPCHK(hipMemsetAsync(deg_, 0, (r + 16) * 4, stream), "memset deg");
-        HIPCHK(dalloc(&cstart_, r + 16), "hipMalloc cstart");
-        HIPCHK(dalloc(&child_, r), "hipMalloc child");
-        HIPCHK(dalloc(&defer_, r / 3 + 64), "hipMalloc defer");
-        HIPCHK(dalloc(&bigl_, r / 65 + 64), "hipMalloc bigl");
-        HIPCHK(dalloc(&scan_sums_, r / kScanTile + 2), "hipMalloc scan sums");
         HIPCHK(dalloc(&rec_, r), "hipMalloc run records");
         cap_runs_ = r;
         gen_++;
     }
+    return ensure_splitters(S);
+}
+
+// Radix-sort scratch of the global level 1 (R runs): two element arrays, the look-back words
+// (256 per tile), the histograms / counters, the lists of long sibling groups.
+int Engine::ensure_radix(uint64_t R) {
+    if (R > cap_rs_) {
+        dfree(rs_elem_[0]); dfree(rs_elem_[1]); dfree(rs_status_); dfree(rs_bigl_);
+        const uint64_t r = R + (R >> 3) + 4096;
+        HIPCHK(dalloc(&rs_elem_[0], r), "hipMalloc radix elements");
+        HIPCHK(dalloc(&rs_elem_[1], r), "hipMalloc radix elements");
+        HIPCHK(dalloc(&rs_status_, (r / kRsTileA + 2) * kRsBins), "hipMalloc radix look-back");
+        HIPCHK(dalloc(&rs_bigl_, r / 65 + 64), "hipMalloc radix long groups");
+        cap_rs_ = r;
+        gen_++;
+    }
+    if (!rs_small_) {
+        HIPCHK(dalloc(&rs_small_, (uint64_t)kRsSmall), "hipMalloc radix counters");
+        gen_++;
+    }
+    return CRDT_HIP_OK;
+}
+
+int Engine::ensure_splitters(uint64_t S) {
     if (S > cap_splitters_) {
-        dfree(sw_); dfree(snext_); dfree(pred_); dfree(v0_); dfree(v1_); dfree(p0_); dfree(p1_);
+        dfree(swn_); dfree(spref_); dfree(sup_); dfree(spred_); dfree(svp_[0]); dfree(svp_[1]);
         const uint64_t sc = S + (S >> 3) + 1024;
-        HIPCHK(dalloc(&sw_, sc), "hipMalloc sw");
-        HIPCHK(dalloc(&snext_, sc), "hipMalloc snext");
-        HIPCHK(dalloc(&pred_, sc), "hipMalloc pred");
-        HIPCHK(dalloc(&v0_, sc), "hipMalloc v0");
-        HIPCHK(dalloc(&v1_, sc), "hipMalloc v1");
-        HIPCHK(dalloc(&p0_, sc), "hipMalloc p0");
-        HIPCHK(dalloc(&p1_, sc), "hipMalloc p1");
+        HIPCHK(dalloc(&swn_, sc), "hipMalloc splitter weights");
+        HIPCHK(dalloc(&spref_, sc), "hipMalloc splitter prefixes");
+        // (supers: one per kSup regular splitters and one per document: fewer than the splitters)
+        HIPCHK(dalloc(&sup_, sc), "hipMalloc supers");
+        HIPCHK(dalloc(&spred_, sc), "hipMalloc super links");
+        HIPCHK(dalloc(&svp_[0], sc), "hipMalloc super ranks");
+        HIPCHK(dalloc(&svp_[1], sc), "hipMalloc super ranks");
         cap_splitters_ = sc;
         gen_++;
     }
@@ -3231,8 +3472,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.pstart = r_pstart_;                                                             \
     a.doc_root = doc_root_;                                                           \
     a.doc_p0 = doc_p0_;                                                               \
-    a.deg = deg_; a.cstart = cstart_; a.child = child_; a.rec = rec_;                 \
-    a.defer = defer_; a.bigl = bigl_; a.ctl = ctl_; a.sw = sw_; a.snext = snext_;     \
+    a.rec = rec_; a.ctl = ctl_; a.swn = swn_;                                         \
     a.roff = roff_;                                                                   \
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
     a.leafcp = leafcp_; a.gcp = gcp_; a.res = res_;                                   \
@@ -3341,35 +3581,86 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     a.S = S;
     a.step_limit = 2u * R + 4u;
     const uint32_t gR = grid_for(R), gS = grid_for(S);
-    const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
-    k_count<<<gR, kBlock, 0, s>>>(a);
+    // sort A by parent run (document starts: R) and sort B by run id, 8 bits per pass
+    const uint32_t npass = std::max<uint32_t>(1u, (ceil_log2((uint64_t)R + 1u) + 7u) / 8u);
+    const uint64_t tilesA = ((uint64_t)R + kRsTileA - 1) / kRsTileA;
+    const uint64_t tilesB = ((uint64_t)R + kRsTileB - 1) / kRsTileB;
+    rs_npass_ = npass;
+    RsArgs r{};
+    r.R = R;
+    r.npass = npass;
+    r.rctl = rs_small_ + kRsCtl;
+    r.status = rs_status_;
+    r.bigl = rs_bigl_;
+    r.fc = roff_;  // (free until k_walk2)
+    HIPCHK(hipMemsetAsync(rs_small_, 0, kRsSmall * 4ull, s), "clear radix counters");
+    HIPCHK(hipMemsetAsync(roff_, 0xFF, R * 4ull, s), "clear first children");
+    r.hist = rs_small_;
+    k_rs_hist<<<std::min<uint32_t>(gR, 2048u), kBlock, 0, s>>>(a, r);
     MARK(S_COUNT);
-    k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_);
-    k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, R);
-    k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_, cstart_);
-    // (the counts are consumed: back to the all-zero state the next wave's k_count expects)
-    HIPCHK(hipMemsetAsync(deg_, 0, R * 4ull, s), "memset deg");
+    k_rs_scan<<<1, kRsBins, 0, s>>>(r);
     MARK(S_SCAN);
-    k_place<<<gR, kBlock, 0, s>>>(a);
+    r.tctr = r.rctl;
+    for (uint32_t k = 0; k < npass; ++k) {
+        r.pass = k;
+        r.in = k ? rs_elem_[(k - 1) & 1] : nullptr;
+        r.out = rs_elem_[k & 1];
+        HIPCHK(hipMemsetAsync(rs_status_, 0, tilesA * kRsBins * 4ull, s), "clear look-back");
+        if (k == 0)
+            k_rs_pass<uint4, 0, kRsItemsA><<<(uint32_t)tilesA, kRsThreads, 0, s>>>(a, r);
+        else
+            k_rs_pass<uint4, 1, kRsItemsA><<<(uint32_t)tilesA, kRsThreads, 0, s>>>(a, r);
+    }
     MARK(S_PLACE);
-    k_link<<<gR, kBlock, 0, s>>>(a);
-    k_sortmid<<<kMidGrid, kBlock, 0, s>>>(a);
-    k_sortbig<<<kBigGrid, kBigThreads, 0, s>>>(a);
+    uint4* E = rs_elem_[(npass - 1) & 1];
+    uint2* B0 = reinterpret_cast<uint2*>(rs_elem_[npass & 1]);  // (the other element array:
+    uint2* B1 = B0 + cap_rs_;                                     //  room for two pair arrays)
+    r.B = B0;
+    k_rs_order<<<gR, kBlock, 0, s>>>(a, r, E);
+    k_rs_big<<<kBigGrid, kBigThreads, 0, s>>>(a, r, E);
     MARK(S_LINK);
+    // sort B: the pairs by run id; its last pass writes the next siblings in run order over the
+    // element array of sort A (dead once the pairs are out)
+    uint32_t* ns = reinterpret_cast<uint32_t*>(E);
+    r.hist = rs_small_ + kRsHistB;
+    r.tctr = r.rctl + kRsMaxPass;
+    for (uint32_t k = 0; k < npass; ++k) {
+        r.pass = k;
+        r.in = (k & 1) ? B1 : B0;
+        r.out = k + 1 == npass ? static_cast<void*>(ns) : static_cast<void*>((k & 1) ? B0 : B1);
+        HIPCHK(hipMemsetAsync(rs_status_, 0, tilesB * kRsBins * 4ull, s), "clear look-back");
+        if (k + 1 == npass)
+            k_rs_pass<uint2, 2, kRsItemsB><<<(uint32_t)tilesB, kRsThreads, 0, s>>>(a, r);
+        else
+            k_rs_pass<uint2, 1, kRsItemsB><<<(uint32_t)tilesB, kRsThreads, 0, s>>>(a, r);
+    }
+    k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);
+    MARK(S_SORTB);
     k_walk1<<<gS, kBlock, 0, s>>>(a);
     MARK(S_WALK1);
-    HIPCHK(hipMemsetAsync(pred_, 0xFF, S * 4ull, s), "memset pred");
-    k_pred<<<gS, kBlock, 0, s>>>(snext_, S, pred_);
-    k_winit<<<gS, kBlock, 0, s>>>(sw_, pred_, S, v0_, p0_);
-    // a document's list holds at most 2 * (ceil(runs / M) + 1) + 1 splitters
-    rounds = ceil_log2(2ull * ((p.rmax + (1u << log2m_w) - 1) >> log2m_w) + 4);
-    uint32_t *vi = v0_, *pi = p0_, *vo = v1_, *po = p1_;
-    for (uint32_t r = 0; r < rounds; ++r) {
-        k_wstep<<<gS, kBlock, 0, s>>>(vi, pi, S, vo, po);
-        std::swap(vi, vo);
-        std::swap(pi, po);
-    }
-    const uint32_t* spref = vi;
+    SupArgs sa{};
+    sa.S = S;
+    sa.Sreg = Sreg;
+    sa.Sc = ((Sreg + kSup - 1u) >> kSupLog2) + w.ndocs;
+    sa.step_limit = S + 4u;
+    sa.swn = swn_;
+    sa.sup = sup_;
+    sa.pred = spred_;
+    sa.vp[0] = svp_[0];
+    sa.vp[1] = svp_[1];
+    sa.spref = spref_;
+    sa.ctl = ctl_;
+    const uint32_t gC = grid_for(sa.Sc);
+    HIPCHK(hipMemsetAsync(spred_, 0xFF, sa.Sc * 4ull, s), "memset pred");
+    k_sup1<<<gC, kBlock, 0, s>>>(sa);
+    k_sup_init<<<gC, kBlock, 0, s>>>(sa);
+    // a document's list holds at most 2 * (ceil(runs / M) + 1) + 1 splitters, of which at most
+    // that / kSup + 2 are supers
+    rounds = ceil_log2(2ull * ((p.rmax + (1u << log2m_w) - 1) >> log2m_w) / kSup + 8);
+    for (uint32_t k = 0; k < rounds; ++k)
+        k_sup_step<<<gC, kBlock, 0, s>>>(svp_[k & 1], sa.Sc, svp_[(k + 1) & 1]);
+    k_sup2<<<gC, kBlock, 0, s>>>(sa, svp_[rounds & 1]);
+    const uint32_t* spref = spref_;
     MARK(S_RANK);
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
@@ -3424,7 +3715,8 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
                         std::vector<uint32_t>& stage_launches) {
     const uint32_t g1 = p.lds1 ? 0u : 1u;
     const bool expand_run = !p.fuse;
-    const uint32_t launches[S_N] = {1, 6, 0, g1, 3 * g1, g1, 3 * g1, g1, (2 + rounds) * g1, 2 * g1,
+    const uint32_t launches[S_N] = {1, 6, (rs_npass_ + 1) * g1, g1, g1, rs_npass_ * g1, 2 * g1, g1,
+                                    (3 + rounds) * g1, 2 * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
                                     p.lds1 ? 2u : 0u};
@@ -3482,6 +3774,7 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     const uint64_t rows = cap_runs_;  // run rows k_runs could write
     rc = ensure_runs(p.R, Sreg + w.ndocs);
     if (rc) return rc;
+    if (!p.lds1 && (rc = ensure_radix(p.R))) return rc;
     if (p.R > rows) {
         // more runs than rows: the run records again, now that they fit (k_runs only reads
         // level-0 outputs, so it can run twice)
@@ -3506,8 +3799,6 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     runs_ += p.R;
     if (!errs && hctl[C_VISITED] != p.R) errs |= 16u;  // unreachable runs: a cycle
     if (errs) {
-        // restore the all-zero invariant (stream-ordered, as every use of deg_)
-        (void)hipMemsetAsync(deg_, 0, (cap_runs_ + 16) * 4, stream);
         (void)hipStreamSynchronize(stream);
         err = "malformed op log detected on device (flags " + std::to_string(errs) + ")";
         return CRDT_HIP_EBADLOG;

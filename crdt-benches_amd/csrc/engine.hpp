@@ -260,11 +260,19 @@ private:
     uint32_t *r_head_ = nullptr, *r_pstart_ = nullptr, *r_parent_ = nullptr,
              *roff_ = nullptr;
     uint64_t* r_key_ = nullptr;
-    uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
-             *bigl_ = nullptr, *scan_sums_ = nullptr, *ctl_ = nullptr;
+    uint32_t* ctl_ = nullptr;
+    // radix-sort scratch of the global level 1 (engine.hip k_rs_*)
+    uint64_t cap_rs_ = 0;
+    uint4* rs_elem_[2] = {nullptr, nullptr};
+    uint32_t *rs_status_ = nullptr, *rs_small_ = nullptr;
+    uint2* rs_bigl_ = nullptr;
+    uint32_t rs_npass_ = 0;
     uint4* rec_ = nullptr;
-    uint32_t *sw_ = nullptr, *snext_ = nullptr, *pred_ = nullptr, *v0_ = nullptr, *v1_ = nullptr,
-             *p0_ = nullptr, *p1_ = nullptr;
+    uint2* swn_ = nullptr;     // per splitter {sublist weight, next splitter}
+    uint32_t* spref_ = nullptr;  // per splitter: exclusive prefix along its list
+    uint2* sup_ = nullptr;     // super-splitters (engine.hip k_sup1): {weight, next}
+    uint32_t* spred_ = nullptr;
+    uint2* svp_[2] = {nullptr, nullptr};
     uint32_t* host_out_ = nullptr;       // pinned image of every wave's result block
     uint64_t cap_host_out_ = 0;          // bytes
     uint32_t probe_doc_ = 0;             // 1 + document whose k_doctree phases are printed
@@ -306,6 +314,8 @@ private:
     int merge_async(DeviceLogs& L, uint64_t* digests, uint64_t* lens, uint64_t* cps,
                     crdt_hip_stats* st);
     int ensure_runs(uint64_t runs, uint64_t splitters);
+    int ensure_radix(uint64_t runs);
+    int ensure_splitters(uint64_t splitters);
     int ensure_scratch(const Wave& w);
     int ensure_host_out(const DeviceLogs& L);
     uint32_t* host_block(const DeviceLogs& L, uint32_t wi) const;

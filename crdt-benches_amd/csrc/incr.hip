@@ -66,7 +66,8 @@ struct IncArgs {
     const uint32_t* parent;     // replica slot arrays (slot = id)
     const uint64_t* key;
     const uint8_t* cp;
-    uint32_t* rank;             // slot -> rank
+    const uint32_t* rank;       // slot -> rank (the order of n0 items)
+    uint32_t* rank2;            // slot -> rank in the new order (every slot 0..n0 + m written)
     const uint32_t* seq;        // rank -> slot (n0 + 1 entries)
     uint32_t* seq2;             // the new order (n0 + 1 + m entries)
     uint32_t* lb_flag;          // per tile: look-back status (call epoch << 2 | state)
@@ -461,7 +462,7 @@ __device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, u
         const uint32_t np = k + c;
         a.seq2[np] = sl[q];
         cwl[np - o0] = cwq[q];
-        a.rank[sl[q]] = np;
+        a.rank2[sl[q]] = np;
         const uint32_t w = word_bytes(cwq[q]);
         bytes += w;
         cps += w ? 1u : 0u;
@@ -473,7 +474,7 @@ __device__ __forceinline__ uint2 inc_splice_tile(const IncArgs& a, uint32_t b, u
         const uint32_t cwj = slot_word(a.cp, sj);
         a.seq2[np] = sj;
         cwl[np - o0] = cwj;
-        a.rank[sj] = np;
+        a.rank2[sj] = np;
         const uint32_t w = word_bytes(cwj);
         bytes += w;
         cps += w ? 1u : 0u;
@@ -704,29 +705,33 @@ int inc_reserve(Engine& E, IncState& s, uint64_t items, uint64_t bytes) {
     if (need > s.cap) {
         // grown with the contents kept: the current order and the ranks are copied over
         const uint64_t cap = std::max<uint64_t>({need, 2 * s.cap, 4096});
-        uint32_t *q0 = nullptr, *q1 = nullptr, *rk = nullptr;
+        uint32_t *q0 = nullptr, *q1 = nullptr, *r0 = nullptr, *r1 = nullptr;
         hipError_t e = dalloc(&q0, cap);
         if (e == hipSuccess) e = dalloc(&q1, cap);
-        if (e == hipSuccess) e = dalloc(&rk, cap);
+        if (e == hipSuccess) e = dalloc(&r0, cap);
+        if (e == hipSuccess) e = dalloc(&r1, cap);
         if (e == hipSuccess && s.cap) {
             e = hipMemcpyAsync(q0, s.seq[s.cur], s.cap * 4, hipMemcpyDeviceToDevice, E.stream);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(rk, s.rank, s.cap * 4, hipMemcpyDeviceToDevice, E.stream);
+                e = hipMemcpyAsync(r0, s.rank[s.cur], s.cap * 4, hipMemcpyDeviceToDevice, E.stream);
         }
         if (e == hipSuccess) e = hipStreamSynchronize(E.stream);
         if (e != hipSuccess) {
             dfree(q0);
             dfree(q1);
-            dfree(rk);
+            dfree(r0);
+            dfree(r1);
             s.valid = false;
             return ifail(E, "incremental order arrays", e);
         }
         dfree(s.seq[0]);
         dfree(s.seq[1]);
-        dfree(s.rank);
+        dfree(s.rank[0]);
+        dfree(s.rank[1]);
         s.seq[0] = q0;
         s.seq[1] = q1;
-        s.rank = rk;
+        s.rank[0] = r0;
+        s.rank[1] = r1;
         s.cur = 0;
         s.cap = cap;
     }
@@ -766,7 +771,8 @@ IncArgs make_args(Replica& r, IncState& s, uint32_t n0, uint32_t m) {
     a.parent = r.logs.parent;
     a.key = r.logs.key;
     a.cp = r.logs.cp;
-    a.rank = s.rank;
+    a.rank = s.rank[s.cur];
+    a.rank2 = s.rank[s.cur ^ 1];
     a.seq = s.seq[s.cur];
     a.seq2 = s.seq[s.cur ^ 1];
     a.lb_flag = s.lb_flag;
@@ -796,12 +802,12 @@ int inc_run(Engine& E, IncState& s, IncArgs& a, bool sync) {
     hipStream_t st = E.stream;
     ICHK(inc_setup(), "incremental merge setup");
     const bool prof = inc_profile();
-    static hipEvent_t ev[2] = {};
-    static uint64_t* tsp = nullptr;
+    hipEvent_t* ev = s.pev;  // (per state: a state lives on one context and device)
     if (prof && !ev[0]) {
-        for (auto& e : ev) ICHK(hipEventCreate(&e), "event");
-        ICHK(dalloc(&tsp, 16), "timestamps");
+        for (int k = 0; k < 2; ++k) ICHK(hipEventCreate(&ev[k]), "event");
+        ICHK(dalloc(&s.tsp, 16), "timestamps");
     }
+    uint64_t* tsp = s.tsp;
     a.tsp = prof ? tsp : nullptr;
     const auto h0 = std::chrono::steady_clock::now();
     if (prof) ICHK(hipEventRecord(ev[0], st), "event");
@@ -897,7 +903,11 @@ int inc_rebuild(Engine& E, Replica& r, IncState& s) {
 IncState::~IncState() {
     dfree(seq[0]);
     dfree(seq[1]);
-    dfree(rank);
+    dfree(rank[0]);
+    dfree(rank[1]);
+    dfree(tsp);
+    for (hipEvent_t e : pev)
+        if (e) (void)hipEventDestroy(e);
     dfree(lb_flag);
     dfree(lb_agg);
     dfree(lb_inc);
@@ -923,7 +933,9 @@ int replica_merge_inc(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_
         return CRDT_HIP_OK;
     }
     ICHK(hipSetDevice(E.device), "hipSetDevice");
-    bool fast = s.valid && r.n >= s.n && r.n - s.n <= kIncMax;
+    // (the look-back packs {bytes, codepoints} as two u32 halves: a text of 4 GiB or more merges
+    // in full)
+    bool fast = s.valid && r.n >= s.n && r.n - s.n <= kIncMax && r.vis_bytes < (1ull << 32);
     if (fast) {
         rc = inc_reserve(E, s, r.n, r.vis_bytes);  // (grows keeping the order)
         if (rc) return rc;

@@ -28,6 +28,7 @@ uint32_t get32(const uint8_t* p) {
 OpLog::OpLog() {
     chunks_.push_back(new_chunk());
     fen_build();
+    nxt_.push_back(NIL);
 }
 
 void OpLog::reserve(size_t items, size_t dels) {
@@ -38,6 +39,7 @@ void OpLog::reserve(size_t items, size_t dels) {
     cp.reserve(items);
     agent.reserve(items);
     deleted.reserve(items);
+    nxt_.reserve(items + 1);
 }
 
 OpLog::Chunk OpLog::new_chunk() const {
@@ -139,6 +141,7 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
         std::string e = rebuild_index();
         if (!e.empty()) return e;
     }
+    if (!fugue) return insert_rga(pos, cps, k);
     if (pos > nvis_) return "insert position out of range";
     if (k == 0) return "";
     if ((uint64_t)size() + k >= 0x7FFFFFF0ull) return "op log too large";
@@ -236,7 +239,154 @@ std::string OpLog::insert(uint64_t pos, const uint32_t* cps, size_t k) {
     return "";
 }
 
+// ---- RGA: gap buffer of visible id spans + full-list successors --------------------------------
+void OpLog::gb_move(uint64_t pos) {
+    while (gvis_ > pos) {
+        GSpan& sp = gb_[g0_ - 1];
+        if (gvis_ - sp.len >= pos) {
+            gb_[--g1_] = sp;
+            --g0_;
+            gvis_ -= sp.len;
+        } else {  // split: the part after pos goes right of the gap
+            const uint32_t o = (uint32_t)(pos - (gvis_ - sp.len));
+            gb_[--g1_] = GSpan{sp.id + o, sp.len - o};
+            sp.len = o;
+            gvis_ = pos;
+        }
+    }
+    while (gvis_ < pos) {
+        GSpan& sp = gb_[g1_];
+        if (gvis_ + sp.len <= pos) {
+            gb_[g0_++] = sp;
+            ++g1_;
+            gvis_ += sp.len;
+        } else {
+            const uint32_t o = (uint32_t)(pos - gvis_);
+            gb_[g0_++] = GSpan{sp.id, o};
+            sp.id += o;
+            sp.len -= o;
+            gvis_ = pos;
+        }
+    }
+}
+
+void OpLog::gb_reserve(size_t k) {
+    if (g1_ - g0_ >= k) return;
+    const size_t tail = gb_.size() - g1_;
+    const size_t cap = std::max<size_t>({2 * gb_.size(), gb_.size() + k + 64, 1024});
+    gb_.resize(cap);
+    std::memmove(gb_.data() + cap - tail, gb_.data() + g1_, tail * sizeof(GSpan));
+    g1_ = cap - tail;
+}
+
+std::string OpLog::insert_rga(uint64_t pos, const uint32_t* cps, size_t k) {
+    if (pos > nvis_) return "insert position out of range";
+    if (k == 0) return "";
+    if ((uint64_t)size() + k >= 0x7FFFFFF0ull) return "op log too large";
+    const uint32_t first = size() + 1;
+    gb_reserve(2);  // (a split and a new span)
+    gb_move(pos);
+    // origin_left: the pos-th visible item, the last one before the gap
+    const uint32_t left = pos ? gb_[g0_ - 1].id + gb_[g0_ - 1].len - 1u : 0u;
+    const uint32_t right = nxt_[left];  // origin_right (tombstones included)
+    // the new items follow left in the full list, before whatever followed it
+    nxt_[left] = first;
+    const size_t n0 = parent.size();
+    if (k == 1) {  // typing: one item
+        parent.push_back(left);
+        oright.push_back(right);
+        lamport.push_back(++max_lamport);
+        agent.push_back(local_agent);
+        deleted.push_back(0);
+        cp.push_back(cps[0]);
+        nxt_.push_back(right);
+    } else {  // a paste: every column grown once, then filled
+        parent.resize(n0 + k);
+        oright.resize(n0 + k, right);
+        lamport.resize(n0 + k);
+        agent.resize(n0 + k, local_agent);
+        deleted.resize(n0 + k, 0);
+        cp.resize(n0 + k);
+        nxt_.resize(n0 + 1 + k);
+        uint32_t* P = parent.data() + n0;
+        uint32_t* L = lamport.data() + n0;
+        uint32_t* N = nxt_.data() + n0 + 1;
+        P[0] = left;
+        for (size_t j = 1; j < k; ++j) P[j] = first + (uint32_t)j - 1;
+        for (size_t j = 0; j < k; ++j) {
+            L[j] = max_lamport + 1 + (uint32_t)j;
+            N[j] = first + (uint32_t)j + 1;
+        }
+        N[k - 1] = right;
+        max_lamport += (uint32_t)k;
+        std::memcpy(cp.data() + n0, cps, k * sizeof(uint32_t));
+    }
+    if (g0_ && gb_[g0_ - 1].id + gb_[g0_ - 1].len == first)
+        gb_[g0_ - 1].len += (uint32_t)k;  // typing on: the span before the gap grows
+    else
+        gb_[g0_++] = GSpan{first, (uint32_t)k};
+    gvis_ += k;
+    nvis_ += k;
+    return "";
+}
+
+std::string OpLog::remove_rga(uint64_t start, uint64_t end) {
+    if (end < start || end > nvis_) return "remove range out of range";
+    uint64_t left = end - start;
+    if (!left) return "";
+    gb_reserve(1);
+    gb_move(start);
+    nvis_ -= left;
+    while (left) {  // the visible items right of the gap, span by span
+        GSpan& sp = gb_[g1_];
+        const uint32_t take = (uint32_t)std::min<uint64_t>(left, sp.len);
+        const size_t m0 = del_ops.size();
+        del_ops.resize(m0 + take);
+        uint32_t* D = del_ops.data() + m0;
+        for (uint32_t j = 0; j < take; ++j) D[j] = sp.id + j;
+        std::memset(deleted.data() + sp.id - 1, 1, take);
+        if (take == sp.len) {
+            ++g1_;
+        } else {
+            sp.id += take;
+            sp.len -= take;
+        }
+        left -= take;
+    }
+    return "";
+}
+
+// The gap buffer and the successors from the full document order (ids, tombstones included).
+std::string OpLog::rebuild_index_rga(const std::vector<uint32_t>& order) {
+    nxt_.assign((size_t)size() + 1, NIL);
+    gb_.assign(1024, GSpan{0, 0});
+    g0_ = 0;
+    g1_ = gb_.size();
+    uint32_t prev = 0;
+    uint64_t v = 0;
+    for (uint32_t id : order) {
+        nxt_[prev] = id;
+        prev = id;
+        if (deleted[id - 1]) continue;
+        ++v;
+        if (g0_ && gb_[g0_ - 1].id + gb_[g0_ - 1].len == id) {
+            gb_[g0_ - 1].len++;
+        } else {
+            gb_reserve(1);
+            gb_[g0_++] = GSpan{id, 1};
+        }
+    }
+    gvis_ = v;
+    nvis_ = v;
+    stale_ = false;
+    return "";
+}
+
 std::string OpLog::insert_utf8(uint64_t pos, const char* s, size_t nbytes) {
+    if (nbytes == 1 && (unsigned char)s[0] < 0x80u) {  // typing one ASCII character
+        const uint32_t c = (unsigned char)s[0];
+        return insert(pos, &c, 1);
+    }
     cps_.clear();
     if (!utf8_decode(s, nbytes, cps_)) return "invalid UTF-8";
     return insert(pos, cps_.data(), cps_.size());
@@ -283,6 +433,7 @@ std::string OpLog::remove(uint64_t start, uint64_t end) {
         std::string e = rebuild_index();
         if (!e.empty()) return e;
     }
+    if (!fugue) return remove_rga(start, end);
     if (end < start || end > nvis_) return "remove range out of range";
     uint64_t left = end - start;
     if (!left) return "";
@@ -357,30 +508,21 @@ std::string OpLog::rebuild_index() {
         if (lamport[a - 1] != lamport[b - 1]) return lamport[a - 1] > lamport[b - 1];
         return agent[a - 1] > agent[b - 1];
     };
-    chunks_.clear();
-    chunks_.push_back(new_chunk());
-    nvis_ = 0;
-    hint_c_ = SIZE_MAX;
-    hint_si_ = SIZE_MAX;
+    std::vector<uint32_t> order;
+    order.reserve(n);
     std::vector<uint32_t> stack;
     stack.reserve(n + 1);
     stack.push_back(0);
-    size_t seen = 0;
     while (!stack.empty()) {
         uint32_t v = stack.back();
         stack.pop_back();
-        if (v) {
-            ++seen;
-            index_append(v);
-        }
+        if (v) order.push_back(v);
         uint32_t a = start[v], b = start[v + 1];
         std::sort(kids.begin() + a, kids.begin() + b, [&](uint32_t x, uint32_t y) { return newer(y, x); });
         for (uint32_t j = a; j < b; ++j) stack.push_back(kids[j]);  // oldest pushed first
     }
-    if (seen != n) return "malformed op log (cycle)";
-    fen_build();
-    stale_ = false;
-    return "";
+    if (order.size() != n) return "malformed op log (cycle)";
+    return rebuild_index_rga(order);
 }
 
 // Appends item v to the end of the rebuilt sequence.

@@ -65,7 +65,26 @@ public:
     void reserve(size_t items, size_t dels = 0);
 
 private:
-    // Positional index: the document sequence (tombstones included) as spans of consecutive
+    // RGA positional index: the visible items in document order as a gap buffer of spans (runs
+    // of consecutive ids; typing extends the span before the gap), the gap at the last edit and
+    // the visible items before it (gvis_), so an edit next to the previous one moves nothing and a
+    // jump moves the spans in between, not the items; and the full-list successor of every item
+    // (tombstones included; nxt_[0] = the first item) for origin_right.  Fugue logs use the span
+    // index below: an insert there needs to know whether its left neighbour has a right child.
+    struct GSpan {
+        uint32_t id, len;
+    };
+    std::vector<GSpan> gb_;        // gap [g0_, g1_)
+    size_t g0_ = 0, g1_ = 0;
+    uint64_t gvis_ = 0;            // visible items in gb_[0, g0_)
+    std::vector<uint32_t> nxt_;    // per id 0..n: next item in the full list (NIL: last)
+    void gb_move(uint64_t pos);    // the gap at visible position pos (a span split if needed)
+    void gb_reserve(size_t k);
+    std::string insert_rga(uint64_t pos, const uint32_t* cps, size_t k);
+    std::string remove_rga(uint64_t start, uint64_t end);
+    std::string rebuild_index_rga(const std::vector<uint32_t>& order);
+
+    // Positional index (Fugue): the document sequence (tombstones included) as spans of consecutive
     // item ids that are also consecutive in document order and share one deleted state, packed
     // into chunks of at most kSpanMax spans with a Fenwick tree over the chunks' visible counts.
     struct Span {

@@ -22,10 +22,13 @@ constexpr uint32_t kIncMax = 4096;  // most items a fast-path merge appends
 struct IncState {
     bool valid = false;
     uint32_t n = 0;                  // items the order covers
-    uint64_t cap = 0;                // entries of seq[0], seq[1], rank
+    uint64_t cap = 0;                // entries of seq[0], seq[1], rank[0], rank[1]
     uint32_t* seq[2] = {nullptr, nullptr};  // rank -> slot (ping-pong: seq[cur] is current)
     int cur = 0;
-    uint32_t* rank = nullptr;        // slot -> rank
+    // slot -> rank, ping-pong like seq: a merge reads the old ranks of the new roots' parents in
+    // every workgroup while the splices of other workgroups write the new ranks, so they are
+    // two arrays (rank[cur] read, rank[cur ^ 1] written)
+    uint32_t* rank[2] = {nullptr, nullptr};
     uint32_t* lb_flag = nullptr;     // per tile of the order: look-back status, aggregate and
     uint64_t* lb_agg = nullptr;      //   inclusive prefix of the text (incr.hip inc_lookback)
     uint64_t* lb_inc = nullptr;
@@ -37,6 +40,9 @@ struct IncState {
     uint64_t* dres = nullptr;        //   (its device address)
     uint64_t calls = 0;              // calls made (stamps the result block)
     std::vector<uint32_t> hseq;      // (rebuild staging)
+    // (CRDT_INC_PROFILE) this state's profile events and phase timestamps
+    hipEvent_t pev[2] = {nullptr, nullptr};
+    uint64_t* tsp = nullptr;
     IncState() = default;
     IncState(const IncState&) = delete;
     IncState& operator=(const IncState&) = delete;

@@ -102,11 +102,12 @@ typedef struct {
 enum {
     CRDT_HIP_STAGE_CLASSIFY = 0, /* level 0: seq/jump bits, weights, per-tile UTF-8           */
     CRDT_HIP_STAGE_RUNS = 1,     /* level 0: head bitvector, tile scan, run records, text     */
-    CRDT_HIP_STAGE_RPARENT = 2,  /* level 0: parent run and weight of every run               */
-    CRDT_HIP_STAGE_COUNT = 3,    /* level 1: child count per parent run                       */
-    CRDT_HIP_STAGE_SCAN = 4,     /* level 1: exclusive scan of child counts                   */
-    CRDT_HIP_STAGE_PLACE = 5,    /* level 1: children scattered into parent segments          */
-    CRDT_HIP_STAGE_LINK = 6,     /* level 1: sibling sort + first-child / next-sibling        */
+    CRDT_HIP_STAGE_SORTB = 2,    /* level 1: radix sort of the (run, next sibling) pairs by
+                                    run id, and the run records in run order                  */
+    CRDT_HIP_STAGE_COUNT = 3,    /* level 1: digit histograms of the radix sort by parent run */
+    CRDT_HIP_STAGE_SCAN = 4,     /* level 1: bucket starts of both radix sorts                */
+    CRDT_HIP_STAGE_PLACE = 5,    /* level 1: radix passes, runs by parent run (LDS-staged)    */
+    CRDT_HIP_STAGE_LINK = 6,     /* level 1: sibling order of each group, first children      */
     CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums                          */
     CRDT_HIP_STAGE_RANK = 8,     /* level 1: ranking of the splitter lists                    */
     CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets                  */

@@ -160,3 +160,36 @@ def test_incremental_state_survives_clone_and_fugue_takes_the_full_path(ctx, ora
     f.apply_updates([up.encode_from(0)])
     cps, nb, path, text = f.merge_inc(text=True)
     assert path == 0 and text == b"fugue text"
+
+
+def test_incremental_len_on_a_document_with_more_tiles_than_cus(ctx, oracle):
+    """A 2.2 M-item document: 538 tiles of 4096 old ranks, more than the GPU has CUs (k_inc holds
+    ~136 KB of LDS, one workgroup per CU), so later workgroups start after earlier ones have
+    spliced.  Every batch is a set of small local edits whose roots hang under parents spread
+    over the whole document; each checkpoint's text is compared with the oracle's merge.  (Reads
+    of the old ranks and writes of the new ones are separate arrays, incr.hip rank / rank2.)"""
+    import random
+    rng = random.Random(0x1C4)
+    log = crdt_hip.OpLog()
+    base = "".join(chr(ord("a") + i % 26) for i in range(2_200_000))
+    log.insert(0, base)
+    r = crdt_hip.Replica(ctx)
+    r.apply_updates([log.encode_from(0)])
+    assert r.merge_inc()[2] == 0
+    length = len(base)
+    for c in range(4):
+        v = log.version()
+        for _ in range(150):
+            pos = rng.randrange(0, length)
+            if rng.random() < 0.3 and pos + 2 < length:
+                log.remove(pos, pos + 2)
+                length -= 2
+            else:
+                s = "".join(rng.choice("XYZ") for _ in range(rng.randint(1, 4)))
+                log.insert(pos, s)
+                length += len(s)
+        r.apply_updates([log.encode_from(v)])
+        cps, nb, path, text = r.merge_inc(text=True)
+        assert path == 1, c
+        assert nb == length
+        assert text == oracle.merge(to_anchor(log.arrays())), f"checkpoint {c}"
