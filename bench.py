@@ -484,6 +484,7 @@ def traces_workload(args) -> int:
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
     ctx.set_param("level1", args.level1)
+    ctx.set_param("contraction", args.contraction)
     if not args.fuse_text:  # (the engine's default is 1; builds before the parameter lack it)
         ctx.set_param("fuse_text", 0)
     ctx.set_param("lanes", args.lanes)
@@ -493,8 +494,6 @@ def traces_workload(args) -> int:
         ctx.set_param("stile_text", args.stile_text)
     if args.nsq_list != 1:  # (likewise)
         ctx.set_param("nsq_list", args.nsq_list)
-    if args.cp2 != 0:  # (likewise)
-        ctx.set_param("cp2", args.cp2)
     ctx.set_param("lane_gate", args.lane_gate)
     ctx.set_param("max_wave_slots", 1 << args.wave_slots_log2)
     ctx.set_param("plan_cache", args.plan_cache)
@@ -608,6 +607,30 @@ def traces_workload(args) -> int:
             }
             out["digests_ok"] = out["digests_ok"] and cres["digests_ok"]
             cb.close()
+    # companion line: the same headline batch over the plain SoA (no compact list of the non-seq
+    # items' parents and keys: the level-0 kernels gather them from the columns), so that the
+    # headline's dependence on that one-time index is measured, not assumed
+    if args.plain_companion:
+        ctx.set_param("nsq_list", 0)
+        pa = argparse.Namespace(replicas=args.replicas, relabel=args.relabel, warmup=1, steps=3)
+        pres = traces_rank(pa, comm, make_batch, inputs)
+        ctx.set_param("nsq_list", args.nsq_list)
+        if rank == 0:
+            pb, ps = pres["batch"], pres["stats"]
+            out["companion_plain_soa"] = {
+                "workload": "config 3 (%d replicas per GPU, relabel=%s) without the compact list "
+                            "of the non-seq items' parents and keys (nsq_list 0)"
+                            % (pa.replicas, pa.relabel),
+                "value": pres["value"], "unit": "patches/s", "ms_per_step": pres["step_s"] * 1e3,
+                "steps": pa.steps, "digests_ok": pres["digests_ok"],
+                "input_encoding_ms": pres["encode_s"] * 1e3,
+                "kernels_ms": {k: v / 1e6 for k, v in
+                               {k: float(np.mean([s_["stage_ns"][k] for s_ in ps]))
+                                for k in ps[0]["stage_ns"]}.items() if v > 2e4},
+            }
+            out["digests_ok"] = out["digests_ok"] and pres["digests_ok"]
+        if rank == 0:
+            pres["batch"].close()
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:  # (the CPU lines belong to the N=1 run)
             threads = args.cpu_threads or host_cpus()["threads"]
@@ -631,6 +654,7 @@ def side_workload(args) -> int:
     ctx = crdt_hip.Context(local)
     comm = Comm(world, rank, ctx)
     ctx.set_param("level1", args.level1)
+    ctx.set_param("contraction", args.contraction)
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
     t_setup = time.perf_counter()
@@ -909,13 +933,14 @@ def parse_args(argv=None):
     ap.add_argument("--stile-text", type=int, default=1, choices=[0, 1],
                     help="1: fused level 1 stages text from the tile segments (k_runs skips the "
                          "slot-order copy)")
-    ap.add_argument("--cp2", type=int, default=0, choices=[0, 1],
-                    help="1: resident batches carry the 2-byte character column (input encoding; "
-                         "escaped codepoints in a side table); 0: the 3-byte column (default: "
-                         "faster, DESIGN.md section 4)")
     ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1],
                     help="1: resident batches carry the compact list of the non-seq items' parents "
                          "(input encoding; k_classify streams it); 0: k_classify gathers them")
+    ap.add_argument("--plain-companion", type=int, default=1, choices=[0, 1],
+                    help="1: a companion line of the headline batch without the compact nsq list")
+    ap.add_argument("--contraction", type=int, default=0, choices=[0, 1, 2],
+                    help="run contraction of RGA waves: 0 by the input (none when most items lack "
+                         "the previous-slot flag), 1 always, 2 never")
     ap.add_argument("--level1", type=int, default=0, choices=[0, 1],
                     help="0: per-document LDS level 1 where it fits (default), 1: global kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

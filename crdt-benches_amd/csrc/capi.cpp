@@ -213,10 +213,10 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.stile_text = value == 1;
         return 0;
     }
-    if (k == "cp2") {  // 1: batches get the 2-byte character column (Engine::build_cp2)
-        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "cp2 must be 0 or 1");
-        ctx->eng.cp2_column = value == 1;
-        return 0;
+    if (k == "contraction") {  // run contraction: 0 by the input, 1 always, 2 never (Wave::nocon)
+        if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "contraction must be 0, 1 or 2");
+        ctx->eng.contraction = (uint32_t)value;
+        return CRDT_HIP_OK;
     }
     if (k == "nsq_list") {  // 1: batches get the compact nsq parent list (Engine::build_nsq)
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0 or 1");

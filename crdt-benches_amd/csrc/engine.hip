@@ -157,22 +157,12 @@ struct L0Args {
     const uint32_t* nsq_pre;
     const uint64_t* nsq_key;    // (beside nsq_par) the keys of the nsq items: every nsq item that
                                 //   survives is a run head, whose key k_runs then need not gather
-    // resident batches (Engine::build_cp2): the 2-byte character column (an ASCII character, or
-    // an escape to xcp, and the three flags), the escaped codepoints in slot order with their
-    // prefix count per 64 slots (offset to the wave), and one bit per 16 slots with an escape
-    // (global group index = xgrp_off + wave-relative group).  sparse_nib: the weight nibbles are
-    // written only for 16-slot groups with an escape (k_runs takes the visible bits elsewhere)
-    const uint16_t* in_cp2;
-    const uint32_t* xcp;
-    const uint32_t* xpre;
-    const uint32_t* xgrp;
-    uint64_t xgrp_off;
-    uint32_t sparse_nib;
+    // 1: no run contraction (Wave::nocon): every item heads its own run, so k_classify reads no
+    // parents and sets no jump bits, k_heads marks every item, and k_runs reads each run's parent
+    // and key from the columns in slot order (a run's parent run is its document start's run
+    // plus the parent's item index).  RGA waves only.
+    uint32_t nocon;
 };
-// the 2-byte character word: ASCII character (bits 0-6), escape (bit 7: the codepoint is the
-// slot's entry in xcp), left child (13), previous-slot flag (14), tombstone (15)
-constexpr uint32_t kCp2Esc = 0x80u;
-__host__ __device__ constexpr uint32_t cp2_flags_to_word(uint32_t v) { return ((v >> 13) & 7u) << 21; }
 
 constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-byte character
 // Fugue (left children).  A run whose head has left children is numbered as two rows: a content
@@ -206,7 +196,6 @@ constexpr uint32_t kRecTree = 1u << 31;  // k_runs record of a head with two row
 //    head, and k_runs reads its parent there (coalesced) instead of gathering it.
 // The stream part reads 3 bytes per slot and waits for one round trip; the parent part is one
 // more round trip at the end of the block, hidden behind the other blocks' streams.
-template <bool CP2>
 __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint32_t lds[kBlock / 64];
     __shared__ uint32_t jl[kScanTile / 32];
@@ -230,54 +219,17 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     // slots hold junk and are masked below
     uint4 cq[3] = {};
     uint2 doc = make_uint2(0, 0);
-    uint32_t xp = 0;  // (CP2) escapes before the thread's 64-slot chunk
     if (live) {
-        if (CP2) {
-            const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp2 + gs);  // 32 B, 16-aligned
-            cq[0] = cv[0];
-            cq[1] = cv[1];
-#ifndef CRDT_CP2_XPRE_LATE
-            xp = a.xpre[gs >> 6];
-#endif
-        } else {
-            const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B
+        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B
 #pragma unroll
-            for (int q = 0; q < 3; ++q) cq[q] = cv[q];
-        }
+        for (int q = 0; q < 3; ++q) cq[q] = cv[q];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
     }
 
     const uint32_t n = doc.y, l0 = gs - doc.x;
     ldoc[threadIdx.x] = doc;
     uint32_t C[16];
-    uint32_t escm = 0;  // (CP2) slots whose codepoint is in xcp
-    if (CP2) {
-        // the 16 two-byte words from 8 dwords; flags moved to the three-byte word's positions
-        const uint32_t CW[8] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z, cq[1].w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t v = (CW[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-            C[k] = (v & 0x7Fu) | cp2_flags_to_word(v);
-            escm |= ((v & kCp2Esc) ? 1u : 0u) << k;
-        }
-        // escaped codepoints (not on the traces' hot path: a wave-uniform branch): the entry of
-        // the chunk's first escape, plus the escapes of the chunk's groups before this one (the
-        // chunk's four groups are lanes 4c..4c+3)
-        if (__ballot(escm != 0u)) {
-#ifdef CRDT_CP2_XPRE_LATE
-            if (live) xp = a.xpre[gs >> 6];
-#endif
-            const uint32_t cnt = (uint32_t)__popc(escm), l4 = threadIdx.x & ~3u;
-            const uint32_t e0 = (uint32_t)__shfl((int)cnt, (int)(l4 & 63u));
-            const uint32_t e1 = (uint32_t)__shfl((int)cnt, (int)((l4 + 1u) & 63u));
-            const uint32_t e2 = (uint32_t)__shfl((int)cnt, (int)((l4 + 2u) & 63u));
-            const uint32_t g = threadIdx.x & 3u;
-            uint32_t idx = xp + (g > 0 ? e0 : 0u) + (g > 1 ? e1 : 0u) + (g > 2 ? e2 : 0u);
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if ((escm >> k) & 1u) C[k] |= a.xcp[idx++];
-        }
-    } else {
+    {
         // the 16 three-byte values from 12 dwords (constant shifts: value k at byte 3k)
         const uint32_t CW[13] = {cq[0].x, cq[0].y, cq[0].z, cq[0].w, cq[1].x, cq[1].y, cq[1].z,
                                  cq[1].w, cq[2].x, cq[2].y, cq[2].z, cq[2].w, 0u};
@@ -338,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
         // (sparse: only the groups with an escaped codepoint can weigh more than one byte per
         // visible slot; k_runs reads the nibbles of exactly those, by the same escape bits)
-        if (!CP2 || !a.sparse_nib || escm) a.wnib[gs >> 4] = nib;
+        a.wnib[gs >> 4] = nib;
         a.visb[gs >> 4] = (uint16_t)vis;
     }
     // one scan for both: nsq items << 16 | weight (a tile holds at most 4096 and 16,384)
@@ -392,6 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         for (uint32_t i = threadIdx.x; i < (tw + 15u) / 16u; i += kBlock) dst[i] = src[i];
     }
     if (cl && T != nhi - nlo && threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 1u);  // list != flags
+    if (a.nocon) return;  // (no contraction: no jump bits; k_runs checks the parents)
     if (T == 0) {  // (block-uniform) no nsq item: no jump bit from this tile
         if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = 0u;
         return;
@@ -503,7 +456,15 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
         }
     }
     const uint64_t hw0 = hw;  // the run boundaries (before the dead-run drop)
-    {
+    if (a.nocon) {
+        // no contraction: every item heads its own run, none is dropped
+        hw = 0;
+        if (gs < a.nslots) {
+            const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+            const uint32_t l0 = gs - doc.x, n = doc.y;
+            if (l0 <= n) hw = low_mask64(n + 1u - l0);  // (the document start and its items)
+        }
+    } else {
         // the next word's live slots before its first head keep this word's last run
         const uint64_t hn = (uint64_t)__shfl_down((long long)hw, 1);
         const uint64_t ln = (uint64_t)__shfl_down((long long)lv, 1);
@@ -648,22 +609,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
         if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
-        if (a.sparse_nib) {
-            // one weight per visible slot unless the group holds an escaped codepoint (then
-            // k_classify wrote its nibbles); the visible bits are loaded with the escape word,
-            // not behind it
-            const uint64_t gb = a.xgrp_off + (gs >> 4);
-            const uint32_t xg = a.xgrp[gb >> 5];
-            const uint32_t v = a.visb[gs >> 4];
-            if ((xg >> (gb & 31u)) & 1u) {
-                nib = a.wnib[gs >> 4];
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) nib |= (uint64_t)((v >> j) & 1u) << (4 * j);
-            }
-        } else {
-            nib = a.wnib[gs >> 4];
-        }
+        nib = a.wnib[gs >> 4];
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         nsq = a.nsqb[gs >> 4];
         lnsq[threadIdx.x] = (uint16_t)nsq;
@@ -741,11 +687,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         a.doc_p0[d] = pre.y + (ex & 0xFFFFu);
     }
     if (tile + 1u == a.ntiles && threadIdx.x == 0) a.r_pstart[pre.x + nh + totd] = pre.y + tw_all;
-#ifdef CRDT_EXP_NOTEXT
-    if (false) {
-#else
     if (copy) {
-#endif
         uint32_t* d32 = reinterpret_cast<uint32_t*>(a.sbytes);
         if (m < hi) d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
         for (m += 4u * kBlock; m < hi; m += 4u * kBlock) {
@@ -776,15 +718,30 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         // (resident batches) its key from the same index of the key list, a seq head's gathered
         const uint32_t nw = lnsq[li >> 4];
         const uint32_t lix = lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u));
-#ifdef CRDT_EXP_NOKEY
-        const uint64_t key = g;  // (timing experiment: no key gather)
-#else
-#ifndef CRDT_NO_NSQ_KEY
         const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
-#else
-        const uint64_t key = a.in_key[g];  // (A/B build: every head's key gathered)
-#endif
-#endif
+        if (!FUGUE && a.nocon) {
+            // no contraction: the run's parent and key from the columns (heads are every slot of
+            // the tile's items, so these reads are in slot order); parent run = the document
+            // start's run + the parent's item index
+            uint32_t pr = kNil;
+            uint64_t k = 0;
+            if (!root) {
+                uint32_t p = a.in_parent[g];
+                k = a.in_key[g];
+                if (p > dc.y || p == g - dc.x) {
+                    atomicOr(&a.ctl[C_ERR], 1u);
+                    p = 0;
+                }
+                pr = rho - (g - dc.x) + p;
+            }
+            a.r_head[rho] = g;
+            a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
+            if (rho < a.cap_rows) {
+                a.r_parent[rho] = pr;
+                a.r_key[rho] = k;
+            }
+            continue;
+        }
         uint32_t p = (!sq && !root) ? pls[lix] : 0u;
         a.r_head[rho] = g;
         a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
@@ -811,9 +768,6 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
                 rows += (uint32_t)__popcll(hb & lw & mask);
             }
             pr = tp + hl + rows - 1u;
-#ifdef CRDT_EXP_NOHREC
-            pr = rho - 1u;  // (timing experiment: a valid chain, no head-record gathers)
-#endif
         }
         if (rt < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
             a.r_parent[rt] = pr;
@@ -1055,10 +1009,19 @@ __device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uin
 // elements per wave and digit (ballot matching: stable within the wave), publishes the tile's
 // digit counts, takes the counts of every earlier tile by decoupled look-back (one thread per
 // digit), reorders the tile by digit in LDS and writes each digit's stretch contiguously.
-constexpr uint32_t kRsThreads = 512;
+#ifndef CRDT_RS_THREADS
+#define CRDT_RS_THREADS 512
+#endif
+#ifndef CRDT_RS_ITEMS_A
+#define CRDT_RS_ITEMS_A 8
+#endif
+#ifndef CRDT_RS_ITEMS_B
+#define CRDT_RS_ITEMS_B 16
+#endif
+constexpr uint32_t kRsThreads = CRDT_RS_THREADS;
 constexpr uint32_t kRsWaves = kRsThreads / 64;
-constexpr uint32_t kRsItemsA = 8;                        // sort A: 4096 x 16 B per tile
-constexpr uint32_t kRsItemsB = 16;                       // sort B: 8192 x 8 B per tile
+constexpr uint32_t kRsItemsA = CRDT_RS_ITEMS_A;          // sort A: 4096 x 16 B per tile
+constexpr uint32_t kRsItemsB = CRDT_RS_ITEMS_B;          // sort B: 8192 x 8 B per tile
 constexpr uint32_t kRsTileA = kRsThreads * kRsItemsA;
 constexpr uint32_t kRsTileB = kRsThreads * kRsItemsB;
 constexpr uint32_t kRsBins = 256;
@@ -1435,39 +1398,74 @@ __device__ __forceinline__ bool splitter_arc(const TreeArgs& a, uint32_t s, uint
     return up || a.in_parent[v] != kNil;  // a document start's down arc has its own splitter
 }
 
+// One step of a sublist walk from arc (v, up) with v's record r: the next arc, or false at the
+// end of the sublist (the next arc is a splitter: *nxt = its index) or of the document's tour.
+// A leaf's up arc follows its down arc from the same record.
+__device__ __forceinline__ bool walk_next(const uint4& r, uint32_t m, uint32_t& v, bool& up,
+                                          uint32_t& nxt) {
+    const uint32_t mask = (1u << m) - 1u;
+    uint32_t nv;
+    bool nup;
+    if (!up && r.x != kNil) {
+        nv = r.x;
+        nup = false;
+    } else {
+        if (!up && (v & mask) == 0) {  // a leaf whose up arc is a splitter
+            nxt = ((v >> m) << 1) | 1u;
+            return false;
+        }
+        if (r.z != kNil) { nv = r.z; nup = false; }
+        else if (r.w != kNil) { nv = r.w; nup = true; }
+        else return false;  // up arc of a document start: end of that document's tour
+    }
+    if ((nv & mask) == 0) {
+        nxt = ((nv >> m) << 1) | (nup ? 1u : 0u);
+        return false;
+    }
+    v = nv;
+    up = nup;
+    return true;
+}
+
+// Walks are chains of dependent random loads (one record per arc), so every thread advances
+// kWalkIlp sublists at once: that many loads in flight per thread instead of one.
+#ifndef CRDT_WALK_ILP
+#define CRDT_WALK_ILP 2
+#endif
+constexpr int kWalkIlp = CRDT_WALK_ILP;
+
 __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= a.S) return;
-    const uint32_t m = a.log2m, mask = (1u << m) - 1u;
-    uint32_t v;
-    bool up;
-    uint32_t sum = 0, steps = 0, nxt = kNil;
-    if (splitter_arc(a, s, v, up)) {
-        for (;;) {
-            const uint4 r = a.rec[v];
-            uint32_t nv;
-            bool nup;
-            if (!up) {
-                sum += r.y;
-                if (r.x != kNil) {
-                    nv = r.x;
-                    nup = false;
-                    goto next1;
-                }
-                // a leaf: its up arc follows, from the same record
-                if ((v & mask) == 0) { nxt = ((v >> m) << 1) | 1u; break; }
-            }
-            if (r.z != kNil) { nv = r.z; nup = false; }
-            else if (r.w != kNil) { nv = r.w; nup = true; }
-            else break;  // up arc of a document start: end of that document's tour
-        next1:
-            if ((nv & mask) == 0) { nxt = ((nv >> m) << 1) | (nup ? 1u : 0u); break; }
-            v = nv;
-            up = nup;
-            if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
+    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * kWalkIlp;
+    uint32_t v[kWalkIlp], sum[kWalkIlp], nxt[kWalkIlp], live = 0, steps = 0;
+    bool up[kWalkIlp];
+#pragma unroll
+    for (int q = 0; q < kWalkIlp; ++q) {
+        const uint32_t s = base + q;
+        sum[q] = 0;
+        nxt[q] = kNil;
+        v[q] = 0;
+        up[q] = false;
+        if (s < a.S && splitter_arc(a, s, v[q], up[q])) live |= 1u << q;
+    }
+    while (live) {
+        uint4 r[kWalkIlp];
+#pragma unroll
+        for (int q = 0; q < kWalkIlp; ++q)
+            if ((live >> q) & 1u) r[q] = a.rec[v[q]];
+#pragma unroll
+        for (int q = 0; q < kWalkIlp; ++q) {
+            if (!((live >> q) & 1u)) continue;
+            if (!up[q]) sum[q] += r[q].y;
+            if (!walk_next(r[q], a.log2m, v[q], up[q], nxt[q])) live &= ~(1u << q);
+        }
+        if (++steps > a.step_limit) {
+            atomicOr(&a.ctl[C_ERR], 2u);
+            break;
         }
     }
-    a.swn[s] = make_uint2(sum, nxt);
+#pragma unroll
+    for (int q = 0; q < kWalkIlp; ++q)
+        if (base + q < a.S) a.swn[base + q] = make_uint2(sum[q], nxt[q]);
 }
 
 // Ranking of the splitter lists (exclusive prefix of the sublist weights along each document's
@@ -1611,36 +1609,39 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
 
 // Re-walk: every run passed on a down arc gets its offset inside its document.
 __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __restrict__ spref) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t m = a.log2m, mask = (1u << m) - 1u;
-    uint32_t v = 0;
-    bool up = false;
-    const bool live = s < a.S && splitter_arc(a, s, v, up);
-    uint32_t off = live ? spref[s] : 0u;
-    uint32_t steps = 0, runs = 0;
-    for (; live;) {
-        const uint4 r = a.rec[v];
-        uint32_t nv;
-        bool nup;
-        if (!up) {
-            if (r.y) a.roff[v] = off;  // runs without visible bytes are never expanded
-            off += r.y;
-            ++runs;
-            if (r.x != kNil) {
-                nv = r.x;
-                nup = false;
-                goto next2;
-            }
-            if ((v & mask) == 0) break;  // a leaf whose up arc is a splitter
+    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * kWalkIlp;
+    uint32_t v[kWalkIlp], off[kWalkIlp], live = 0, steps = 0, runs = 0, nxt;
+    bool up[kWalkIlp];
+#pragma unroll
+    for (int q = 0; q < kWalkIlp; ++q) {
+        const uint32_t s = base + q;
+        v[q] = 0;
+        up[q] = false;
+        off[q] = 0;
+        if (s < a.S && splitter_arc(a, s, v[q], up[q])) {
+            live |= 1u << q;
+            off[q] = spref[s];
         }
-        if (r.z != kNil) { nv = r.z; nup = false; }
-        else if (r.w != kNil) { nv = r.w; nup = true; }
-        else break;
-    next2:
-        if ((nv & mask) == 0) break;
-        v = nv;
-        up = nup;
-        if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
+    }
+    while (live) {
+        uint4 r[kWalkIlp];
+#pragma unroll
+        for (int q = 0; q < kWalkIlp; ++q)
+            if ((live >> q) & 1u) r[q] = a.rec[v[q]];
+#pragma unroll
+        for (int q = 0; q < kWalkIlp; ++q) {
+            if (!((live >> q) & 1u)) continue;
+            if (!up[q]) {
+                if (r[q].y) a.roff[v[q]] = off[q];  // runs without visible bytes are never expanded
+                off[q] += r[q].y;
+                ++runs;
+            }
+            if (!walk_next(r[q], a.log2m, v[q], up[q], nxt)) live &= ~(1u << q);
+        }
+        if (++steps > a.step_limit) {
+            atomicOr(&a.ctl[C_ERR], 2u);
+            break;
+        }
     }
     // reachability: every run of the wave must be visited exactly once
     const uint32_t tot = wave_sum(runs);
@@ -2829,62 +2830,41 @@ __global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt) {
     if (c * 64ull >= a.nslots) return;
     cnt[c] = (uint32_t)__popcll(chunk_nsq_bits(a, c * 64u));
 }
+// The list itself: one workgroup per 4096-slot tile (16 slots per thread, k_classify's layout):
+// the tile's nsq items listed in LDS in slot order (a block scan of the per-thread counts), then
+// their parents and keys read by the whole block and written to the tile's range of the list as
+// consecutive words.
 __global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t* pre, uint32_t* out,
                                                         uint64_t* kout) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c * 64ull >= a.nslots) return;
-    uint32_t o = pre[c];
-    for (uint64_t b = chunk_nsq_bits(a, c * 64u); b; b &= b - 1ull) {
-        const uint32_t g = c * 64u + (uint32_t)__builtin_ctzll(b);
-        out[o] = a.in_parent[g];
-        kout[o++] = a.in_key[g];
-    }
-}
-
-// ---- the 2-byte character column of a resident batch (Engine::build_cp2) ---------------------
-// One thread per 64-slot chunk of a wave.  Escapes: items whose codepoint is not ASCII.
-__global__ __launch_bounds__(kBlock) void k_cp2_count(L0Args a, uint32_t* cnt) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c * 64ull >= a.nslots) return;
-    const uint32_t gs = c * 64u;
-    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-    const uint32_t l0 = gs - doc.x, n = doc.y;
-    uint32_t k = 0;
-    for (uint32_t j = 0; j < 64; ++j) {
-        const bool it = (l0 + j - 1u) < n;
-        k += (it && (cp3_get(a.in_cp, gs + j) & kCpMask) >= 0x80u) ? 1u : 0u;
-    }
-    cnt[c] = k;
-}
-__global__ __launch_bounds__(kBlock) void k_cp2_fill(L0Args a, const uint32_t* pre, uint16_t* cp2,
-                                                     uint32_t* xcp, uint32_t* xgrp) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c * 64ull >= a.nslots) return;
-    const uint32_t gs = c * 64u;
-    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-    const uint32_t l0 = gs - doc.x, n = doc.y;
-    uint32_t o = pre[c], gbits = 0;
-    for (uint32_t j = 0; j < 64; ++j) {
-        const bool it = (l0 + j - 1u) < n;
-        const uint32_t v = cp3_get(a.in_cp, gs + j), cp = v & kCpMask;
-        uint32_t w = 0;
-        if (it) {
-            w = ((v >> 21) & 7u) << 13;
-            if (cp >= 0x80u) {
-                w |= kCp2Esc;
-                xcp[o++] = cp;
-                gbits |= 1u << (j >> 4);
-            } else {
-                w |= cp;
-            }
+    __shared__ uint32_t lds[kBlock / 64];
+    __shared__ uint16_t lst[kScanTile];
+    const uint32_t tile = blockIdx.x, t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
+    uint32_t nsq = 0;
+    if (gs < a.nslots) {
+        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B
+        const uint4 q0 = cv[0], q1 = cv[1], q2 = cv[2];
+        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        const uint32_t CW[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                 q2.x, q2.y, q2.z, q2.w, 0u};
+        const uint32_t l0 = gs - doc.x, n = doc.y;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
+            const uint32_t c = ((CW[wd] >> sh) | (sh > 8 ? CW[wd + 1] << (32 - sh) : 0u)) & 0x00FFFFFFu;
+            const bool it = (l0 + (uint32_t)k - 1u) < n;
+            nsq |= (it && !(c & kSeqBit) ? 1u : 0u) << k;
         }
-        cp2[gs + j] = (uint16_t)w;
     }
-    for (uint32_t g = 0; g < 4; ++g)
-        if ((gbits >> g) & 1u) {
-            const uint64_t gi = a.xgrp_off + 4ull * c + g;
-            atomicOr(&xgrp[gi >> 5], 1u << (gi & 31u));
-        }
+    uint32_t T;
+    uint32_t i = block_excl_scan<kBlock / 64>((uint32_t)__popc(nsq), lds, T);
+    for (; nsq; nsq &= nsq - 1u) lst[i++] = (uint16_t)(threadIdx.x * kScanItems + __builtin_ctz(nsq));
+    __syncthreads();
+    const uint32_t o = pre[tile * (kScanTile / 64)];
+    for (uint32_t k = threadIdx.x; k < T; k += kBlock) {
+        const uint32_t g = t0 + lst[k];
+        out[o + k] = a.in_parent[g];
+        kout[o + k] = a.in_key[g];
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_replicate(
@@ -2956,8 +2936,6 @@ void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
     dfree(nsq_par); dfree(nsq_pre); dfree(nsq_key);
     nsq_items = 0;
-    dfree(cp2); dfree(xcp); dfree(xpre); dfree(xgrp);
-    nesc = 0;
     dfree(docs_rel); dfree(doc_rank); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
@@ -3030,14 +3008,12 @@ std::string Engine::init(int dev) {
 int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
     // (a new slot layout: the compact nsq list, if any, no longer matches it)
-    if (L.nsq_par || L.nsq_pre || L.nsq_key || L.cp2) {
+    if (L.nsq_par || L.nsq_pre || L.nsq_key) {
         (void)hipStreamSynchronize(stream);
         dfree(L.nsq_par);
         dfree(L.nsq_pre);
         dfree(L.nsq_key);
         L.nsq_items = 0;
-        dfree(L.cp2); dfree(L.xcp); dfree(L.xpre); dfree(L.xgrp);
-        L.nesc = 0;
     }
     L.log2m = kDocAlignLog2;
     L.docs = docs;
@@ -3090,16 +3066,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         slot += ds;
     }
     L.total_slots = slot;
-    for (Wave& w : L.waves) {  // a plan learnt on logs of the same shape
-        const WaveShape sh = shape_of(w);
-        for (const ShapeHint& h : shape_hints_)
-            if (h.shape == sh) {
-                w.hint_runs = h.runs;
-                w.hint_rmax = h.rmax;
-                w.hint_lds = true;
-                break;
-            }
-    }
+    apply_shape_hints(L);
     const uint64_t nchunks = slot / M;
     if (slot > L.cap_slots) {
         dfree(L.parent); dfree(L.key); dfree(L.cp);
@@ -3199,6 +3166,7 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
     for (uint64_t g = 0; g < S; ++g) cp3_put(c.data(), g, kDelBit);
     std::vector<uint64_t> key(S, 0);
     L.fugue = false;
+    std::vector<uint64_t> nsq_doc(n, 0);
     for (uint32_t d = 0; d < n; ++d) {
         const crdt_hip_oplog_view& v = views[d];
         const uint64_t b = L.doc_slot[d] + 1;
@@ -3223,8 +3191,14 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
             key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
             cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
                                          (v.parent[i] == i ? kSeqBit : 0u));
+            nsq_doc[d] += v.parent[i] != i;
         }
     }
+    for (Wave& w : L.waves) {
+        w.nsq_items = 0;
+        for (uint32_t k = 0; k < w.ndocs; ++k) w.nsq_items += nsq_doc[w.first_doc + k];
+    }
+    set_contraction(L);
     // on the engine's stream (a null-stream copy does not wait for the non-blocking streams the
     // kernels run on, nor they for it), then waited for: the host columns are freed on return
     HIPCHK(hipMemcpyAsync(L.parent, par.data(), S * 4, hipMemcpyHostToDevice, stream), "upload parent");
@@ -3454,13 +3428,8 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.xcd = xcd_order ? 1u : 0u;                                  \
     a0.nsq_par = L.nsq_par;                                         \
     a0.nsq_key = L.nsq_key;                                         \
-    a0.in_cp2 = L.cp2 ? L.cp2 + w.slot0 : nullptr;                  \
-    a0.xcp = L.xcp;                                                 \
-    a0.xpre = L.xpre ? L.xpre + (w.slot0 >> 6) : nullptr;           \
-    a0.xgrp = L.xgrp;                                               \
-    a0.xgrp_off = w.slot0 >> 4;                                     \
-    a0.sparse_nib = (L.cp2 && !ord) ? 1u : 0u;                      \
     a0.nsq_pre = L.nsq_pre ? L.nsq_pre + (w.slot0 >> 6) : nullptr;  \
+    a0.nocon = (w.nocon && !L.fugue) ? 1u : 0u;                     \
     a0.copy_text = 1u
 
 // Tree / digest argument block (run counts come from ctl where the kernels need them).
@@ -3495,10 +3464,7 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text
     const uint32_t nq = (uint32_t)(jbits_words(w.nslots) / 4) * (L.fugue ? 2u : 1u);
     k_clear<<<std::min<uint32_t>(grid_for(nq), 2048u), 256, 0, s>>>(ctl_, reinterpret_cast<uint4*>(jbits_), nq);
     MARK(-1);
-    if (a0.in_cp2)
-        k_classify<true><<<ntiles, kBlock, 0, s>>>(a0);
-    else
-        k_classify<false><<<ntiles, kBlock, 0, s>>>(a0);
+    k_classify<<<ntiles, kBlock, 0, s>>>(a0);
     MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
@@ -3580,7 +3546,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     a.Sreg = Sreg;
     a.S = S;
     a.step_limit = 2u * R + 4u;
-    const uint32_t gR = grid_for(R), gS = grid_for(S);
+    const uint32_t gR = grid_for(R);
     // sort A by parent run (document starts: R) and sort B by run id, 8 bits per pass
     const uint32_t npass = std::max<uint32_t>(1u, (ceil_log2((uint64_t)R + 1u) + 7u) / 8u);
     const uint64_t tilesA = ((uint64_t)R + kRsTileA - 1) / kRsTileA;
@@ -3636,7 +3602,8 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     }
     k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);
     MARK(S_SORTB);
-    k_walk1<<<gS, kBlock, 0, s>>>(a);
+    const uint32_t gW = grid_for(((uint64_t)S + kWalkIlp - 1) / kWalkIlp);
+    k_walk1<<<gW, kBlock, 0, s>>>(a);
     MARK(S_WALK1);
     SupArgs sa{};
     sa.S = S;
@@ -3663,7 +3630,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     const uint32_t* spref = spref_;
     MARK(S_RANK);
     k_doctotals<<<1, 1024, 0, s>>>(a);
-    k_walk2<<<gS, kBlock, 0, s>>>(a, spref);
+    k_walk2<<<gW, kBlock, 0, s>>>(a, spref);
     MARK(S_WALK2);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
@@ -4210,7 +4177,7 @@ int Engine::synth_tree(DeviceLogs& R, uint32_t n, uint32_t p_chain_pct, uint32_t
     HIPCHK(hipGetLastError(), "synth launch");
     HIPCHK(hipStreamSynchronize(stream), "synth");
     const int rc2 = build_nsq(R);
-    return rc2 ? rc2 : build_cp2(R);
+    return rc2;
 }
 
 int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,
@@ -4254,7 +4221,7 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     dfree(drslot);
     if (e != hipSuccess) return fail("replicate", e);
     const int rc2 = build_nsq(R);
-    return rc2 ? rc2 : build_cp2(R);
+    return rc2;
 }
 
 // The compact nsq parent list of resident logs (input encoding, once per batch): count the nsq
@@ -4267,7 +4234,10 @@ int Engine::build_nsq(DeviceLogs& L) {
     dfree(L.nsq_pre);
     dfree(L.nsq_key);
     L.nsq_items = 0;
-    if (!L.total_slots || !nsq_list) return CRDT_HIP_OK;
+    if (!L.total_slots || !nsq_list) {
+        set_contraction(L);
+        return CRDT_HIP_OK;
+    }
     const bool ord = false;  // (L0ARGS)
     const uint64_t nch = L.total_slots / 64 + 64;  // (a last tile's range ends within)
     if (nch >= (1ull << 32)) return CRDT_HIP_OK;
@@ -4292,60 +4262,50 @@ int Engine::build_nsq(DeviceLogs& L) {
     HIPCHK(dalloc(&L.nsq_key, (uint64_t)total + 1), "hipMalloc nsq keys");
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
-        k_nsq_scatter<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(
+        k_nsq_scatter<<<(uint32_t)((w.nslots + kScanTile - 1) / kScanTile), kBlock, 0, stream>>>(
             a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par, L.nsq_key);
     }
     HIPCHK(hipGetLastError(), "nsq list launch");
+    // every wave's count of items without the previous-slot flag (its run contraction)
+    for (Wave& w : L.waves) {
+        uint32_t b[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(&b[0], L.nsq_pre + (w.slot0 >> 6), 4, hipMemcpyDeviceToHost, stream), "nsq counts");
+        HIPCHK(hipMemcpyAsync(&b[1], L.nsq_pre + ((w.slot0 + w.nslots) >> 6), 4, hipMemcpyDeviceToHost, stream),
+               "nsq counts");
+        HIPCHK(hipStreamSynchronize(stream), "nsq counts");
+        w.nsq_items = b[1] - b[0];
+    }
     HIPCHK(hipStreamSynchronize(stream), "nsq list");
     L.nsq_items = total;
+    set_contraction(L);
     return CRDT_HIP_OK;
 }
 
-// The 2-byte character column of resident logs (input encoding, once per batch): every slot's
-// character as one ASCII byte or an escape, with the three flags; the escaped codepoints in slot
-// order (xcp) with a prefix count per 64 slots (xpre); one bit per 16 slots holding an escape
-// (xgrp).  k_classify then reads 2 bytes per slot instead of 3, and writes the weight nibbles only
-// for groups with an escape (k_runs weighs the other groups by their visible bits).
-int Engine::build_cp2(DeviceLogs& L) {
-    HIPCHK(hipStreamSynchronize(stream), "character column");
-    dfree(L.cp2); dfree(L.xcp); dfree(L.xpre); dfree(L.xgrp);
-    L.nesc = 0;
-    if (!L.total_slots || !cp2_column) return CRDT_HIP_OK;
-    const bool ord = false;  // (L0ARGS)
-    const uint64_t nch = L.total_slots / 64 + 64;
-    if (nch >= (1ull << 32)) return CRDT_HIP_OK;
-    const uint64_t ngw = L.total_slots / 16 / 32 + 2;
-    HIPCHK(dalloc(&L.xpre, nch + 1), "hipMalloc escape prefix");
-    HIPCHK(dalloc(&L.xgrp, ngw), "hipMalloc escape groups");
-    HIPCHK(dalloc(&L.cp2, L.total_slots), "hipMalloc character column");
-    HIPCHK(hipMemsetAsync(L.xpre, 0, (nch + 1) * 4, stream), "escape prefix");
-    HIPCHK(hipMemsetAsync(L.xgrp, 0, ngw * 4, stream), "escape groups");
-    for (const Wave& w : L.waves) {
-        L0ARGS(a0);
-        k_cp2_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.xpre + (w.slot0 >> 6));
+// Run contraction per wave (Wave::nocon) from its count of items without the previous-slot flag;
+// the plans learnt for the shape (which includes the mode) then apply again.
+void Engine::set_contraction(DeviceLogs& L) const {
+    for (Wave& w : L.waves) {
+        uint64_t items = 0;
+        for (uint32_t k = 0; k < w.ndocs; ++k) items += L.docs[w.first_doc + k].n;
+        w.nocon = contraction == 2 ||
+                  (contraction == 0 && items && (double)w.nsq_items >= kNoconShare * (double)items);
     }
-    const uint32_t n = (uint32_t)nch, nb = (n + kScanTile - 1) / kScanTile;
-    uint32_t* sums = nullptr;
-    HIPCHK(dalloc(&sums, nb), "hipMalloc escape scan");
-    k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.xpre, n, sums);
-    k_scan_top<<<1, 1024, 0, stream>>>(sums, nb, L.xpre, n);
-    k_scan_apply<<<nb, kBlock, 0, stream>>>(L.xpre, n, sums, L.xpre);
-    uint32_t total = 0;
-    hipError_t e = hipMemcpyAsync(&total, L.xpre + n, 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    dfree(sums);
-    if (e != hipSuccess) return fail("escape scan", e);
-    HIPCHK(dalloc(&L.xcp, (uint64_t)total + 1), "hipMalloc escaped codepoints");
-    for (const Wave& w : L.waves) {
-        L0ARGS(a0);
-        k_cp2_fill<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(
-            a0, L.xpre + (w.slot0 >> 6), L.cp2 + w.slot0, L.xcp, L.xgrp);
-    }
-    HIPCHK(hipGetLastError(), "character column launch");
-    HIPCHK(hipStreamSynchronize(stream), "character column");
-    L.nesc = total;
-    return CRDT_HIP_OK;
+    apply_shape_hints(L);
 }
-#undef L0ARGS
+
+// Every wave of L takes the launch plan learnt on logs of its shape, if any.
+void Engine::apply_shape_hints(DeviceLogs& L) const {
+    for (Wave& w : L.waves) {
+        const WaveShape sh = shape_of(w);
+        w.hint_lds = false;
+        for (const ShapeHint& h : shape_hints_)
+            if (h.shape == sh) {
+                w.hint_runs = h.runs;
+                w.hint_rmax = h.rmax;
+                w.hint_lds = true;
+                break;
+            }
+    }
+}
 
 }  // namespace crdt

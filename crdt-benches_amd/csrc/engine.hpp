@@ -39,6 +39,12 @@ struct Wave {
     // flags C_REPLAN if the wave outgrew it) and the host merges such a wave again.
     uint32_t hint_runs = 0, hint_rmax = 0;
     bool hint_lds = false;  // the wave took the per-document LDS level 1 with fused text
+    // no run contraction (L0Args::nocon): most of the wave's items lack the previous-slot flag
+    // (relabelled ids, uniformly random parents), so runs would not contract and level 0 skips
+    // the parent scatter of the jump bits and the run-parent lookups; set with the wave's
+    // encoding (Engine::build_nsq, Engine::upload) or forced by Engine::contraction
+    bool nocon = false;
+    uint64_t nsq_items = 0;  // items of the wave without the previous-slot flag (if known)
 };
 
 // Stage timing of one wave: an event at its start and after every stage that ran.
@@ -113,15 +119,6 @@ struct DeviceLogs {
     uint64_t* nsq_key = nullptr;   // beside nsq_par: the items' keys (k_runs reads a non-seq
                                    //   head's key there instead of gathering it)
     uint64_t nsq_items = 0;
-    // Resident batches (Engine::build_cp2): the 2-byte character column (ASCII byte or escape,
-    // plus the flags), the escaped codepoints in slot order and their prefix count per 64 slots,
-    // and one bit per 16 slots that hold an escape.  Null: k_classify reads the 3-byte column.
-    uint16_t* cp2 = nullptr;
-    uint32_t* xcp = nullptr;
-    uint32_t* xpre = nullptr;
-    uint32_t* xgrp = nullptr;
-    uint64_t nesc = 0;
-
     void release();
     ~DeviceLogs() { release(); }
 };
@@ -162,11 +159,9 @@ public:
     // resident batches get the compact list of the non-seq items' parents (build_nsq); 0: the
     // level-0 kernels gather the parent column instead (A/B)
     bool nsq_list = true;
-    // resident batches get the 2-byte character column (build_cp2); off by default: same-box A/B
-    // at the headline config, k_classify 3.79 -> 3.97 ms and k_runs 3.55 -> 3.72 ms per step with
-    // it (one byte per slot less is not what bounds them; the decode and the sparse weights cost
-    // more), so the 3-byte column stays the default
-    bool cp2_column = false;
+    // run contraction of RGA waves: 0 = by the wave's input (no contraction when at least
+    // kNoconShare of its items lack the previous-slot flag), 1 = always, 2 = never
+    uint32_t contraction = 0;
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -220,8 +215,10 @@ public:
 
     // The compact nsq parent list of L (after its last plan; see DeviceLogs::nsq_par).
     int build_nsq(DeviceLogs& L);
-    // The 2-byte character column of L (after its last plan; see DeviceLogs::cp2).
-    int build_cp2(DeviceLogs& L);
+    // Wave::nocon of every wave of L from its nsq_items and the contraction parameter.
+    void set_contraction(DeviceLogs& L) const;
+    void apply_shape_hints(DeviceLogs& L) const;
+    static constexpr double kNoconShare = 0.75;
 
     // Materialise `replicas` relabelled copies of `bases` (already uploaded in B) into R.
     int replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t relabel,
@@ -289,9 +286,10 @@ private:
     struct WaveShape {
         uint32_t ndocs, nslots;
         uint64_t text_cap, order_cap, max_doc_text;
+        bool nocon;
         bool operator==(const WaveShape& o) const {
             return ndocs == o.ndocs && nslots == o.nslots && text_cap == o.text_cap &&
-                   order_cap == o.order_cap && max_doc_text == o.max_doc_text;
+                   order_cap == o.order_cap && max_doc_text == o.max_doc_text && nocon == o.nocon;
         }
     };
     struct ShapeHint {
@@ -301,7 +299,7 @@ private:
     std::vector<ShapeHint> shape_hints_;  // most recent first, at most kShapeHints
     static constexpr size_t kShapeHints = 64;
     static WaveShape shape_of(const Wave& w) {
-        return WaveShape{w.ndocs, w.nslots, w.text_cap, w.order_cap, w.max_doc_text};
+        return WaveShape{w.ndocs, w.nslots, w.text_cap, w.order_cap, w.max_doc_text, w.nocon};
     }
     void learn_shape(const Wave& w);
     void forget_shape(const Wave& w);

@@ -49,6 +49,11 @@ constexpr uint32_t kSpliceRanks = 4;                                // old ranks
 constexpr uint32_t kSpliceTile = kIncThreads * kSpliceRanks;        // old ranks per tile
 constexpr uint32_t kIncGroupMax = 1024;  // largest sibling group ranked in inc_forest
 constexpr uint32_t kIncThinGroup = 32;   // more roots than this: ranked one wave per root
+// Roots that do not sort above every old item (a concurrent insert) take their place from a
+// search of their parent's old subtree (inc_anchor): at most kIncHard of them per call, each
+// search over at most kIncScan ranks (else the call merges in full)
+constexpr uint32_t kIncHard = 256;
+constexpr uint32_t kIncScan = 1u << 16;
 #ifndef CRDT_INC_RUNS
 #define CRDT_INC_RUNS 1
 #endif
@@ -59,7 +64,7 @@ constexpr uint32_t kDelBitI = 0x00800000u;
 // device counters (u64)
 enum ICtl { I_MAXKEY = 0, I_MAXKEY_B, I_N };  // the largest key, two slots (calls alternate)
 // flag bits (the result block): the fast path does not apply (the host merges in full)
-constexpr uint64_t F_KEY = 1, F_ORDER = 2, F_GROUP = 4, F_TEXT = 8;
+constexpr uint64_t F_KEY = 1, F_ORDER = 2, F_GROUP = 4, F_TEXT = 8;  // (F_KEY: too many searches)
 
 struct IncArgs {
     uint32_t n0, m;             // items the order covers, items appended since
@@ -113,7 +118,20 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
            + 2u * mmax               // vrk: ranks among many roots, then run heads (u16)
            + 2u * mmax               // rend: the last item of each run (u16)
            + 2u * (mmax + 2u)        // cs: children by segment, sorted (u16)
+           + 4u * mmax               // PR: a root's parent's old rank (u32)
+           + 6u * kIncHard           // the roots whose place needs a search: parent, item
            + 64u;
+}
+
+// Order of the new items in one sibling group: the roots (children of the virtual root) by anchor
+// rank, then among roots at the same anchor the one whose parent ranks later first (the anchor
+// item's own new children come before those of its ancestors, whose old subtrees end there), then
+// by key descending, ties by the greater index; other groups have A = PR = 0: key order.
+__device__ __forceinline__ bool root_before(uint32_t aj, uint32_t pj, uint64_t kj, uint32_t j,
+                                            uint32_t ai, uint32_t pi, uint64_t ki, uint32_t i) {
+    if (aj != ai) return aj < ai;
+    if (pj != pi) return pj > pi;
+    return kj > ki || (kj == ki && j > i);
 }
 
 #define INC_TS(i) \
@@ -124,7 +142,8 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
 // the batch, so that no per-item loop runs over empty slots
 template <uint32_t Q>
 __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint32_t* red,
-                                           uint32_t& flag, const uint32_t (&sl)[kSpliceRanks],
+                                           uint32_t& flag, uint32_t& nhard, uint32_t& found,
+                                           const uint32_t (&sl)[kSpliceRanks],
                                            uint32_t (&cwq)[kSpliceRanks]) {
     static_assert(Q * kIncThreads <= kIncMax, "items per thread");
     const uint32_t t = threadIdx.x, m = a.m, n0 = a.n0;
@@ -137,7 +156,13 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     uint16_t* vrk = ch + (kIncMax + 2u);                    // kIncMax: ranks among the roots
     uint16_t* rend = vrk + kIncMax;                         // kIncMax: the last item of a run
     uint16_t* cs = rend + kIncMax;                          // kIncMax + 2: ch sorted
-    if (t == 0) flag = 0;
+    uint32_t* PR = reinterpret_cast<uint32_t*>(cs + (kIncMax + 2u));  // kIncMax
+    uint32_t* hp = PR + kIncMax;                            // kIncHard: parents of the searched
+    uint16_t* hx = reinterpret_cast<uint16_t*>(hp + kIncHard);  //   roots, and the roots
+    if (t == 0) {
+        flag = 0;
+        nhard = 0;
+    }
     INC_TS(0);
     const uint64_t maxkey0 = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
     // ---- load: parents, keys, anchors; child counts (each child keeps its place among its
@@ -168,13 +193,23 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             uint32_t li;
             if (pp[q] <= n0) {  // a root: after its old parent, ahead of the parent's old children
                 li = m;
-                A[i] = a.rank[pp[q]];
-                if (kk[q] <= maxkey0) bad |= (uint32_t)F_KEY;
+                A[i] = PR[i] = a.rank[pp[q]];
+                if (kk[q] <= maxkey0) {
+                    // some old sibling may sort above it: its place comes from a search below
+                    const uint32_t h = atomicAdd(&nhard, 1u);
+                    if (h < kIncHard) {
+                        hp[h] = pp[q];
+                        hx[h] = (uint16_t)i;
+                    } else {
+                        bad |= (uint32_t)F_KEY;
+                    }
+                }
             } else {
                 const uint32_t l = pp[q] - (n0 + 1u);
                 if (l >= i) bad |= (uint32_t)F_ORDER;  // (parents precede their children)
                 li = l < i ? l : m;
                 A[i] = 0;
+                PR[i] = 0;
             }
             lp[i] = (uint16_t)li;
             plc[q] = atomicAdd(&start[li], 1u);
@@ -182,6 +217,42 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         if (bad) atomicOr(&flag, bad);
     }
     INC_TS(1);
+    __syncthreads();
+    // ---- the places of the roots that may sort below an old sibling (concurrent inserts): in
+    // the RGA pre-order a root x of key k under old parent p follows p's old children that sort
+    // above it, with their subtrees, so it goes before the first rank after p that holds an old
+    // child of p with a key <= k (x's id is greater than every old one: equal keys put x first)
+    // or that leaves p's subtree (an item whose parent ranks before p); its anchor is the rank
+    // before that.  The block searches 1024 ranks at a time, one root after the other.
+    {
+        const uint32_t nh = min(nhard, kIncHard);
+        for (uint32_t h = 0; h < nh && !flag; ++h) {
+            const uint32_t i = hx[h], p = hp[h], r0 = PR[i];
+            const uint64_t k = keys[i];
+            if (t == 0) found = 0xFFFFFFFFu;
+            __syncthreads();
+            for (uint32_t c = 0;; c += kIncThreads) {
+                const uint32_t r = r0 + 1u + c + t;
+                bool stop = r > n0;  // (the document's end)
+                if (!stop) {
+                    const uint32_t sl = a.seq[r], pr = a.parent[sl];
+                    stop = pr == p ? a.key[sl] <= k : a.rank[pr] < r0;
+                }
+                if (stop) atomicMin(&found, r);
+                __syncthreads();
+                const uint32_t f = found;
+                __syncthreads();
+                if (f != 0xFFFFFFFFu) {
+                    if (t == 0) A[i] = f - 1u;
+                    break;
+                }
+                if (c + kIncThreads >= kIncScan) {
+                    if (t == 0) atomicOr(&flag, (uint32_t)F_KEY);
+                    break;
+                }
+            }
+        }
+    }
     INC_TS(2);
     __syncthreads();
     // ---- segment starts: exclusive scan over nodes 0..m (m + 1 <= kIncMax + 1 counts) ----
@@ -219,14 +290,12 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         const uint32_t lane = t & 63u;
         for (uint32_t idx = t >> 6; idx < nv; idx += kIncThreads / 64) {
             const uint32_t i = ch[v0 + idx];
-            const uint32_t ai = A[i];
+            const uint32_t ai = A[i], pi = PR[i];
             const uint64_t ki = keys[i];
             uint32_t r = 0;
             for (uint32_t s = lane; s < nv; s += 64) {
                 const uint32_t j = ch[v0 + s];
-                const uint32_t aj = A[j];
-                const uint64_t kj = keys[j];
-                r += (aj < ai || (aj == ai && (kj > ki || (kj == ki && j > i)))) ? 1u : 0u;
+                r += root_before(A[j], PR[j], keys[j], j, ai, pi, ki, i) ? 1u : 0u;
             }
             r = wave_sum(r);
             if (lane == 0) vrk[i] = (uint16_t)r;
@@ -247,14 +316,12 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             atomicOr(&flag, (uint32_t)F_GROUP);
             continue;
         }
-        const uint32_t ai = A[i];
+        const uint32_t ai = A[i], pi = PR[i];
         const uint64_t ki = keys[i];
         uint32_t r = 0;
         for (uint32_t s = g0; s < g1; ++s) {
             const uint32_t j = ch[s];
-            const uint32_t aj = A[j];
-            const uint64_t kj = keys[j];
-            r += (aj < ai || (aj == ai && (kj > ki || (kj == ki && j > i)))) ? 1u : 0u;
+            r += root_before(A[j], PR[j], keys[j], j, ai, pi, ki, i) ? 1u : 0u;
         }
         rk[q] = r;
     }
@@ -599,7 +666,7 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     __shared__ uint32_t red[kIncThreads / 64];
     __shared__ uint32_t rsum[2 * (kIncThreads / 64)];
     __shared__ uint32_t cb[2];
-    __shared__ uint32_t flag;
+    __shared__ uint32_t flag, nhard, found;
     __shared__ uint64_t excl_lds;
     const uint32_t b = blockIdx.x;
     // the tile's old order, loaded before the forest so that the round trip overlaps it
@@ -613,11 +680,11 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     uint32_t cwq[kSpliceRanks];
     if (a.m) {
         if (a.m <= kIncThreads)
-            inc_forest<1>(a, lds, red, flag, sl, cwq);
+            inc_forest<1>(a, lds, red, flag, nhard, found, sl, cwq);
         else if (a.m <= 2u * kIncThreads)
-            inc_forest<2>(a, lds, red, flag, sl, cwq);
+            inc_forest<2>(a, lds, red, flag, nhard, found, sl, cwq);
         else
-            inc_forest<kIncMax / kIncThreads>(a, lds, red, flag, sl, cwq);
+            inc_forest<kIncMax / kIncThreads>(a, lds, red, flag, nhard, found, sl, cwq);
     } else {
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);

@@ -132,11 +132,16 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * other), "lane_gate" (default 1: lanes take turns at the HBM-bound level 0), "plan_cache"
  * (default 1: a merge of logs merged before enqueues every wave with the launch plan the earlier
  * merge learnt, checked on the device, and waits once instead of after each wave's level 0),
- * "l1_split" (default 1: such enqueued waves run level 1 on a low-priority stream of their lane,
- * so that the next wave's level 0 is favoured when the two compete for the CUs), "tail_wave_div"
- * (default 4: a merge of several waves ends with a wave of at most max_wave_slots / 4 slots,
- * whose level 1 is the only part of the merge that overlaps nothing; 0 = plain greedy waves).
- * Results never depend on these. */
+ * "l1_split" (default 0; 1: such enqueued waves run level 1 on a low-priority stream of their
+ * lane, so that the next wave's level 0 is favoured when the two compete for the CUs),
+ * "tail_wave_div" (default 0; k: a merge of several waves ends with a wave of at most
+ * max_wave_slots / k slots), "xcd_order" (default 1: XCD-aware tile order in level 0),
+ * "stile_text" (default 1: the per-document merge stages text from the per-tile segments),
+ * "nsq_list" (default 1: resident batches get the compact list of the parents and keys of the
+ * items without the previous-slot flag), "contraction" (run contraction of RGA waves, decided
+ * when a batch is built or logs are uploaded: 0 = by the input (default: no contraction when at
+ * least 3/4 of a wave's items lack the previous-slot flag), 1 = always, 2 = never), "fuse_text"
+ * (default 1).  Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);
 
 /* ---- op log: host-side resolver (positional patch -> anchor op) ---------------------------- */

@@ -84,10 +84,10 @@ def _with_item_id(u: bytes, k: int, lamport: int, agent: int) -> bytes:
     return bytes(b)
 
 
-def test_concurrent_update_falls_back_to_full_merge(ctx, oracle):
+def test_concurrent_update_takes_the_incremental_path(ctx, oracle):
     """An update whose item sorts below an older sibling (a concurrent insert that lost the
-    race: its key is below the replica's largest key) cannot go the fast way: the full merge runs
-    and puts it after the older sibling's subtree, as the oracle does."""
+    race: its key is below the replica's largest key) is placed by a search of its parent's old
+    subtree: after the older sibling's subtree, as the oracle does, without a full merge."""
     a = crdt_hip.OpLog(agent=1)
     h = crdt_hip.OpLog(agent=1)  # the host log fed the same (patched) updates
     r = crdt_hip.Replica(ctx)
@@ -109,9 +109,9 @@ def test_concurrent_update_falls_back_to_full_merge(ctx, oracle):
     u = _with_item_id(a.encode_from(v), 0, 1, 0)  # X's key (1, agent 0) < 'h' (1, agent 1)
     ship(u)
     cps, nb, path, text = r.merge_inc(text=True)
-    assert path == 0
+    assert path == 1
     assert text == oracle.merge(to_anchor(h.arrays())) == b"hello worldXY"
-    # the state was rebuilt: a later local edit goes the fast way again
+    # a later local edit goes the fast way too
     v = a.version()
     a.insert(2, "--")
     ship(a.encode_from(v))
@@ -193,3 +193,34 @@ def test_incremental_len_on_a_document_with_more_tiles_than_cus(ctx, oracle):
         assert path == 1, c
         assert nb == length
         assert text == oracle.merge(to_anchor(log.arrays())), f"checkpoint {c}"
+
+
+def test_concurrent_roots_placed_by_search_match_oracle(ctx, oracle):
+    """Local edit batches in which every 5th update's items carry a key below the replica's
+    largest (a random lamport, an agent of their own): their roots are placed by searching the
+    parent's old subtree.  The oracle's merge of the same log at every checkpoint."""
+    import random
+    rng = random.Random(0xC0C0)
+    t, patches, updates = trace_updates("sveltecomponent")
+    r = crdt_hip.Replica(ctx)
+    host = crdt_hip.OpLog(agent=0)
+    paths = []
+    maxlam = 0
+    for c, i in enumerate(range(0, 2000, 10)):
+        batch = []
+        for j, u in enumerate(updates[i:i + 10]):
+            n = struct.unpack_from("<I", u, 12)[0]
+            if n and (i + j) % 5 == 0 and maxlam > 2:
+                lam = rng.randint(1, maxlam - 1)
+                for k in range(n):
+                    u = _with_item_id(u, k, lam + k, 1000 + i + j)
+            for k in range(n):
+                maxlam = max(maxlam, struct.unpack_from("<I", u, 24 + 8 * n + 4 * k)[0])
+            batch.append(u)
+        r.apply_updates(batch)
+        for u in batch:
+            host.apply_update(u)
+        cps, nb, path, text = r.merge_inc(text=True)
+        paths.append(path)
+        assert text == oracle.merge(to_anchor(host.arrays())), f"checkpoint {c}"
+    assert paths[0] == 0 and paths[1:].count(1) >= len(paths) - 5, paths

@@ -486,10 +486,10 @@ def test_rccl_single_rank_allgather(ctx):
 
 @pytest.mark.parametrize("relabel", ["rotate", "shuffle"])
 def test_batch_mixed_ascii_and_escaped_codepoints(ctx, oracle, relabel):
-    """Resident batches can read the 2-byte character column (Engine::build_cp2, param cp2):
-    ASCII characters inline, every other codepoint an escape into a side table.  Documents with a few escaped
-    codepoints scattered among ASCII (2-, 3- and 4-byte UTF-8, some deleted), relabelled, against
-    the oracle; and the same batch with the 3-byte column (cp2 off) gives the same digests."""
+    """Documents with a few multi-byte codepoints scattered among ASCII (2-, 3- and 4-byte UTF-8,
+    some deleted), relabelled, as resident batches against the oracle: with the compact list of
+    the non-seq items' parents and keys (Engine::build_nsq, the default) and without it (param
+    nsq_list 0: the level-0 kernels gather the parent and key columns), the same digests."""
     rng = np.random.default_rng(11)
     logs = []
     for n, p_esc in ((30_000, 0.02), (5_000, 0.3), (20_000, 0.0005)):
@@ -504,15 +504,78 @@ def test_batch_mixed_ascii_and_escaped_codepoints(ctx, oracle, relabel):
     refs = [oracle.merge(to_anchor(lg)) for lg in logs]
     want = [oracle.tree_digest(r) for r in refs]
     digests = {}
-    for cp2 in (1, 0):
-        ctx.set_param("cp2", cp2)
+    for nsq in (0, 1):
+        ctx.set_param("nsq_list", nsq)
         try:
             b = ctx.batch(logs, replicas=3, relabel=relabel, seed=21)
             d, l, _ = b.merge()
             b.close()
         finally:
-            ctx.set_param("cp2", 0)
+            ctx.set_param("nsq_list", 1)
         for i, (x, y) in enumerate(zip(d, l)):
-            assert int(x) == want[i % 3] and int(y) == len(refs[i % 3]), (cp2, i)
-        digests[cp2] = list(map(int, d))
+            assert int(x) == want[i % 3] and int(y) == len(refs[i % 3]), (nsq, i)
+        digests[nsq] = list(map(int, d))
     assert digests[0] == digests[1]
+
+
+@pytest.mark.parametrize("relabel", ["rotate", "shuffle"])
+def test_run_contraction_modes_agree(oracle, golden, relabel):
+    """Run contraction by the input (0), always (1) and never (2: every item heads its own run,
+    k_classify reads no parents, k_runs takes each run's parent from the column) give the same
+    digests on relabelled trace batches; without contraction a wave numbers one run per item and
+    document start.  By the input, the shuffled batch (no consecutive ids) goes uncontracted and
+    the rotated one contracts."""
+    bases = [resolved(n) for n in TRACES]
+    runs = {}
+    for mode in (0, 1, 2):
+        c = crdt_hip.Context(0)
+        c.set_param("contraction", mode)
+        b = c.batch(bases, replicas=2, relabel=relabel, seed=77)
+        for _ in range(2):  # (the synchronous merge, then the learnt-plan merge)
+            dig, lens, st = b.merge()
+            for r in range(b.docs):
+                name = TRACES[r % 4]
+                assert "%016x" % dig[r] == golden[name]["tree_digest"], (mode, r)
+                assert lens[r] == golden[name]["end_bytes"], (mode, r)
+        runs[mode] = st["runs"]
+        assert (st["runs"] == st["items"] + b.docs) == (mode == 2) or mode == 0
+        b.close()
+        c.close()
+    assert runs[0] == (runs[2] if relabel == "shuffle" else runs[1])
+    assert runs[1] < runs[2]
+
+
+def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle):
+    """The same without contraction on uploaded logs (the level-1 cases: agents, wide sibling
+    groups, heavy runs, multi-byte text), and a parent out of range is still reported."""
+    c = crdt_hip.Context(0)
+    c.set_param("contraction", 2)
+    logs = _level1_cases()
+    dig, lens, st = c.merge_batch(logs, stats=True)
+    for i, lg in enumerate(logs):
+        ref = oracle.merge(to_anchor(lg)) if lg.n else b""
+        assert lens[i] == len(ref), i
+        assert dig[i] == oracle.tree_digest(ref), i
+    bad_parent = crdt_hip.LogArrays([0, 5], [1, 2], [0, 0], [0, 0], [97, 98])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        c.merge(bad_parent)
+    assert e.value.code == -5
+    c.close()
+
+
+@pytest.mark.parametrize("knob", ["xcd_order", "stile_text"])
+def test_level0_knobs_off_match_golden(golden, knob):
+    """The XCD-aware tile order and the per-document text staged from the tile segments only
+    change where work runs and where text is read from: off, the digests stay the traces'."""
+    bases = [resolved(n) for n in TRACES]
+    c = crdt_hip.Context(0)
+    c.set_param(knob, 0)
+    b = c.batch(bases, replicas=3, relabel="rotate", seed=9)
+    for _ in range(2):
+        dig, lens, st = b.merge()
+        for r in range(b.docs):
+            name = TRACES[r % 4]
+            assert "%016x" % dig[r] == golden[name]["tree_digest"], (knob, r)
+            assert lens[r] == golden[name]["end_bytes"], (knob, r)
+    b.close()
+    c.close()

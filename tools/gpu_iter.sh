@@ -13,11 +13,15 @@ if [ "${K:-}" != none ]; then
   case $st in 0) ;; *) grep -E "FAILED|Error|assert" gpurun_out/${R}_gpu_tests.log | head -30; exit $st;; esac
 fi
 IFS=';' read -ra L <<< "${LINES:-}"
-for item in "${L[@]}"; do
+# ABLIBS="libA.so libB.so": every line once per library build (CRDT_HIP_LIB), in alternation
+for item0 in "${L[@]}"; do
+ for lib in ${ABLIBS:-libcrdt_hip.so}; do
+  item=$item0
   [ -z "$item" ] && continue
   name=${item%%:*}; args=${item#*:}
+  [ -n "${ABLIBS:-}" ] && name=${name}_${lib%.so}
   echo "== $name: $args"
-  timeout -k 10 ${BT:-300} python -u bench.py --no-cpu-baseline $args > gpurun_out/${R}_$name.json 2> gpurun_out/${R}_$name.err
+  CRDT_HIP_LIB=$lib timeout -k 10 ${BT:-300} python -u bench.py --no-cpu-baseline $args > gpurun_out/${R}_$name.json 2> gpurun_out/${R}_$name.err
   st=$?
   python3 -c "
 import json,sys
@@ -25,6 +29,7 @@ d=json.loads(open('gpurun_out/${R}_$name.json').read().strip().splitlines()[-1])
 ks=d.get('kernels_ms') or {k:v['ms'] for k,v in d.get('kernels',{}).items() if v.get('launches')}
 print(round(d['ms_per_step'],3),'ok' if d.get('digests_ok') else 'DIGEST?',{k:round(v,3) for k,v in ks.items()})" 2>/dev/null
   case $st in 0) ;; *) echo "status $st"; tail -5 gpurun_out/${R}_$name.err; exit $st;; esac
+ done
 done
 # optional kernel trace of one bench line: PROF="name:args"
 if [ -n "${PROF:-}" ]; then
