@@ -485,6 +485,7 @@ def traces_workload(args) -> int:
         ctx.set_param("splitter_stride", args.splitter_stride)
     ctx.set_param("level1", args.level1)
     ctx.set_param("contraction", args.contraction)
+    ctx.set_param("l1_group", args.l1_group)
     if not args.fuse_text:  # (the engine's default is 1; builds before the parameter lack it)
         ctx.set_param("fuse_text", 0)
     ctx.set_param("lanes", args.lanes)
@@ -655,6 +656,7 @@ def side_workload(args) -> int:
     comm = Comm(world, rank, ctx)
     ctx.set_param("level1", args.level1)
     ctx.set_param("contraction", args.contraction)
+    ctx.set_param("l1_group", args.l1_group)
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
     t_setup = time.perf_counter()
@@ -938,6 +940,9 @@ def parse_args(argv=None):
                          "(input encoding; k_classify streams it); 0: k_classify gathers them")
     ap.add_argument("--plain-companion", type=int, default=1, choices=[0, 1],
                     help="1: a companion line of the headline batch without the compact nsq list")
+    ap.add_argument("--l1-group", type=int, default=0, choices=[0, 1, 2],
+                    help="global level-1 sibling grouping: 0 by the largest document, 1 counting, "
+                         "2 radix sorts")
     ap.add_argument("--contraction", type=int, default=0, choices=[0, 1, 2],
                     help="run contraction of RGA waves: 0 by the input (none when most items lack "
                          "the previous-slot flag), 1 always, 2 never")

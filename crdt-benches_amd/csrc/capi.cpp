@@ -218,6 +218,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.contraction = (uint32_t)value;
         return CRDT_HIP_OK;
     }
+    if (k == "l1_group") {  // global level-1 sibling grouping: 0 auto, 1 counting, 2 radix sorts
+        if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "l1_group must be 0, 1 or 2");
+        ctx->eng.l1_group = (uint32_t)value;
+        return CRDT_HIP_OK;
+    }
     if (k == "nsq_list") {  // 1: batches get the compact nsq parent list (Engine::build_nsq)
         if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0 or 1");
         ctx->eng.nsq_list = value == 1;

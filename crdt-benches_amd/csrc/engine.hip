@@ -57,13 +57,18 @@ constexpr int kScanTile = kBlock * kScanItems;
 constexpr uint32_t kDocAlignLog2 = 6;  // slot-level document alignment (chunk table: 1/64)
 constexpr uint32_t kLeaf = 4096;
 constexpr uint64_t kMaxWaveText = (1ull << 32) - (1ull << 20);  // weight prefixes are u32
-constexpr int kBigGrid = 256;   // k_rs_big workgroups
+constexpr int kBigGrid = 256;   // k_rs_big / k_sortbig workgroups
+constexpr int kMidGrid = 4096;  // k_sortmid workgroups
+// level-1 sibling grouping by counting (k_count ...) for waves whose largest document has at
+// most this many runs (its child counts, placement and keys then stay within a few MB)
+constexpr uint32_t kCsrDocRuns = 1u << 16;
+constexpr uint32_t kCsrWaveRuns = 1u << 23;  // (or every wave this small: fewer launches)
 constexpr int kBigThreads = 1024;
 
 // ctl words (device, zeroed per wave)
 enum Ctl {
-    C_RSV0 = 0,     // (unused)
-    C_RSV1 = 1,     // (unused)
+    C_NBIGRUN = 0,  // runs listed by k_walk2 for k_bigruns (longer than kWalkText bytes)
+    C_NDEFER = 1,   // (CSR grouping) parents with 9 or more children
     C_ERR = 2,      // error bits: 1 bad parent, 2 walk overrun, 4 text overflow, 8 write out
                     //   of range, 16 unreachable runs (cycle)
     C_RTOTAL = 3,   // runs of the wave
@@ -71,6 +76,7 @@ enum Ctl {
     C_RMAX = 5,     // most runs in one document
     C_VISITED = 6,  // runs visited by k_walk2
     C_UNFUSED = 7,  // documents whose text k_doctree left to k_expand
+    C_NBIG = 9,     // (CSR grouping) parents with more than 64 children
     C_REPLAN = 8,   // the wave outgrew the launch plan it was enqueued with (runs / largest
                     //   document above the planned capacity): every later kernel of the wave
                     //   exits at once and the host merges the wave again with a fresh plan
@@ -889,7 +895,10 @@ struct TreeArgs {
     const uint32_t* pstart;      // weight prefix per run (+ sentinel): weight = [g + 1] - [g]
     const uint32_t* doc_root;    // per document: its document-start run
     const uint32_t* doc_p0;      // per document: weight prefix at its start
-    uint4* rec;  // per run {first_child, weight, next_sibling, parent}
+    // per run two uint4 (one 32-byte line): {first_child, weight, next_sibling, parent} and
+    // {weight prefix (its slot-order text), -, -, -}
+    uint4* rec;
+    uint32_t rsh;      // log2 of the uint4 per record (1: the second line, for walk-written text)
     uint32_t* ctl;
     uint2* swn;        // per splitter {sublist weight, next splitter}
     uint32_t* roff;
@@ -908,7 +917,18 @@ struct TreeArgs {
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
+    // text written by k_walk2 (text mode of the grid-wide level 1): every run of up to kWalkText
+    // bytes is copied from the slot-order text at its document offset by the walker that passes
+    // it (bytes consecutive along a sublist); longer runs are listed for k_bigruns
+    uint32_t walk_text;
+    const uint8_t* sbytes;
+    const uint32_t* r_head;
+    const uint32_t* chunk_doc;
+    uint32_t log2c;          // chunk_doc granularity (slots per entry, log2)
+    uint2* bigrun;           // {run, document offset} of the runs longer than kWalkText
+    uint32_t bigrun_cap;
 };
+constexpr uint32_t kWalkText = 32;
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n,
                                                          uint32_t* __restrict__ sums) {
@@ -1009,8 +1029,15 @@ __device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uin
 // elements per wave and digit (ballot matching: stable within the wave), publishes the tile's
 // digit counts, takes the counts of every earlier tile by decoupled look-back (one thread per
 // digit), reorders the tile by digit in LDS and writes each digit's stretch contiguously.
-#ifndef CRDT_RS_THREADS
-#define CRDT_RS_THREADS 512
+// Tile shapes, measured on config 5 (750 M runs, tools/gpu_iter.sh A/B of builds): sort A
+// 1024 threads x 8 elements (8192 x 16 B, one workgroup per CU) 25.3 ms for four passes against
+// 28.5 for 512 x 8 and 35-38 for 2048-element tiles; sort B 512 x 16 (8192 x 8 B, two workgroups
+// per CU) 21.6 against 24.8 for 1024 x 8 or 512 x 8.
+#ifndef CRDT_RS_THREADS_A
+#define CRDT_RS_THREADS_A 1024
+#endif
+#ifndef CRDT_RS_THREADS_B
+#define CRDT_RS_THREADS_B 512
 #endif
 #ifndef CRDT_RS_ITEMS_A
 #define CRDT_RS_ITEMS_A 8
@@ -1018,12 +1045,12 @@ __device__ __forceinline__ void cx(uint64_t& ka, uint32_t& ia, uint64_t& kb, uin
 #ifndef CRDT_RS_ITEMS_B
 #define CRDT_RS_ITEMS_B 16
 #endif
-constexpr uint32_t kRsThreads = CRDT_RS_THREADS;
-constexpr uint32_t kRsWaves = kRsThreads / 64;
-constexpr uint32_t kRsItemsA = CRDT_RS_ITEMS_A;          // sort A: 4096 x 16 B per tile
-constexpr uint32_t kRsItemsB = CRDT_RS_ITEMS_B;          // sort B: 8192 x 8 B per tile
-constexpr uint32_t kRsTileA = kRsThreads * kRsItemsA;
-constexpr uint32_t kRsTileB = kRsThreads * kRsItemsB;
+constexpr uint32_t kRsThreadsA = CRDT_RS_THREADS_A;
+constexpr uint32_t kRsThreadsB = CRDT_RS_THREADS_B;
+constexpr uint32_t kRsItemsA = CRDT_RS_ITEMS_A;
+constexpr uint32_t kRsItemsB = CRDT_RS_ITEMS_B;
+constexpr uint32_t kRsTileA = kRsThreadsA * kRsItemsA;   // sort A: 8192 x 16 B per tile
+constexpr uint32_t kRsTileB = kRsThreadsB * kRsItemsB;   // sort B: 8192 x 8 B per tile
 constexpr uint32_t kRsBins = 256;
 constexpr uint32_t kRsMaxPass = 4;
 constexpr uint32_t kRsAgg = 0x80000000u;  // look-back word: a tile's digit count (else prefix + 1)
@@ -1035,9 +1062,12 @@ constexpr uint32_t kRsCtl = 2 * kRsMaxPass * kRsBins;
 constexpr uint32_t kRsBig = 8;
 constexpr uint32_t kRsSmall = kRsCtl + 16;
 constexpr uint32_t kRsBigLds = 8192;  // groups of up to this many children sort in LDS
+constexpr uint32_t kRsPlaceBits = 14;  // sort B: the low bits of the run id are placed in LDS
 
 struct RsArgs {
     uint32_t R, pass, npass;
+    uint32_t npassB;     // passes of sort B (the bits of the run id above kRsPlaceBits)
+    uint32_t shift0;     // bit of the first digit (sort B sorts the bits above kRsPlaceBits)
     const void* in;      // the previous pass's output (or the order pass's pairs)
     void* out;
     uint32_t* hist;      // this sort's [pass][256] bucket starts
@@ -1080,11 +1110,11 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(TreeArgs a, RsArgs r) {
 __global__ __launch_bounds__(kRsBins) void k_rs_scan(RsArgs r) {
     __shared__ uint32_t lds[kRsBins / 64];
     const uint32_t d = threadIdx.x;
-    for (uint32_t k = 0; k < r.npass; ++k) {
+    for (uint32_t k = 0; k < max(r.npass, r.npassB); ++k) {
         uint32_t tot;
         const uint32_t v = r.hist[k * kRsBins + d];
         r.hist[k * kRsBins + d] = block_excl_scan<kRsBins / 64>(v, lds, tot);
-        const uint64_t P = 1ull << (8u * k), Q = P << 8;
+        const uint64_t P = 1ull << (kRsPlaceBits + 8u * k), Q = P << 8;
         const uint64_t rem = r.R % Q, lo = (uint64_t)d * P;
         const uint64_t cnt = (r.R / Q) * P + (rem > lo ? std::min<uint64_t>(rem - lo, P) : 0ull);
         r.hist[kRsHistB + k * kRsBins + d] = block_excl_scan<kRsBins / 64>((uint32_t)cnt, lds, tot);
@@ -1096,10 +1126,10 @@ __device__ __forceinline__ uint32_t rs_lanes_below(uint64_t m) {
 }
 
 // One pass.  T: uint4 (sort A) or uint2 (sort B), the sort key in .x.  MODE 0: the first pass of
-// A (elements built from r_parent / r_key); 1: elements from r.in to r.out; 2: the last pass of
-// B (r.out[position] = .y, the next sibling: a permutation lands in run order).
-template <class T, int MODE, int ITEMS>
-__global__ __launch_bounds__(kRsThreads) void k_rs_pass(TreeArgs a, RsArgs r) {
+// A (elements built from r_parent / r_key); 1: elements from r.in to r.out.
+template <class T, int MODE, int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
+    constexpr uint32_t kRsThreads = THREADS, kRsWaves = THREADS / 64;
     constexpr uint32_t TILE = kRsThreads * ITEMS;
     __shared__ T buf[TILE];
     __shared__ uint32_t wc[kRsWaves][kRsBins + 1];  // per wave and digit (+1: invalid elements)
@@ -1111,7 +1141,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(TreeArgs a, RsArgs r) {
     if (t == 0) tsh = atomicAdd(&r.tctr[r.pass], 1u);
     for (uint32_t i = t; i < kRsWaves * (kRsBins + 1); i += kRsThreads) (&wc[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t tile = tsh, R = r.R, sh = 8u * r.pass;
+    const uint32_t tile = tsh, R = r.R, sh = r.shift0 + 8u * r.pass;
     // wave wv takes elements [base, base + 64 ITEMS) of the tile, lane-striped
     const uint32_t base = tile * TILE + wv * (64u * ITEMS);
     T e[ITEMS];
@@ -1221,11 +1251,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(TreeArgs a, RsArgs r) {
         const uint32_t i = (uint32_t)k * kRsThreads + t;
         if (i < nval) {
             const T x = buf[i];
-            const uint32_t o = gof[(x.x >> sh) & 255u] + i;
-            if constexpr (MODE == 2)
-                reinterpret_cast<uint32_t*>(r.out)[o] = x.y;
-            else
-                reinterpret_cast<T*>(r.out)[o] = x;
+            reinterpret_cast<T*>(r.out)[gof[(x.x >> sh) & 255u] + i] = x;
         }
     }
 }
@@ -1369,6 +1395,27 @@ __global__ __launch_bounds__(kBigThreads) void k_rs_big(TreeArgs a, RsArgs r, ui
     }
 }
 
+// Sort B's last step.  Its passes sorted the pairs by the run id's bits above kRsPlaceBits only;
+// the ids are a permutation of 0..R-1, so block b of 2^kRsPlaceBits pairs holds exactly the ids
+// [b 2^kRsPlaceBits, (b + 1) 2^kRsPlaceBits): one workgroup puts the next siblings in id order in
+// LDS and writes them out as consecutive words.
+__global__ __launch_bounds__(1024) void k_rs_place(TreeArgs a, const uint2* __restrict__ B,
+                                                   uint32_t* __restrict__ ns) {
+    __shared__ uint32_t buf[1u << kRsPlaceBits];
+    const uint32_t base = blockIdx.x << kRsPlaceBits;
+    const uint32_t n = min(1u << kRsPlaceBits, a.R - base);
+    uint32_t bad = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) {
+        const uint2 e = B[base + i];
+        const uint32_t o = e.x - base;
+        if (o < n) buf[o] = e.y;
+        else bad = 1;
+    }
+    if (bad) atomicOr(&a.ctl[C_ERR], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) ns[base + i] = buf[i];
+}
+
 // The run records in run order, every input coalesced: {first child, weight, next sibling,
 // parent} (a document start, or a run with a malformed parent: no parent, no sibling).
 __global__ __launch_bounds__(kBlock) void k_rs_records(TreeArgs a, const uint32_t* __restrict__ fc,
@@ -1377,7 +1424,219 @@ __global__ __launch_bounds__(kBlock) void k_rs_records(TreeArgs a, const uint32_
     if (g >= a.R) return;
     bool bad;
     const uint32_t p = rs_parent(a, g, bad);
-    a.rec[g] = make_uint4(fc[g], a.pstart[g + 1] - a.pstart[g], ns[g], p == a.R ? kNil : p);
+    const uint32_t p0 = a.pstart[g];
+    a.rec[g << a.rsh] = make_uint4(fc[g], a.pstart[g + 1] - p0, ns[g], p == a.R ? kNil : p);
+    if (a.rsh) a.rec[(g << 1) + 1u] = make_uint4(p0, 0u, 0u, 0u);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Level 1, grid-wide, documents of up to kCsrDocRuns runs: sibling groups by counting
+// ---------------------------------------------------------------------------------------------
+// A child count per parent (one atomic per run, whose return value is the child's place in its
+// parent's segment), an exclusive scan, a placement scatter, then the sibling order per parent
+// (pairs inline, up to 8 by a register network, 9..64 one wave per group, wider one workgroup per
+// group).  The atomics, the placement and the key reads land inside the run's own document, so
+// when every document's runs span a few MB they hit the caches: measured faster than the radix
+// sorts on such waves (the Fugue trace line: 7.3 against 19.4 ms of grouping per step); the
+// radix sorts take waves with a larger document (config 5).
+__global__ __launch_bounds__(kBlock) void k_count(TreeArgs a, uint32_t* __restrict__ deg) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.R) return;
+    const uint32_t p = a.in_parent[g];
+    if (p == kNil) return;
+    if (p >= a.R || p == g) { atomicOr(&a.ctl[C_ERR], 1u); return; }
+    // the child's place in its parent's segment comes with the count (roff is free until
+    // k_walk2), so that k_place needs no second atomic
+    a.roff[g] = atomicAdd(&deg[p], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_place(TreeArgs a, const uint32_t* __restrict__ cstart,
+                                                  uint32_t* __restrict__ child) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.R) return;
+    const uint32_t p = a.in_parent[g];
+    if (p == kNil || p >= a.R || p == g) return;  // flagged by k_count
+    child[cstart[p] + a.roff[g]] = g;  // (the place k_count's atomic handed out)
+}
+
+// Compare-exchange for a descending sort of (key, id) pairs held in registers.
+__device__ __forceinline__ void cxi(uint64_t& ka, uint32_t& ia, uint64_t& kb, uint32_t& ib) {
+    if (rs_before(kb, ib, ka, ia)) {
+        const uint64_t tk = ka; ka = kb; kb = tk;
+        const uint32_t ti = ia; ia = ib; ib = ti;
+    }
+}
+
+struct CsrArgs {
+    const uint32_t* cstart;  // per run: its children's segment start (cstart[R] = the total)
+    uint32_t* child;         // children grouped by parent
+    uint32_t* defer;         // parents with 9 or more children
+    uint32_t* bigl;          // parents with more than 64 children
+};
+
+// Run records: {first child, weight} written by the run itself, {next sibling, parent} by
+// whoever orders its sibling group (a.rsh: 1 when the records carry a second line).
+__device__ __forceinline__ void set_dn(const TreeArgs& a, uint32_t g, uint32_t fc, uint32_t w) {
+    reinterpret_cast<uint2*>(a.rec + (g << a.rsh))[0] = make_uint2(fc, w);
+    if (a.rsh) a.rec[(g << 1) + 1u] = make_uint4(a.pstart[g], 0u, 0u, 0u);
+}
+__device__ __forceinline__ void set_upr(const TreeArgs& a, uint32_t c, uint32_t ns, uint32_t p) {
+    reinterpret_cast<uint2*>(a.rec + (c << a.rsh))[1] = make_uint2(ns, p);
+}
+__device__ __forceinline__ void set_fcr(const TreeArgs& a, uint32_t p, uint32_t c) {
+    reinterpret_cast<uint32_t*>(a.rec + (p << a.rsh))[0] = c;
+}
+
+// Up to 8 siblings: Batcher's 19-comparator odd-even merge network (padding key 0 sorts last:
+// every child key has lamport >= 1).
+__device__ __forceinline__ uint32_t link_small(const TreeArgs& a, const CsrArgs& c_, uint32_t g,
+                                               uint32_t s0, uint32_t cnt) {
+    uint64_t k[8];
+    uint32_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = (uint32_t)i < cnt ? c_.child[s0 + i] : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = (uint32_t)i < cnt ? a.key[c[i]] : 0ull;
+    cxi(k[0], c[0], k[1], c[1]); cxi(k[2], c[2], k[3], c[3]);
+    cxi(k[4], c[4], k[5], c[5]); cxi(k[6], c[6], k[7], c[7]);
+    cxi(k[0], c[0], k[2], c[2]); cxi(k[1], c[1], k[3], c[3]);
+    cxi(k[4], c[4], k[6], c[6]); cxi(k[5], c[5], k[7], c[7]);
+    cxi(k[1], c[1], k[2], c[2]); cxi(k[5], c[5], k[6], c[6]);
+    cxi(k[0], c[0], k[4], c[4]); cxi(k[1], c[1], k[5], c[5]);
+    cxi(k[2], c[2], k[6], c[6]); cxi(k[3], c[3], k[7], c[7]);
+    cxi(k[2], c[2], k[4], c[4]); cxi(k[3], c[3], k[5], c[5]);
+    cxi(k[1], c[1], k[2], c[2]); cxi(k[3], c[3], k[4], c[4]); cxi(k[5], c[5], k[6], c[6]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if ((uint32_t)i < cnt) set_upr(a, c[i], (uint32_t)i + 1 < cnt ? c[i + 1 < 8 ? i + 1 : 7] : kNil, g);
+    return c[0];
+}
+
+__global__ __launch_bounds__(kBlock) void k_link(TreeArgs a, CsrArgs c_) {
+    __shared__ uint32_t nblk, bbase;
+    if (threadIdx.x == 0) nblk = 0;
+    __syncthreads();
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    bool defer = false;
+    if (g < a.R) {
+        const uint32_t w = a.pstart[g + 1] - a.pstart[g];
+        if (a.in_parent[g] == kNil) set_upr(a, g, kNil, kNil);  // no sibling, no parent
+        const uint32_t s0 = c_.cstart[g], cnt = c_.cstart[g + 1] - s0;
+        uint32_t fc = kNil;
+        if (cnt == 1) {
+            const uint32_t c0 = c_.child[s0];
+            fc = c0;
+            set_upr(a, c0, kNil, g);
+        } else if (cnt == 2) {
+            uint32_t c0 = c_.child[s0], c1 = c_.child[s0 + 1];
+            if (rs_before(a.key[c1], c1, a.key[c0], c0)) { const uint32_t t = c0; c0 = c1; c1 = t; }
+            fc = c0;
+            set_upr(a, c0, c1, g);
+            set_upr(a, c1, kNil, g);
+        } else if (cnt <= 8) {
+            if (cnt) fc = link_small(a, c_, g, s0, cnt);
+        } else {
+            defer = true;  // first_child written by the sort kernels
+        }
+        set_dn(a, g, fc, w);
+    }
+    // deferred segments: one global atomic per block
+    uint32_t slot = 0;
+    if (defer) slot = atomicAdd(&nblk, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && nblk) bbase = atomicAdd(&a.ctl[C_NDEFER], nblk);
+    __syncthreads();
+    if (defer) c_.defer[bbase + slot] = g;
+}
+
+// One wave per deferred segment of 9..64 children: rank = #siblings before it, then ds_permute
+// scatters ids into rank order and shuffles hand each lane its successor.
+__global__ __launch_bounds__(kBlock) void k_sortmid(TreeArgs a, CsrArgs c_) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = (gridDim.x * kBlock) >> 6;
+    const uint32_t nd = a.ctl[C_NDEFER];
+    for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6; i < nd; i += nw) {
+        const uint32_t p = c_.defer[i];
+        const uint32_t s0 = c_.cstart[p], cnt = c_.cstart[p + 1] - s0;
+        if (cnt > 64) {
+            if (lane == 0) c_.bigl[atomicAdd(&a.ctl[C_NBIG], 1u)] = p;
+            continue;
+        }
+        const bool on = lane < cnt;
+        const uint32_t c = on ? c_.child[s0 + lane] : 0u;
+        const uint64_t k = on ? a.key[c] : 0ull;
+        const uint32_t khi = (uint32_t)(k >> 32), klo = (uint32_t)k;
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t hj = (uint32_t)__shfl((int)khi, (int)j);
+            const uint32_t lj = (uint32_t)__shfl((int)klo, (int)j);
+            const uint32_t cj = (uint32_t)__shfl((int)c, (int)j);
+            rank += rs_before(((uint64_t)hj << 32) | lj, cj, k, c) ? 1u : 0u;
+        }
+        // lane r <- id of rank r
+        const uint32_t sorted =
+            (uint32_t)__builtin_amdgcn_ds_permute((int)((on ? rank : lane) << 2), (int)c);
+        const uint32_t succ = (uint32_t)__shfl((int)sorted, (int)((lane + 1) & 63));
+        const uint32_t ns_of_rank = (lane + 1 < cnt) ? succ : kNil;
+        const uint32_t ns = (uint32_t)__shfl((int)ns_of_rank, (int)(on ? rank : 0));
+        if (on) {
+            set_upr(a, c, ns, p);
+            if (rank == 0) set_fcr(a, p, c);
+        }
+    }
+}
+
+// Bitonic sort (descending by key, run id) of one sibling segment of more than 64 children, in
+// LDS up to kRsBigLds children, else in place in the child array ("flip" formulation: the
+// padding to a power of two is never stored).
+__global__ __launch_bounds__(kBigThreads) void k_sortbig(TreeArgs a, CsrArgs c_) {
+    __shared__ uint64_t skey[kRsBigLds];
+    __shared__ uint32_t sid[kRsBigLds];
+    const uint32_t nb = a.ctl[C_NBIG];
+    for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+        const uint32_t p = c_.bigl[bi];
+        const uint32_t s0 = c_.cstart[p], cnt = c_.cstart[p + 1] - s0;
+        uint32_t P = 1;
+        while (P < cnt) P <<= 1;
+        uint32_t* seg = c_.child + s0;
+        const bool lds = P <= kRsBigLds;
+        if (lds) {
+            for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) {
+                sid[i] = seg[i];
+                skey[i] = a.key[seg[i]];
+            }
+            __syncthreads();
+        }
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < P / 2; t += kBigThreads) {
+                    const uint32_t i = (t / j) * 2 * j + (t % j);
+                    const uint32_t l = (j == (k >> 1)) ? (i ^ (k - 1)) : (i ^ j);
+                    if (l >= cnt) continue;
+                    if (lds) {
+                        if (rs_before(skey[l], sid[l], skey[i], sid[i])) {
+                            const uint64_t tk = skey[i]; skey[i] = skey[l]; skey[l] = tk;
+                            const uint32_t ti = sid[i]; sid[i] = sid[l]; sid[l] = ti;
+                        }
+                    } else {
+                        const uint32_t ci = seg[i], cl = seg[l];
+                        if (rs_before(a.key[cl], cl, a.key[ci], ci)) { seg[i] = cl; seg[l] = ci; }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (lds) {
+            for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) seg[i] = sid[i];
+            __syncthreads();
+        }
+        for (uint32_t i = threadIdx.x; i < cnt; i += kBigThreads) {
+            const uint32_t c = seg[i];
+            set_upr(a, c, i + 1 < cnt ? seg[i + 1] : kNil, p);
+        }
+        if (threadIdx.x == 0) set_fcr(a, p, seg[0]);
+        __syncthreads();
+    }
 }
 
 // Euler-tour walks (sublist list ranking).  Regular splitters: both arcs of every run that is
@@ -1451,7 +1710,7 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
         uint4 r[kWalkIlp];
 #pragma unroll
         for (int q = 0; q < kWalkIlp; ++q)
-            if ((live >> q) & 1u) r[q] = a.rec[v[q]];
+            if ((live >> q) & 1u) r[q] = a.rec[v[q] << a.rsh];
 #pragma unroll
         for (int q = 0; q < kWalkIlp; ++q) {
             if (!((live >> q) & 1u)) continue;
@@ -1474,18 +1733,21 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
 // pointer jumping (kSup times fewer entries than the splitters), then every super walks its stretch
 // of the splitter list once more writing the prefixes.  Two dependent gathers per splitter plus a
 // few rounds over the supers, instead of log2(list length) rounds over all splitters.
-constexpr uint32_t kSupLog2 = 6, kSup = 1u << kSupLog2;
-__device__ __forceinline__ bool is_super(uint32_t s, uint32_t Sreg) { return s >= Sreg || (s & (kSup - 1u)) == 0u; }
-// compact index of a super: regular ones first, then one per document
-__device__ __forceinline__ uint32_t super_idx(uint32_t s, uint32_t Sreg) {
-    return s >= Sreg ? ((Sreg + kSup - 1u) >> kSupLog2) + (s - Sreg) : s >> kSupLog2;
+// (kSup = 2^slog2: 64 on large waves, where the walks are throughput-bound; 8 on small ones,
+// where a stretch walk is a chain of dependent loads that bounds the kernel)
+__device__ __forceinline__ bool is_super(uint32_t s, uint32_t Sreg, uint32_t slog2) {
+    return s >= Sreg || (s & ((1u << slog2) - 1u)) == 0u;
 }
-__device__ __forceinline__ uint32_t super_of(uint32_t c, uint32_t Sreg) {
-    const uint32_t nr = (Sreg + kSup - 1u) >> kSupLog2;
-    return c >= nr ? Sreg + (c - nr) : c << kSupLog2;
+// compact index of a super: regular ones first, then one per document
+__device__ __forceinline__ uint32_t super_idx(uint32_t s, uint32_t Sreg, uint32_t slog2) {
+    return s >= Sreg ? ((Sreg + (1u << slog2) - 1u) >> slog2) + (s - Sreg) : s >> slog2;
+}
+__device__ __forceinline__ uint32_t super_of(uint32_t c, uint32_t Sreg, uint32_t slog2) {
+    const uint32_t nr = (Sreg + (1u << slog2) - 1u) >> slog2;
+    return c >= nr ? Sreg + (c - nr) : c << slog2;
 }
 struct SupArgs {
-    uint32_t S, Sreg, Sc, step_limit;
+    uint32_t S, Sreg, Sc, step_limit, slog2;
     const uint2* swn;    // per splitter {weight, next}
     uint2* sup;          // per super {stretch weight, next super (compact, kNil: end)}
     uint32_t* pred;      // per super: its predecessor (kNil: a list head or unused)
@@ -1496,13 +1758,13 @@ struct SupArgs {
 __global__ __launch_bounds__(kBlock) void k_sup1(SupArgs a) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= a.Sc) return;
-    uint32_t x = super_of(c, a.Sreg), sum = 0, nx = kNil, steps = 0;
+    uint32_t x = super_of(c, a.Sreg, a.slog2), sum = 0, nx = kNil, steps = 0;
     if (x < a.S) {
         for (;;) {
             const uint2 w = a.swn[x];
             sum += w.x;
             if (w.y == kNil) break;
-            if (is_super(w.y, a.Sreg)) { nx = super_idx(w.y, a.Sreg); break; }
+            if (is_super(w.y, a.Sreg, a.slog2)) { nx = super_idx(w.y, a.Sreg, a.slog2); break; }
             x = w.y;
             if (++steps > a.step_limit) { atomicOr(&a.ctl[C_ERR], 2u); break; }
         }
@@ -1531,14 +1793,14 @@ __global__ __launch_bounds__(kBlock) void k_sup_step(const uint2* __restrict__ i
 __global__ __launch_bounds__(kBlock) void k_sup2(SupArgs a, const uint2* __restrict__ vp) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= a.Sc) return;
-    uint32_t x = super_of(c, a.Sreg), steps = 0;
+    uint32_t x = super_of(c, a.Sreg, a.slog2), steps = 0;
     if (x >= a.S) return;
     uint32_t pref = vp[c].x;
     for (;;) {
         const uint2 w = a.swn[x];
         a.spref[x] = pref;
         pref += w.x;
-        if (w.y == kNil || is_super(w.y, a.Sreg)) break;
+        if (w.y == kNil || is_super(w.y, a.Sreg, a.slog2)) break;
         x = w.y;
         if (++steps > a.step_limit) break;
     }
@@ -1607,10 +1869,15 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     }
 }
 
-// Re-walk: every run passed on a down arc gets its offset inside its document.
+// Re-walk: every run passed on a down arc gets its offset inside its document; in text mode the
+// walker copies the run's bytes there itself (the next line of the record holds the run's place
+// in the slot-order text), so the document is written in order along each sublist and no run
+// offset is stored; runs longer than kWalkText bytes are listed for k_bigruns.
 __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __restrict__ spref) {
     const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * kWalkIlp;
-    uint32_t v[kWalkIlp], off[kWalkIlp], live = 0, steps = 0, runs = 0, nxt;
+    uint32_t v[kWalkIlp], off[kWalkIlp], live = 0, steps = 0, runs = 0, nxt, bad = 0;
+    uint64_t tb[kWalkIlp];
+    uint32_t tl[kWalkIlp];
     bool up[kWalkIlp];
 #pragma unroll
     for (int q = 0; q < kWalkIlp; ++q) {
@@ -1618,22 +1885,47 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
         v[q] = 0;
         up[q] = false;
         off[q] = 0;
+        tb[q] = 0;
+        tl[q] = 0;
         if (s < a.S && splitter_arc(a, s, v[q], up[q])) {
             live |= 1u << q;
             off[q] = spref[s];
+            if (a.walk_text) {  // the walk's document: its output offset and length
+                const uint32_t d = s >= a.Sreg ? s - a.Sreg : a.chunk_doc[a.r_head[v[q]] >> a.log2c];
+                tb[q] = a.toff[d];
+                tl[q] = a.tlen[d];
+            }
         }
     }
     while (live) {
-        uint4 r[kWalkIlp];
+        uint4 r[kWalkIlp], x[kWalkIlp];
 #pragma unroll
         for (int q = 0; q < kWalkIlp; ++q)
-            if ((live >> q) & 1u) r[q] = a.rec[v[q]];
+            if ((live >> q) & 1u) {
+                r[q] = a.rec[v[q] << a.rsh];
+                if (a.walk_text) x[q] = a.rec[(v[q] << 1) + 1u];  // (the same 32-byte line)
+            }
 #pragma unroll
         for (int q = 0; q < kWalkIlp; ++q) {
             if (!((live >> q) & 1u)) continue;
             if (!up[q]) {
-                if (r[q].y) a.roff[v[q]] = off[q];  // runs without visible bytes are never expanded
-                off[q] += r[q].y;
+                const uint32_t w = r[q].y;
+                if (w && !a.walk_text) {
+                    a.roff[v[q]] = off[q];  // (runs without visible bytes are never expanded)
+                } else if (w) {
+                    if ((uint64_t)off[q] + w > tl[q]) {
+                        bad = 1;
+                    } else if (w <= kWalkText) {
+                        uint8_t* o = a.text + tb[q] + off[q];
+                        const uint8_t* src = a.sbytes + x[q].x;
+                        for (uint32_t b = 0; b < w; ++b) o[b] = src[b];
+                    } else {
+                        const uint32_t k = atomicAdd(&a.ctl[C_NBIGRUN], 1u);
+                        if (k < a.bigrun_cap) a.bigrun[k] = make_uint2(v[q], off[q]);
+                        else bad = 1;
+                    }
+                }
+                off[q] += w;
                 ++runs;
             }
             if (!walk_next(r[q], a.log2m, v[q], up[q], nxt)) live &= ~(1u << q);
@@ -1643,9 +1935,25 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
             break;
         }
     }
+    if (bad) atomicOr(&a.ctl[C_ERR], 8u);
     // reachability: every run of the wave must be visited exactly once
     const uint32_t tot = wave_sum(runs);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
+}
+
+// The runs k_walk2 listed (longer than kWalkText bytes): one wave per run, the bytes in order.
+__global__ __launch_bounds__(kBlock) void k_bigruns(TreeArgs a) {
+    if (replan(a.ctl)) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = min(a.ctl[C_NBIGRUN], a.bigrun_cap);
+    for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6; i < n; i += (gridDim.x * kBlock) >> 6) {
+        const uint2 e = a.bigrun[i];
+        const uint4 r = a.rec[e.x << 1], x = a.rec[(e.x << 1) + 1u];
+        const uint32_t d = a.chunk_doc[a.r_head[e.x] >> a.log2c];
+        uint8_t* o = a.text + a.toff[d] + e.y;
+        const uint8_t* src = a.sbytes + x.x;
+        for (uint32_t b = lane; b < r.y; b += 64u) o[b] = src[b];
+    }
 }
 __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, uint64_t seed);
 
@@ -2949,6 +3257,8 @@ Engine::~Engine() {
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
     dfree(rs_elem_[0]); dfree(rs_elem_[1]); dfree(rs_status_); dfree(rs_bigl_);
     dfree(rs_small_);
+    dfree(bigrun_);
+    dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(out_); dfree(rec_); dfree(swn_); dfree(spref_); dfree(sup_); dfree(spred_);
     dfree(svp_[0]); dfree(svp_[1]); dfree(tlen_); dfree(loff_); dfree(toff_);
     dfree(leafh_); dfree(ghash_); dfree(text_);
@@ -3281,11 +3591,28 @@ int Engine::ensure_runs(uint64_t R, uint64_t S) {
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
         HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
-        HIPCHK(dalloc(&rec_, r), "hipMalloc run records");
+        HIPCHK(dalloc(&rec_, 2 * r), "hipMalloc run records");  // (two uint4 per run)
         cap_runs_ = r;
         gen_++;
     }
     return ensure_splitters(S);
+}
+
+// Counting-path scratch of the global level 1 (R runs): child counts, segment starts, children,
+// the deferred and long group lists, scan sums.
+int Engine::ensure_csr(uint64_t R) {
+    if (R <= cap_csr_) return CRDT_HIP_OK;
+    dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
+    const uint64_t r = R + (R >> 3) + 4096;
+    HIPCHK(dalloc(&deg_, r + 16), "hipMalloc child counts");
+    HIPCHK(dalloc(&cstart_, r + 16), "hipMalloc segment starts");
+    HIPCHK(dalloc(&child_, r), "hipMalloc children");
+    HIPCHK(dalloc(&defer_, r / 9 + 64), "hipMalloc deferred groups");
+    HIPCHK(dalloc(&bigl_, r / 65 + 64), "hipMalloc long groups");
+    HIPCHK(dalloc(&scan_sums_, r / kScanTile + 2), "hipMalloc scan sums");
+    cap_csr_ = r;
+    gen_++;
+    return CRDT_HIP_OK;
 }
 
 // Radix-sort scratch of the global level 1 (R runs): two element arrays, the look-back words
@@ -3449,7 +3776,15 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.docs = L.docs_rel + w.first_doc;                                                \
     a.text = text_;                                                                   \
     a.text_cap = ord ? w.order_cap : cap_text_ - 64;                                  \
-    a.align = ord ? 1u : 16u
+    a.align = ord ? 1u : 16u;                                                         \
+    a.walk_text = 0;                                                                  \
+    a.rsh = 0;                                                                        \
+    a.sbytes = sbytes_;                                                               \
+    a.r_head = r_head_;                                                               \
+    a.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);                                 \
+    a.log2c = L.log2m;                                                                \
+    a.bigrun = bigrun_;                                                               \
+    a.bigrun_cap = (uint32_t)std::min<uint64_t>(cap_bigrun_, 0xFFFFFFFFull)
 
 int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text,
                           uint32_t cap_runs, uint32_t cap_rmax, StageClock& ck) {
@@ -3547,68 +3882,99 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     a.S = S;
     a.step_limit = 2u * R + 4u;
     const uint32_t gR = grid_for(R);
-    // sort A by parent run (document starts: R) and sort B by run id, 8 bits per pass
-    const uint32_t npass = std::max<uint32_t>(1u, (ceil_log2((uint64_t)R + 1u) + 7u) / 8u);
-    const uint64_t tilesA = ((uint64_t)R + kRsTileA - 1) / kRsTileA;
-    const uint64_t tilesB = ((uint64_t)R + kRsTileB - 1) / kRsTileB;
-    rs_npass_ = npass;
-    RsArgs r{};
-    r.R = R;
-    r.npass = npass;
-    r.rctl = rs_small_ + kRsCtl;
-    r.status = rs_status_;
-    r.bigl = rs_bigl_;
-    r.fc = roff_;  // (free until k_walk2)
-    HIPCHK(hipMemsetAsync(rs_small_, 0, kRsSmall * 4ull, s), "clear radix counters");
-    HIPCHK(hipMemsetAsync(roff_, 0xFF, R * 4ull, s), "clear first children");
-    r.hist = rs_small_;
-    k_rs_hist<<<std::min<uint32_t>(gR, 2048u), kBlock, 0, s>>>(a, r);
-    MARK(S_COUNT);
-    k_rs_scan<<<1, kRsBins, 0, s>>>(r);
-    MARK(S_SCAN);
-    r.tctr = r.rctl;
-    for (uint32_t k = 0; k < npass; ++k) {
-        r.pass = k;
-        r.in = k ? rs_elem_[(k - 1) & 1] : nullptr;
-        r.out = rs_elem_[k & 1];
-        HIPCHK(hipMemsetAsync(rs_status_, 0, tilesA * kRsBins * 4ull, s), "clear look-back");
-        if (k == 0)
-            k_rs_pass<uint4, 0, kRsItemsA><<<(uint32_t)tilesA, kRsThreads, 0, s>>>(a, r);
-        else
-            k_rs_pass<uint4, 1, kRsItemsA><<<(uint32_t)tilesA, kRsThreads, 0, s>>>(a, r);
+    // text mode of a wave without run contraction: the walkers write the text (runs are single
+    // items), from records that carry their place in the slot-order text (two lines per run)
+    a.walk_text = walk_text(w, ord, p) ? 1u : 0u;
+    a.rsh = a.walk_text;
+    if (l1_csr_) {  // (chosen by run_wave, which sized the scratch)
+        CsrArgs c_{cstart_, child_, defer_, bigl_};
+        const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
+        HIPCHK(hipMemsetAsync(deg_, 0, (R + 1ull) * 4ull, s), "clear child counts");
+        k_count<<<gR, kBlock, 0, s>>>(a, deg_);
+        MARK(S_COUNT);
+        k_scan_reduce<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_);
+        k_scan_top<<<1, 1024, 0, s>>>(scan_sums_, nb, cstart_, R);
+        k_scan_apply<<<nb, kBlock, 0, s>>>(deg_, R, scan_sums_, cstart_);
+        MARK(S_SCAN);
+        k_place<<<gR, kBlock, 0, s>>>(a, cstart_, child_);
+        MARK(S_PLACE);
+        k_link<<<gR, kBlock, 0, s>>>(a, c_);
+        k_sortmid<<<kMidGrid, kBlock, 0, s>>>(a, c_);
+        k_sortbig<<<kBigGrid, kBigThreads, 0, s>>>(a, c_);
+        MARK(S_LINK);
+    } else {
+        // sort A by parent run (document starts: R) and sort B by run id, 8 bits per pass
+        const uint32_t npass = std::max<uint32_t>(1u, (ceil_log2((uint64_t)R + 1u) + 7u) / 8u);
+        const uint64_t tilesA = ((uint64_t)R + kRsTileA - 1) / kRsTileA;
+        const uint64_t tilesB = ((uint64_t)R + kRsTileB - 1) / kRsTileB;
+        rs_npass_ = npass;
+        RsArgs r{};
+        r.R = R;
+        r.npass = npass;
+        {
+            const uint32_t bits = ceil_log2((uint64_t)R);  // (run ids < R)
+            r.npassB = bits > kRsPlaceBits ? (bits - kRsPlaceBits + 7u) / 8u : 0u;
+        }
+        rs_npassB_ = r.npassB;
+        r.shift0 = 0;
+        r.rctl = rs_small_ + kRsCtl;
+        r.status = rs_status_;
+        r.bigl = rs_bigl_;
+        r.fc = roff_;  // (free until k_walk2)
+        HIPCHK(hipMemsetAsync(rs_small_, 0, kRsSmall * 4ull, s), "clear radix counters");
+        HIPCHK(hipMemsetAsync(roff_, 0xFF, R * 4ull, s), "clear first children");
+        r.hist = rs_small_;
+        k_rs_hist<<<std::min<uint32_t>(gR, 2048u), kBlock, 0, s>>>(a, r);
+        MARK(S_COUNT);
+        k_rs_scan<<<1, kRsBins, 0, s>>>(r);
+        MARK(S_SCAN);
+        r.tctr = r.rctl;
+        for (uint32_t k = 0; k < npass; ++k) {
+            r.pass = k;
+            r.in = k ? rs_elem_[(k - 1) & 1] : nullptr;
+            r.out = rs_elem_[k & 1];
+            HIPCHK(hipMemsetAsync(rs_status_, 0, tilesA * kRsBins * 4ull, s), "clear look-back");
+            if (k == 0)
+                k_rs_pass<uint4, 0, kRsItemsA, kRsThreadsA><<<(uint32_t)tilesA, kRsThreadsA, 0, s>>>(a, r);
+            else
+                k_rs_pass<uint4, 1, kRsItemsA, kRsThreadsA><<<(uint32_t)tilesA, kRsThreadsA, 0, s>>>(a, r);
+        }
+        MARK(S_PLACE);
+        uint4* E = rs_elem_[(npass - 1) & 1];
+        uint2* B0 = reinterpret_cast<uint2*>(rs_elem_[npass & 1]);  // (the other element array:
+        uint2* B1 = B0 + cap_rs_;                                     //  room for two pair arrays)
+        r.B = B0;
+        k_rs_order<<<gR, kBlock, 0, s>>>(a, r, E);
+        k_rs_big<<<kBigGrid, kBigThreads, 0, s>>>(a, r, E);
+        MARK(S_LINK);
+        // sort B: the pairs by the run id's bits above kRsPlaceBits, then k_rs_place puts each
+        // block's next siblings in run order (over the element array of sort A: dead once the
+        // pairs are out)
+        uint32_t* ns = reinterpret_cast<uint32_t*>(E);
+        r.hist = rs_small_ + kRsHistB;
+        r.tctr = r.rctl + kRsMaxPass;
+        r.shift0 = kRsPlaceBits;
+        const uint2* Bf = B0;
+        for (uint32_t k = 0; k < r.npassB; ++k) {
+            r.pass = k;
+            r.in = (k & 1) ? B1 : B0;
+            r.out = (k & 1) ? B0 : B1;
+            Bf = (k & 1) ? B0 : B1;
+            HIPCHK(hipMemsetAsync(rs_status_, 0, tilesB * kRsBins * 4ull, s), "clear look-back");
+            k_rs_pass<uint2, 1, kRsItemsB, kRsThreadsB><<<(uint32_t)tilesB, kRsThreadsB, 0, s>>>(a, r);
+        }
+        k_rs_place<<<(uint32_t)(((uint64_t)R + (1u << kRsPlaceBits) - 1) >> kRsPlaceBits), 1024, 0, s>>>(a, Bf, ns);
+        k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);
+        MARK(S_SORTB);
     }
-    MARK(S_PLACE);
-    uint4* E = rs_elem_[(npass - 1) & 1];
-    uint2* B0 = reinterpret_cast<uint2*>(rs_elem_[npass & 1]);  // (the other element array:
-    uint2* B1 = B0 + cap_rs_;                                     //  room for two pair arrays)
-    r.B = B0;
-    k_rs_order<<<gR, kBlock, 0, s>>>(a, r, E);
-    k_rs_big<<<kBigGrid, kBigThreads, 0, s>>>(a, r, E);
-    MARK(S_LINK);
-    // sort B: the pairs by run id; its last pass writes the next siblings in run order over the
-    // element array of sort A (dead once the pairs are out)
-    uint32_t* ns = reinterpret_cast<uint32_t*>(E);
-    r.hist = rs_small_ + kRsHistB;
-    r.tctr = r.rctl + kRsMaxPass;
-    for (uint32_t k = 0; k < npass; ++k) {
-        r.pass = k;
-        r.in = (k & 1) ? B1 : B0;
-        r.out = k + 1 == npass ? static_cast<void*>(ns) : static_cast<void*>((k & 1) ? B0 : B1);
-        HIPCHK(hipMemsetAsync(rs_status_, 0, tilesB * kRsBins * 4ull, s), "clear look-back");
-        if (k + 1 == npass)
-            k_rs_pass<uint2, 2, kRsItemsB><<<(uint32_t)tilesB, kRsThreads, 0, s>>>(a, r);
-        else
-            k_rs_pass<uint2, 1, kRsItemsB><<<(uint32_t)tilesB, kRsThreads, 0, s>>>(a, r);
-    }
-    k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);
-    MARK(S_SORTB);
     const uint32_t gW = grid_for(((uint64_t)S + kWalkIlp - 1) / kWalkIlp);
     k_walk1<<<gW, kBlock, 0, s>>>(a);
     MARK(S_WALK1);
     SupArgs sa{};
     sa.S = S;
     sa.Sreg = Sreg;
-    sa.Sc = ((Sreg + kSup - 1u) >> kSupLog2) + w.ndocs;
+    sa.slog2 = S >= (1u << 22) ? 6u : 3u;
+    sa.Sc = ((Sreg + (1u << sa.slog2) - 1u) >> sa.slog2) + w.ndocs;
     sa.step_limit = S + 4u;
     sa.swn = swn_;
     sa.sup = sup_;
@@ -3623,7 +3989,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     k_sup_init<<<gC, kBlock, 0, s>>>(sa);
     // a document's list holds at most 2 * (ceil(runs / M) + 1) + 1 splitters, of which at most
     // that / kSup + 2 are supers
-    rounds = ceil_log2(2ull * ((p.rmax + (1u << log2m_w) - 1) >> log2m_w) / kSup + 8);
+    rounds = ceil_log2((2ull * ((p.rmax + (1u << log2m_w) - 1) >> log2m_w) >> sa.slog2) + 8);
     for (uint32_t k = 0; k < rounds; ++k)
         k_sup_step<<<gC, kBlock, 0, s>>>(svp_[k & 1], sa.Sc, svp_[(k + 1) & 1]);
     k_sup2<<<gC, kBlock, 0, s>>>(sa, svp_[rounds & 1]);
@@ -3631,6 +3997,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     MARK(S_RANK);
     k_doctotals<<<1, 1024, 0, s>>>(a);
     k_walk2<<<gW, kBlock, 0, s>>>(a, spref);
+    if (a.walk_text) k_bigruns<<<1024, kBlock, 0, s>>>(a);
     MARK(S_WALK2);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
@@ -3681,9 +4048,12 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
                         const StageClock& ck, const uint32_t* hctl, std::vector<float>& stage_ms,
                         std::vector<uint32_t>& stage_launches) {
     const uint32_t g1 = p.lds1 ? 0u : 1u;
-    const bool expand_run = !p.fuse;
-    const uint32_t launches[S_N] = {1, 6, (rs_npass_ + 1) * g1, g1, g1, rs_npass_ * g1, 2 * g1, g1,
-                                    (3 + rounds) * g1, 2 * g1,
+    const bool wt = walk_text(w, ord, p);
+    const bool expand_run = !p.fuse && !wt;
+    const uint32_t rs = l1_csr_ ? 0u : 1u;
+    const uint32_t launches[S_N] = {1, 6, (rs_npassB_ + 2) * g1 * rs, g1, (rs ? 1u : 3u) * g1,
+                                    (rs ? rs_npass_ : 1u) * g1, (rs ? 2u : 3u) * g1, g1,
+                                    (3 + rounds) * g1, (wt ? 3u : 2u) * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
                                     p.lds1 ? 2u : 0u};
@@ -3741,7 +4111,18 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     const uint64_t rows = cap_runs_;  // run rows k_runs could write
     rc = ensure_runs(p.R, Sreg + w.ndocs);
     if (rc) return rc;
-    if (!p.lds1 && (rc = ensure_radix(p.R))) return rc;
+    // sibling grouping of the global level 1: by counting when every document's runs stay within
+    // a few MB (the atomics and gathers land in cache), else by the two radix sorts
+    l1_csr_ = l1_group == 1 || (l1_group == 0 && (p.rmax <= kCsrDocRuns || p.R <= kCsrWaveRuns));
+    if (!p.lds1 && !l1_csr_ && (rc = ensure_radix(p.R))) return rc;
+    if (!p.lds1 && l1_csr_ && (rc = ensure_csr(p.R))) return rc;
+    if (walk_text(w, ord, p) && w.text_cap / (kWalkText + 1) + 64 > cap_bigrun_) {
+        dfree(bigrun_);
+        cap_bigrun_ = 0;
+        HIPCHK(dalloc(&bigrun_, w.text_cap / (kWalkText + 1) + 64), "hipMalloc long runs");
+        cap_bigrun_ = w.text_cap / (kWalkText + 1) + 64;
+        gen_++;
+    }
     if (p.R > rows) {
         // more runs than rows: the run records again, now that they fit (k_runs only reads
         // level-0 outputs, so it can run twice)
@@ -3753,7 +4134,9 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     rc = p.lds1 ? launch_lds_level1(L, w, ord, p, false, ck)
                 : launch_global_level1(L, w, ord, p, ck, rounds);
     if (rc) return rc;
-    rc = launch_tail(L, w, ord, p.fuse, ck, hctl);
+    // (text mode of the global level 1 without run contraction: k_walk2 and k_bigruns wrote the
+    // text)
+    rc = launch_tail(L, w, ord, p.fuse || walk_text(w, ord, p), ck, hctl);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s), "merge wave");
     uint32_t errs = hctl[C_ERR];

@@ -162,6 +162,9 @@ public:
     // run contraction of RGA waves: 0 = by the wave's input (no contraction when at least
     // kNoconShare of its items lack the previous-slot flag), 1 = always, 2 = never
     uint32_t contraction = 0;
+    // sibling grouping of the global level 1: 0 = by the largest document (counting up to
+    // kCsrDocRuns runs, else radix sorts), 1 = always counting, 2 = always radix sorts
+    uint32_t l1_group = 0;
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
@@ -263,7 +266,13 @@ private:
     uint4* rs_elem_[2] = {nullptr, nullptr};
     uint32_t *rs_status_ = nullptr, *rs_small_ = nullptr;
     uint2* rs_bigl_ = nullptr;
-    uint32_t rs_npass_ = 0;
+    uint32_t *deg_ = nullptr, *cstart_ = nullptr, *child_ = nullptr, *defer_ = nullptr,
+             *bigl_ = nullptr, *scan_sums_ = nullptr;  // counting-path scratch (engine.hip k_count)
+    uint64_t cap_csr_ = 0;
+    bool l1_csr_ = false;      // the last global level 1 grouped siblings by counting
+    uint2* bigrun_ = nullptr;  // k_walk2's list of runs longer than kWalkText bytes
+    uint64_t cap_bigrun_ = 0;
+    uint32_t rs_npass_ = 0, rs_npassB_ = 0;
     uint4* rec_ = nullptr;
     uint2* swn_ = nullptr;     // per splitter {sublist weight, next splitter}
     uint32_t* spref_ = nullptr;  // per splitter: exclusive prefix along its list
@@ -313,12 +322,15 @@ private:
                     crdt_hip_stats* st);
     int ensure_runs(uint64_t runs, uint64_t splitters);
     int ensure_radix(uint64_t runs);
+    int ensure_csr(uint64_t runs);
     int ensure_splitters(uint64_t splitters);
     int ensure_scratch(const Wave& w);
     int ensure_host_out(const DeviceLogs& L);
     uint32_t* host_block(const DeviceLogs& L, uint32_t wi) const;
     int ensure_events(std::vector<hipEvent_t>& ev, size_t n);
     L1Plan plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord, bool force_global) const;
+    // the global level 1 of a text-mode wave without run contraction: k_walk2 writes the text
+    static bool walk_text(const Wave& w, bool ord, const L1Plan& p) { return !p.lds1 && !ord && w.nocon; }
     int clock_mark(StageClock& c, int stage);
     // The launches of one wave, in stream order.
     int launch_runs(DeviceLogs& L, const Wave& w, bool ord);

@@ -255,13 +255,15 @@ def _level1_cases():
     return logs
 
 
-@pytest.mark.parametrize("level1", [0, 1])
-def test_level1_paths_match_oracle(oracle, level1):
-    """Per-document LDS level 1 (k_doctree, default) and the global level-1 kernels must give
-    the oracle's bytes and digests, including sibling groups of every sort width (> 64 makes
-    the LDS path hand the wave to the global path) and a run heavier than 0xFFFF bytes."""
+@pytest.mark.parametrize("level1,group", [(0, 0), (1, 1), (1, 2)])
+def test_level1_paths_match_oracle(oracle, level1, group):
+    """Per-document LDS level 1 (k_doctree, default) and the global level-1 kernels, with their
+    sibling groups by counting (group 1) and by the two radix sorts (group 2), must give the
+    oracle's bytes and digests, including sibling groups of every sort width (> 64 makes the LDS
+    path hand the wave to the global path) and a run heavier than 0xFFFF bytes."""
     c = crdt_hip.Context(0)
     c.set_param("level1", level1)
+    c.set_param("l1_group", group)
     logs = _level1_cases()
     dig, lens, st = c.merge_batch(logs, stats=True)
     for i, lg in enumerate(logs):
@@ -545,11 +547,16 @@ def test_run_contraction_modes_agree(oracle, golden, relabel):
     assert runs[1] < runs[2]
 
 
-def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle):
+@pytest.mark.parametrize("level1,group", [(0, 0), (1, 1), (1, 2)])
+def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle, level1, group):
     """The same without contraction on uploaded logs (the level-1 cases: agents, wide sibling
-    groups, heavy runs, multi-byte text), and a parent out of range is still reported."""
+    groups, heavy runs, multi-byte text), on the per-document and on the global level 1 (there
+    the walkers write the text, runs longer than 32 bytes through k_bigruns), and a parent out of
+    range is still reported."""
     c = crdt_hip.Context(0)
     c.set_param("contraction", 2)
+    c.set_param("level1", level1)
+    c.set_param("l1_group", group)
     logs = _level1_cases()
     dig, lens, st = c.merge_batch(logs, stats=True)
     for i, lg in enumerate(logs):
