@@ -70,15 +70,13 @@ KERNEL_BYTES = {
     # head stage (k_heads: nsq/visible/jump bits in, head records out) and k_runs: head records,
     # nibbles; per run: key + parent slot + rank lookup in, record row out; text move
     "runs": (0.875, 38.0, 2.0),
-    # global level 1 (radix): histograms (parent in); per pass 16 B element in + out; order pass
-    # (element in, pair + first child out); sort B per pass 8 B in + out (last: 4 B out), records
-    # (first child, next sibling, parent, weight prefix in; 16 B out) -- per pass counts in
-    # stage_launches, priced per run in alg_bytes below
+    # global level 1, sibling groups by counting: parent in + child count (count), placement
+    # (place), keys and links (link); the radix form is priced in level1_run_bytes below
     "count": (0.0, 4.0, 0.0),
     "scan": (0.0, 0.0, 0.0),
     "place": (0.0, 32.0, 0.0),
     "link": (0.0, 28.0, 0.0),
-    "sortb": (0.0, 16.0, 0.0),
+    "sortb": (0.0, 0.0, 0.0),
     "walk1": (0.0, 16.0, 0.0),
     "rank": (0.0, 0.5, 0.0),
     "walk2": (0.0, 20.0, 0.0),
@@ -86,6 +84,23 @@ KERNEL_BYTES = {
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out
 }
+
+
+def level1_run_bytes(k: str, per_wave: dict, text_mode: bool):
+    """Bytes per run of a global level-1 stage in its radix form, or None for the
+    counting form (KERNEL_BYTES).  per_wave: the stage launches per wave (passes)."""
+    if k == "count":      # k_rs_hist: parent in
+        return 4.0
+    if k == "place":      # sort A: first pass parent + key in, 16-B element out; then 16 in + 16 out
+        return 28.0 + 32.0 * (per_wave["place"] - 1)
+    if k == "link":       # k_rs_order: element in, pair + first child out
+        return 28.0
+    if k == "sortb":      # sort B passes (8 + 8), k_rs_place (8 in, 4 out), k_rs_records (16 in,
+        #                   16 out; text mode: the second 16-B line and the run's bytes)
+        return 16.0 * (per_wave["sortb"] - 2) + 12.0 + 32.0 + (17.0 if text_mode else 0.0)
+    return None
+
+
 STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs",
                 "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
 # HBM bytes per item of each kernel from rocprofv3 PMC passes of this build (FETCH_SIZE x2 for
@@ -417,18 +432,38 @@ def traces_rank(args, comm, make_batch, inputs) -> dict | None:
     return res if rank == 0 else None
 
 
-def roofline_fields(stats, batch, items_per_gpu, step_s) -> dict:
-    """Per-kernel algorithmic GB/s, the dominant kernel's roofline, the pipeline's fraction."""
+def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> dict:
+    """Per-kernel algorithmic GB/s, the dominant kernel's roofline, the pipeline's fraction.
+    pmc: the PMC traffic file describes this workload (the headline config); else traffic is
+    null rather than another workload's bytes."""
     stage_ns = {k: float(np.mean([s["stage_ns"][k] for s in stats])) for k in stats[0]["stage_ns"]}
     launches = stats[0]["stage_launches"]
     slots = items_per_gpu + batch.docs  # items + one document-start slot per document
     runs = stats[0]["runs"]
     text_bytes = stats[0]["text_bytes"]
 
+    waves = max(1, stats[0]["waves"])
+    per_wave = {k: launches[k] / waves for k in launches}
+    radix = bool(launches.get("sortb"))
+    # text mode (waves without run contraction on the global level 1): the re-walk stage is
+    # k_tcopy + k_walk_ovf (+ k_doctotals), 4 launches per k_walk1 launch instead of 2
+    text_mode = bool(launches.get("walk1")) and launches.get("walk2", 0) == 4 * launches["walk1"]
+
     def alg_bytes(k):
         per_slot, per_run, per_text = KERNEL_BYTES[k]
         if k == "doctree" and launches.get("expand", 1):
             per_text = 0.0  # expansion left to k_expand: no text in or out of k_doctree
+        if radix and level1_run_bytes(k, per_wave, text_mode) is not None:
+            per_run = level1_run_bytes(k, per_wave, text_mode)
+        if text_mode:
+            if k == "classify":
+                per_run = 0.0   # no contraction: no parents read, no jump bits
+            elif k == "runs":
+                per_run = 32.0  # parent + key in; head, prefix, parent, key out
+            elif k == "walk1":
+                per_run, per_text = 32.0, 1.0  # the 32-byte record line; the staged text out
+            elif k == "walk2":
+                per_run, per_text = 0.5, 2.0   # splitter words; staged text in, document out
         return per_slot * slots + per_run * runs + per_text * text_bytes
 
     per_kernel = {k: {"ms": stage_ns[k] / 1e6, "launches": launches[k],
@@ -437,14 +472,13 @@ def roofline_fields(stats, batch, items_per_gpu, step_s) -> dict:
 
     # one launch of a stage's main kernel per wave (a stage's helper kernels, e.g. k_doctotals
     # beside k_doctree, are timed inside the stage: a few percent of it)
-    waves = max(1, stats[0]["waves"])
 
     def roof(k):
         ns = stage_ns[k] / waves
         b = alg_bytes(k) / waves
         return {"bound": "hbm", "kernel": STAGE_KERNEL.get(k, k), "achieved": b / ns,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": b / ns / HBM_PEAK_GBPS,
-                "traffic": measured_traffic(k, items_per_gpu / waves),
+                "traffic": measured_traffic(k, items_per_gpu / waves) if pmc else None,
                 "alg_bytes_per_launch": b, "launch_us": ns / 1e3}
 
     # the dominant kernel = the stage with the most device time per step (HIP events, summed
@@ -522,7 +556,10 @@ def traces_workload(args) -> int:
             ctx.set_param("lanes", 1)
             iso_stats = [batch.merge()[2] for _ in range(3)][1:]
             ctx.set_param("lanes", args.lanes)
-        rf = roofline_fields(iso_stats, batch, items_per_gpu, res["step_s"])
+        # (the committed PMC bytes per item were measured at the headline config)
+        headline = (args.relabel == "rotate" and args.order != "fugue" and args.replicas == 4096
+                    and args.nsq_list == 1)
+        rf = roofline_fields(iso_stats, batch, items_per_gpu, res["step_s"], pmc=headline)
         rf_lanes = None
         if args.lanes > 1:
             rf_lanes = {k: round(float(np.mean([s["stage_ns"][k] for s in stats])) / 1e6, 4)

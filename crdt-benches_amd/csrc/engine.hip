@@ -67,16 +67,17 @@ constexpr int kBigThreads = 1024;
 
 // ctl words (device, zeroed per wave)
 enum Ctl {
-    C_NBIGRUN = 0,  // runs listed by k_walk2 for k_bigruns (longer than kWalkText bytes)
+    C_NBIGRUN = 0,  // (unused)
     C_NDEFER = 1,   // (CSR grouping) parents with 9 or more children
     C_ERR = 2,      // error bits: 1 bad parent, 2 walk overrun, 4 text overflow, 8 write out
                     //   of range, 16 unreachable runs (cycle)
     C_RTOTAL = 3,   // runs of the wave
     C_WTOTAL = 4,   // weight total of the wave
     C_RMAX = 5,     // most runs in one document
-    C_VISITED = 6,  // runs visited by k_walk2
+    C_VISITED = 6,  // runs visited by k_walk2 (text mode: k_walk1)
     C_UNFUSED = 7,  // documents whose text k_doctree left to k_expand
     C_NBIG = 9,     // (CSR grouping) parents with more than 64 children
+    C_NOVF = 10,    // (text mode) sublists listed by k_tcopy for k_walk_ovf
     C_REPLAN = 8,   // the wave outgrew the launch plan it was enqueued with (runs / largest
                     //   document above the planned capacity): every later kernel of the wave
                     //   exits at once and the host merges the wave again with a fresh plan
@@ -917,18 +918,31 @@ struct TreeArgs {
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
-    // text written by k_walk2 (text mode of the grid-wide level 1): every run of up to kWalkText
-    // bytes is copied from the slot-order text at its document offset by the walker that passes
-    // it (bytes consecutive along a sublist); longer runs are listed for k_bigruns
+    // text mode of the grid-wide level 1 (waves without run contraction: every run is one item):
+    // a run's bytes (one codepoint) ride in the second line of its record, k_walk1 writes each
+    // sublist's text in walk order to its splitter's kWalkTmp-byte slot of wtmp, k_tcopy moves
+    // the slots to the document once the splitters are ranked, and k_walk_ovf walks the few
+    // sublists with more text again for the rest
     uint32_t walk_text;
     const uint8_t* sbytes;
     const uint32_t* r_head;
     const uint32_t* chunk_doc;
     uint32_t log2c;          // chunk_doc granularity (slots per entry, log2)
-    uint2* bigrun;           // {run, document offset} of the runs longer than kWalkText
-    uint32_t bigrun_cap;
+    uint8_t* wtmp;
+    uint32_t* ovf;           // splitters whose sublists carry more than kWalkTmp bytes
 };
-constexpr uint32_t kWalkText = 32;
+constexpr uint32_t kWalkText = 4;      // (one codepoint)
+constexpr uint32_t kWalkTmpLog2 = 7;   // 128 bytes per sublist: ~4x the mean at 64 arcs per sublist
+constexpr uint32_t kWalkTmp = 1u << kWalkTmpLog2;
+
+// The second line of a run record in text mode: {its place in the slot-order text, its bytes
+// packed little-endian when there are at most kWalkText of them}.
+__device__ __forceinline__ uint4 text_line(const TreeArgs& a, uint32_t p0, uint32_t w) {
+    uint32_t b = 0;
+    if (w <= kWalkText)
+        for (uint32_t i = 0; i < w; ++i) b |= (uint32_t)a.sbytes[p0 + i] << (8u * i);
+    return make_uint4(p0, b, 0u, 0u);
+}
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n,
                                                          uint32_t* __restrict__ sums) {
@@ -1425,8 +1439,9 @@ __global__ __launch_bounds__(kBlock) void k_rs_records(TreeArgs a, const uint32_
     bool bad;
     const uint32_t p = rs_parent(a, g, bad);
     const uint32_t p0 = a.pstart[g];
-    a.rec[g << a.rsh] = make_uint4(fc[g], a.pstart[g + 1] - p0, ns[g], p == a.R ? kNil : p);
-    if (a.rsh) a.rec[(g << 1) + 1u] = make_uint4(p0, 0u, 0u, 0u);
+    const uint32_t w = a.pstart[g + 1] - p0;
+    a.rec[g << a.rsh] = make_uint4(fc[g], w, ns[g], p == a.R ? kNil : p);
+    if (a.rsh) a.rec[(g << 1) + 1u] = text_line(a, p0, w);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1478,7 +1493,7 @@ struct CsrArgs {
 // whoever orders its sibling group (a.rsh: 1 when the records carry a second line).
 __device__ __forceinline__ void set_dn(const TreeArgs& a, uint32_t g, uint32_t fc, uint32_t w) {
     reinterpret_cast<uint2*>(a.rec + (g << a.rsh))[0] = make_uint2(fc, w);
-    if (a.rsh) a.rec[(g << 1) + 1u] = make_uint4(a.pstart[g], 0u, 0u, 0u);
+    if (a.rsh) a.rec[(g << 1) + 1u] = text_line(a, a.pstart[g], w);
 }
 __device__ __forceinline__ void set_upr(const TreeArgs& a, uint32_t c, uint32_t ns, uint32_t p) {
     reinterpret_cast<uint2*>(a.rec + (c << a.rsh))[1] = make_uint2(ns, p);
@@ -1686,35 +1701,62 @@ __device__ __forceinline__ bool walk_next(const uint4& r, uint32_t m, uint32_t& 
     return true;
 }
 
-// Walks are chains of dependent random loads (one record per arc), so every thread advances
-// kWalkIlp sublists at once: that many loads in flight per thread instead of one.
-#ifndef CRDT_WALK_ILP
-#define CRDT_WALK_ILP 2
-#endif
-constexpr int kWalkIlp = CRDT_WALK_ILP;
-
+// Walks are chains of dependent random loads (one record per arc), so a thread can advance ILP
+// sublists at once: that many loads in flight per thread instead of one.  Measured: 2 pays on
+// waves without contraction (random trees, short sublists of single items), 1 on contracted
+// waves (Fugue, config 4), whose walks diverge more.
+// Text mode (TEXT): the walker also writes its sublist's text in walk order, the bytes of each
+// run from its record's second line, into its splitter's kWalkTmp-byte slot of wtmp (a dword
+// store per 4 bytes), and counts the runs it passes (reachability).
+template <int ILP, bool TEXT>
 __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
-    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * kWalkIlp;
-    uint32_t v[kWalkIlp], sum[kWalkIlp], nxt[kWalkIlp], live = 0, steps = 0;
-    bool up[kWalkIlp];
+    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * ILP;
+    uint32_t v[ILP], sum[ILP], nxt[ILP], acc[ILP], live = 0, steps = 0, runs = 0;
+    bool up[ILP];
 #pragma unroll
-    for (int q = 0; q < kWalkIlp; ++q) {
+    for (int q = 0; q < ILP; ++q) {
         const uint32_t s = base + q;
         sum[q] = 0;
         nxt[q] = kNil;
         v[q] = 0;
         up[q] = false;
+        acc[q] = 0;
         if (s < a.S && splitter_arc(a, s, v[q], up[q])) live |= 1u << q;
     }
     while (live) {
-        uint4 r[kWalkIlp];
+        uint4 r[ILP], x[ILP];
 #pragma unroll
-        for (int q = 0; q < kWalkIlp; ++q)
-            if ((live >> q) & 1u) r[q] = a.rec[v[q] << a.rsh];
+        for (int q = 0; q < ILP; ++q)
+            if ((live >> q) & 1u) {
+                r[q] = a.rec[v[q] << (TEXT ? 1 : a.rsh)];
+                if constexpr (TEXT) x[q] = a.rec[(v[q] << 1) + 1u];  // (the same 32-byte line)
+            }
 #pragma unroll
-        for (int q = 0; q < kWalkIlp; ++q) {
+        for (int q = 0; q < ILP; ++q) {
             if (!((live >> q) & 1u)) continue;
-            if (!up[q]) sum[q] += r[q].y;
+            if (!up[q]) {
+                const uint32_t w = r[q].y;
+                if constexpr (TEXT) {
+                    ++runs;
+                    if (w > kWalkText) {
+                        atomicOr(&a.ctl[C_ERR], 8u);  // (runs are single items here)
+                    } else {
+                        // append the run's bytes to the slot while they fit in it
+                        uint32_t* slot = reinterpret_cast<uint32_t*>(
+                            a.wtmp + ((uint64_t)(base + q) << kWalkTmpLog2));
+                        for (uint32_t b = 0; b < w; ++b) {
+                            const uint32_t o = sum[q] + b;
+                            if (o >= kWalkTmp) break;
+                            acc[q] |= ((x[q].y >> (8u * b)) & 255u) << (8u * (o & 3u));
+                            if ((o & 3u) == 3u) {
+                                slot[o >> 2] = acc[q];
+                                acc[q] = 0;
+                            }
+                        }
+                    }
+                }
+                sum[q] += w;
+            }
             if (!walk_next(r[q], a.log2m, v[q], up[q], nxt[q])) live &= ~(1u << q);
         }
         if (++steps > a.step_limit) {
@@ -1723,8 +1765,17 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
         }
     }
 #pragma unroll
-    for (int q = 0; q < kWalkIlp; ++q)
-        if (base + q < a.S) a.swn[base + q] = make_uint2(sum[q], nxt[q]);
+    for (int q = 0; q < ILP; ++q) {
+        if (base + q >= a.S) continue;
+        a.swn[base + q] = make_uint2(sum[q], nxt[q]);
+        // (the partial last dword of the slot; the bytes past the text are never copied)
+        if (TEXT && (sum[q] & 3u) && sum[q] < kWalkTmp)
+            reinterpret_cast<uint32_t*>(a.wtmp + ((uint64_t)(base + q) << kWalkTmpLog2))[sum[q] >> 2] = acc[q];
+    }
+    if constexpr (TEXT) {
+        const uint32_t tot = wave_sum(runs);
+        if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
+    }
 }
 
 // Ranking of the splitter lists (exclusive prefix of the sublist weights along each document's
@@ -1869,62 +1920,35 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     }
 }
 
-// Re-walk: every run passed on a down arc gets its offset inside its document; in text mode the
-// walker copies the run's bytes there itself (the next line of the record holds the run's place
-// in the slot-order text), so the document is written in order along each sublist and no run
-// offset is stored; runs longer than kWalkText bytes are listed for k_bigruns.
+// Re-walk: every run passed on a down arc with visible bytes gets its offset inside its document
+// (for k_expand), and every run passed is counted (reachability).
+template <int ILP>
 __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __restrict__ spref) {
-    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * kWalkIlp;
-    uint32_t v[kWalkIlp], off[kWalkIlp], live = 0, steps = 0, runs = 0, nxt, bad = 0;
-    uint64_t tb[kWalkIlp];
-    uint32_t tl[kWalkIlp];
-    bool up[kWalkIlp];
+    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * ILP;
+    uint32_t v[ILP], off[ILP], live = 0, steps = 0, runs = 0, nxt;
+    bool up[ILP];
 #pragma unroll
-    for (int q = 0; q < kWalkIlp; ++q) {
+    for (int q = 0; q < ILP; ++q) {
         const uint32_t s = base + q;
         v[q] = 0;
         up[q] = false;
         off[q] = 0;
-        tb[q] = 0;
-        tl[q] = 0;
         if (s < a.S && splitter_arc(a, s, v[q], up[q])) {
             live |= 1u << q;
             off[q] = spref[s];
-            if (a.walk_text) {  // the walk's document: its output offset and length
-                const uint32_t d = s >= a.Sreg ? s - a.Sreg : a.chunk_doc[a.r_head[v[q]] >> a.log2c];
-                tb[q] = a.toff[d];
-                tl[q] = a.tlen[d];
-            }
         }
     }
     while (live) {
-        uint4 r[kWalkIlp], x[kWalkIlp];
+        uint4 r[ILP];
 #pragma unroll
-        for (int q = 0; q < kWalkIlp; ++q)
-            if ((live >> q) & 1u) {
-                r[q] = a.rec[v[q] << a.rsh];
-                if (a.walk_text) x[q] = a.rec[(v[q] << 1) + 1u];  // (the same 32-byte line)
-            }
+        for (int q = 0; q < ILP; ++q)
+            if ((live >> q) & 1u) r[q] = a.rec[v[q] << a.rsh];
 #pragma unroll
-        for (int q = 0; q < kWalkIlp; ++q) {
+        for (int q = 0; q < ILP; ++q) {
             if (!((live >> q) & 1u)) continue;
             if (!up[q]) {
                 const uint32_t w = r[q].y;
-                if (w && !a.walk_text) {
-                    a.roff[v[q]] = off[q];  // (runs without visible bytes are never expanded)
-                } else if (w) {
-                    if ((uint64_t)off[q] + w > tl[q]) {
-                        bad = 1;
-                    } else if (w <= kWalkText) {
-                        uint8_t* o = a.text + tb[q] + off[q];
-                        const uint8_t* src = a.sbytes + x[q].x;
-                        for (uint32_t b = 0; b < w; ++b) o[b] = src[b];
-                    } else {
-                        const uint32_t k = atomicAdd(&a.ctl[C_NBIGRUN], 1u);
-                        if (k < a.bigrun_cap) a.bigrun[k] = make_uint2(v[q], off[q]);
-                        else bad = 1;
-                    }
-                }
+                if (w) a.roff[v[q]] = off[q];  // (runs without visible bytes are never expanded)
                 off[q] += w;
                 ++runs;
             }
@@ -1935,26 +1959,78 @@ __global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __
             break;
         }
     }
-    if (bad) atomicOr(&a.ctl[C_ERR], 8u);
     // reachability: every run of the wave must be visited exactly once
     const uint32_t tot = wave_sum(runs);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
 }
 
-// The runs k_walk2 listed (longer than kWalkText bytes): one wave per run, the bytes in order.
-__global__ __launch_bounds__(kBlock) void k_bigruns(TreeArgs a) {
+// The document of splitter s (whose first arc is v's).
+__device__ __forceinline__ uint32_t splitter_doc(const TreeArgs& a, uint32_t s, uint32_t v) {
+    return s >= a.Sreg ? s - a.Sreg : a.chunk_doc[a.r_head[v] >> a.log2c];
+}
+
+// Text mode, once the splitters are ranked: every sublist's staged text (up to kWalkTmp bytes)
+// to its place in its document, one thread per splitter, dword stores where the destination is
+// aligned; sublists with more text are listed for k_walk_ovf.  The sublist's whole range is
+// bounds-checked here (its weight is the walk's).
+__global__ __launch_bounds__(kBlock) void k_tcopy(TreeArgs a, const uint32_t* __restrict__ spref) {
     if (replan(a.ctl)) return;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n = min(a.ctl[C_NBIGRUN], a.bigrun_cap);
-    for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6; i < n; i += (gridDim.x * kBlock) >> 6) {
-        const uint2 e = a.bigrun[i];
-        const uint4 r = a.rec[e.x << 1], x = a.rec[(e.x << 1) + 1u];
-        const uint32_t d = a.chunk_doc[a.r_head[e.x] >> a.log2c];
-        uint8_t* o = a.text + a.toff[d] + e.y;
-        const uint8_t* src = a.sbytes + x.x;
-        for (uint32_t b = lane; b < r.y; b += 64u) o[b] = src[b];
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t v;
+    bool up;
+    if (s >= a.S || !splitter_arc(a, s, v, up)) return;
+    const uint32_t n = a.swn[s].x;
+    if (!n) return;
+    const uint32_t d = splitter_doc(a, s, v), o = spref[s];
+    if ((uint64_t)o + n > a.tlen[d]) {
+        atomicOr(&a.ctl[C_ERR], 8u);
+        return;
+    }
+    if (n > kWalkTmp) a.ovf[atomicAdd(&a.ctl[C_NOVF], 1u)] = s;  // (room for every splitter)
+    const uint32_t m = min(n, kWalkTmp);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtmp + ((uint64_t)s << kWalkTmpLog2));
+    uint8_t* dst = a.text + a.toff[d] + o;
+    auto byte_at = [&](uint32_t i) { return (src[i >> 2] >> (8u * (i & 3u))) & 255u; };
+    const uint32_t head = min(m, (4u - (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u);
+    uint32_t i = 0;
+    for (; i < head; ++i) dst[i] = (uint8_t)byte_at(i);
+    const uint32_t sh = 8u * (i & 3u);
+    for (; i + 4u <= m; i += 4u) {
+        const uint32_t lo = src[i >> 2];
+        const uint32_t wd = sh ? (lo >> sh) | (src[(i >> 2) + 1u] << (32u - sh)) : lo;
+        *reinterpret_cast<uint32_t*>(dst + i) = wd;
+    }
+    for (; i < m; ++i) dst[i] = (uint8_t)byte_at(i);
+}
+
+// Text mode: the sublists k_tcopy listed, walked again; each writes the bytes past its first
+// kWalkTmp.
+__global__ __launch_bounds__(kBlock) void k_walk_ovf(TreeArgs a, const uint32_t* __restrict__ spref) {
+    if (replan(a.ctl)) return;
+    const uint32_t n = a.ctl[C_NOVF];
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uint32_t s = a.ovf[i];
+        uint32_t v, nxt, off = 0, steps = 0;
+        bool up;
+        if (!splitter_arc(a, s, v, up)) continue;
+        uint8_t* out = a.text + a.toff[splitter_doc(a, s, v)] + spref[s];
+        for (bool go = true; go;) {
+            const uint4 r = a.rec[v << 1];
+            if (!up) {
+                const uint32_t w = r.y;
+                if (w <= kWalkText && off + w > kWalkTmp) {  // (k_walk1 flagged longer runs)
+                    const uint32_t b0 = off >= kWalkTmp ? 0u : kWalkTmp - off;
+                    const uint32_t x = a.rec[(v << 1) + 1u].y;
+                    for (uint32_t b = b0; b < w; ++b) out[off + b] = (uint8_t)(x >> (8u * b));
+                }
+                off += w;
+            }
+            go = walk_next(r, a.log2m, v, up, nxt);
+            if (++steps > a.step_limit) break;  // (k_walk1 flagged it)
+        }
     }
 }
+
 __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, uint64_t seed);
 
 // ---------------------------------------------------------------------------------------------
@@ -3257,7 +3333,8 @@ Engine::~Engine() {
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
     dfree(rs_elem_[0]); dfree(rs_elem_[1]); dfree(rs_status_); dfree(rs_bigl_);
     dfree(rs_small_);
-    dfree(bigrun_);
+    dfree(wtmp_);
+    dfree(ovf_);
     dfree(deg_); dfree(cstart_); dfree(child_); dfree(defer_); dfree(bigl_); dfree(scan_sums_);
     dfree(out_); dfree(rec_); dfree(swn_); dfree(spref_); dfree(sup_); dfree(spred_);
     dfree(svp_[0]); dfree(svp_[1]); dfree(tlen_); dfree(loff_); dfree(toff_);
@@ -3756,7 +3833,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.nsq_par = L.nsq_par;                                         \
     a0.nsq_key = L.nsq_key;                                         \
     a0.nsq_pre = L.nsq_pre ? L.nsq_pre + (w.slot0 >> 6) : nullptr;  \
-    a0.nocon = (w.nocon && !L.fugue) ? 1u : 0u;                     \
+    a0.nocon = w.nocon ? 1u : 0u;                                   \
     a0.copy_text = 1u
 
 // Tree / digest argument block (run counts come from ctl where the kernels need them).
@@ -3783,8 +3860,8 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.r_head = r_head_;                                                               \
     a.chunk_doc = L.chunk_doc + (w.slot0 >> L.log2m);                                 \
     a.log2c = L.log2m;                                                                \
-    a.bigrun = bigrun_;                                                               \
-    a.bigrun_cap = (uint32_t)std::min<uint64_t>(cap_bigrun_, 0xFFFFFFFFull)
+    a.wtmp = wtmp_;                                                                   \
+    a.ovf = ovf_
 
 int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text,
                           uint32_t cap_runs, uint32_t cap_rmax, StageClock& ck) {
@@ -3920,7 +3997,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         r.rctl = rs_small_ + kRsCtl;
         r.status = rs_status_;
         r.bigl = rs_bigl_;
-        r.fc = roff_;  // (free until k_walk2)
+        r.fc = roff_;  // (free until k_walk2; unused in text mode)
         HIPCHK(hipMemsetAsync(rs_small_, 0, kRsSmall * 4ull, s), "clear radix counters");
         HIPCHK(hipMemsetAsync(roff_, 0xFF, R * 4ull, s), "clear first children");
         r.hist = rs_small_;
@@ -3967,8 +4044,15 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);
         MARK(S_SORTB);
     }
-    const uint32_t gW = grid_for(((uint64_t)S + kWalkIlp - 1) / kWalkIlp);
-    k_walk1<<<gW, kBlock, 0, s>>>(a);
+    // two walkers per thread on waves without contraction, one on contracted waves (§5b)
+    const uint32_t ilp = a.walk_text ? 2u : 1u;
+    const uint32_t gW = grid_for(((uint64_t)S + ilp - 1) / ilp);
+    if (a.walk_text) {
+        HIPCHK(hipMemsetAsync(ctl_ + C_NOVF, 0, 4, s), "clear overflow count");
+        k_walk1<2, true><<<gW, kBlock, 0, s>>>(a);
+    } else {
+        k_walk1<1, false><<<gW, kBlock, 0, s>>>(a);
+    }
     MARK(S_WALK1);
     SupArgs sa{};
     sa.S = S;
@@ -3996,8 +4080,13 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     const uint32_t* spref = spref_;
     MARK(S_RANK);
     k_doctotals<<<1, 1024, 0, s>>>(a);
-    k_walk2<<<gW, kBlock, 0, s>>>(a, spref);
-    if (a.walk_text) k_bigruns<<<1024, kBlock, 0, s>>>(a);
+    if (a.walk_text) {
+        // the staged sublist texts out, then the rest of the longer sublists
+        k_tcopy<<<grid_for(S), kBlock, 0, s>>>(a, spref);
+        k_walk_ovf<<<1024, kBlock, 0, s>>>(a, spref);
+    } else {
+        k_walk2<1><<<gW, kBlock, 0, s>>>(a, spref);
+    }
     MARK(S_WALK2);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
@@ -4053,7 +4142,7 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
     const uint32_t rs = l1_csr_ ? 0u : 1u;
     const uint32_t launches[S_N] = {1, 6, (rs_npassB_ + 2) * g1 * rs, g1, (rs ? 1u : 3u) * g1,
                                     (rs ? rs_npass_ : 1u) * g1, (rs ? 2u : 3u) * g1, g1,
-                                    (3 + rounds) * g1, (wt ? 3u : 2u) * g1,
+                                    (3 + rounds) * g1, (wt ? 4u : 2u) * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
                                     p.lds1 ? 2u : 0u};
@@ -4116,11 +4205,16 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     l1_csr_ = l1_group == 1 || (l1_group == 0 && (p.rmax <= kCsrDocRuns || p.R <= kCsrWaveRuns));
     if (!p.lds1 && !l1_csr_ && (rc = ensure_radix(p.R))) return rc;
     if (!p.lds1 && l1_csr_ && (rc = ensure_csr(p.R))) return rc;
-    if (walk_text(w, ord, p) && w.text_cap / (kWalkText + 1) + 64 > cap_bigrun_) {
-        dfree(bigrun_);
-        cap_bigrun_ = 0;
-        HIPCHK(dalloc(&bigrun_, w.text_cap / (kWalkText + 1) + 64), "hipMalloc long runs");
-        cap_bigrun_ = w.text_cap / (kWalkText + 1) + 64;
+    if (walk_text(w, ord, p) && (uint64_t)Sreg + w.ndocs > cap_wtmp_) {
+        // a kWalkTmp-byte text slot per splitter (+ slack for k_tcopy's dword reads) and the
+        // overflow list
+        dfree(wtmp_);
+        dfree(ovf_);
+        cap_wtmp_ = 0;
+        const uint64_t ns = (uint64_t)Sreg + w.ndocs;
+        HIPCHK(dalloc(&wtmp_, (ns << kWalkTmpLog2) + 64), "hipMalloc sublist text");
+        HIPCHK(dalloc(&ovf_, ns), "hipMalloc sublist overflow list");
+        cap_wtmp_ = ns;
         gen_++;
     }
     if (p.R > rows) {
@@ -4134,8 +4228,8 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     rc = p.lds1 ? launch_lds_level1(L, w, ord, p, false, ck)
                 : launch_global_level1(L, w, ord, p, ck, rounds);
     if (rc) return rc;
-    // (text mode of the global level 1 without run contraction: k_walk2 and k_bigruns wrote the
-    // text)
+    // (text mode of the global level 1 without run contraction: k_tcopy and k_walk_ovf wrote
+    // the text)
     rc = launch_tail(L, w, ord, p.fuse || walk_text(w, ord, p), ck, hctl);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s), "merge wave");
@@ -4670,8 +4764,11 @@ void Engine::set_contraction(DeviceLogs& L) const {
     for (Wave& w : L.waves) {
         uint64_t items = 0;
         for (uint32_t k = 0; k < w.ndocs; ++k) items += L.docs[w.first_doc + k].n;
-        w.nocon = contraction == 2 ||
-                  (contraction == 0 && items && (double)w.nsq_items >= kNoconShare * (double)items);
+        // (Fugue logs always contract: level 0 has no uncontracted form of the two-row heads, and
+        // their items never carry the previous-slot flag)
+        w.nocon = !L.fugue && (contraction == 2 ||
+                               (contraction == 0 && items &&
+                                (double)w.nsq_items >= kNoconShare * (double)items));
     }
     apply_shape_hints(L);
 }

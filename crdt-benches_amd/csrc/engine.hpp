@@ -270,8 +270,9 @@ private:
              *bigl_ = nullptr, *scan_sums_ = nullptr;  // counting-path scratch (engine.hip k_count)
     uint64_t cap_csr_ = 0;
     bool l1_csr_ = false;      // the last global level 1 grouped siblings by counting
-    uint2* bigrun_ = nullptr;  // k_walk2's list of runs longer than kWalkText bytes
-    uint64_t cap_bigrun_ = 0;
+    uint8_t* wtmp_ = nullptr;  // text mode: the first kWalkTmp bytes of every sublist's text
+    uint64_t cap_wtmp_ = 0;    // (splitters)
+    uint32_t* ovf_ = nullptr;  // text mode: splitters whose sublist holds more than kWalkTmp bytes
     uint32_t rs_npass_ = 0, rs_npassB_ = 0;
     uint4* rec_ = nullptr;
     uint2* swn_ = nullptr;     // per splitter {sublist weight, next splitter}

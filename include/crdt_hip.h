@@ -102,15 +102,19 @@ typedef struct {
 enum {
     CRDT_HIP_STAGE_CLASSIFY = 0, /* level 0: seq/jump bits, weights, per-tile UTF-8           */
     CRDT_HIP_STAGE_RUNS = 1,     /* level 0: head bitvector, tile scan, run records, text     */
-    CRDT_HIP_STAGE_SORTB = 2,    /* level 1: radix sort of the (run, next sibling) pairs by
+    CRDT_HIP_STAGE_SORTB = 2,    /* level 1 (radix): sort of the (run, next sibling) pairs by
                                     run id, and the run records in run order                  */
-    CRDT_HIP_STAGE_COUNT = 3,    /* level 1: digit histograms of the radix sort by parent run */
-    CRDT_HIP_STAGE_SCAN = 4,     /* level 1: bucket starts of both radix sorts                */
-    CRDT_HIP_STAGE_PLACE = 5,    /* level 1: radix passes, runs by parent run (LDS-staged)    */
+    CRDT_HIP_STAGE_COUNT = 3,    /* level 1: child counts (counting) or the digit histograms
+                                    of the sort by parent run (radix)                         */
+    CRDT_HIP_STAGE_SCAN = 4,     /* level 1: segment starts / radix bucket starts             */
+    CRDT_HIP_STAGE_PLACE = 5,    /* level 1: runs grouped by parent run: placement (counting)
+                                    or LDS-staged onesweep radix passes                       */
     CRDT_HIP_STAGE_LINK = 6,     /* level 1: sibling order of each group, first children      */
-    CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums                          */
+    CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums (text mode: and each
+                                    sublist's text staged in walk order)                      */
     CRDT_HIP_STAGE_RANK = 8,     /* level 1: ranking of the splitter lists                    */
-    CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets                  */
+    CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets (text mode: the
+                                    staged sublist texts copied to their documents)           */
     CRDT_HIP_STAGE_EXPAND = 10,  /* runs copy their UTF-8 to their document offset            */
     CRDT_HIP_STAGE_DIGEST = 11,  /* per-document tree digest                                  */
     CRDT_HIP_STAGE_DOCTREE = 12, /* level 1 in LDS: whole run tree of a document per workgroup

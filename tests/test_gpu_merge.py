@@ -547,16 +547,20 @@ def test_run_contraction_modes_agree(oracle, golden, relabel):
     assert runs[1] < runs[2]
 
 
-@pytest.mark.parametrize("level1,group", [(0, 0), (1, 1), (1, 2)])
-def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle, level1, group):
+@pytest.mark.parametrize("level1,group,stride", [(0, 0, 0), (1, 1, 0), (1, 2, 0), (1, 1, 4096),
+                                                  (1, 2, 4096)])
+def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle, level1, group, stride):
     """The same without contraction on uploaded logs (the level-1 cases: agents, wide sibling
     groups, heavy runs, multi-byte text), on the per-document and on the global level 1 (there
-    the walkers write the text, runs longer than 32 bytes through k_bigruns), and a parent out of
-    range is still reported."""
+    the first walk stages each sublist's text, k_tcopy places it, and with 4096 runs per splitter
+    most sublists hold more than the 128 staged bytes, whose rest k_walk_ovf writes), and a parent
+    out of range is still reported."""
     c = crdt_hip.Context(0)
     c.set_param("contraction", 2)
     c.set_param("level1", level1)
     c.set_param("l1_group", group)
+    if stride:
+        c.set_param("splitter_stride", stride)
     logs = _level1_cases()
     dig, lens, st = c.merge_batch(logs, stats=True)
     for i, lg in enumerate(logs):
