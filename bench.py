@@ -763,6 +763,8 @@ def downstream_workload(args) -> int:
     world, rank, local = rank_env()
     ctx = crdt_hip.Context(local)
     comm = Comm(world, rank, ctx)
+    if args.nsq_list != 1:  # (each merge rebuilds the replica's compact nsq list; 0: gathers)
+        ctx.set_param("nsq_list", args.nsq_list)
     with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
         golden = json.load(f)
     t_setup = time.perf_counter()
@@ -838,6 +840,7 @@ def downstream_workload(args) -> int:
                                    + ("clone / apply / merge_len calls" if args.stepwise or args.pcie
                                       else "one crdt_hip_replica_replay call per closure"),
                        "updates": total_patches, "order": args.order,
+                       "nsq_list": args.nsq_list,
                        "encoded_bytes": int(sum(w[4] for w in work)),
                        "parallelism": f"replicas x{world} (no data-path collective)"},
             "per_trace": {w[0]: {"ms": per[w[0]] / args.steps * 1e3,

@@ -3318,8 +3318,10 @@ inline uint32_t ceil_log2(uint64_t x) {
 // =============================================================================================
 void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
-    dfree(nsq_par); dfree(nsq_pre); dfree(nsq_key);
+    dfree(nsq_par); dfree(nsq_pre); dfree(nsq_key); dfree(nsq_sums);
     nsq_items = 0;
+    nsq_ok = false;
+    nsq_cap = nsq_pre_cap = nsq_sums_cap = 0;
     dfree(docs_rel); dfree(doc_rank); dfree(chunk_doc);
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
@@ -3395,13 +3397,8 @@ std::string Engine::init(int dev) {
 int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
     const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
     // (a new slot layout: the compact nsq list, if any, no longer matches it)
-    if (L.nsq_par || L.nsq_pre || L.nsq_key) {
-        (void)hipStreamSynchronize(stream);
-        dfree(L.nsq_par);
-        dfree(L.nsq_pre);
-        dfree(L.nsq_key);
-        L.nsq_items = 0;
-    }
+    L.nsq_ok = false;
+    L.nsq_items = 0;
     L.log2m = kDocAlignLog2;
     L.docs = docs;
     L.doc_slot.resize(docs.size());
@@ -3830,9 +3827,9 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.cap_rmax = 0xFFFFFFFFu;                                      \
     a0.cap_rows = (uint32_t)std::min<uint64_t>(cap_runs_, 0xFFFFFFFFull);  \
     a0.xcd = xcd_order ? 1u : 0u;                                  \
-    a0.nsq_par = L.nsq_par;                                         \
-    a0.nsq_key = L.nsq_key;                                         \
-    a0.nsq_pre = L.nsq_pre ? L.nsq_pre + (w.slot0 >> 6) : nullptr;  \
+    a0.nsq_par = L.nsq_ok ? L.nsq_par : nullptr;                    \
+    a0.nsq_key = L.nsq_ok ? L.nsq_key : nullptr;                    \
+    a0.nsq_pre = L.nsq_ok ? L.nsq_pre + (w.slot0 >> 6) : nullptr;   \
     a0.nocon = w.nocon ? 1u : 0u;                                   \
     a0.copy_text = 1u
 
@@ -4707,41 +4704,30 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
 // sector per nsq item), and k_runs reads the parents of its nsq heads there.
 int Engine::build_nsq(DeviceLogs& L) {
     HIPCHK(hipStreamSynchronize(stream), "nsq list");
-    dfree(L.nsq_par);
-    dfree(L.nsq_pre);
-    dfree(L.nsq_key);
+    L.nsq_ok = false;
     L.nsq_items = 0;
     if (!L.total_slots || !nsq_list) {
         set_contraction(L);
         return CRDT_HIP_OK;
     }
-    const bool ord = false;  // (L0ARGS)
     const uint64_t nch = L.total_slots / 64 + 64;  // (a last tile's range ends within)
     if (nch >= (1ull << 32)) return CRDT_HIP_OK;
-    HIPCHK(dalloc(&L.nsq_pre, nch + 1), "hipMalloc nsq prefix");
-    HIPCHK(hipMemsetAsync(L.nsq_pre, 0, (nch + 1) * 4, stream), "nsq prefix");
-    for (const Wave& w : L.waves) {
-        L0ARGS(a0);
-        k_nsq_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6));
-    }
-    const uint32_t n = (uint32_t)nch, nb = (n + kScanTile - 1) / kScanTile;
-    uint32_t* sums = nullptr;
-    HIPCHK(dalloc(&sums, nb), "hipMalloc nsq scan");
-    k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, sums);
-    k_scan_top<<<1, 1024, 0, stream>>>(sums, nb, L.nsq_pre, n);
-    k_scan_apply<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, sums, L.nsq_pre);
+    if (int rc = nsq_reserve_prefix(L)) return rc;
+    nsq_count_scan(L);
+    const uint32_t n = (uint32_t)nch;
     uint32_t total = 0;
     hipError_t e = hipMemcpyAsync(&total, L.nsq_pre + n, 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    dfree(sums);
     if (e != hipSuccess) return fail("nsq scan", e);
-    HIPCHK(dalloc(&L.nsq_par, (uint64_t)total + 1), "hipMalloc nsq list");
-    HIPCHK(dalloc(&L.nsq_key, (uint64_t)total + 1), "hipMalloc nsq keys");
-    for (const Wave& w : L.waves) {
-        L0ARGS(a0);
-        k_nsq_scatter<<<(uint32_t)((w.nslots + kScanTile - 1) / kScanTile), kBlock, 0, stream>>>(
-            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par, L.nsq_key);
+    if ((uint64_t)total + 1 > L.nsq_cap) {
+        dfree(L.nsq_par);
+        dfree(L.nsq_key);
+        L.nsq_cap = 0;
+        HIPCHK(dalloc(&L.nsq_par, (uint64_t)total + 1), "hipMalloc nsq list");
+        HIPCHK(dalloc(&L.nsq_key, (uint64_t)total + 1), "hipMalloc nsq keys");
+        L.nsq_cap = (uint64_t)total + 1;
     }
+    nsq_scatter(L);
     HIPCHK(hipGetLastError(), "nsq list launch");
     // every wave's count of items without the previous-slot flag (its run contraction)
     for (Wave& w : L.waves) {
@@ -4754,7 +4740,80 @@ int Engine::build_nsq(DeviceLogs& L) {
     }
     HIPCHK(hipStreamSynchronize(stream), "nsq list");
     L.nsq_items = total;
+    L.nsq_ok = true;
     set_contraction(L);
+    return CRDT_HIP_OK;
+}
+
+// Room for the nsq prefix counts and their scan scratch of L's slot layout.
+int Engine::nsq_reserve_prefix(DeviceLogs& L) {
+    const uint64_t nch = L.total_slots / 64 + 64;
+    if (nch + 1 > L.nsq_pre_cap) {
+        dfree(L.nsq_pre);
+        L.nsq_pre_cap = 0;
+        HIPCHK(dalloc(&L.nsq_pre, nch + 1), "hipMalloc nsq prefix");
+        L.nsq_pre_cap = nch + 1;
+        gen_++;  // (captured replays point at the old arrays)
+    }
+    const uint64_t nb = (nch + kScanTile - 1) / kScanTile;
+    if (nb > L.nsq_sums_cap) {
+        dfree(L.nsq_sums);
+        L.nsq_sums_cap = 0;
+        HIPCHK(dalloc(&L.nsq_sums, nb), "hipMalloc nsq scan");
+        L.nsq_sums_cap = nb;
+        gen_++;
+    }
+    return CRDT_HIP_OK;
+}
+
+// Counts of the nsq items per 64-slot chunk, scanned in place into L.nsq_pre (launches only).
+void Engine::nsq_count_scan(DeviceLogs& L) {
+    const bool ord = false;  // (L0ARGS)
+    const uint32_t n = (uint32_t)(L.total_slots / 64 + 64), nb = (n + kScanTile - 1) / kScanTile;
+    (void)hipMemsetAsync(L.nsq_pre, 0, (n + 1ull) * 4, stream);
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_nsq_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6));
+    }
+    k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, L.nsq_sums);
+    k_scan_top<<<1, 1024, 0, stream>>>(L.nsq_sums, nb, L.nsq_pre, n);
+    k_scan_apply<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, L.nsq_sums, L.nsq_pre);
+}
+
+// The list itself, every wave's tiles (launches only).
+void Engine::nsq_scatter(DeviceLogs& L) {
+    const bool ord = false;  // (L0ARGS)
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_nsq_scatter<<<(uint32_t)((w.nslots + kScanTile - 1) / kScanTile), kBlock, 0, stream>>>(
+            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par, L.nsq_key);
+    }
+}
+
+int Engine::nsq_reserve(DeviceLogs& L) {
+    L.nsq_ok = false;
+    if (!nsq_list || !L.total_slots || L.total_slots / 64 + 64 >= (1ull << 32)) return CRDT_HIP_OK;
+    if (int rc = nsq_reserve_prefix(L)) return rc;
+    if (L.total_slots + 1 > L.nsq_cap) {  // (every slot an nsq item, at most)
+        dfree(L.nsq_par);
+        dfree(L.nsq_key);
+        L.nsq_cap = 0;
+        HIPCHK(dalloc(&L.nsq_par, L.total_slots + 1), "hipMalloc nsq list");
+        HIPCHK(dalloc(&L.nsq_key, L.total_slots + 1), "hipMalloc nsq keys");
+        L.nsq_cap = L.total_slots + 1;
+        gen_++;
+    }
+    return CRDT_HIP_OK;
+}
+
+int Engine::nsq_launch(DeviceLogs& L) {
+    if (!nsq_list || !L.nsq_pre || L.nsq_cap < L.total_slots + 1 ||
+        L.nsq_pre_cap < L.total_slots / 64 + 65)
+        return CRDT_HIP_OK;  // (nsq_reserve found no room: the merge gathers from the columns)
+    nsq_count_scan(L);
+    nsq_scatter(L);
+    HIPCHK(hipGetLastError(), "nsq list launch");
+    L.nsq_ok = true;
     return CRDT_HIP_OK;
 }
 

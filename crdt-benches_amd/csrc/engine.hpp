@@ -119,6 +119,11 @@ struct DeviceLogs {
     uint64_t* nsq_key = nullptr;   // beside nsq_par: the items' keys (k_runs reads a non-seq
                                    //   head's key there instead of gathering it)
     uint64_t nsq_items = 0;
+    // the list matches the current slot layout and contents (plan() clears it; the arrays keep
+    // their capacity, so that a replica rebuilds its list inside a captured replay)
+    bool nsq_ok = false;
+    uint64_t nsq_cap = 0, nsq_pre_cap = 0, nsq_sums_cap = 0;
+    uint32_t* nsq_sums = nullptr;  // (scan scratch)
     void release();
     ~DeviceLogs() { release(); }
 };
@@ -218,8 +223,15 @@ public:
 
     // The compact nsq parent list of L (after its last plan; see DeviceLogs::nsq_par).
     int build_nsq(DeviceLogs& L);
+    int nsq_reserve_prefix(DeviceLogs& L);
+    void nsq_count_scan(DeviceLogs& L);
+    void nsq_scatter(DeviceLogs& L);
     // Wave::nocon of every wave of L from its nsq_items and the contraction parameter.
     void set_contraction(DeviceLogs& L) const;
+    // The compact nsq list of logs that change (replicas): room for every slot (nsq_reserve,
+    // may allocate), then the list built by launches alone (nsq_launch, capturable).
+    int nsq_reserve(DeviceLogs& L);
+    int nsq_launch(DeviceLogs& L);
     void apply_shape_hints(DeviceLogs& L) const;
     static constexpr double kNoconShare = 0.75;
 

@@ -705,6 +705,9 @@ int replica_merge(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_t* l
     std::vector<DocInfo> docs{DocInfo{r.n, r.vis_bytes}};
     rc = E.plan(r.logs, docs);
     if (rc) return rc;
+    // the compact list of the non-seq items, rebuilt for the decoded contents (as a resident
+    // batch's input encoding builds it once)
+    if ((rc = E.nsq_reserve(r.logs)) || (rc = E.nsq_launch(r.logs))) return rc;
     return E.merge(r.logs, Engine::TEXT, digest, len, st, text, nullptr, cps);
 }
 
@@ -754,6 +757,8 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
         std::vector<DocInfo> docs{DocInfo{st.n_after, b_plan}};
         rc = E.plan(w.logs, docs);
         if (rc) return rc;
+        rc = E.nsq_reserve(w.logs);
+        if (rc) return rc;
         if (!E.plans_known(w.logs)) {
             st.known = false;  // the shape's plan was forgotten: learn it again below
         } else {
@@ -782,6 +787,7 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
                         hipSuccess)
                         rc = hip_fail(E, "copy update counters", hipGetLastError());
                 }
+                if (!rc) rc = E.nsq_launch(w.logs);  // (the decoded contents' nsq list)
                 if (!rc) rc = E.merge_async_enqueue(w.logs, m);
                 hipGraph_t g = nullptr;
                 const hipError_t ce = hipStreamEndCapture(s, &g);

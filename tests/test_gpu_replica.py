@@ -259,11 +259,22 @@ def test_resident_update_batch_rejects_bad_updates(ctx):
     ub.close()
 
 
+@pytest.mark.parametrize("nsq", [1, 0])
 @pytest.mark.parametrize("name", TRACES)
-def test_replay_closure_matches_golden(ctx, golden, py_trace, name):
+def test_replay_closure_matches_golden(ctx, golden, py_trace, name, nsq):
     """crdt_hip_replica_replay: the downstream closure (main.rs:63-69) in one call.  The first
     call learns the sizes, later ones merge right behind the decode (speculated sizes checked on
-    the device); every call must give the trace's document, and init must stay unchanged."""
+    the device); every call must give the trace's document, and init must stay unchanged.  With
+    nsq 1 (the default) every merge rebuilds the replica's compact list of the non-seq items
+    from the decoded contents (inside the captured closure), with 0 level 0 gathers them."""
+    ctx.set_param("nsq_list", nsq)
+    try:
+        _replay_closure(ctx, golden, py_trace, name)
+    finally:
+        ctx.set_param("nsq_list", 1)
+
+
+def _replay_closure(ctx, golden, py_trace, name):
     t = crdt_hip.Trace(trace_path(name))
     patches = [t.patch(i) for i in range(len(t))]
     up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
