@@ -975,9 +975,10 @@ def parse_args(argv=None):
     ap.add_argument("--stile-text", type=int, default=1, choices=[0, 1],
                     help="1: fused level 1 stages text from the tile segments (k_runs skips the "
                          "slot-order copy)")
-    ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1],
-                    help="1: resident batches carry the compact list of the non-seq items' parents "
-                         "(input encoding; k_classify streams it); 0: k_classify gathers them")
+    ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1, 2],
+                    help="1: resident batches (input encoding) and replicas of 2^22+ slots (every "
+                         "merge) carry the compact list of the non-seq items' parents and keys; "
+                         "2: every replica too; 0: the level-0 kernels gather them")
     ap.add_argument("--plain-companion", type=int, default=1, choices=[0, 1],
                     help="1: a companion line of the headline batch without the compact nsq list")
     ap.add_argument("--l1-group", type=int, default=0, choices=[0, 1, 2],

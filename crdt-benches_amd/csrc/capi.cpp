@@ -223,9 +223,9 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.l1_group = (uint32_t)value;
         return CRDT_HIP_OK;
     }
-    if (k == "nsq_list") {  // 1: batches get the compact nsq parent list (Engine::build_nsq)
-        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0 or 1");
-        ctx->eng.nsq_list = value == 1;
+    if (k == "nsq_list") {  // the compact nsq parent list (Engine::build_nsq, nsq_launch)
+        if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0, 1 or 2");
+        ctx->eng.nsq_list = (uint32_t)value;
         return 0;
     }
     if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)

@@ -3209,36 +3209,25 @@ __device__ __forceinline__ uint64_t chunk_nsq_bits(const L0Args& a, uint32_t gs)
     }
     return bits;
 }
-__global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt) {
+__global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt, uint64_t* mask) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c * 64ull >= a.nslots) return;
-    cnt[c] = (uint32_t)__popcll(chunk_nsq_bits(a, c * 64u));
+    const uint64_t b = chunk_nsq_bits(a, c * 64u);
+    cnt[c] = (uint32_t)__popcll(b);
+    mask[c] = b;
 }
 // The list itself: one workgroup per 4096-slot tile (16 slots per thread, k_classify's layout):
-// the tile's nsq items listed in LDS in slot order (a block scan of the per-thread counts), then
-// their parents and keys read by the whole block and written to the tile's range of the list as
-// consecutive words.
-__global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t* pre, uint32_t* out,
+// the tile's nsq items (k_nsq_count's masks) listed in LDS in slot order (a block scan of the
+// per-thread counts), then their parents and keys read by the whole block and written to the
+// tile's range of the list as consecutive words.
+__global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t* pre,
+                                                        const uint64_t* mask, uint32_t* out,
                                                         uint64_t* kout) {
     __shared__ uint32_t lds[kBlock / 64];
     __shared__ uint16_t lst[kScanTile];
     const uint32_t tile = blockIdx.x, t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
     uint32_t nsq = 0;
-    if (gs < a.nslots) {
-        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B
-        const uint4 q0 = cv[0], q1 = cv[1], q2 = cv[2];
-        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        const uint32_t CW[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                 q2.x, q2.y, q2.z, q2.w, 0u};
-        const uint32_t l0 = gs - doc.x, n = doc.y;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
-            const uint32_t c = ((CW[wd] >> sh) | (sh > 8 ? CW[wd + 1] << (32 - sh) : 0u)) & 0x00FFFFFFu;
-            const bool it = (l0 + (uint32_t)k - 1u) < n;
-            nsq |= (it && !(c & kSeqBit) ? 1u : 0u) << k;
-        }
-    }
+    if (gs < a.nslots) nsq = (uint32_t)(mask[gs >> 6] >> (gs & 63u)) & 0xFFFFu;
     uint32_t T;
     uint32_t i = block_excl_scan<kBlock / 64>((uint32_t)__popc(nsq), lds, T);
     for (; nsq; nsq &= nsq - 1u) lst[i++] = (uint16_t)(threadIdx.x * kScanItems + __builtin_ctz(nsq));
@@ -3318,7 +3307,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 // =============================================================================================
 void DeviceLogs::release() {
     dfree(parent); dfree(key); dfree(cp);
-    dfree(nsq_par); dfree(nsq_pre); dfree(nsq_key); dfree(nsq_sums);
+    dfree(nsq_par); dfree(nsq_pre); dfree(nsq_key); dfree(nsq_sums); dfree(nsq_mask);
     nsq_items = 0;
     nsq_ok = false;
     nsq_cap = nsq_pre_cap = nsq_sums_cap = 0;
@@ -4750,7 +4739,9 @@ int Engine::nsq_reserve_prefix(DeviceLogs& L) {
     const uint64_t nch = L.total_slots / 64 + 64;
     if (nch + 1 > L.nsq_pre_cap) {
         dfree(L.nsq_pre);
+        dfree(L.nsq_mask);
         L.nsq_pre_cap = 0;
+        HIPCHK(dalloc(&L.nsq_mask, nch + 1), "hipMalloc nsq masks");
         HIPCHK(dalloc(&L.nsq_pre, nch + 1), "hipMalloc nsq prefix");
         L.nsq_pre_cap = nch + 1;
         gen_++;  // (captured replays point at the old arrays)
@@ -4773,7 +4764,8 @@ void Engine::nsq_count_scan(DeviceLogs& L) {
     (void)hipMemsetAsync(L.nsq_pre, 0, (n + 1ull) * 4, stream);
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
-        k_nsq_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6));
+        k_nsq_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6),
+                                                                   L.nsq_mask + (w.slot0 >> 6));
     }
     k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, L.nsq_sums);
     k_scan_top<<<1, 1024, 0, stream>>>(L.nsq_sums, nb, L.nsq_pre, n);
@@ -4786,13 +4778,15 @@ void Engine::nsq_scatter(DeviceLogs& L) {
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
         k_nsq_scatter<<<(uint32_t)((w.nslots + kScanTile - 1) / kScanTile), kBlock, 0, stream>>>(
-            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_par, L.nsq_key);
+            a0, L.nsq_pre + (w.slot0 >> 6), L.nsq_mask + (w.slot0 >> 6), L.nsq_par, L.nsq_key);
     }
 }
 
 int Engine::nsq_reserve(DeviceLogs& L) {
     L.nsq_ok = false;
-    if (!nsq_list || !L.total_slots || L.total_slots / 64 + 64 >= (1ull << 32)) return CRDT_HIP_OK;
+    if (!nsq_list || (nsq_list == 1 && L.total_slots < kNsqReplicaSlots) || !L.total_slots ||
+        L.total_slots / 64 + 64 >= (1ull << 32))
+        return CRDT_HIP_OK;
     if (int rc = nsq_reserve_prefix(L)) return rc;
     if (L.total_slots + 1 > L.nsq_cap) {  // (every slot an nsq item, at most)
         dfree(L.nsq_par);
@@ -4807,7 +4801,8 @@ int Engine::nsq_reserve(DeviceLogs& L) {
 }
 
 int Engine::nsq_launch(DeviceLogs& L) {
-    if (!nsq_list || !L.nsq_pre || L.nsq_cap < L.total_slots + 1 ||
+    if (!nsq_list || (nsq_list == 1 && L.total_slots < kNsqReplicaSlots) || !L.nsq_pre ||
+        L.nsq_cap < L.total_slots + 1 ||
         L.nsq_pre_cap < L.total_slots / 64 + 65)
         return CRDT_HIP_OK;  // (nsq_reserve found no room: the merge gathers from the columns)
     nsq_count_scan(L);

@@ -124,6 +124,7 @@ struct DeviceLogs {
     bool nsq_ok = false;
     uint64_t nsq_cap = 0, nsq_pre_cap = 0, nsq_sums_cap = 0;
     uint32_t* nsq_sums = nullptr;  // (scan scratch)
+    uint64_t* nsq_mask = nullptr;  // (the nsq items of every 64-slot chunk, for the scatter)
     void release();
     ~DeviceLogs() { release(); }
 };
@@ -161,9 +162,12 @@ public:
     bool plan_shrink = false;  // test hook: enqueue with half the learnt plan (forces C_REPLAN)
     bool doctree_lds_max = false;  // experiment hook: k_doctree always takes the whole LDS
     bool fuse_text = true;         // k_doctree writes the text when it fits LDS (else k_expand)
-    // resident batches get the compact list of the non-seq items' parents (build_nsq); 0: the
-    // level-0 kernels gather the parent column instead (A/B)
-    bool nsq_list = true;
+    // the compact list of the non-seq items' parents and keys: 1 = resident batches (build_nsq)
+    // and replicas of at least kNsqReplicaSlots slots (rebuilt by every merge: below that size
+    // the rebuild's launches cost more than the gathers it saves, measured on the downstream
+    // closures), 2 = every replica too, 0 = never (level 0 gathers the columns)
+    uint32_t nsq_list = 1;
+    static constexpr uint64_t kNsqReplicaSlots = 1ull << 22;
     // run contraction of RGA waves: 0 = by the wave's input (no contraction when at least
     // kNoconShare of its items lack the previous-slot flag), 1 = always, 2 = never
     uint32_t contraction = 0;

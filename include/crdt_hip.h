@@ -141,12 +141,14 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * "tail_wave_div" (default 0; k: a merge of several waves ends with a wave of at most
  * max_wave_slots / k slots), "xcd_order" (default 1: XCD-aware tile order in level 0),
  * "stile_text" (default 1: the per-document merge stages text from the per-tile segments),
- * "nsq_list" (default 1: resident batches get the compact list of the parents and keys of the
- * items without the previous-slot flag), "contraction" (run contraction of RGA waves, decided
+ * "nsq_list" (the compact list of the parents and keys of the items without the previous-slot
+ * flag: 1 (default) = resident batches, and replicas of at least 2^22 slots, whose merges rebuild
+ * it; 2 = every replica too; 0 = never), "contraction" (run contraction of RGA waves, decided
  * when a batch is built or logs are uploaded: 0 = by the input (default: no contraction when at
  * least 3/4 of a wave's items lack the previous-slot flag), 1 = always, 2 = never), "l1_group"
  * (sibling grouping of the global level 1: 0 = by counting when the wave's largest document has
- * at most 2^20 runs, else by radix sorts (default), 1 = always counting, 2 = always radix sorts),
+ * at most 2^16 runs or the wave at most 2^23, else by radix sorts (default), 1 = always
+ * counting, 2 = always radix sorts),
  * "fuse_text"
  * (default 1).  Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);

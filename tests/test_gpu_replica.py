@@ -259,14 +259,15 @@ def test_resident_update_batch_rejects_bad_updates(ctx):
     ub.close()
 
 
-@pytest.mark.parametrize("nsq", [1, 0])
+@pytest.mark.parametrize("nsq", [2, 0])
 @pytest.mark.parametrize("name", TRACES)
 def test_replay_closure_matches_golden(ctx, golden, py_trace, name, nsq):
     """crdt_hip_replica_replay: the downstream closure (main.rs:63-69) in one call.  The first
     call learns the sizes, later ones merge right behind the decode (speculated sizes checked on
     the device); every call must give the trace's document, and init must stay unchanged.  With
-    nsq 1 (the default) every merge rebuilds the replica's compact list of the non-seq items
-    from the decoded contents (inside the captured closure), with 0 level 0 gathers them."""
+    nsq_list 2 every merge rebuilds the replica's compact list of the non-seq items from the
+    decoded contents (inside the captured closure; the default does so from 2^22 slots up), with
+    0 level 0 gathers them."""
     ctx.set_param("nsq_list", nsq)
     try:
         _replay_closure(ctx, golden, py_trace, name)
