@@ -22,10 +22,15 @@
 //     text.  Deletes change no order: the tombstone bits the decode set make those items weigh
 //     nothing.
 //
-// Anything else — a root whose key is not above every old key (a concurrent update), more than
-// kIncMax new items, a Fugue replica — falls back to a full merge (engine ORDER mode), which also
-// rebuilds the state.  Every fast-path merge is checked against the decode's counters (bytes and
-// codepoints of the visible text) by the host.
+// A root whose key is not above every old key (a concurrent update) takes its place from a search
+// of its parent's old subtree.  Fugue replicas (in-order: left children, the item, right children)
+// take the same path: a new right child of an old item goes right after it, a new left child right
+// before it while it has no left child (the resolver's local edits: a left child is only ever given
+// to the leftmost node of a right subtree), the forest's tour carries an item's place on the up arc
+// of its last left child, and runs are not contracted.  Anything else — more than kIncMax new
+// items, a Fugue root that needs a search — falls back to a full merge (engine ORDER mode), which
+// also rebuilds the state.  Every fast-path merge is checked against the decode's counters (bytes
+// and codepoints of the visible text) by the host.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -60,6 +65,8 @@ constexpr uint32_t kIncScan = 1u << 16;
 constexpr bool kIncRuns = CRDT_INC_RUNS;  // contract runs of new items before the tour
 constexpr uint32_t kCpMaskI = 0x001FFFFFu;
 constexpr uint32_t kDelBitI = 0x00800000u;
+constexpr uint32_t kLeftBitI = 0x00200000u;  // (Fugue) a left child
+constexpr uint64_t kLeftKeyI = 1ull << 48;   // (Fugue) the key bit of a left child
 
 // device counters (u64)
 enum ICtl { I_MAXKEY = 0, I_MAXKEY_B, I_N };  // the largest key, two slots (calls alternate)
@@ -85,6 +92,7 @@ struct IncArgs {
     uint64_t* hres;             // host-mapped result {flag, bytes, codepoints, call number}
     uint64_t* tsp;              // (CRDT_INC_PROFILE) phase timestamps of the forest, or null
     uint64_t call;              // this call's number (a stale result block is detected)
+    const uint32_t* hasl;       // (Fugue) 1 bit per old slot: it has a left child
 };
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32i_t;
@@ -140,7 +148,7 @@ __device__ __forceinline__ bool root_before(uint32_t aj, uint32_t pj, uint64_t k
 // the forest's own dependent loads so that the splice does not wait for them)
 // Q: items per thread (m <= Q * kIncThreads); the caller picks the smallest instance that holds
 // the batch, so that no per-item loop runs over empty slots
-template <uint32_t Q>
+template <uint32_t Q, bool FG>
 __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint32_t* red,
                                            uint32_t& flag, uint32_t& nhard, uint32_t& found,
                                            const uint32_t (&sl)[kSpliceRanks],
@@ -189,9 +197,22 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             plc[q] = 0;
             if (i >= m) continue;
             keys[i] = kk[q];
-            kmax = max(kmax, kk[q]);
+            const uint64_t kv = kk[q] & ~kLeftKeyI;  // (the key without the Fugue side bit)
+            kmax = max(kmax, kv);
             uint32_t li;
-            if (pp[q] <= n0) {  // a root: after its old parent, ahead of the parent's old children
+            if (FG && pp[q] <= n0) {
+                // a Fugue root: a right child goes right after its old parent, a left child right
+                // before it (the parent must have no old left child); right roots first at a
+                // shared anchor (PR 1 before 0), each side by key; a root that an old sibling may
+                // precede is not searched for (F_KEY: the full merge)
+                li = m;
+                const bool left = (kk[q] & kLeftKeyI) != 0ull;
+                const uint32_t rp = a.rank[pp[q]];
+                A[i] = left ? rp - 1u : rp;
+                PR[i] = left ? 0u : 1u;
+                if (kv <= maxkey0 || (left && (rp == 0u || ((a.hasl[pp[q] >> 5] >> (pp[q] & 31u)) & 1u))))
+                    bad |= (uint32_t)F_KEY;
+            } else if (pp[q] <= n0) {  // a root: after its old parent, ahead of the parent's old children
                 li = m;
                 A[i] = PR[i] = a.rank[pp[q]];
                 if (kk[q] <= maxkey0) {
@@ -346,7 +367,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
 #pragma unroll
         for (int k = 0; k < (int)Q; ++k) {
             const uint32_t i = i0 + (uint32_t)k;
-            const bool cont = kIncRuns && i < m && i > 0 && lp[i] == i - 1u &&
+            const bool cont = kIncRuns && !FG && i < m && i > 0 && lp[i] == i - 1u &&
                               start[i] - start[i - 1u] == 1u;
             h[k] = (i < m && !cont) ? i : 0u;
             mx = max(mx, h[k]);
@@ -370,7 +391,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             run = max(run, h[k]);
             if (i >= m) continue;
             hd[i] = (uint16_t)run;
-            const bool next_cont = kIncRuns && i + 1u < m && lp[i + 1u] == i &&
+            const bool next_cont = kIncRuns && !FG && i + 1u < m && lp[i + 1u] == i &&
                                    start[i + 1u] - start[i] == 1u;
             if (!next_cont) rend[run] = (uint16_t)i;
         }
@@ -378,19 +399,32 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     __syncthreads();
     // ---- Euler tour of the run forest: down(h) = 2h, up(h) = 2h + 1 (h a run head or V = m),
     // end E; succ in the low 16 bits, the arc's weight (a run's length on its down arc) high ----
+    // (Fugue: an item's place is on its down arc when it has no left child, else on the up arc of
+    // its last left child; fl[q] bit 0: x has a left child, bit 1: x is its parent's last one)
     const uint32_t E = 2u * m + 2u, V = m;
+    uint32_t fl[Q];
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t x = t + (uint32_t)q * kIncThreads;
+        fl[q] = 0;
         if (x >= m || hd[x] != x) continue;
         const uint32_t e = rend[x];
         const uint32_t c0 = start[e], c1 = start[e + 1u];
         const uint32_t sd = c1 > c0 ? 2u * cs[c0] : 2u * x + 1u;
         const uint32_t p = lp[x], pos = start[p] + rk[q];
         const uint32_t pr = p == V ? V : hd[p];  // (a parent is always the last item of its run)
-        const uint32_t su = pos + 1u < start[p + 1u] ? 2u * cs[pos + 1u] : 2u * pr + 1u;
-        tour[2u * x] = sd | ((e - x + 1u) << 16);
-        tour[2u * x + 1u] = su;
+        const bool more = pos + 1u < start[p + 1u];
+        const uint32_t su = more ? 2u * cs[pos + 1u] : 2u * pr + 1u;
+        if (FG) {
+            const bool hasl = c1 > c0 && (keys[cs[c0]] & kLeftKeyI);
+            const bool lastl = p != V && (keys[x] & kLeftKeyI) && !(more && (keys[cs[pos + 1u]] & kLeftKeyI));
+            fl[q] = (hasl ? 1u : 0u) | (lastl ? 2u : 0u);
+            tour[2u * x] = sd | ((hasl ? 0u : 1u) << 16);
+            tour[2u * x + 1u] = su | ((lastl ? 1u : 0u) << 16);
+        } else {
+            tour[2u * x] = sd | ((e - x + 1u) << 16);
+            tour[2u * x + 1u] = su;
+        }
     }
     if (t == 0) {
         const uint32_t c0 = start[V], c1 = start[V + 1u];
@@ -440,12 +474,33 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
 #pragma unroll
     for (int q = 0; q < (int)Q; ++q) {
         const uint32_t x = t + (uint32_t)q * kIncThreads;
-        if (x < m) {
+        if (x >= m) continue;
+        if (FG) {
+            // the place of x (no left child), of x's parent (x its last left child)
+            if (!(fl[q] & 1u)) {
+                const uint32_t px = m - (tour[2u * x] >> 16);
+                os[px] = n0 + 1u + x;
+                oa[px] = 0u;
+            }
+            if (fl[q] & 2u) {
+                const uint32_t px = m - (tour[2u * x + 1u] >> 16);
+                os[px] = n0 + 1u + lp[x];
+                oa[px] = 0u;
+            }
+        } else {
             const uint32_t h = hd[x];
             const uint32_t px = m - (tour[2u * h] >> 16) + (x - h);
             os[px] = n0 + 1u + x;
-            oa[px] = lp[x] == V ? A[x] : 0u;  // (a root's anchor; inside a subtree 0)
+            oa[px] = 0u;
         }
+    }
+    __syncthreads();
+    // a root's anchor at the first place of its subtree (its own place in RGA order; in Fugue
+    // order its leftmost descendant's); the max-scan carries it over the subtree
+#pragma unroll
+    for (int q = 0; q < (int)Q; ++q) {
+        const uint32_t x = t + (uint32_t)q * kIncThreads;
+        if (x < m && lp[x] == V) oa[m - (tour[2u * x] >> 16)] = A[x];
     }
     __syncthreads();
     {
@@ -678,13 +733,20 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
         for (int q = 0; q < (int)kSpliceRanks; ++q) sl[q] = kb + q < k1 ? a.seq[kb + q] : 0u;
     }
     uint32_t cwq[kSpliceRanks];
-    if (a.m) {
+    if (a.m && a.hasl) {  // (Fugue)
         if (a.m <= kIncThreads)
-            inc_forest<1>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<1, true>(a, lds, red, flag, nhard, found, sl, cwq);
         else if (a.m <= 2u * kIncThreads)
-            inc_forest<2>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<2, true>(a, lds, red, flag, nhard, found, sl, cwq);
         else
-            inc_forest<kIncMax / kIncThreads>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<kIncMax / kIncThreads, true>(a, lds, red, flag, nhard, found, sl, cwq);
+    } else if (a.m) {
+        if (a.m <= kIncThreads)
+            inc_forest<1, false>(a, lds, red, flag, nhard, found, sl, cwq);
+        else if (a.m <= 2u * kIncThreads)
+            inc_forest<2, false>(a, lds, red, flag, nhard, found, sl, cwq);
+        else
+            inc_forest<kIncMax / kIncThreads, false>(a, lds, red, flag, nhard, found, sl, cwq);
     } else {
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);
@@ -723,11 +785,21 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     }
 }
 
+// (Fugue) The left-child bits of the parents of the left children among slots [lo, hi].
+__global__ __launch_bounds__(256) void k_inc_hasl(const uint32_t* parent, const uint8_t* cp,
+                                                  uint32_t lo, uint32_t hi, uint32_t* hasl) {
+    for (uint64_t s = lo + blockIdx.x * 256ull + threadIdx.x; s <= hi; s += 256ull * gridDim.x)
+        if (cp_word(cp, (uint32_t)s) & kLeftBitI) {
+            const uint32_t p = parent[s];
+            atomicOr(&hasl[p >> 5], 1u << (p & 31u));
+        }
+}
+
 // The largest sibling key of items 1..n (state rebuild) into ctl[slot].
 __global__ __launch_bounds__(256) void k_inc_maxkey(const uint64_t* key, uint32_t n, uint64_t* dst) {
     uint64_t mx = 0;
     for (uint64_t s = 1 + blockIdx.x * 256ull + threadIdx.x; s <= n; s += 256ull * gridDim.x)
-        mx = max(mx, key[s]);
+        mx = max(mx, key[s] & ~kLeftKeyI);  // (without the Fugue side bit)
 #pragma unroll
     for (int o = 32; o; o >>= 1) {
         const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(mx >> 32), o) << 32) |
@@ -791,14 +863,33 @@ int inc_reserve(Engine& E, IncState& s, uint64_t items, uint64_t bytes) {
             s.valid = false;
             return ifail(E, "incremental order arrays", e);
         }
+        // (Fugue) the left-child bits, kept too
+        uint32_t* h0 = nullptr;
+        const uint64_t hw = cap / 32 + 1, hw_old = s.cap ? s.cap / 32 + 1 : 0;
+        e = dalloc(&h0, hw);
+        if (e == hipSuccess) e = hipMemsetAsync(h0, 0, hw * 4, E.stream);
+        if (e == hipSuccess && hw_old)
+            e = hipMemcpyAsync(h0, s.hasl, hw_old * 4, hipMemcpyDeviceToDevice, E.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(E.stream);
+        if (e != hipSuccess) {
+            dfree(q0);
+            dfree(q1);
+            dfree(r0);
+            dfree(r1);
+            dfree(h0);
+            s.valid = false;
+            return ifail(E, "incremental left-child bits", e);
+        }
         dfree(s.seq[0]);
         dfree(s.seq[1]);
         dfree(s.rank[0]);
         dfree(s.rank[1]);
+        dfree(s.hasl);
         s.seq[0] = q0;
         s.seq[1] = q1;
         s.rank[0] = r0;
         s.rank[1] = r1;
+        s.hasl = h0;
         s.cur = 0;
         s.cap = cap;
     }
@@ -851,7 +942,17 @@ IncArgs make_args(Replica& r, IncState& s, uint32_t n0, uint32_t m) {
     a.ctl = s.ctl;
     a.hres = s.dres;
     a.call = ++s.calls;
+    a.hasl = r.logs.fugue ? s.hasl : nullptr;  // (selects the Fugue forest)
     return a;
+}
+
+// (Fugue) set the left-child bits of the parents of the left children among slots [lo, hi].
+int inc_hasl(Engine& E, Replica& r, IncState& s, uint32_t lo, uint32_t hi) {
+    if (!r.logs.fugue || hi < lo) return CRDT_HIP_OK;
+    k_inc_hasl<<<std::max<uint32_t>(1, std::min<uint32_t>(grid_for(hi - lo + 1u, 256), 1024)), 256, 0,
+                 E.stream>>>(r.logs.parent, r.logs.cp, lo, hi, s.hasl);
+    ICHK(hipGetLastError(), "left-child bits");
+    return CRDT_HIP_OK;
 }
 
 // CRDT_INC_PROFILE=1: per call, the kernel's device time (events), the forest's phases and the
@@ -952,6 +1053,10 @@ int inc_rebuild(Engine& E, Replica& r, IncState& s) {
     const uint64_t next = s.calls + 1;
     k_inc_maxkey<<<std::max<uint32_t>(1, std::min<uint32_t>(grid_for(r.n, 256), 1024)), 256, 0, st>>>(
         r.logs.key, r.n, s.ctl + I_MAXKEY + ((next & 1u) ^ 1u));
+    if (r.logs.fugue) {  // the left-child bits of the whole log
+        ICHK(hipMemsetAsync(s.hasl, 0, (s.cap / 32 + 1) * 4, st), "clear left-child bits");
+        if ((rc = inc_hasl(E, r, s, 1u, r.n))) return rc;
+    }
     IncArgs a = make_args(r, s, r.n, 0);  // m = 0: the splice copies the order and sets the ranks
     rc = inc_run(E, s, a, true);
     if (rc) return rc;
@@ -975,6 +1080,7 @@ IncState::~IncState() {
     dfree(tsp);
     for (hipEvent_t e : pev)
         if (e) (void)hipEventDestroy(e);
+    dfree(hasl);
     dfree(lb_flag);
     dfree(lb_agg);
     dfree(lb_inc);
@@ -989,16 +1095,6 @@ int replica_merge_inc(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_
     if (rc) return rc;
     IncState& s = r.inc;
     if (path) *path = 0;
-    if (r.logs.fugue) {  // (the fast path covers RGA order only)
-        std::vector<uint8_t> t;
-        uint64_t len = 0, dig = 0, c = 0;
-        rc = replica_merge(E, r, text ? &t : nullptr, &len, &dig, nullptr, &c);
-        if (rc) return rc;
-        if (text) *text = std::move(t);
-        if (bytes) *bytes = len;
-        if (cps) *cps = c;
-        return CRDT_HIP_OK;
-    }
     ICHK(hipSetDevice(E.device), "hipSetDevice");
     // (the look-back packs {bytes, codepoints} as two u32 halves: a text of 4 GiB or more merges
     // in full)
@@ -1018,6 +1114,8 @@ int replica_merge_inc(Engine& E, Replica& r, std::vector<uint8_t>* text, uint64_
                 s.valid = false;
                 return CRDT_HIP_EBADLOG;
             }
+            // (Fugue) the new left children's parents have one now
+            if ((rc = inc_hasl(E, r, s, a.n0 + 1u, a.n0 + a.m))) return rc;
             s.cur ^= 1;
             s.n = r.n;
             if (path) *path = 1;

@@ -29,6 +29,9 @@ struct IncState {
     // every workgroup while the splices of other workgroups write the new ranks, so they are
     // two arrays (rank[cur] read, rank[cur ^ 1] written)
     uint32_t* rank[2] = {nullptr, nullptr};
+    // (Fugue replicas) 1 bit per slot: the item has a left child (a new left child of an old
+    // item goes right before it only while it has none)
+    uint32_t* hasl = nullptr;
     uint32_t* lb_flag = nullptr;     // per tile of the order: look-back status, aggregate and
     uint64_t* lb_agg = nullptr;      //   inclusive prefix of the text (incr.hip inc_lookback)
     uint64_t* lb_inc = nullptr;

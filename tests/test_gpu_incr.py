@@ -15,6 +15,7 @@ import crdt_hip
 from conftest import trace_path
 from test_gpu_merge import to_anchor
 from test_gpu_replica import trace_updates
+from test_fugue import fugue_updates, to_anchor as fugue_anchor
 
 pytestmark = pytest.mark.gpu
 
@@ -142,7 +143,7 @@ def test_deletes_only_and_many_roots(ctx, oracle):
     assert cps == len(text.decode())
 
 
-def test_incremental_state_survives_clone_and_fugue_takes_the_full_path(ctx, oracle):
+def test_incremental_state_survives_clone_and_fugue_state_starts_with_a_full_merge(ctx, oracle):
     t, patches, updates = trace_updates("sveltecomponent")
     r = crdt_hip.Replica(ctx)
     r.apply_updates(updates[:5000])
@@ -153,7 +154,7 @@ def test_incremental_state_survives_clone_and_fugue_takes_the_full_path(ctx, ora
     r.apply_updates(updates[5000:5200])
     assert r.merge_inc()[2] == 1
     assert r.merge_inc(text=True)[3] == c.merge_inc(text=True)[3]
-    # Fugue replicas always merge in full (the fast path orders RGA trees only)
+    # a Fugue replica's first call builds its state (full merge)
     up = crdt_hip.OpLog(fugue=True)
     up.insert(0, "fugue text")
     f = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
@@ -224,3 +225,63 @@ def test_concurrent_roots_placed_by_search_match_oracle(ctx, oracle):
         paths.append(path)
         assert text == oracle.merge(to_anchor(host.arrays())), f"checkpoint {c}"
     assert paths[0] == 0 and paths[1:].count(1) >= len(paths) - 5, paths
+
+
+@pytest.mark.parametrize("name,K", [("sveltecomponent", 300), ("automerge-paper", 1000)])
+def test_fugue_incremental_len_matches_oracle(ctx, oracle, name, K):
+    """Fugue replicas on the incremental path: the trace replayed on a Fugue upstream, its
+    version-2 updates applied to a Fugue replica K patches at a time, len() after each batch.
+    Local edits give a new item either a right child's place (right after its old parent) or a
+    left child's place under the leftmost node of a right subtree (right before that node, which
+    has no left child): every batch after the first takes the fast path (path 1) unless it holds
+    more than 4096 items, and every checkpoint is the oracle's in-order merge of the same log."""
+    t, up, updates = fugue_updates(name)
+    r = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
+    host = crdt_hip.OpLog(fugue=True)
+    paths = []
+    for c, i in enumerate(range(0, len(updates), K)):
+        batch = updates[i:i + K]
+        n_before = r.info()[0]
+        r.apply_updates(batch)
+        for u in batch:
+            host.apply_update(u)
+        cps, nb, path, text = r.merge_inc(text=True)
+        paths.append(path if r.info()[0] - n_before <= 4096 else "big")
+        assert (cps, nb) == (len(text.decode()), len(text))
+        assert text == oracle.merge_fugue(fugue_anchor(host.arrays())), f"checkpoint {c}"
+    assert text.decode() == t.end_content
+    assert paths[0] in (0, "big") and all(p in (1, "big") for p in paths[1:]), paths
+
+
+def test_fugue_left_child_of_a_node_with_left_children_falls_back(ctx, oracle):
+    """A remote Fugue insert that makes a new left child of an old item which already has one
+    (its place would need a search of the old left subtree) merges in full, and correctly; the
+    next local edit is incremental again."""
+    a = crdt_hip.OpLog(fugue=True)
+    h = crdt_hip.OpLog(fugue=True)  # the host log fed the same (patched) updates
+    r = crdt_hip.Replica(ctx, crdt_hip.OpLog(fugue=True))
+
+    def ship(u):
+        r.apply_updates([u])
+        h.apply_update(u)
+
+    a.insert(0, "abc")
+    ship(a.encode_from(0))
+    assert r.merge_inc(text=True)[3] == b"abc"
+    v = a.version()
+    a.insert(0, "x")  # a left child of 'a' (the leftmost node)
+    ship(a.encode_from(v))
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == b"xabc"
+    v = a.version()
+    a.insert(0, "y")  # a left child of 'x' ...
+    u = bytearray(a.encode_from(v))
+    struct.pack_into("<I", u, 24, 1)  # ... re-parented under 'a' (id 1), which has 'x' already
+    ship(bytes(u))
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 0 and text == oracle.merge_fugue(fugue_anchor(h.arrays())) == b"yxabc"
+    v = h.version()
+    h.insert(len(text), "!")
+    r.apply_updates([h.encode_from(v)])
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == oracle.merge_fugue(fugue_anchor(h.arrays())) == b"yxabc!"
