@@ -1100,17 +1100,44 @@ __device__ __forceinline__ uint32_t rs_parent(const TreeArgs& a, uint32_t g, boo
     return (p == kNil || bad) ? a.R : p;
 }
 
-// Digit histograms of every pass of sort A (LDS, then one global add per bin and block).
+// Digit histograms of every pass of sort A (LDS, then one global add per bin and block).  Each
+// thread counts 16 consecutive runs at a time and adds a digit's count to LDS only when the digit
+// changes: the high digits of a wave's parents are nearly constant when documents are small (all
+// parents of a document share them), and per-run LDS atomics on one bin serialise.
+constexpr uint32_t kRsHistRun = 16;
 __global__ __launch_bounds__(kBlock) void k_rs_hist(TreeArgs a, RsArgs r) {
     __shared__ uint32_t h[kRsMaxPass * kRsBins];
     for (uint32_t i = threadIdx.x; i < r.npass * kRsBins; i += kBlock) h[i] = 0;
     __syncthreads();
     uint32_t bad_any = 0;
-    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < a.R; g += gridDim.x * kBlock) {
-        bool bad;
-        const uint32_t pv = rs_parent(a, g, bad);
-        bad_any |= bad ? 1u : 0u;
-        for (uint32_t k = 0; k < r.npass; ++k) atomicAdd(&h[k * kRsBins + ((pv >> (8u * k)) & 255u)], 1u);
+    const uint32_t nch = (a.R + kRsHistRun - 1u) / kRsHistRun;
+    for (uint32_t c = blockIdx.x * kBlock + threadIdx.x; c < nch; c += gridDim.x * kBlock) {
+        uint32_t prev[kRsMaxPass], cnt[kRsMaxPass];
+#pragma unroll
+        for (int k = 0; k < (int)kRsMaxPass; ++k) {
+            prev[k] = 0;
+            cnt[k] = 0;
+        }
+        const uint32_t g0 = c * kRsHistRun, g1 = min(a.R, g0 + kRsHistRun);
+        for (uint32_t g = g0; g < g1; ++g) {
+            bool bad;
+            const uint32_t pv = rs_parent(a, g, bad);
+            bad_any |= bad ? 1u : 0u;
+#pragma unroll
+            for (int k = 0; k < (int)kRsMaxPass; ++k) {
+                if ((uint32_t)k >= r.npass) break;
+                const uint32_t d = (pv >> (8u * k)) & 255u;
+                if (cnt[k] && d != prev[k]) {
+                    atomicAdd(&h[k * kRsBins + prev[k]], cnt[k]);
+                    cnt[k] = 0;
+                }
+                prev[k] = d;
+                ++cnt[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < (int)kRsMaxPass; ++k)
+            if (cnt[k]) atomicAdd(&h[k * kRsBins + prev[k]], cnt[k]);
     }
     if (bad_any) atomicOr(&a.ctl[C_ERR], 1u);
     __syncthreads();
