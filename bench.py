@@ -878,7 +878,7 @@ def upstream_inc_workload(args) -> int:
         expect.append(up.log.visible_len())
     init = crdt_hip.HipMerge.from_str(t.start_content).log
 
-    def loop(incremental, per_ck):
+    def loop(incremental, per_ck, check_text=False):
         r = crdt_hip.Replica(ctx, init if init.view().n else None)
         ok, paths = True, 0
         for c, ub in enumerate(chunks):
@@ -891,13 +891,17 @@ def upstream_inc_workload(args) -> int:
                 cps, nb, _ = r.merge_len()
             per_ck.append(time.perf_counter() - t0)
             ok &= cps == expect[c]
+        if check_text:  # (untimed: the final document itself, not only its length)
+            text = r.merge_inc(text=True)[3] if incremental else r.merge()[0]
+            ok &= text == t.end_content.encode()
         r.close()
         return ok, paths
 
     res = {}
+    text_ok = True
     for mode in ("incremental", "full"):
-        for _ in range(args.warmup):
-            loop(mode != "full", [])
+        for w in range(args.warmup):
+            text_ok &= loop(mode != "full", [], check_text=(w == 0))[0]
         comm.barrier()
         per_ck: list = []
         t0 = time.perf_counter()
@@ -913,21 +917,24 @@ def upstream_inc_workload(args) -> int:
                      "len_ms_median": float(np.median(per_ck)) * 1e3,
                      "incremental_calls": paths // max(1, args.steps)}
     inc, full = res["incremental"], res["full"]
-    ok = inc["ok"] and full["ok"]
+    ok = inc["ok"] and full["ok"] and (text_ok or not args.warmup)
     if rank == 0:
         out = {
             "metric": METRIC, "value": len(patches) / (inc["ms_per_step"] / 1e3),
             "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": inc["ms_per_step"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32", "data": "trace",
-            "config": {"workload": f"upstream (main.rs:28-36) with len() every {K} patches: "
-                                   "apply the chunk's updates to a device replica + len()",
+            "config": {"workload": f"extension workload (not in the reference, which asserts "
+                                   f"len() once after the loop): upstream (main.rs:28-36) with "
+                                   f"len() every {K} patches: apply the chunk's updates to a "
+                                   "device replica + len()",
                        "trace": name, "patches": len(patches), "checkpoints": len(chunks),
                        "updates_resident": True},
             "incremental": inc, "full": full,
             "len_speedup_mean": full["len_ms_mean"] / inc["len_ms_mean"],
             "len_speedup_median": full["len_ms_median"] / inc["len_ms_median"],
             "lens_ok": bool(ok),
+            "final_text_ok": bool(text_ok) if args.warmup else None,
         }
         print(json.dumps(out), flush=True)
     comm.close()
