@@ -20,10 +20,13 @@ import csv, collections, re, sys
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 n = collections.Counter()
 for r in csv.DictReader(open(sys.argv[1])):
-    k = re.split(r"[<(]", r["Kernel_Name"].replace("crdt::(anonymous namespace)::", "").replace("void ", ""), 1)[0]
+    nm = r["Kernel_Name"].replace("crdt::(anonymous namespace)::", "").replace("void ", "")
+    # (template instances apart: k_rs_pass<uint4, 0, ...> vs <uint2, 1, ...>)
+    k = re.split(r"\(", nm, 1)[0].replace("HIP_vector_type<unsigned int, ", "u").replace("u>", "")[:48]
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    n[k] += 1  # (rows: dispatches x counters of the pass)
 for k in sorted(agg, key=lambda k: -sum(agg[k].values())):
     if k.startswith("k_"):
-        print(f"  {k:16s} " + " ".join(f"{c}={v:.4g}" for c, v in sorted(agg[k].items())))
+        print(f"  {k:48s} n={n[k]} " + " ".join(f"{c}={v:.4g}" for c, v in sorted(agg[k].items())))
 PY
 done
