@@ -445,9 +445,11 @@ def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> di
     waves = max(1, stats[0]["waves"])
     per_wave = {k: launches[k] / waves for k in launches}
     radix = bool(launches.get("sortb"))
-    # text mode (waves without run contraction on the global level 1): the re-walk stage is
+    # text mode (the global level 1's first walk stages the text): the re-walk stage is
     # k_tcopy + k_walk_ovf (+ k_doctotals), 4 launches per k_walk1 launch instead of 2
     text_mode = bool(launches.get("walk1")) and launches.get("walk2", 0) == 4 * launches["walk1"]
+    # waves without run contraction: every live item is a run
+    nocon = runs > 0.5 * slots
 
     def alg_bytes(k):
         per_slot, per_run, per_text = KERNEL_BYTES[k]
@@ -455,13 +457,16 @@ def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> di
             per_text = 0.0  # expansion left to k_expand: no text in or out of k_doctree
         if radix and level1_run_bytes(k, per_wave, text_mode) is not None:
             per_run = level1_run_bytes(k, per_wave, text_mode)
-        if text_mode:
+        if nocon:
             if k == "classify":
                 per_run = 0.0   # no contraction: no parents read, no jump bits
             elif k == "runs":
                 per_run = 32.0  # parent + key in; head, prefix, parent, key out
-            elif k == "walk1":
-                per_run, per_text = 32.0, 1.0  # the 32-byte record line; the staged text out
+        if text_mode:
+            if k == "walk1":
+                # the 32-byte record line; the staged text out (+ in from the slot-order text
+                # when runs are longer than the record carries)
+                per_run, per_text = 32.0, 1.0 if nocon else 2.0
             elif k == "walk2":
                 per_run, per_text = 0.5, 2.0   # splitter words; staged text in, document out
         return per_slot * slots + per_run * runs + per_text * text_bytes

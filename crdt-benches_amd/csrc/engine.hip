@@ -918,22 +918,20 @@ struct TreeArgs {
     uint8_t* text;
     uint64_t text_cap;
     uint32_t align;  // per-document output alignment (16 for text, 1 for order)
-    // text mode of the grid-wide level 1 (waves without run contraction: every run is one item):
-    // a run's bytes (one codepoint) ride in the second line of its record, k_walk1 writes each
-    // sublist's text in walk order to its splitter's kWalkTmp-byte slot of wtmp, k_tcopy moves
-    // the slots to the document once the splitters are ranked, and k_walk_ovf walks the few
-    // sublists with more text again for the rest
-    uint32_t walk_text;
+    // text mode of the grid-wide level 1: the second line of a run's record holds its place in
+    // the slot-order text (and its bytes, up to kWalkText of them), k_walk1 writes each sublist's
+    // text in walk order to its splitter's 2^wtmp_log2-byte slot of wtmp, k_tcopy moves the slots
+    // to the document once the splitters are ranked, and k_walk_ovf walks the few sublists with
+    // more text again for the rest
+    uint32_t walk_text, wtmp_log2;
     const uint8_t* sbytes;
     const uint32_t* r_head;
     const uint32_t* chunk_doc;
     uint32_t log2c;          // chunk_doc granularity (slots per entry, log2)
     uint8_t* wtmp;
-    uint32_t* ovf;           // splitters whose sublists carry more than kWalkTmp bytes
+    uint32_t* ovf;           // splitters whose sublists carry more text than their slot
 };
-constexpr uint32_t kWalkText = 4;      // (one codepoint)
-constexpr uint32_t kWalkTmpLog2 = 7;   // 128 bytes per sublist: ~4x the mean at 64 arcs per sublist
-constexpr uint32_t kWalkTmp = 1u << kWalkTmpLog2;
+constexpr uint32_t kWalkText = 4;  // (one codepoint: every run of a wave without contraction)
 
 // The second line of a run record in text mode: {its place in the slot-order text, its bytes
 // packed little-endian when there are at most kWalkText of them}.
@@ -1765,16 +1763,18 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
                 const uint32_t w = r[q].y;
                 if constexpr (TEXT) {
                     ++runs;
-                    if (w > kWalkText) {
-                        atomicOr(&a.ctl[C_ERR], 8u);  // (runs are single items here)
-                    } else {
-                        // append the run's bytes to the slot while they fit in it
+                    // append the run's bytes to the slot while they fit in it: up to kWalkText
+                    // from the record, longer runs from the slot-order text
+                    const uint32_t sb = 1u << a.wtmp_log2;
+                    if (w && sum[q] < sb) {
                         uint32_t* slot = reinterpret_cast<uint32_t*>(
-                            a.wtmp + ((uint64_t)(base + q) << kWalkTmpLog2));
-                        for (uint32_t b = 0; b < w; ++b) {
+                            a.wtmp + ((uint64_t)(base + q) << a.wtmp_log2));
+                        const uint32_t n = min(w, sb - sum[q]);
+                        const uint8_t* src = a.sbytes + x[q].x;
+                        for (uint32_t b = 0; b < n; ++b) {
                             const uint32_t o = sum[q] + b;
-                            if (o >= kWalkTmp) break;
-                            acc[q] |= ((x[q].y >> (8u * b)) & 255u) << (8u * (o & 3u));
+                            const uint32_t c = w <= kWalkText ? (x[q].y >> (8u * b)) & 255u : src[b];
+                            acc[q] |= c << (8u * (o & 3u));
                             if ((o & 3u) == 3u) {
                                 slot[o >> 2] = acc[q];
                                 acc[q] = 0;
@@ -1796,8 +1796,8 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
         if (base + q >= a.S) continue;
         a.swn[base + q] = make_uint2(sum[q], nxt[q]);
         // (the partial last dword of the slot; the bytes past the text are never copied)
-        if (TEXT && (sum[q] & 3u) && sum[q] < kWalkTmp)
-            reinterpret_cast<uint32_t*>(a.wtmp + ((uint64_t)(base + q) << kWalkTmpLog2))[sum[q] >> 2] = acc[q];
+        if (TEXT && (sum[q] & 3u) && sum[q] < (1u << a.wtmp_log2))
+            reinterpret_cast<uint32_t*>(a.wtmp + ((uint64_t)(base + q) << a.wtmp_log2))[sum[q] >> 2] = acc[q];
     }
     if constexpr (TEXT) {
         const uint32_t tot = wave_sum(runs);
@@ -1996,7 +1996,7 @@ __device__ __forceinline__ uint32_t splitter_doc(const TreeArgs& a, uint32_t s, 
     return s >= a.Sreg ? s - a.Sreg : a.chunk_doc[a.r_head[v] >> a.log2c];
 }
 
-// Text mode, once the splitters are ranked: every sublist's staged text (up to kWalkTmp bytes)
+// Text mode, once the splitters are ranked: every sublist's staged text (up to its slot's bytes)
 // to its place in its document, one thread per splitter, dword stores where the destination is
 // aligned; sublists with more text are listed for k_walk_ovf.  The sublist's whole range is
 // bounds-checked here (its weight is the walk's).
@@ -2013,9 +2013,10 @@ __global__ __launch_bounds__(kBlock) void k_tcopy(TreeArgs a, const uint32_t* __
         atomicOr(&a.ctl[C_ERR], 8u);
         return;
     }
-    if (n > kWalkTmp) a.ovf[atomicAdd(&a.ctl[C_NOVF], 1u)] = s;  // (room for every splitter)
-    const uint32_t m = min(n, kWalkTmp);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtmp + ((uint64_t)s << kWalkTmpLog2));
+    const uint32_t sb = 1u << a.wtmp_log2;
+    if (n > sb) a.ovf[atomicAdd(&a.ctl[C_NOVF], 1u)] = s;  // (room for every splitter)
+    const uint32_t m = min(n, sb);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtmp + ((uint64_t)s << a.wtmp_log2));
     uint8_t* dst = a.text + a.toff[d] + o;
     auto byte_at = [&](uint32_t i) { return (src[i >> 2] >> (8u * (i & 3u))) & 255u; };
     const uint32_t head = min(m, (4u - (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u);
@@ -2030,11 +2031,10 @@ __global__ __launch_bounds__(kBlock) void k_tcopy(TreeArgs a, const uint32_t* __
     for (; i < m; ++i) dst[i] = (uint8_t)byte_at(i);
 }
 
-// Text mode: the sublists k_tcopy listed, walked again; each writes the bytes past its first
-// kWalkTmp.
+// Text mode: the sublists k_tcopy listed, walked again; each writes the bytes past its slot.
 __global__ __launch_bounds__(kBlock) void k_walk_ovf(TreeArgs a, const uint32_t* __restrict__ spref) {
     if (replan(a.ctl)) return;
-    const uint32_t n = a.ctl[C_NOVF];
+    const uint32_t n = a.ctl[C_NOVF], sb = 1u << a.wtmp_log2;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const uint32_t s = a.ovf[i];
         uint32_t v, nxt, off = 0, steps = 0;
@@ -2045,10 +2045,12 @@ __global__ __launch_bounds__(kBlock) void k_walk_ovf(TreeArgs a, const uint32_t*
             const uint4 r = a.rec[v << 1];
             if (!up) {
                 const uint32_t w = r.y;
-                if (w <= kWalkText && off + w > kWalkTmp) {  // (k_walk1 flagged longer runs)
-                    const uint32_t b0 = off >= kWalkTmp ? 0u : kWalkTmp - off;
-                    const uint32_t x = a.rec[(v << 1) + 1u].y;
-                    for (uint32_t b = b0; b < w; ++b) out[off + b] = (uint8_t)(x >> (8u * b));
+                if (w && off + w > sb) {
+                    const uint32_t b0 = off >= sb ? 0u : sb - off;
+                    const uint4 x = a.rec[(v << 1) + 1u];
+                    const uint8_t* src = a.sbytes + x.x;
+                    for (uint32_t b = b0; b < w; ++b)
+                        out[off + b] = w <= kWalkText ? (uint8_t)(x.y >> (8u * b)) : src[b];
                 }
                 off += w;
             }
@@ -3976,6 +3978,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
     // items), from records that carry their place in the slot-order text (two lines per run)
     a.walk_text = walk_text(w, ord, p) ? 1u : 0u;
     a.rsh = a.walk_text;
+    a.wtmp_log2 = wtmp_log2_;
     if (l1_csr_) {  // (chosen by run_wave, which sized the scratch)
         CsrArgs c_{cstart_, child_, defer_, bigl_};
         const uint32_t nb = (uint32_t)((R + kScanTile - 1) / kScanTile);
@@ -4058,14 +4061,15 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         MARK(S_SORTB);
     }
     // two walkers per thread on waves without contraction, one on contracted waves (§5b)
-    const uint32_t ilp = a.walk_text ? 2u : 1u;
+    const uint32_t ilp = w.nocon ? 2u : 1u;
     const uint32_t gW = grid_for(((uint64_t)S + ilp - 1) / ilp);
-    if (a.walk_text) {
-        HIPCHK(hipMemsetAsync(ctl_ + C_NOVF, 0, 4, s), "clear overflow count");
+    if (a.walk_text) HIPCHK(hipMemsetAsync(ctl_ + C_NOVF, 0, 4, s), "clear overflow count");
+    if (a.walk_text && ilp == 2)
         k_walk1<2, true><<<gW, kBlock, 0, s>>>(a);
-    } else {
+    else if (a.walk_text)
+        k_walk1<1, true><<<gW, kBlock, 0, s>>>(a);
+    else
         k_walk1<1, false><<<gW, kBlock, 0, s>>>(a);
-    }
     MARK(S_WALK1);
     SupArgs sa{};
     sa.S = S;
@@ -4218,17 +4222,26 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
     l1_csr_ = l1_group == 1 || (l1_group == 0 && (p.rmax <= kCsrDocRuns || p.R <= kCsrWaveRuns));
     if (!p.lds1 && !l1_csr_ && (rc = ensure_radix(p.R))) return rc;
     if (!p.lds1 && l1_csr_ && (rc = ensure_csr(p.R))) return rc;
-    if (walk_text(w, ord, p) && (uint64_t)Sreg + w.ndocs > cap_wtmp_) {
-        // a kWalkTmp-byte text slot per splitter (+ slack for k_tcopy's dword reads) and the
-        // overflow list
-        dfree(wtmp_);
-        dfree(ovf_);
-        cap_wtmp_ = 0;
+    if (walk_text(w, ord, p)) {
+        // a text slot per splitter of ~4x the mean sublist text (128 B .. 4 KiB; + slack for
+        // k_tcopy's dword reads) and the overflow list
         const uint64_t ns = (uint64_t)Sreg + w.ndocs;
-        HIPCHK(dalloc(&wtmp_, (ns << kWalkTmpLog2) + 64), "hipMalloc sublist text");
-        HIPCHK(dalloc(&ovf_, ns), "hipMalloc sublist overflow list");
-        cap_wtmp_ = ns;
-        gen_++;
+        wtmp_log2_ = std::min<uint32_t>(12u, std::max<uint32_t>(
+                         7u, ceil_log2(4ull * hctl[C_WTOTAL] / std::max<uint64_t>(1, ns) + 1)));
+        if ((ns << wtmp_log2_) + 64 > cap_wtmp_) {
+            dfree(wtmp_);
+            cap_wtmp_ = 0;
+            HIPCHK(dalloc(&wtmp_, (ns << wtmp_log2_) + 64), "hipMalloc sublist text");
+            cap_wtmp_ = (ns << wtmp_log2_) + 64;
+            gen_++;
+        }
+        if (ns > cap_ovf_) {
+            dfree(ovf_);
+            cap_ovf_ = 0;
+            HIPCHK(dalloc(&ovf_, ns), "hipMalloc sublist overflow list");
+            cap_ovf_ = ns;
+            gen_++;
+        }
     }
     if (p.R > rows) {
         // more runs than rows: the run records again, now that they fit (k_runs only reads

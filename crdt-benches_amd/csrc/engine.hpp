@@ -286,9 +286,11 @@ private:
              *bigl_ = nullptr, *scan_sums_ = nullptr;  // counting-path scratch (engine.hip k_count)
     uint64_t cap_csr_ = 0;
     bool l1_csr_ = false;      // the last global level 1 grouped siblings by counting
-    uint8_t* wtmp_ = nullptr;  // text mode: the first kWalkTmp bytes of every sublist's text
-    uint64_t cap_wtmp_ = 0;    // (splitters)
-    uint32_t* ovf_ = nullptr;  // text mode: splitters whose sublist holds more than kWalkTmp bytes
+    uint8_t* wtmp_ = nullptr;  // text mode: the first 2^wtmp_log2_ bytes of every sublist's text
+    uint64_t cap_wtmp_ = 0;    // (bytes)
+    uint32_t wtmp_log2_ = 7;
+    uint32_t* ovf_ = nullptr;  // text mode: splitters whose sublist holds more than its slot
+    uint64_t cap_ovf_ = 0;
     uint32_t rs_npass_ = 0, rs_npassB_ = 0;
     uint4* rec_ = nullptr;
     uint2* swn_ = nullptr;     // per splitter {sublist weight, next splitter}
@@ -347,7 +349,14 @@ private:
     int ensure_events(std::vector<hipEvent_t>& ev, size_t n);
     L1Plan plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord, bool force_global) const;
     // the global level 1 of a text-mode wave without run contraction: k_walk2 writes the text
-    static bool walk_text(const Wave& w, bool ord, const L1Plan& p) { return !p.lds1 && !ord && w.nocon; }
+    // text written by the first walk (grid-wide level 1, TEXT mode; CRDT_WALK_TEXT_ALL 0: only on
+    // waves without contraction, the others by k_walk2 + k_expand)
+#ifndef CRDT_WALK_TEXT_ALL
+#define CRDT_WALK_TEXT_ALL 1
+#endif
+    static bool walk_text(const Wave& w, bool ord, const L1Plan& p) {
+        return !p.lds1 && !ord && (w.nocon || CRDT_WALK_TEXT_ALL);
+    }
     int clock_mark(StageClock& c, int stage);
     // The launches of one wave, in stream order.
     int launch_runs(DeviceLogs& L, const Wave& w, bool ord);
