@@ -1770,10 +1770,18 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
                         uint32_t* slot = reinterpret_cast<uint32_t*>(
                             a.wtmp + ((uint64_t)(base + q) << a.wtmp_log2));
                         const uint32_t n = min(w, sb - sum[q]);
-                        const uint8_t* src = a.sbytes + x[q].x;
-                        for (uint32_t b = 0; b < n; ++b) {
+                        // (longer runs: the slot-order text a dword at a time)
+                        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.sbytes);
+                        uint32_t wd = x[q].y, sa = x[q].x;
+                        for (uint32_t b = 0; b < n; ++b, ++sa) {
+                            uint32_t c;
+                            if (w <= kWalkText) {
+                                c = (wd >> (8u * b)) & 255u;
+                            } else {
+                                if (b == 0 || (sa & 3u) == 0) wd = src[sa >> 2];
+                                c = (wd >> (8u * (sa & 3u))) & 255u;
+                            }
                             const uint32_t o = sum[q] + b;
-                            const uint32_t c = w <= kWalkText ? (x[q].y >> (8u * b)) & 255u : src[b];
                             acc[q] |= c << (8u * (o & 3u));
                             if ((o & 3u) == 3u) {
                                 slot[o >> 2] = acc[q];
