@@ -4068,8 +4068,9 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);
         MARK(S_SORTB);
     }
-    // two walkers per thread on waves without contraction, one on contracted waves (§5b)
-    const uint32_t ilp = w.nocon ? 2u : 1u;
+    // two walkers per thread on waves without contraction in text mode, else one (§5b; the
+    // grids of both walks are sized by it)
+    const uint32_t ilp = a.walk_text && w.nocon ? 2u : 1u;
     const uint32_t gW = grid_for(((uint64_t)S + ilp - 1) / ilp);
     if (a.walk_text) HIPCHK(hipMemsetAsync(ctl_ + C_NOVF, 0, 4, s), "clear overflow count");
     if (a.walk_text && ilp == 2)
