@@ -199,8 +199,8 @@ constexpr uint32_t kRecTree = 1u << 31;  // k_runs record of a head with two row
 //    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
 //  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
 //    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG;
-//  * the parents themselves, in slot order, to the tile's plist segment: every nsq item is a run
-//    head, and k_runs reads its parent there (coalesced) instead of gathering it.
+//  * the parents themselves (as wave slots), in slot order, to the tile's plist segment: every
+//    nsq item is a run head, and k_runs reads its parent there (coalesced) instead of gathering it.
 // The stream part reads 3 bytes per slot and waits for one round trip; the parent part is one
 // more round trip at the end of the block, hidden behind the other blocks' streams.
 __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
@@ -386,13 +386,16 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         for (int j = 0; j < 4; ++j) {
             if (o[j] == 0xFFFFu) continue;
             const uint32_t oi = o[j] & 0x7FFFu;
-            if (!cl) pl[t + (uint32_t)j * kBlock] = p[j];
             const uint2 d = ldoc[oi / kScanItems];
+            // the parent's index in its document (the compact list holds wave slots); plist
+            // gets the wave slot, as the list has it
+            const uint32_t pj = cl ? p[j] - d.x : p[j];
+            if (!cl) pl[t + (uint32_t)j * kBlock] = d.x + pj;
             const bool left = (o[j] >> 15) != 0u;
-            if (p[j] > d.y || p[j] == t0 + oi - d.x || (left && p[j] == 0u)) {
+            if (pj > d.y || pj == t0 + oi - d.x || (left && pj == 0u)) {
                 bad = 1u;  // (the document start has no left children)
             } else {
-                const uint32_t ps = d.x + p[j];
+                const uint32_t ps = d.x + pj;
                 if (ps / kScanTile == tile)
                     atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
                 else
@@ -601,6 +604,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     __shared__ uint16_t lnpf[kBlock];  // non-seq items of the tile before every thread
     __shared__ uint16_t ldp[FUGUE ? kBlock : 1];  // Fugue: two-row heads before every thread
     __shared__ uint16_t ldm[FUGUE ? kBlock : 1];  //   and every thread's two-row head bits
+    __shared__ uint16_t lmap[FUGUE ? 1 : kBlock]; // (prefetch) list entry -> head rank in tile
     const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
@@ -612,6 +616,27 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     // plist segment k_classify wrote
     const uint32_t nlo = a.nsq_par ? a.nsq_pre[tile * (kScanTile / 64)] : 0u;
     const uint32_t* pls = a.nsq_par ? a.nsq_par + nlo : a.plist + (uint64_t)tile * kScanTile;
+    // (RGA, contracted, compact list) the tile's first kBlock list entries are prefetched, one per
+    // thread: the parent slot and the key, then the parent's head record and tile prefix, so that
+    // the per-head phase below finds a non-seq head's parent run and key in registers instead of
+    // waiting for two dependent gathers
+#ifndef CRDT_RUNS_PREFETCH
+#define CRDT_RUNS_PREFETCH 1
+#endif
+    const bool pf = CRDT_RUNS_PREFETCH && !FUGUE && !a.nocon && a.nsq_par != nullptr;
+    uint32_t pf_ps = 0, pf_tp = 0;
+    uint4 pf_hr = make_uint4(0, 0, 0, 0);
+    uint64_t pf_key = 0;
+    bool pf_on = false;
+    if (pf) {
+        const uint32_t nhi = a.nsq_pre[min(tile * kScanTile + kScanTile, a.nslots) >> 6];
+        if (nlo + threadIdx.x < nhi) {
+            pf_ps = a.nsq_par[nlo + threadIdx.x];
+            pf_key = a.nsq_key[nlo + threadIdx.x];
+            pf_on = true;
+        }
+    }
+    if (!FUGUE) lmap[threadIdx.x] = 0xFFFFu;
     if (gs < a.nslots) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
@@ -622,6 +647,10 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         lnsq[threadIdx.x] = (uint16_t)nsq;
     }
     ldoc[threadIdx.x] = doc;
+    if (pf_on && pf_ps < a.nslots) {  // (a parent out of range is flagged; see below)
+        pf_hr = a.hrec[pf_ps >> 6];
+        pf_tp = a.tile_hw[pf_ps / kScanTile].x;
+    }
     // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
     // offset is known: thread t's destination dword needs source dwords t and t+1 whatever the
     // offset's alignment (the segment is kTileBytes long, so both are in bounds).
@@ -679,12 +708,15 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     uint32_t m = lo + 4u * threadIdx.x;
     {
         uint32_t r = ex >> 16, p = ex & 0xFFFFu;
+        uint32_t q = offq + incq - cq;  // (the thread's first list entry)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             if (hm & (1u << j)) {
+                if (!FUGUE && pf && ((nsq >> j) & 1u) && q < kBlock) lmap[q] = (uint16_t)r;
                 rec[r++] = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p |
                            ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
             }
+            q += (nsq >> j) & 1u;
             p += (uint32_t)(nib >> (4 * j)) & 15u;
         }
     }
@@ -708,8 +740,35 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             for (uint32_t g = max(hi, lo); g < D + tw; ++g) a.sbytes[g] = src[g - D];
     }
     __syncthreads();
-    // one thread per head: every gather of a stage issued before any is used
     const uint32_t tbase = tile * kScanTile;
+    // the prefetched list entries that are run heads: one per thread, by list index
+    if (!FUGUE && pf_on && lmap[threadIdx.x] != 0xFFFFu) {
+        const uint32_t i = lmap[threadIdx.x];
+        const uint32_t rv = rec[i];
+        const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
+        const uint32_t rho = pre.x + i;
+        const uint2 dc = ldoc[li >> 4];
+        const uint32_t pj = pf_ps - dc.x;
+        uint32_t ps = pf_ps;
+        uint4 hr = pf_hr;
+        uint32_t tp = pf_tp;
+        if (pj > dc.y || pj == g - dc.x) {  // (flagged by k_classify: under the document start;
+                                            //  also every parent slot out of range)
+            ps = dc.x;
+            hr = a.hrec[ps >> 6];
+            tp = a.tile_hw[ps / kScanTile].x;
+        }
+        const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
+        const uint32_t b = ps & 63u;
+        const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
+        a.r_head[rho] = g;
+        a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
+        if (rho < a.cap_rows) {
+            a.r_parent[rho] = tp + hr.z + (uint32_t)__popcll(hb & mask) - 1u;
+            a.r_key[rho] = pf_key;
+        }
+    }
+    // one thread per head (the rest): every gather of a stage issued before any is used
     for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
         const uint32_t rv = rec[i];
         const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
@@ -725,6 +784,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         // (resident batches) its key from the same index of the key list, a seq head's gathered
         const uint32_t nw = lnsq[li >> 4];
         const uint32_t lix = lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u));
+        if (!FUGUE && pf && !sq && !root && lix < kBlock) continue;  // (done above)
         const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
         if (!FUGUE && a.nocon) {
             // no contraction: the run's parent and key from the columns (heads are every slot of
@@ -749,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
             }
             continue;
         }
-        uint32_t p = (!sq && !root) ? pls[lix] : 0u;
+        uint32_t ps = (!sq && !root) ? pls[lix] : 0u;  // (the parent as a wave slot)
         a.r_head[rho] = g;
         a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
         if (two) {
@@ -761,8 +821,8 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         if (sq) {
             pr = rho - 1u;  // the parent is the slot before the head: the previous run's last row
         } else if (!root) {
-            if (p > dc.y || p == g - dc.x) p = 0;  // flagged by k_classify
-            const uint32_t ps = dc.x + p;
+            const uint32_t p = ps - dc.x;
+            if (p > dc.y || p == g - dc.x) ps = dc.x;  // flagged by k_classify
             const uint4 hr = a.hrec[ps >> 6];
             const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
             const uint32_t hl = hr.z;
@@ -3272,7 +3332,9 @@ __global__ __launch_bounds__(kBlock) void k_nsq_scatter(L0Args a, const uint32_t
     const uint32_t o = pre[tile * (kScanTile / 64)];
     for (uint32_t k = threadIdx.x; k < T; k += kBlock) {
         const uint32_t g = t0 + lst[k];
-        out[o + k] = a.in_parent[g];
+        // the parent as a wave slot (its document's base + its index; the consumers recover the
+        // index for their range checks)
+        out[o + k] = a.docs[a.chunk_doc[g >> a.log2m]].x + a.in_parent[g];
         kout[o + k] = a.in_key[g];
     }
 }
