@@ -604,7 +604,6 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     __shared__ uint16_t lnpf[kBlock];  // non-seq items of the tile before every thread
     __shared__ uint16_t ldp[FUGUE ? kBlock : 1];  // Fugue: two-row heads before every thread
     __shared__ uint16_t ldm[FUGUE ? kBlock : 1];  //   and every thread's two-row head bits
-    __shared__ uint16_t lmap[FUGUE ? 1 : kBlock]; // (prefetch) list entry -> head rank in tile
     const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
@@ -616,27 +615,6 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     // plist segment k_classify wrote
     const uint32_t nlo = a.nsq_par ? a.nsq_pre[tile * (kScanTile / 64)] : 0u;
     const uint32_t* pls = a.nsq_par ? a.nsq_par + nlo : a.plist + (uint64_t)tile * kScanTile;
-    // (RGA, contracted, compact list) the tile's first kBlock list entries are prefetched, one per
-    // thread: the parent slot and the key, then the parent's head record and tile prefix, so that
-    // the per-head phase below finds a non-seq head's parent run and key in registers instead of
-    // waiting for two dependent gathers
-#ifndef CRDT_RUNS_PREFETCH
-#define CRDT_RUNS_PREFETCH 1
-#endif
-    const bool pf = CRDT_RUNS_PREFETCH && !FUGUE && !a.nocon && a.nsq_par != nullptr;
-    uint32_t pf_ps = 0, pf_tp = 0;
-    uint4 pf_hr = make_uint4(0, 0, 0, 0);
-    uint64_t pf_key = 0;
-    bool pf_on = false;
-    if (pf) {
-        const uint32_t nhi = a.nsq_pre[min(tile * kScanTile + kScanTile, a.nslots) >> 6];
-        if (nlo + threadIdx.x < nhi) {
-            pf_ps = a.nsq_par[nlo + threadIdx.x];
-            pf_key = a.nsq_key[nlo + threadIdx.x];
-            pf_on = true;
-        }
-    }
-    if (!FUGUE) lmap[threadIdx.x] = 0xFFFFu;
     if (gs < a.nslots) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
         hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
@@ -647,10 +625,6 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         lnsq[threadIdx.x] = (uint16_t)nsq;
     }
     ldoc[threadIdx.x] = doc;
-    if (pf_on && pf_ps < a.nslots) {  // (a parent out of range is flagged; see below)
-        pf_hr = a.hrec[pf_ps >> 6];
-        pf_tp = a.tile_hw[pf_ps / kScanTile].x;
-    }
     // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
     // offset is known: thread t's destination dword needs source dwords t and t+1 whatever the
     // offset's alignment (the segment is kTileBytes long, so both are in bounds).
@@ -708,15 +682,12 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     uint32_t m = lo + 4u * threadIdx.x;
     {
         uint32_t r = ex >> 16, p = ex & 0xFFFFu;
-        uint32_t q = offq + incq - cq;  // (the thread's first list entry)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             if (hm & (1u << j)) {
-                if (!FUGUE && pf && ((nsq >> j) & 1u) && q < kBlock) lmap[q] = (uint16_t)r;
                 rec[r++] = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p |
                            ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
             }
-            q += (nsq >> j) & 1u;
             p += (uint32_t)(nib >> (4 * j)) & 15u;
         }
     }
@@ -741,34 +712,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     }
     __syncthreads();
     const uint32_t tbase = tile * kScanTile;
-    // the prefetched list entries that are run heads: one per thread, by list index
-    if (!FUGUE && pf_on && lmap[threadIdx.x] != 0xFFFFu) {
-        const uint32_t i = lmap[threadIdx.x];
-        const uint32_t rv = rec[i];
-        const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
-        const uint32_t rho = pre.x + i;
-        const uint2 dc = ldoc[li >> 4];
-        const uint32_t pj = pf_ps - dc.x;
-        uint32_t ps = pf_ps;
-        uint4 hr = pf_hr;
-        uint32_t tp = pf_tp;
-        if (pj > dc.y || pj == g - dc.x) {  // (flagged by k_classify: under the document start;
-                                            //  also every parent slot out of range)
-            ps = dc.x;
-            hr = a.hrec[ps >> 6];
-            tp = a.tile_hw[ps / kScanTile].x;
-        }
-        const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
-        const uint32_t b = ps & 63u;
-        const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
-        a.r_head[rho] = g;
-        a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
-        if (rho < a.cap_rows) {
-            a.r_parent[rho] = tp + hr.z + (uint32_t)__popcll(hb & mask) - 1u;
-            a.r_key[rho] = pf_key;
-        }
-    }
-    // one thread per head (the rest): every gather of a stage issued before any is used
+    // one thread per head: every gather of a stage issued before any is used
     for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
         const uint32_t rv = rec[i];
         const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
@@ -784,7 +728,6 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         // (resident batches) its key from the same index of the key list, a seq head's gathered
         const uint32_t nw = lnsq[li >> 4];
         const uint32_t lix = lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u));
-        if (!FUGUE && pf && !sq && !root && lix < kBlock) continue;  // (done above)
         const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
         if (!FUGUE && a.nocon) {
             // no contraction: the run's parent and key from the columns (heads are every slot of
@@ -1158,44 +1101,34 @@ __device__ __forceinline__ uint32_t rs_parent(const TreeArgs& a, uint32_t g, boo
     return (p == kNil || bad) ? a.R : p;
 }
 
-// Digit histograms of every pass of sort A (LDS, then one global add per bin and block).  Each
-// thread counts 16 consecutive runs at a time and adds a digit's count to LDS only when the digit
-// changes: the high digits of a wave's parents are nearly constant when documents are small (all
-// parents of a document share them), and per-run LDS atomics on one bin serialise.
-constexpr uint32_t kRsHistRun = 16;
+// Digit histograms of every pass of sort A (LDS, then one global add per bin and block).  A wave
+// whose 64 runs share a digit adds them with one LDS atomic: the high digits of the parents are
+// nearly constant over a wave when documents are small (all parents of a document share them),
+// and 64 per-lane atomics on one bin serialise.
 __global__ __launch_bounds__(kBlock) void k_rs_hist(TreeArgs a, RsArgs r) {
     __shared__ uint32_t h[kRsMaxPass * kRsBins];
     for (uint32_t i = threadIdx.x; i < r.npass * kRsBins; i += kBlock) h[i] = 0;
     __syncthreads();
     uint32_t bad_any = 0;
-    const uint32_t nch = (a.R + kRsHistRun - 1u) / kRsHistRun;
-    for (uint32_t c = blockIdx.x * kBlock + threadIdx.x; c < nch; c += gridDim.x * kBlock) {
-        uint32_t prev[kRsMaxPass], cnt[kRsMaxPass];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t end = (a.R + 63u) & ~63u;  // (whole waves in every round: the ballots below)
+    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < end; g += gridDim.x * kBlock) {
+        const bool valid = g < a.R;
+        bool bad = false;
+        const uint32_t pv = valid ? rs_parent(a, g, bad) : 0u;
+        bad_any |= bad ? 1u : 0u;
+        const uint64_t vm = __ballot(valid);
 #pragma unroll
         for (int k = 0; k < (int)kRsMaxPass; ++k) {
-            prev[k] = 0;
-            cnt[k] = 0;
-        }
-        const uint32_t g0 = c * kRsHistRun, g1 = min(a.R, g0 + kRsHistRun);
-        for (uint32_t g = g0; g < g1; ++g) {
-            bool bad;
-            const uint32_t pv = rs_parent(a, g, bad);
-            bad_any |= bad ? 1u : 0u;
-#pragma unroll
-            for (int k = 0; k < (int)kRsMaxPass; ++k) {
-                if ((uint32_t)k >= r.npass) break;
-                const uint32_t d = (pv >> (8u * k)) & 255u;
-                if (cnt[k] && d != prev[k]) {
-                    atomicAdd(&h[k * kRsBins + prev[k]], cnt[k]);
-                    cnt[k] = 0;
-                }
-                prev[k] = d;
-                ++cnt[k];
+            if ((uint32_t)k >= r.npass) break;
+            const uint32_t d = (pv >> (8u * k)) & 255u;
+            const uint32_t d0 = (uint32_t)__shfl((int)d, 0);  // (lane 0 is valid when any lane is)
+            if (__ballot(valid && d != d0) == 0ull) {
+                if (lane == 0u && vm) atomicAdd(&h[k * kRsBins + d0], (uint32_t)__popcll(vm));
+            } else if (valid) {
+                atomicAdd(&h[k * kRsBins + d], 1u);
             }
         }
-#pragma unroll
-        for (int k = 0; k < (int)kRsMaxPass; ++k)
-            if (cnt[k]) atomicAdd(&h[k * kRsBins + prev[k]], cnt[k]);
     }
     if (bad_any) atomicOr(&a.ctl[C_ERR], 1u);
     __syncthreads();
