@@ -16,6 +16,7 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
     echo "== pmc $ctr at 4096"
     timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/${R}_${ctr} -o run \
         -- python3 bench.py --steps 1 --warmup 1 --lanes 1 --no-cpu-baseline --companion-replicas 0 \
+        --plain-companion 0 \
         > gpurun_out/${R}_${ctr}.log 2>&1
     st=$?; echo "status $st"; tail -2 gpurun_out/${R}_${ctr}.log
     case $st in 0) ;; *) exit $st;; esac
