@@ -488,7 +488,7 @@ def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> di
 
     # the dominant kernel = the stage with the most device time per step (HIP events, summed
     # over its launches; with lanes a stage's launches can overlap another lane's)
-    timed = [k for k in stage_ns if launches[k]]
+    timed = [k for k in stage_ns if launches[k] and stage_ns[k] > 0]
     dom = max(timed, key=lambda k: stage_ns[k])
     out = roof(dom)
     out["traffic_source"] = PMC_FILE if out["traffic"] is not None else None
