@@ -1890,10 +1890,11 @@ __global__ __launch_bounds__(kBlock) void k_sup2(SupArgs a, const uint2* __restr
 // descriptor (document, first run, runs, text prefix, text bytes, output offset), so that a
 // k_doctree workgroup finds all of it in one round of loads.
 __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
-    __shared__ uint64_t st[1024];
-    __shared__ uint32_t sl[1024];
+    __shared__ uint64_t wt[16];  // per wave: its inclusive size total
+    __shared__ uint32_t wl[16];  // (leaves)
     if (replan(a.ctl)) return;
     const uint32_t wtotal = a.ctl[C_WTOTAL];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint64_t carry_t = 0;
     uint32_t carry_l = 0;
     const uint64_t am = (uint64_t)a.align - 1u;
@@ -1913,21 +1914,38 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
         }
         const uint64_t sz = ((uint64_t)tl + am) & ~am;
         const uint32_t nl = a.align > 1 ? (tl + kLeaf - 1u) / kLeaf : 0u;
-        st[threadIdx.x] = sz;
-        sl[threadIdx.x] = nl;
-        __syncthreads();
-        for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scans
-            const uint64_t xt = threadIdx.x >= o ? st[threadIdx.x - o] : 0ull;
-            const uint32_t xl = threadIdx.x >= o ? sl[threadIdx.x - o] : 0u;
-            __syncthreads();
-            st[threadIdx.x] += xt;
-            sl[threadIdx.x] += xl;
-            __syncthreads();
+        // inclusive scans: the leaves by DPP, the 64-bit sizes by shuffles, then across the waves
+        uint32_t il = wave_incl_scan(nl);
+        uint64_t it = sz;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = ((uint64_t)(uint32_t)__shfl_up((int)(it >> 32), o) << 32) |
+                               (uint32_t)__shfl_up((int)(uint32_t)it, o);
+            if (lane >= (uint32_t)o) it += y;
         }
+        if (lane == 63u) {
+            wt[wv] = it;
+            wl[wv] = il;
+        }
+        __syncthreads();
+        uint64_t bt = 0, ct = 0;
+        uint32_t bl = 0, cl = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            if (w < (int)wv) {
+                bt += wt[w];
+                bl += wl[w];
+            }
+            ct += wt[w];
+            cl += wl[w];
+        }
+        __syncthreads();
+        it += bt;
+        il += bl;
         if (d < a.ndocs) {
-            const uint64_t to = carry_t + st[threadIdx.x] - sz;
+            const uint64_t to = carry_t + it - sz;
             a.toff[d] = to;
-            a.loff[d] = carry_l + sl[threadIdx.x] - nl;
+            a.loff[d] = carry_l + il - nl;
             if (a.wg) {
                 const uint32_t k = a.rank[d];
                 const uint2 dr = a.docs[d];
@@ -1937,9 +1955,8 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
                                                t0 | (min(t1 - t0, 0xFFFu) << 20));
             }
         }
-        carry_t += st[1023];
-        carry_l += sl[1023];
-        __syncthreads();
+        carry_t += ct;
+        carry_l += cl;
     }
     if (threadIdx.x == 0) {
         a.toff[a.ndocs] = carry_t;
