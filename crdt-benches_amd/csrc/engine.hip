@@ -2225,10 +2225,6 @@ __device__ __forceinline__ uint64_t doc_key(const uint64_t* keys, uint32_t v) {
 // per lane (256-byte coalesced stores per wave): byte y belongs to the run of the last set bit
 // at or before y.  Returns false (nothing written) when the document does not fit.
 constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
-#ifndef CRDT_DOC_WARM
-#define CRDT_DOC_WARM 1
-#endif
-constexpr uint32_t kDocAhead = 256;  // (one workgroup per CU: the next round of documents)
 // Staging from the tiles' text segments (DocArgs::stile_text): the document's text is the part
 // [p0, p0 + tl) of the weight range of tiles t0 .. t0 + nt, each tile's share contiguous in its
 // kTileBytes segment, staged at offset (weight position - p0 + sh).  tpx = the tiles' weight
@@ -2439,13 +2435,6 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     // the plan check and the workgroup's document (written by k_doctotals in LPT order: document,
     // first run, runs, text offset / length) in one round of loads
     const uint4 wg = a.wg[2u * widx], wg1 = a.wg[2u * widx + 1u];
-#if CRDT_DOC_WARM
-    // the document kDocAhead descriptors on (the one this XCD's CUs will most likely take after
-    // this round of documents: the dispatcher deals workgroups to the XCDs in turn)
-    const bool warm = widx + kDocAhead < a.ndocs;
-    const uint4 wgn = warm ? a.wg[2u * (widx + kDocAhead)] : make_uint4(0, 0, 0, 0);
-    const uint4 wgn1 = warm ? a.wg[2u * (widx + kDocAhead) + 1u] : make_uint4(0, 0, 0, 0);
-#endif
     if (replan(a.ctl)) return;
     const uint32_t d = wg.x, base = wg.y, R = wg.z;
     (void)d;
@@ -2892,34 +2881,6 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     }
     const uint32_t wsum = wave_sum(runs);
     if ((t & 63u) == 0 && wsum) atomicAdd(&visited_lds, wsum);
-#if CRDT_DOC_WARM
-    // warm the caches with the next document's inputs while this one writes its text: one load
-    // per 64-byte line of its run columns and of its text's tile segments, off this document's
-    // critical path (the results only feed a sink, checked at the end)
-    uint32_t sink = 0;
-    if (warm) {
-        const uint32_t bn = wgn.y, rn = wgn.z;
-        const uint32_t l16 = (rn + 15u) >> 4, l8 = (rn + 7u) >> 3;  // 4-byte / 8-byte columns
-        const uint32_t t0n = wgn1.w & 0xFFFFFu, ntn = wgn1.w >> 20;
-        const uint32_t lt = a.stile_text ? min(kTileBytes, (wgn1.x / (ntn + 1u)) * 5u / 4u + 64u) >> 6 : 0u;
-        const uint32_t nl = 2u * l16 + l8 + lt * (ntn + 1u);
-        uint32_t x[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t i = t + (uint32_t)k * kDocThreads;
-            if (i >= nl) continue;
-            if (i < l16) x[k] = a.r_parent[bn + 16u * i];
-            else if (i < 2u * l16) x[k] = a.r_pstart[bn + 16u * (i - l16)];
-            else if (i < 2u * l16 + l8) x[k] = (uint32_t)a.r_key[bn + 8u * (i - 2u * l16)];
-            else {
-                const uint32_t j = i - 2u * l16 - l8, tt = j / lt;
-                x[k] = *reinterpret_cast<const uint32_t*>(a.stile + (uint64_t)(t0n + tt) * kTileBytes +
-                                                          64u * (j - tt * lt));
-            }
-        }
-        sink = x[0] ^ x[1] ^ x[2] ^ x[3];
-    }
-#endif
     __syncthreads();
     PROBE(9);
     if (a.text) {
@@ -2991,9 +2952,6 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
         if (visited_lds) atomicAdd(&a.ctl[C_VISITED], visited_lds);
         if (flags & 4u) atomicOr(&a.ctl[C_ERR], 2u);
     }
-#if CRDT_DOC_WARM
-    if (sink == 0x9E3779B9u && a.probe == 0xFFFFFFFFu) a.ctl[C_UNFUSED] = 0u;  // (never: a sink)
-#endif
 }
 
 // Level 1 in LDS: one workgroup per document descriptor (LPT order).  (A persistent form that
