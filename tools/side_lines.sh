@@ -20,3 +20,5 @@ run big1b_p0 --workload big1b --p-chain 0 --steps 3 --warmup 1
 run downstream --workload downstream --steps 20 --warmup 3
 run downstream_pcie --workload downstream --pcie --steps 10 --warmup 2
 run upstream_inc --workload upstream_inc --steps 3 --warmup 1
+run downstream_fugue --workload downstream --order fugue --steps 20 --warmup 3
+run shuffle --relabel shuffle --replicas 1024 --steps 3 --warmup 1 --companion-replicas 0 --plain-companion 0
