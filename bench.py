@@ -77,9 +77,9 @@ KERNEL_BYTES = {
     "place": (0.0, 32.0, 0.0),
     "link": (0.0, 28.0, 0.0),
     "sortb": (0.0, 0.0, 0.0),
-    "walk1": (0.0, 16.0, 0.0),
+    "walk1": (0.0, 24.0, 0.0),       # the run record in; its sublist offset and sublist out
     "rank": (0.0, 0.5, 0.0),
-    "walk2": (0.0, 20.0, 0.0),
+    "walk2": (0.0, 24.0, 0.0),       # k_roff: weight prefix, sublist, offset in; offset out
     "expand": (0.0, 16.0, 2.0),      # run prefix/weight/head/offset; slot-order text -> document
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out

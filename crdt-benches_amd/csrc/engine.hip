@@ -24,7 +24,7 @@
 //                                        by parent run: sibling groups contiguous and keyed
 //    k_rs_order / k_rs_big               sibling order: {run, next sibling} pairs, first children
 //    k_rs_pass (sort B) / k_rs_records   the pairs by run id; the run records in run order
-//    k_walk1 / k_sup1 / k_sup_step / k_sup2 / k_walk2
+//    k_walk1 / k_sup1 / k_sup_step / k_sup2 / k_roff (text mode: k_tcopy / k_walk_ovf)
 //                                        Euler-tour list ranking (sublists from splitters
 //                                        run id % M == 0, pointer jumping over the splitter
 //                                        lists); weighted so the rank is each run's byte offset
@@ -74,7 +74,7 @@ enum Ctl {
     C_RTOTAL = 3,   // runs of the wave
     C_WTOTAL = 4,   // weight total of the wave
     C_RMAX = 5,     // most runs in one document
-    C_VISITED = 6,  // runs visited by k_walk2 (text mode: k_walk1)
+    C_VISITED = 6,  // runs passed by k_walk1
     C_UNFUSED = 7,  // documents whose text k_doctree left to k_expand
     C_NBIG = 9,     // (CSR grouping) parents with more than 64 children
     C_NOVF = 10,    // (text mode) sublists listed by k_tcopy for k_walk_ovf
@@ -906,6 +906,7 @@ struct TreeArgs {
     uint32_t* ctl;
     uint2* swn;        // per splitter {sublist weight, next splitter}
     uint32_t* roff;
+    uint32_t* rsid;    // per run with visible bytes: the splitter whose sublist holds its down arc
     uint32_t* tlen;
     uint64_t* toff;
     uint32_t* loff;
@@ -1479,7 +1480,7 @@ __global__ __launch_bounds__(kBlock) void k_count(TreeArgs a, uint32_t* __restri
     if (p == kNil) return;
     if (p >= a.R || p == g) { atomicOr(&a.ctl[C_ERR], 1u); return; }
     // the child's place in its parent's segment comes with the count (roff is free until
-    // k_walk2), so that k_place needs no second atomic
+    // k_walk1), so that k_place needs no second atomic
     a.roff[g] = atomicAdd(&deg[p], 1u);
 }
 
@@ -1754,6 +1755,15 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
             if (!((live >> q) & 1u)) continue;
             if (!up[q]) {
                 const uint32_t w = r[q].y;
+                if constexpr (!TEXT) {
+                    // the run's offset inside its sublist and the sublist: k_roff adds the
+                    // sublist's offset once the splitters are ranked (no second walk)
+                    ++runs;
+                    if (w) {
+                        a.roff[v[q]] = sum[q];
+                        a.rsid[v[q]] = base + q;
+                    }
+                }
                 if constexpr (TEXT) {
                     ++runs;
                     // append the run's bytes to the slot while they fit in it: up to kWalkText
@@ -1800,10 +1810,9 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
         if (TEXT && (sum[q] & 3u) && sum[q] < (1u << a.wtmp_log2))
             reinterpret_cast<uint32_t*>(a.wtmp + ((uint64_t)(base + q) << a.wtmp_log2))[sum[q] >> 2] = acc[q];
     }
-    if constexpr (TEXT) {
-        const uint32_t tot = wave_sum(runs);
-        if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
-    }
+    // reachability: every run of the wave must be passed exactly once
+    const uint32_t tot = wave_sum(runs);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
 }
 
 // Ranking of the splitter lists (exclusive prefix of the sublist weights along each document's
@@ -1965,48 +1974,14 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     }
 }
 
-// Re-walk: every run passed on a down arc with visible bytes gets its offset inside its document
-// (for k_expand), and every run passed is counted (reachability).
-template <int ILP>
-__global__ __launch_bounds__(kBlock) void k_walk2(TreeArgs a, const uint32_t* __restrict__ spref) {
-    const uint32_t base = (blockIdx.x * kBlock + threadIdx.x) * ILP;
-    uint32_t v[ILP], off[ILP], live = 0, steps = 0, runs = 0, nxt;
-    bool up[ILP];
-#pragma unroll
-    for (int q = 0; q < ILP; ++q) {
-        const uint32_t s = base + q;
-        v[q] = 0;
-        up[q] = false;
-        off[q] = 0;
-        if (s < a.S && splitter_arc(a, s, v[q], up[q])) {
-            live |= 1u << q;
-            off[q] = spref[s];
-        }
-    }
-    while (live) {
-        uint4 r[ILP];
-#pragma unroll
-        for (int q = 0; q < ILP; ++q)
-            if ((live >> q) & 1u) r[q] = a.rec[v[q] << a.rsh];
-#pragma unroll
-        for (int q = 0; q < ILP; ++q) {
-            if (!((live >> q) & 1u)) continue;
-            if (!up[q]) {
-                const uint32_t w = r[q].y;
-                if (w) a.roff[v[q]] = off[q];  // (runs without visible bytes are never expanded)
-                off[q] += w;
-                ++runs;
-            }
-            if (!walk_next(r[q], a.log2m, v[q], up[q], nxt)) live &= ~(1u << q);
-        }
-        if (++steps > a.step_limit) {
-            atomicOr(&a.ctl[C_ERR], 2u);
-            break;
-        }
-    }
-    // reachability: every run of the wave must be visited exactly once
-    const uint32_t tot = wave_sum(runs);
-    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ctl[C_VISITED], tot);
+// Run offsets in their documents, once the splitters are ranked: the offset inside the sublist
+// (k_walk1) plus the sublist's, one thread per run (a streaming pass in run order and a gather of
+// the splitter prefixes, instead of walking every sublist again).
+__global__ __launch_bounds__(kBlock) void k_roff(TreeArgs a, const uint32_t* __restrict__ spref) {
+    if (replan(a.ctl)) return;
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.R) return;
+    if (a.pstart[g + 1] != a.pstart[g]) a.roff[g] += spref[a.rsid[g]];
 }
 
 // The document of splitter s (whose first arc is v's).
@@ -2089,7 +2064,7 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 // gathers inside one 1024-thread workgroup, with barriers between phases, instead of 7+
 // grid-wide kernels of HBM atomics and dependent HBM gathers.  From global memory it reads
 // r_parent and r_w (coalesced) and r_key (sibling groups of two or more only); it writes the
-// run offsets roff exactly as the global path's k_walk2 does.
+// run offsets roff exactly as the global path's k_walk1 + k_roff do.
 //
 // LDS image until the siblings are sorted (u16 arrays indexed by the local run v in [0, R); run 0
 // is the document start):
@@ -3370,7 +3345,7 @@ Engine::~Engine() {
     dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_); dfree(wgtab_);
-    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(r_key_);
+    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(rsid_); dfree(r_key_);
     dfree(rs_elem_[0]); dfree(rs_elem_[1]); dfree(rs_status_); dfree(rs_bigl_);
     dfree(rs_small_);
     dfree(wtmp_);
@@ -3698,11 +3673,12 @@ int Engine::ensure_scratch(const Wave& w) {
 // Level-1 scratch, sized by the runs of the wave (known after level 0).
 int Engine::ensure_runs(uint64_t R, uint64_t S) {
     if (R > cap_runs_) {
-        dfree(r_parent_); dfree(roff_); dfree(r_key_); dfree(rec_);
+        dfree(r_parent_); dfree(roff_); dfree(rsid_); dfree(r_key_); dfree(rec_);
         const uint64_t r = R + (R >> 3) + 4096;  // headroom against regrowth
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
         HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
+        HIPCHK(dalloc(&rsid_, r), "hipMalloc run sublists");
         HIPCHK(dalloc(&rec_, 2 * r), "hipMalloc run records");  // (two uint4 per run)
         cap_runs_ = r;
         gen_++;
@@ -3882,6 +3858,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.doc_p0 = doc_p0_;                                                               \
     a.rec = rec_; a.ctl = ctl_; a.swn = swn_;                                         \
     a.roff = roff_;                                                                   \
+    a.rsid = rsid_;                                                                   \
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
     a.leafcp = leafcp_; a.gcp = gcp_; a.res = res_;                                   \
     a.rank = L.doc_rank + w.first_doc; a.wg = nullptr;                                \
@@ -4033,7 +4010,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         r.rctl = rs_small_ + kRsCtl;
         r.status = rs_status_;
         r.bigl = rs_bigl_;
-        r.fc = roff_;  // (free until k_walk2; unused in text mode)
+        r.fc = roff_;  // (free until k_walk1)
         HIPCHK(hipMemsetAsync(rs_small_, 0, kRsSmall * 4ull, s), "clear radix counters");
         HIPCHK(hipMemsetAsync(roff_, 0xFF, R * 4ull, s), "clear first children");
         r.hist = rs_small_;
@@ -4123,7 +4100,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         k_tcopy<<<grid_for(S), kBlock, 0, s>>>(a, spref);
         k_walk_ovf<<<1024, kBlock, 0, s>>>(a, spref);
     } else {
-        k_walk2<1><<<gW, kBlock, 0, s>>>(a, spref);
+        k_roff<<<gR, kBlock, 0, s>>>(a, spref);
     }
     MARK(S_WALK2);
     HIPCHK(hipGetLastError(), "level-1 launch");
