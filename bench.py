@@ -79,7 +79,7 @@ KERNEL_BYTES = {
     "sortb": (0.0, 0.0, 0.0),
     "walk1": (0.0, 24.0, 0.0),       # the run record in; its sublist offset and sublist out
     "rank": (0.0, 0.5, 0.0),
-    "walk2": (0.0, 24.0, 0.0),       # k_roff: weight prefix, sublist, offset in; offset out
+    "walk2": (0.0, 20.0, 0.0),       # k_roff: weight prefix, {offset, sublist} in; offset out
     "expand": (0.0, 16.0, 2.0),      # run prefix/weight/head/offset; slot-order text -> document
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out

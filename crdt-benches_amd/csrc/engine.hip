@@ -906,7 +906,7 @@ struct TreeArgs {
     uint32_t* ctl;
     uint2* swn;        // per splitter {sublist weight, next splitter}
     uint32_t* roff;
-    uint32_t* rsid;    // per run with visible bytes: the splitter whose sublist holds its down arc
+    uint2* rloc;       // per run with visible bytes: {offset in its sublist, the sublist}
     uint32_t* tlen;
     uint64_t* toff;
     uint32_t* loff;
@@ -1759,10 +1759,7 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
                     // the run's offset inside its sublist and the sublist: k_roff adds the
                     // sublist's offset once the splitters are ranked (no second walk)
                     ++runs;
-                    if (w) {
-                        a.roff[v[q]] = sum[q];
-                        a.rsid[v[q]] = base + q;
-                    }
+                    if (w) a.rloc[v[q]] = make_uint2(sum[q], base + q);  // (one 8-byte store)
                 }
                 if constexpr (TEXT) {
                     ++runs;
@@ -1981,7 +1978,10 @@ __global__ __launch_bounds__(kBlock) void k_roff(TreeArgs a, const uint32_t* __r
     if (replan(a.ctl)) return;
     const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
     if (g >= a.R) return;
-    if (a.pstart[g + 1] != a.pstart[g]) a.roff[g] += spref[a.rsid[g]];
+    if (a.pstart[g + 1] != a.pstart[g]) {
+        const uint2 l = a.rloc[g];
+        a.roff[g] = l.x + spref[l.y];
+    }
 }
 
 // The document of splitter s (whose first arc is v's).
@@ -3345,7 +3345,7 @@ Engine::~Engine() {
     dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_); dfree(wgtab_);
-    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(rsid_); dfree(r_key_);
+    dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(rloc_); dfree(r_key_);
     dfree(rs_elem_[0]); dfree(rs_elem_[1]); dfree(rs_status_); dfree(rs_bigl_);
     dfree(rs_small_);
     dfree(wtmp_);
@@ -3673,12 +3673,12 @@ int Engine::ensure_scratch(const Wave& w) {
 // Level-1 scratch, sized by the runs of the wave (known after level 0).
 int Engine::ensure_runs(uint64_t R, uint64_t S) {
     if (R > cap_runs_) {
-        dfree(r_parent_); dfree(roff_); dfree(rsid_); dfree(r_key_); dfree(rec_);
+        dfree(r_parent_); dfree(roff_); dfree(rloc_); dfree(r_key_); dfree(rec_);
         const uint64_t r = R + (R >> 3) + 4096;  // headroom against regrowth
         HIPCHK(dalloc(&r_parent_, r), "hipMalloc r_parent");
         HIPCHK(dalloc(&r_key_, r), "hipMalloc r_key");
         HIPCHK(dalloc(&roff_, r), "hipMalloc roff");
-        HIPCHK(dalloc(&rsid_, r), "hipMalloc run sublists");
+        HIPCHK(dalloc(&rloc_, r), "hipMalloc run sublist offsets");
         HIPCHK(dalloc(&rec_, 2 * r), "hipMalloc run records");  // (two uint4 per run)
         cap_runs_ = r;
         gen_++;
@@ -3858,7 +3858,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.doc_p0 = doc_p0_;                                                               \
     a.rec = rec_; a.ctl = ctl_; a.swn = swn_;                                         \
     a.roff = roff_;                                                                   \
-    a.rsid = rsid_;                                                                   \
+    a.rloc = rloc_;                                                                   \
     a.tlen = tlen_; a.toff = toff_; a.loff = loff_; a.leafh = leafh_; a.ghash = ghash_; \
     a.leafcp = leafcp_; a.gcp = gcp_; a.res = res_;                                   \
     a.rank = L.doc_rank + w.first_doc; a.wg = nullptr;                                \

@@ -294,7 +294,7 @@ private:
     uint32_t rs_npass_ = 0, rs_npassB_ = 0;
     uint4* rec_ = nullptr;
     uint2* swn_ = nullptr;     // per splitter {sublist weight, next splitter}
-    uint32_t* rsid_ = nullptr; // per run: the sublist its down arc is in (global level 1)
+    uint2* rloc_ = nullptr;    // per run: {offset in its sublist, the sublist} (global level 1)
     uint32_t* spref_ = nullptr;  // per splitter: exclusive prefix along its list
     uint2* sup_ = nullptr;     // super-splitters (engine.hip k_sup1): {weight, next}
     uint32_t* spred_ = nullptr;
