@@ -79,8 +79,10 @@ KERNEL_BYTES = {
     "sortb": (0.0, 0.0, 0.0),
     "walk1": (0.0, 24.0, 0.0),       # the run record in; its sublist offset and sublist out
     "rank": (0.0, 0.5, 0.0),
-    "walk2": (0.0, 20.0, 0.0),       # k_roff: weight prefix, {offset, sublist} in; offset out
-    "expand": (0.0, 16.0, 2.0),      # run prefix/weight/head/offset; slot-order text -> document
+    "walk2": (0.0, 0.0, 0.0),        # k_doctotals alone (per document; text mode: below)
+    # run prefix/weight/head/offset (global level 1: {offset in sublist, sublist} + the sublist's
+    # prefix, 20 B); slot-order text -> document
+    "expand": (0.0, 16.0, 2.0),
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out
 }
@@ -455,6 +457,8 @@ def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> di
         per_slot, per_run, per_text = KERNEL_BYTES[k]
         if k == "doctree" and launches.get("expand", 1):
             per_text = 0.0  # expansion left to k_expand: no text in or out of k_doctree
+        if k == "expand" and launches.get("walk1"):
+            per_run = 20.0
         if radix and level1_run_bytes(k, per_wave, text_mode) is not None:
             per_run = level1_run_bytes(k, per_wave, text_mode)
         if nocon:

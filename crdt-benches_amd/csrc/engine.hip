@@ -24,7 +24,7 @@
 //                                        by parent run: sibling groups contiguous and keyed
 //    k_rs_order / k_rs_big               sibling order: {run, next sibling} pairs, first children
 //    k_rs_pass (sort B) / k_rs_records   the pairs by run id; the run records in run order
-//    k_walk1 / k_sup1 / k_sup_step / k_sup2 / k_roff (text mode: k_tcopy / k_walk_ovf)
+//    k_walk1 / k_sup1 / k_sup_step / k_sup2 (text mode: k_tcopy / k_walk_ovf)
 //                                        Euler-tour list ranking (sublists from splitters
 //                                        run id % M == 0, pointer jumping over the splitter
 //                                        lists); weighted so the rank is each run's byte offset
@@ -827,6 +827,11 @@ struct ExpandArgs {
     uint8_t* text;
     uint32_t* ctl;
     const uint8_t* fused;  // per document: text already written by k_doctree (or null)
+    // global level 1 (non-null): a run's offset is {offset in its sublist, sublist} (k_walk1)
+    // plus the sublist's prefix, read here instead of a separate pass writing roff
+    const uint2* rloc;
+    const uint32_t* spref;
+    uint32_t nspl;         // splitters of the wave (bounds the sublist index)
 };
 
 // The grid strides over the wave's runs (their count comes from ctl).  After a fused k_doctree
@@ -847,10 +852,18 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a) {
                 const uint32_t h = a.r_head[rho];
                 const uint32_t d = a.chunk_doc[h >> a.log2m];
                 const uint32_t base = a.docs[d].x;
-                const uint32_t ro = a.roff[rho];
+                uint32_t ro = 0;
+                bool bad = false;
+                if (a.rloc) {
+                    const uint2 l = a.rloc[rho];
+                    bad = l.y >= a.nspl;  // (a run no walk reached: flagged by the totals too)
+                    ro = bad ? 0u : l.x + a.spref[l.y];
+                } else {
+                    ro = a.roff[rho];
+                }
                 if (a.fused && a.fused[d]) {
                     dst = ~0ull;  // k_doctree wrote this document (w still counts: bytes stay aligned)
-                } else if ((uint64_t)ro + w > a.tlen[d]) {
+                } else if (bad || (uint64_t)ro + w > a.tlen[d]) {
                     atomicOr(&a.ctl[C_ERR], 8u);
                     dst = ~0ull;  // skipped below
                 } else {
@@ -1756,7 +1769,7 @@ __global__ __launch_bounds__(kBlock) void k_walk1(TreeArgs a) {
             if (!up[q]) {
                 const uint32_t w = r[q].y;
                 if constexpr (!TEXT) {
-                    // the run's offset inside its sublist and the sublist: k_roff adds the
+                    // the run's offset inside its sublist and the sublist: k_expand adds the
                     // sublist's offset once the splitters are ranked (no second walk)
                     ++runs;
                     if (w) a.rloc[v[q]] = make_uint2(sum[q], base + q);  // (one 8-byte store)
@@ -1971,19 +1984,6 @@ __global__ __launch_bounds__(1024) void k_doctotals(TreeArgs a) {
     }
 }
 
-// Run offsets in their documents, once the splitters are ranked: the offset inside the sublist
-// (k_walk1) plus the sublist's, one thread per run (a streaming pass in run order and a gather of
-// the splitter prefixes, instead of walking every sublist again).
-__global__ __launch_bounds__(kBlock) void k_roff(TreeArgs a, const uint32_t* __restrict__ spref) {
-    if (replan(a.ctl)) return;
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.R) return;
-    if (a.pstart[g + 1] != a.pstart[g]) {
-        const uint2 l = a.rloc[g];
-        a.roff[g] = l.x + spref[l.y];
-    }
-}
-
 // The document of splitter s (whose first arc is v's).
 __device__ __forceinline__ uint32_t splitter_doc(const TreeArgs& a, uint32_t s, uint32_t v) {
     return s >= a.Sreg ? s - a.Sreg : a.chunk_doc[a.r_head[v] >> a.log2c];
@@ -2064,7 +2064,7 @@ __device__ uint64_t xxh64_aligned(const uint8_t* __restrict__ p, uint32_t len, u
 // gathers inside one 1024-thread workgroup, with barriers between phases, instead of 7+
 // grid-wide kernels of HBM atomics and dependent HBM gathers.  From global memory it reads
 // r_parent and r_w (coalesced) and r_key (sibling groups of two or more only); it writes the
-// run offsets roff exactly as the global path's k_walk1 + k_roff do.
+// run offsets roff exactly as the global path's k_walk1 + sublist prefixes do.
 //
 // LDS image until the siblings are sorted (u16 arrays indexed by the local run v in [0, R); run 0
 // is the document start):
@@ -3920,6 +3920,7 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
                               bool stile, StageClock& ck) {
     hipStream_t s = cur_;
     TREEARGS(a);
+    tail_nspl_ = 0;  // (k_doctree leaves any offsets k_expand needs in roff)
     DocArgs da{};
     da.ndocs = w.ndocs;
     da.rcap = p.rcap;
@@ -4099,9 +4100,9 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         // the staged sublist texts out, then the rest of the longer sublists
         k_tcopy<<<grid_for(S), kBlock, 0, s>>>(a, spref);
         k_walk_ovf<<<1024, kBlock, 0, s>>>(a, spref);
-    } else {
-        k_roff<<<gR, kBlock, 0, s>>>(a, spref);
     }
+    // (otherwise k_expand adds the sublist prefixes to k_walk1's offsets as it copies the text)
+    tail_nspl_ = a.walk_text ? 0u : S;
     MARK(S_WALK2);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
@@ -4128,6 +4129,9 @@ int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, Stag
     ea.text = text_;
     ea.ctl = ctl_;
     ea.fused = nullptr;
+    ea.rloc = tail_nspl_ ? rloc_ : nullptr;
+    ea.spref = spref_;
+    ea.nspl = tail_nspl_;
     if (!fused) {  // (a fused k_doctree writes every document itself)
         k_expand<<<4096, kBlock, 0, s>>>(ea);
         MARK(S_EXPAND);
@@ -4157,7 +4161,7 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
     const uint32_t rs = l1_csr_ ? 0u : 1u;
     const uint32_t launches[S_N] = {1, 6, (rs_npassB_ + 2) * g1 * rs, g1, (rs ? 1u : 3u) * g1,
                                     (rs ? rs_npass_ : 1u) * g1, (rs ? 2u : 3u) * g1, g1,
-                                    (3 + rounds) * g1, (wt ? 4u : 2u) * g1,
+                                    (3 + rounds) * g1, (wt ? 4u : 1u) * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
                                     p.lds1 ? 2u : 0u};

@@ -289,6 +289,8 @@ private:
     uint8_t* wtmp_ = nullptr;  // text mode: the first 2^wtmp_log2_ bytes of every sublist's text
     uint64_t cap_wtmp_ = 0;    // (bytes)
     uint32_t wtmp_log2_ = 7;
+    uint32_t tail_nspl_ = 0;   // splitters of the last global level 1 whose offsets are in rloc_
+                               //   (0: k_expand reads roff_)
     uint32_t* ovf_ = nullptr;  // text mode: splitters whose sublist holds more than its slot
     uint64_t cap_ovf_ = 0;
     uint32_t rs_npass_ = 0, rs_npassB_ = 0;
