@@ -223,6 +223,12 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.l1_group = (uint32_t)value;
         return CRDT_HIP_OK;
     }
+    if (k == "rs_digit_bits") {  // radix sort A's digit width: 0 auto, 8 or 10
+        if (value != 0 && value != 8 && value != 10)
+            return set_err(ctx, CRDT_HIP_EINVAL, "rs_digit_bits must be 0, 8 or 10");
+        ctx->eng.rs_digit_bits = (uint32_t)value;
+        return CRDT_HIP_OK;
+    }
     if (k == "nsq_list") {  // the compact nsq parent list (Engine::build_nsq, nsq_launch)
         if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0, 1 or 2");
         ctx->eng.nsq_list = (uint32_t)value;

@@ -1080,14 +1080,16 @@ constexpr uint32_t kRsItemsA = CRDT_RS_ITEMS_A;
 constexpr uint32_t kRsItemsB = CRDT_RS_ITEMS_B;
 constexpr uint32_t kRsTileA = kRsThreadsA * kRsItemsA;   // sort A: 8192 x 16 B per tile
 constexpr uint32_t kRsTileB = kRsThreadsB * kRsItemsB;   // sort B: 8192 x 8 B per tile
-constexpr uint32_t kRsBins = 256;
+constexpr uint32_t kRsBins = 256;      // sort B's digits (8 bits); sort A's are 8 or 10 bits
+constexpr uint32_t kRsBinsMax = 1024;
 constexpr uint32_t kRsMaxPass = 4;
+constexpr uint32_t kRsHistA = 3 * kRsBinsMax;  // sort A's bucket starts: 4 x 256 or 3 x 1024
 constexpr uint32_t kRsAgg = 0x80000000u;  // look-back word: a tile's digit count (else prefix + 1)
 constexpr uint32_t kRsLook = 16;          // look-back words read per round trip
 // rs_small_: bucket starts of sort A [pass][bin], of sort B, then counters: tile counters of the
 // passes of A (4) and B (4), the lengths of the deferred and the long group lists
-constexpr uint32_t kRsHistB = kRsMaxPass * kRsBins;
-constexpr uint32_t kRsCtl = 2 * kRsMaxPass * kRsBins;
+constexpr uint32_t kRsHistB = kRsHistA;
+constexpr uint32_t kRsCtl = kRsHistA + kRsMaxPass * kRsBins;
 constexpr uint32_t kRsBig = 8;
 constexpr uint32_t kRsSmall = kRsCtl + 16;
 constexpr uint32_t kRsBigLds = 8192;  // groups of up to this many children sort in LDS
@@ -1095,14 +1097,15 @@ constexpr uint32_t kRsPlaceBits = 14;  // sort B: the low bits of the run id are
 
 struct RsArgs {
     uint32_t R, pass, npass;
+    uint32_t dbits;      // sort A's digit: 8 or 10 bits (sort B's: 8)
     uint32_t npassB;     // passes of sort B (the bits of the run id above kRsPlaceBits)
     uint32_t shift0;     // bit of the first digit (sort B sorts the bits above kRsPlaceBits)
     const void* in;      // the previous pass's output (or the order pass's pairs)
     void* out;
-    uint32_t* hist;      // this sort's [pass][256] bucket starts
+    uint32_t* hist;      // this sort's [pass][bins] bucket starts
     uint32_t* tctr;      // this sort's tile counter per pass
     uint32_t* rctl;      // the counters block
-    uint32_t* status;    // [tiles][256] look-back words (zeroed before every pass)
+    uint32_t* status;    // [tiles][bins] look-back words (zeroed before every pass)
     uint2* bigl;         // {start, children} of each group of more than 64 children
     uint2* B;            // per element of A: {run, next sibling}
     uint32_t* fc;        // per run: its first child (kNil: a leaf)
@@ -1120,8 +1123,9 @@ __device__ __forceinline__ uint32_t rs_parent(const TreeArgs& a, uint32_t g, boo
 // nearly constant over a wave when documents are small (all parents of a document share them),
 // and 64 per-lane atomics on one bin serialise.
 __global__ __launch_bounds__(kBlock) void k_rs_hist(TreeArgs a, RsArgs r) {
-    __shared__ uint32_t h[kRsMaxPass * kRsBins];
-    for (uint32_t i = threadIdx.x; i < r.npass * kRsBins; i += kBlock) h[i] = 0;
+    __shared__ uint32_t h[kRsHistA];
+    const uint32_t db = r.dbits, bins = 1u << db, nb = r.npass * bins;
+    for (uint32_t i = threadIdx.x; i < nb; i += kBlock) h[i] = 0;
     __syncthreads();
     uint32_t bad_any = 0;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1135,35 +1139,40 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(TreeArgs a, RsArgs r) {
 #pragma unroll
         for (int k = 0; k < (int)kRsMaxPass; ++k) {
             if ((uint32_t)k >= r.npass) break;
-            const uint32_t d = (pv >> (8u * k)) & 255u;
+            const uint32_t d = (pv >> (db * k)) & (bins - 1u);
             const uint32_t d0 = (uint32_t)__shfl((int)d, 0);  // (lane 0 is valid when any lane is)
             if (__ballot(valid && d != d0) == 0ull) {
-                if (lane == 0u && vm) atomicAdd(&h[k * kRsBins + d0], (uint32_t)__popcll(vm));
+                if (lane == 0u && vm) atomicAdd(&h[k * bins + d0], (uint32_t)__popcll(vm));
             } else if (valid) {
-                atomicAdd(&h[k * kRsBins + d], 1u);
+                atomicAdd(&h[k * bins + d], 1u);
             }
         }
     }
     if (bad_any) atomicOr(&a.ctl[C_ERR], 1u);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < r.npass * kRsBins; i += kBlock)
+    for (uint32_t i = threadIdx.x; i < nb; i += kBlock)
         if (h[i]) atomicAdd(&r.hist[i], h[i]);
 }
 
 // Single workgroup: bucket starts of every pass of both sorts.  Sort B sorts a permutation of
 // 0..R-1: digit d of pass k is held by full * 256^k values of each complete cycle of 256^(k+1)
 // and by the part of the last cycle's block of d.
-__global__ __launch_bounds__(kRsBins) void k_rs_scan(RsArgs r) {
-    __shared__ uint32_t lds[kRsBins / 64];
-    const uint32_t d = threadIdx.x;
+__global__ __launch_bounds__(kRsBinsMax) void k_rs_scan(RsArgs r) {
+    __shared__ uint32_t lds[kRsBinsMax / 64];
+    const uint32_t d = threadIdx.x, bins = 1u << r.dbits;
     for (uint32_t k = 0; k < max(r.npass, r.npassB); ++k) {
         uint32_t tot;
-        const uint32_t v = r.hist[k * kRsBins + d];
-        r.hist[k * kRsBins + d] = block_excl_scan<kRsBins / 64>(v, lds, tot);
+        if (k < r.npass) {
+            const uint32_t v = d < bins ? r.hist[k * bins + d] : 0u;
+            const uint32_t e = block_excl_scan<kRsBinsMax / 64>(v, lds, tot);
+            if (d < bins) r.hist[k * bins + d] = e;
+        }
         const uint64_t P = 1ull << (kRsPlaceBits + 8u * k), Q = P << 8;
         const uint64_t rem = r.R % Q, lo = (uint64_t)d * P;
-        const uint64_t cnt = (r.R / Q) * P + (rem > lo ? std::min<uint64_t>(rem - lo, P) : 0ull);
-        r.hist[kRsHistB + k * kRsBins + d] = block_excl_scan<kRsBins / 64>((uint32_t)cnt, lds, tot);
+        const uint64_t cnt = d < kRsBins
+            ? (r.R / Q) * P + (rem > lo ? std::min<uint64_t>(rem - lo, P) : 0ull) : 0ull;
+        const uint32_t e = block_excl_scan<kRsBinsMax / 64>((uint32_t)cnt, lds, tot);
+        if (d < kRsBins && k < r.npassB) r.hist[kRsHistB + k * kRsBins + d] = e;
     }
 }
 
@@ -1172,22 +1181,30 @@ __device__ __forceinline__ uint32_t rs_lanes_below(uint64_t m) {
 }
 
 // One pass.  T: uint4 (sort A) or uint2 (sort B), the sort key in .x.  MODE 0: the first pass of
-// A (elements built from r_parent / r_key); 1: elements from r.in to r.out.
-template <class T, int MODE, int ITEMS, int THREADS>
+// A (elements built from r_parent / r_key); 1: elements from r.in to r.out.  DB: digit bits (8,
+// or 10 for sort A when that saves a pass: 3 x 10 bits cover waves of up to 2^30 runs, where 8-bit
+// digits need 4 passes).  The per-wave digit counts share LDS with the reordered tile: every
+// element's tile position is taken from them before the tile is written.
+template <class T, int MODE, int ITEMS, int THREADS, int DB>
 __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
     constexpr uint32_t kRsThreads = THREADS, kRsWaves = THREADS / 64;
     constexpr uint32_t TILE = kRsThreads * ITEMS;
-    __shared__ T buf[TILE];
-    __shared__ uint32_t wc[kRsWaves][kRsBins + 1];  // per wave and digit (+1: invalid elements)
-    __shared__ uint32_t dst[kRsBins];               // the tile's digit starts
-    __shared__ uint32_t gof[kRsBins];               // bucket position of the tile's digit start
+    constexpr uint32_t BINS = 1u << DB;
+    static_assert(BINS <= THREADS, "one thread per digit");
+    constexpr uint32_t kBuf = sizeof(T) * TILE, kWc = 4u * kRsWaves * (BINS + 1u);
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBuf > kWc ? kBuf : kWc];
+    T* buf = reinterpret_cast<T*>(smem);
+    // per wave and digit (+1: invalid elements)
+    uint32_t (*wc)[BINS + 1] = reinterpret_cast<uint32_t (*)[BINS + 1]>(smem);
+    __shared__ uint32_t dst[BINS];               // the tile's digit starts
+    __shared__ uint32_t gof[BINS];               // bucket position of the tile's digit start
     __shared__ uint32_t red[kRsWaves];
     __shared__ uint32_t tsh;
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     if (t == 0) tsh = atomicAdd(&r.tctr[r.pass], 1u);
-    for (uint32_t i = t; i < kRsWaves * (kRsBins + 1); i += kRsThreads) (&wc[0][0])[i] = 0;
+    for (uint32_t i = t; i < kRsWaves * (BINS + 1); i += kRsThreads) (&wc[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t tile = tsh, R = r.R, sh = r.shift0 + 8u * r.pass;
+    const uint32_t tile = tsh, R = r.R, sh = r.shift0 + DB * r.pass;
     // wave wv takes elements [base, base + 64 ITEMS) of the tile, lane-striped
     const uint32_t base = tile * TILE + wv * (64u * ITEMS);
     T e[ITEMS];
@@ -1205,17 +1222,17 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
             }
         }
     }
-    // stable ranks per wave and digit: the lanes holding the same digit (8 ballots), the rank
+    // stable ranks per wave and digit: the lanes holding the same digit (DB ballots), the rank
     // among them, and the wave's running count of the digit in LDS (its leader adds them)
     uint32_t pos[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint32_t i = base + (uint32_t)j * 64u + lane;
         const bool valid = i < R;
-        const uint32_t d = valid ? (e[j].x >> sh) & 255u : kRsBins;
+        const uint32_t d = valid ? (e[j].x >> sh) & (BINS - 1u) : BINS;
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < DB; ++b) {
             const bool bit = (d >> b) & 1u;
             const uint64_t m = __ballot(bit);
             peers &= bit ? m : ~m;
@@ -1228,7 +1245,7 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
     __syncthreads();
     // per digit: the waves' counts -> exclusive prefixes over the waves, the tile's count
     uint32_t c = 0;
-    if (t < kRsBins) {
+    if (t < BINS) {
 #pragma unroll
         for (int w = 0; w < (int)kRsWaves; ++w) {
             const uint32_t x = wc[w][t];
@@ -1236,12 +1253,12 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
             c += x;
         }
         // published at once (look-backs of later tiles wait for it); tile 0 is its own prefix
-        __hip_atomic_store(&r.status[(uint64_t)tile * kRsBins + t], tile == 0 ? c + 1u : (kRsAgg | c),
+        __hip_atomic_store(&r.status[(uint64_t)tile * BINS + t], tile == 0 ? c + 1u : (kRsAgg | c),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint32_t nval;
     const uint32_t ds = block_excl_scan<kRsWaves>(c, red, nval);
-    if (t < kRsBins) {
+    if (t < BINS) {
         dst[t] = ds;
         uint32_t ex = 0;
         if (tile > 0) {
@@ -1253,7 +1270,7 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
                 uint32_t w[kRsLook];
 #pragma unroll
                 for (int q = 0; q < (int)kRsLook; ++q)
-                    w[q] = (int)j - q >= 0 ? __hip_atomic_load(&r.status[(uint64_t)(j - q) * kRsBins + t],
+                    w[q] = (int)j - q >= 0 ? __hip_atomic_load(&r.status[(uint64_t)(j - q) * BINS + t],
                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                            : 1u;
                 uint32_t used = 0;
@@ -1275,20 +1292,24 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
                 j -= used;
                 if (stall) __builtin_amdgcn_s_sleep(1);
             }
-            __hip_atomic_store(&r.status[(uint64_t)tile * kRsBins + t], ex + c + 1u, __ATOMIC_RELAXED,
+            __hip_atomic_store(&r.status[(uint64_t)tile * BINS + t], ex + c + 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-        gof[t] = r.hist[r.pass * kRsBins + t] + ex - ds;  // (+ the element's tile position)
+        gof[t] = r.hist[r.pass * BINS + t] + ex - ds;  // (+ the element's tile position)
     }
     __syncthreads();
-    // the tile in digit order in LDS
+    // every element's place in the tile, then (the counts' LDS is the tile's) the tile in digit
+    // order in LDS
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t d = pos[j] >> 16;
+        pos[j] = d < BINS ? dst[d] + wc[wv][d] + (pos[j] & 0xFFFFu) : 0u;
+    }
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint32_t i = base + (uint32_t)j * 64u + lane;
-        if (i < R) {
-            const uint32_t d = pos[j] >> 16;
-            buf[dst[d] + wc[wv][d] + (pos[j] & 0xFFFFu)] = e[j];
-        }
+        if (i < R) buf[pos[j]] = e[j];
     }
     __syncthreads();
     // out: each digit's stretch lands contiguously at its bucket position
@@ -1297,7 +1318,7 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
         const uint32_t i = (uint32_t)k * kRsThreads + t;
         if (i < nval) {
             const T x = buf[i];
-            reinterpret_cast<T*>(r.out)[gof[(x.x >> sh) & 255u] + i] = x;
+            reinterpret_cast<T*>(r.out)[gof[(x.x >> sh) & (BINS - 1u)] + i] = x;
         }
     }
 }
@@ -3711,7 +3732,7 @@ int Engine::ensure_radix(uint64_t R) {
         const uint64_t r = R + (R >> 3) + 4096;
         HIPCHK(dalloc(&rs_elem_[0], r), "hipMalloc radix elements");
         HIPCHK(dalloc(&rs_elem_[1], r), "hipMalloc radix elements");
-        HIPCHK(dalloc(&rs_status_, (r / kRsTileA + 2) * kRsBins), "hipMalloc radix look-back");
+        HIPCHK(dalloc(&rs_status_, (r / kRsTileA + 2) * kRsBinsMax), "hipMalloc radix look-back");
         HIPCHK(dalloc(&rs_bigl_, r / 65 + 64), "hipMalloc radix long groups");
         cap_rs_ = r;
         gen_++;
@@ -3994,14 +4015,20 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         k_sortbig<<<kBigGrid, kBigThreads, 0, s>>>(a, c_);
         MARK(S_LINK);
     } else {
-        // sort A by parent run (document starts: R) and sort B by run id, 8 bits per pass
-        const uint32_t npass = std::max<uint32_t>(1u, (ceil_log2((uint64_t)R + 1u) + 7u) / 8u);
+        // sort A by parent run (document starts: R), 8-bit digits or 10-bit ones where they save a
+        // pass (waves of 2^24..2^30 runs: 3 passes instead of 4); sort B by run id, 8 bits per pass
+        const uint32_t bitsA = std::max<uint32_t>(1u, ceil_log2((uint64_t)R + 1u));
+        const uint32_t p8 = (bitsA + 7u) / 8u, p10 = (bitsA + 9u) / 10u;
+        const uint32_t dbA = rs_digit_bits ? (p10 <= 3u ? rs_digit_bits : 8u)  // (kRsHistA)
+                                           : (p10 < p8 ? 10u : 8u);
+        const uint32_t npass = dbA == 10u ? p10 : p8;
         const uint64_t tilesA = ((uint64_t)R + kRsTileA - 1) / kRsTileA;
         const uint64_t tilesB = ((uint64_t)R + kRsTileB - 1) / kRsTileB;
         rs_npass_ = npass;
         RsArgs r{};
         r.R = R;
         r.npass = npass;
+        r.dbits = dbA;
         {
             const uint32_t bits = ceil_log2((uint64_t)R);  // (run ids < R)
             r.npassB = bits > kRsPlaceBits ? (bits - kRsPlaceBits + 7u) / 8u : 0u;
@@ -4017,18 +4044,22 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         r.hist = rs_small_;
         k_rs_hist<<<std::min<uint32_t>(gR, 2048u), kBlock, 0, s>>>(a, r);
         MARK(S_COUNT);
-        k_rs_scan<<<1, kRsBins, 0, s>>>(r);
+        k_rs_scan<<<1, kRsBinsMax, 0, s>>>(r);
         MARK(S_SCAN);
         r.tctr = r.rctl;
         for (uint32_t k = 0; k < npass; ++k) {
             r.pass = k;
             r.in = k ? rs_elem_[(k - 1) & 1] : nullptr;
             r.out = rs_elem_[k & 1];
-            HIPCHK(hipMemsetAsync(rs_status_, 0, tilesA * kRsBins * 4ull, s), "clear look-back");
-            if (k == 0)
-                k_rs_pass<uint4, 0, kRsItemsA, kRsThreadsA><<<(uint32_t)tilesA, kRsThreadsA, 0, s>>>(a, r);
-            else
-                k_rs_pass<uint4, 1, kRsItemsA, kRsThreadsA><<<(uint32_t)tilesA, kRsThreadsA, 0, s>>>(a, r);
+            HIPCHK(hipMemsetAsync(rs_status_, 0, tilesA * (1ull << dbA) * 4ull, s), "clear look-back");
+            const dim3 g((uint32_t)tilesA), b(kRsThreadsA);
+            if (dbA == 10u) {
+                if (k == 0) k_rs_pass<uint4, 0, kRsItemsA, kRsThreadsA, 10><<<g, b, 0, s>>>(a, r);
+                else k_rs_pass<uint4, 1, kRsItemsA, kRsThreadsA, 10><<<g, b, 0, s>>>(a, r);
+            } else {
+                if (k == 0) k_rs_pass<uint4, 0, kRsItemsA, kRsThreadsA, 8><<<g, b, 0, s>>>(a, r);
+                else k_rs_pass<uint4, 1, kRsItemsA, kRsThreadsA, 8><<<g, b, 0, s>>>(a, r);
+            }
         }
         MARK(S_PLACE);
         uint4* E = rs_elem_[(npass - 1) & 1];
@@ -4045,6 +4076,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
         r.hist = rs_small_ + kRsHistB;
         r.tctr = r.rctl + kRsMaxPass;
         r.shift0 = kRsPlaceBits;
+        r.dbits = 8;
         const uint2* Bf = B0;
         for (uint32_t k = 0; k < r.npassB; ++k) {
             r.pass = k;
@@ -4052,7 +4084,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
             r.out = (k & 1) ? B0 : B1;
             Bf = (k & 1) ? B0 : B1;
             HIPCHK(hipMemsetAsync(rs_status_, 0, tilesB * kRsBins * 4ull, s), "clear look-back");
-            k_rs_pass<uint2, 1, kRsItemsB, kRsThreadsB><<<(uint32_t)tilesB, kRsThreadsB, 0, s>>>(a, r);
+            k_rs_pass<uint2, 1, kRsItemsB, kRsThreadsB, 8><<<(uint32_t)tilesB, kRsThreadsB, 0, s>>>(a, r);
         }
         k_rs_place<<<(uint32_t)(((uint64_t)R + (1u << kRsPlaceBits) - 1) >> kRsPlaceBits), 1024, 0, s>>>(a, Bf, ns);
         k_rs_records<<<gR, kBlock, 0, s>>>(a, roff_, ns);

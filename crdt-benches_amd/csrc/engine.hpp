@@ -174,6 +174,7 @@ public:
     // sibling grouping of the global level 1: 0 = by the largest document (counting up to
     // kCsrDocRuns runs, else radix sorts), 1 = always counting, 2 = always radix sorts
     uint32_t l1_group = 0;
+    uint32_t rs_digit_bits = 0;  // sort A's digit width: 0 = 10 bits where that saves a pass, else 8
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).

@@ -148,7 +148,8 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * least 3/4 of a wave's items lack the previous-slot flag), 1 = always, 2 = never), "l1_group"
  * (sibling grouping of the global level 1: 0 = by counting when the wave's largest document has
  * at most 2^16 runs or the wave at most 2^23, else by radix sorts (default), 1 = always
- * counting, 2 = always radix sorts),
+ * counting, 2 = always radix sorts), "rs_digit_bits" (digit width of the radix sort by parent:
+ * 0 = 10 bits where that takes fewer passes than 8 (default), 8, 10),
  * "fuse_text"
  * (default 1).  Results never depend on these. */
 int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value);

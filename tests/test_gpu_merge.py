@@ -255,15 +255,17 @@ def _level1_cases():
     return logs
 
 
-@pytest.mark.parametrize("level1,group", [(0, 0), (1, 1), (1, 2)])
-def test_level1_paths_match_oracle(oracle, level1, group):
+@pytest.mark.parametrize("level1,group,dbits", [(0, 0, 0), (1, 1, 0), (1, 2, 0), (1, 2, 10)])
+def test_level1_paths_match_oracle(oracle, level1, group, dbits):
     """Per-document LDS level 1 (k_doctree, default) and the global level-1 kernels, with their
-    sibling groups by counting (group 1) and by the two radix sorts (group 2), must give the
-    oracle's bytes and digests, including sibling groups of every sort width (> 64 makes the LDS
-    path hand the wave to the global path) and a run heavier than 0xFFFF bytes."""
+    sibling groups by counting (group 1) and by the two radix sorts (group 2; sort A with 8-bit
+    or, dbits 10, 10-bit digits), must give the oracle's bytes and digests, including sibling
+    groups of every sort width (> 64 makes the LDS path hand the wave to the global path) and a
+    run heavier than 0xFFFF bytes."""
     c = crdt_hip.Context(0)
     c.set_param("level1", level1)
     c.set_param("l1_group", group)
+    c.set_param("rs_digit_bits", dbits)
     logs = _level1_cases()
     dig, lens, st = c.merge_batch(logs, stats=True)
     for i, lg in enumerate(logs):
@@ -547,9 +549,11 @@ def test_run_contraction_modes_agree(oracle, golden, relabel):
     assert runs[1] < runs[2]
 
 
-@pytest.mark.parametrize("level1,group,stride", [(0, 0, 0), (1, 1, 0), (1, 2, 0), (1, 1, 4096),
-                                                  (1, 2, 4096)])
-def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle, level1, group, stride):
+@pytest.mark.parametrize("level1,group,stride,dbits", [(0, 0, 0, 0), (1, 1, 0, 0), (1, 2, 0, 0),
+                                                        (1, 2, 0, 10), (1, 1, 4096, 0),
+                                                        (1, 2, 4096, 0)])
+def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle, level1, group, stride,
+                                                                   dbits):
     """The same without contraction on uploaded logs (the level-1 cases: agents, wide sibling
     groups, heavy runs, multi-byte text), on the per-document and on the global level 1 (there
     the first walk stages each sublist's text, k_tcopy places it, and with 4096 runs per splitter
@@ -559,6 +563,7 @@ def test_uncontracted_uploads_match_oracle_and_reject_bad_parents(oracle, level1
     c.set_param("contraction", 2)
     c.set_param("level1", level1)
     c.set_param("l1_group", group)
+    c.set_param("rs_digit_bits", dbits)
     if stride:
         c.set_param("splitter_stride", stride)
     logs = _level1_cases()
