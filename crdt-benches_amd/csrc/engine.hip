@@ -3228,16 +3228,18 @@ __device__ __forceinline__ Perm replica_perm(uint32_t kind, uint32_t n, uint64_t
 // blockIdx.x x 256 threads over a document's items.  Replica r is a relabelled copy of base
 // r % nb: item k goes to slot perm(k) and its parent is relabelled the same way.
 // ---- the compact nsq parent list of a resident batch (Engine::build_nsq) ---------------------------
-// One thread per 64-slot chunk of a wave: the chunk's nsq items (items without the previous-slot
-// flag), the same classification as k_classify's.
-__device__ __forceinline__ uint64_t chunk_nsq_bits(const L0Args& a, uint32_t gs) {
-    const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-    const uint32_t l0 = gs - doc.x, n = doc.y;
-    const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 192 B, 16-aligned
-    uint64_t bits = 0;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const uint4 q0 = cv[3 * g], q1 = cv[3 * g + 1], q2 = cv[3 * g + 2];
+// The nsq items (items without the previous-slot flag) of every 64-slot chunk of a wave, the same
+// classification as k_classify's: 16 slots per thread (three 16-byte loads, the lanes of a wave on
+// 3 KiB of consecutive codepoint words), four lanes' 16-bit masks joined into the chunk's mask.
+__global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt, uint64_t* mask) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;  // 16-slot group
+    const uint32_t gs = t * 16u;
+    uint32_t bits = 0;
+    if (gs < a.nslots) {
+        const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        const uint32_t l0 = gs - doc.x, n = doc.y;
+        const uint4* cv = reinterpret_cast<const uint4*>(a.in_cp + 3ull * gs);  // 48 B, 16-aligned
+        const uint4 q0 = cv[0], q1 = cv[1], q2 = cv[2];
         const uint32_t CW[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                                  q2.x, q2.y, q2.z, q2.w, 0u};
 #pragma unroll
@@ -3245,19 +3247,20 @@ __device__ __forceinline__ uint64_t chunk_nsq_bits(const L0Args& a, uint32_t gs)
             const int byte = 3 * k, wd = byte >> 2, sh = 8 * (byte & 3);
             const uint32_t lo = CW[wd] >> sh, hi = sh > 8 ? CW[wd + 1] << (32 - sh) : 0u;
             const uint32_t c = (lo | hi) & 0x00FFFFFFu;
-            const uint32_t slot = 16u * (uint32_t)g + (uint32_t)k;
-            const bool it = (l0 + slot - 1u) < n;
-            bits |= (uint64_t)(it && !(c & kSeqBit) ? 1u : 0u) << slot;
+            const bool it = (l0 + (uint32_t)k - 1u) < n;
+            bits |= (it && !(c & kSeqBit) ? 1u : 0u) << k;
         }
     }
-    return bits;
-}
-__global__ __launch_bounds__(kBlock) void k_nsq_count(L0Args a, uint32_t* cnt, uint64_t* mask) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c * 64ull >= a.nslots) return;
-    const uint64_t b = chunk_nsq_bits(a, c * 64u);
-    cnt[c] = (uint32_t)__popcll(b);
-    mask[c] = b;
+    // (every lane of the wave takes part in the shuffles; a chunk's four groups are lanes
+    // 4i .. 4i + 3 of one wave)
+    const uint32_t lane = threadIdx.x & 63u, l4 = lane & ~3u;
+    const uint32_t b0 = (uint32_t)__shfl((int)bits, (int)l4), b1 = (uint32_t)__shfl((int)bits, (int)l4 + 1);
+    const uint32_t b2 = (uint32_t)__shfl((int)bits, (int)l4 + 2), b3 = (uint32_t)__shfl((int)bits, (int)l4 + 3);
+    if ((lane & 3u) == 0u && gs < a.nslots) {
+        const uint64_t m = (uint64_t)(b0 | (b1 << 16)) | ((uint64_t)(b2 | (b3 << 16)) << 32);
+        cnt[t >> 2] = (uint32_t)__popcll(m);
+        mask[t >> 2] = m;
+    }
 }
 // The list itself: one workgroup per 4096-slot tile (16 slots per thread, k_classify's layout):
 // the tile's nsq items (k_nsq_count's masks) listed in LDS in slot order (a block scan of the
@@ -4838,7 +4841,7 @@ void Engine::nsq_count_scan(DeviceLogs& L) {
     (void)hipMemsetAsync(L.nsq_pre, 0, (n + 1ull) * 4, stream);
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
-        k_nsq_count<<<grid_for(w.nslots / 64), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6),
+        k_nsq_count<<<grid_for((w.nslots + 15) / 16), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6),
                                                                    L.nsq_mask + (w.slot0 >> 6));
     }
     k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, L.nsq_sums);
