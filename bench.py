@@ -652,6 +652,11 @@ def traces_workload(args) -> int:
                                {k: float(np.mean([s["stage_ns"][k] for s in cs]))
                                 for k in cs[0]["stage_ns"]}.items() if v > 2e4},
             }
+            crf = roofline_fields(cs, cb, cb.items, cres["step_s"], pmc=False)
+            out["companion_shuffle"]["rooflines"] = {
+                k: {"kernel": v["kernel"], "frac": v["frac"], "achieved_gbps": v["achieved"],
+                    "launch_us": v["launch_us"]} for k, v in crf["rooflines"].items()}
+            out["companion_shuffle"]["batched_merge"] = crf["batched_merge"]
             out["digests_ok"] = out["digests_ok"] and cres["digests_ok"]
             cb.close()
     # companion line: the same headline batch over the plain SoA (no compact list of the non-seq
@@ -754,6 +759,12 @@ def side_workload(args) -> int:
             "device_ms_per_step": float(np.mean([x["total_ns"] for x in stats])) / 1e6,
             "text_bytes": int(lens[0]), "digest": "%016x" % int(dig[0]), "digests_ok": ok,
         }
+        # every stage's roofline by its algorithmic bytes (DESIGN.md §7 pricing; no PMC here)
+        rf = roofline_fields(stats, batch, batch.items, el / args.steps, pmc=False)
+        out["rooflines"] = {k: {"kernel": v["kernel"], "frac": v["frac"],
+                                "achieved_gbps": v["achieved"], "launch_us": v["launch_us"]}
+                            for k, v in rf["rooflines"].items()}
+        out["batched_merge"] = rf["batched_merge"]
         if patches is not None:
             out["patches_per_s"] = patches * world / (el / args.steps)
         print(json.dumps(out), flush=True)
