@@ -352,10 +352,10 @@ private:
     uint32_t* host_block(const DeviceLogs& L, uint32_t wi) const;
     int ensure_events(std::vector<hipEvent_t>& ev, size_t n);
     L1Plan plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord, bool force_global) const;
-    // the global level 1 of a text-mode wave without run contraction: k_walk2 writes the text
-    // text written by the first walk (grid-wide level 1, TEXT mode) on waves without contraction;
-    // contracted waves keep k_walk2 + k_expand (their long runs and skewed sublist texts made the
-    // staged form 1.1-2.3x slower: DESIGN.md §5b)
+    // text written by the first walk (grid-wide level 1, TEXT mode: k_walk1 stages each sublist's
+    // text, k_tcopy / k_walk_ovf place it) on waves without contraction; contracted waves keep
+    // k_expand (their long runs and skewed sublist texts made the staged form 1.1-2.3x slower:
+    // DESIGN.md §5b)
     static bool walk_text(const Wave& w, bool ord, const L1Plan& p) {
         return !p.lds1 && !ord && w.nocon;
     }

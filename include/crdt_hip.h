@@ -110,12 +110,14 @@ enum {
     CRDT_HIP_STAGE_PLACE = 5,    /* level 1: runs grouped by parent run: placement (counting)
                                     or LDS-staged onesweep radix passes                       */
     CRDT_HIP_STAGE_LINK = 6,     /* level 1: sibling order of each group, first children      */
-    CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums (text mode: and each
-                                    sublist's text staged in walk order)                      */
+    CRDT_HIP_STAGE_WALK1 = 7,    /* level 1: Euler-tour sublist sums and each run's offset in
+                                    its sublist (text mode: each sublist's text staged in walk
+                                    order instead)                                            */
     CRDT_HIP_STAGE_RANK = 8,     /* level 1: ranking of the splitter lists                    */
-    CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: Euler-tour re-walk, run offsets (text mode: the
-                                    staged sublist texts copied to their documents)           */
-    CRDT_HIP_STAGE_EXPAND = 10,  /* runs copy their UTF-8 to their document offset            */
+    CRDT_HIP_STAGE_WALK2 = 9,    /* level 1: per-document totals (text mode: and the staged
+                                    sublist texts copied to their documents)                  */
+    CRDT_HIP_STAGE_EXPAND = 10,  /* runs copy their UTF-8 to their document offset (global
+                                    level 1: offset in the sublist + the sublist's prefix)    */
     CRDT_HIP_STAGE_DIGEST = 11,  /* per-document tree digest                                  */
     CRDT_HIP_STAGE_DOCTREE = 12, /* level 1 in LDS: whole run tree of a document per workgroup
                                     (replaces stages 3-9 when every document fits)           */
