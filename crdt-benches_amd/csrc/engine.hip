@@ -1192,10 +1192,13 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
     constexpr uint32_t BINS = 1u << DB;
     static_assert(BINS <= THREADS, "one thread per digit");
     constexpr uint32_t kBuf = sizeof(T) * TILE, kWc = 4u * kRsWaves * (BINS + 1u);
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kBuf > kWc ? kBuf : kWc];
+    // (the counts share the tile's LDS only where both would not fit: 10-bit digits of 16-byte
+    // elements; elsewhere sharing costs a barrier and a pass over the positions)
+    constexpr bool kAlias = kBuf + kWc + 8u * BINS > 156u * 1024u;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kAlias ? (kBuf > kWc ? kBuf : kWc) : kBuf + kWc];
     T* buf = reinterpret_cast<T*>(smem);
     // per wave and digit (+1: invalid elements)
-    uint32_t (*wc)[BINS + 1] = reinterpret_cast<uint32_t (*)[BINS + 1]>(smem);
+    uint32_t (*wc)[BINS + 1] = reinterpret_cast<uint32_t (*)[BINS + 1]>(smem + (kAlias ? 0u : kBuf));
     __shared__ uint32_t dst[BINS];               // the tile's digit starts
     __shared__ uint32_t gof[BINS];               // bucket position of the tile's digit start
     __shared__ uint32_t red[kRsWaves];
@@ -1298,14 +1301,14 @@ __global__ __launch_bounds__(THREADS) void k_rs_pass(TreeArgs a, RsArgs r) {
         gof[t] = r.hist[r.pass * BINS + t] + ex - ds;  // (+ the element's tile position)
     }
     __syncthreads();
-    // every element's place in the tile, then (the counts' LDS is the tile's) the tile in digit
-    // order in LDS
+    // every element's place in the tile, then (where the counts' LDS is the tile's, after a
+    // barrier) the tile in digit order in LDS
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint32_t d = pos[j] >> 16;
         pos[j] = d < BINS ? dst[d] + wc[wv][d] + (pos[j] & 0xFFFFu) : 0u;
     }
-    __syncthreads();
+    if constexpr (kAlias) __syncthreads();
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint32_t i = base + (uint32_t)j * 64u + lane;
