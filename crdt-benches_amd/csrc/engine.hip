@@ -3490,6 +3490,9 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         slot += ds;
     }
     L.total_slots = slot;
+    // (replicas and single documents: the waves contract unless contraction is 2; uploads and
+    // built batches decide per wave from their nsq counts afterwards, set_contraction)
+    for (Wave& w : L.waves) w.nocon = !L.fugue && contraction == 2;
     apply_shape_hints(L);
     const uint64_t nchunks = slot / M;
     if (slot > L.cap_slots) {

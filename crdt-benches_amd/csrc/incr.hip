@@ -55,8 +55,9 @@ constexpr uint32_t kSpliceTile = kIncThreads * kSpliceRanks;        // old ranks
 constexpr uint32_t kIncGroupMax = 1024;  // largest sibling group ranked in inc_forest
 constexpr uint32_t kIncThinGroup = 32;   // more roots than this: ranked one wave per root
 // Roots that do not sort above every old item (a concurrent insert) take their place from a
-// search of their parent's old subtree (inc_anchor): at most kIncHard of them per call, each
-// search over at most kIncScan ranks (else the call merges in full)
+// search of their parent's old subtree (k_inc_search, one workgroup per root, before k_inc): at
+// most kIncHard of them per call, each search over at most kIncScan ranks (else the call merges
+// in full)
 constexpr uint32_t kIncHard = 256;
 constexpr uint32_t kIncScan = 1u << 16;
 #ifndef CRDT_INC_RUNS
@@ -93,6 +94,7 @@ struct IncArgs {
     uint64_t* tsp;              // (CRDT_INC_PROFILE) phase timestamps of the forest, or null
     uint64_t call;              // this call's number (a stale result block is detected)
     const uint32_t* hasl;       // (Fugue) 1 bit per old slot: it has a left child
+    uint32_t* hanc;             // per new item: a searched root's anchor rank (k_inc_search)
 };
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32i_t;
@@ -127,7 +129,6 @@ __host__ __device__ constexpr uint32_t inc_forest_lds(uint32_t mmax) {
            + 2u * mmax               // rend: the last item of each run (u16)
            + 2u * (mmax + 2u)        // cs: children by segment, sorted (u16)
            + 4u * mmax               // PR: a root's parent's old rank (u32)
-           + 6u * kIncHard           // the roots whose place needs a search: parent, item
            + 64u;
 }
 
@@ -150,7 +151,7 @@ __device__ __forceinline__ bool root_before(uint32_t aj, uint32_t pj, uint64_t k
 // the batch, so that no per-item loop runs over empty slots
 template <uint32_t Q, bool FG>
 __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint32_t* red,
-                                           uint32_t& flag, uint32_t& nhard, uint32_t& found,
+                                           uint32_t& flag, uint32_t& nhard,
                                            const uint32_t (&sl)[kSpliceRanks],
                                            uint32_t (&cwq)[kSpliceRanks]) {
     static_assert(Q * kIncThreads <= kIncMax, "items per thread");
@@ -165,8 +166,6 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     uint16_t* rend = vrk + kIncMax;                         // kIncMax: the last item of a run
     uint16_t* cs = rend + kIncMax;                          // kIncMax + 2: ch sorted
     uint32_t* PR = reinterpret_cast<uint32_t*>(cs + (kIncMax + 2u));  // kIncMax
-    uint32_t* hp = PR + kIncMax;                            // kIncHard: parents of the searched
-    uint16_t* hx = reinterpret_cast<uint16_t*>(hp + kIncHard);  //   roots, and the roots
     if (t == 0) {
         flag = 0;
         nhard = 0;
@@ -178,13 +177,14 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     uint32_t plc[Q];
     uint64_t kmax = 0;
     {
-        uint32_t pp[Q];
+        uint32_t pp[Q], ha[Q];
         uint64_t kk[Q];
 #pragma unroll
         for (int q = 0; q < (int)Q; ++q) {
             const uint32_t i = t + (uint32_t)q * kIncThreads;
             pp[q] = i < m ? a.parent[n0 + 1u + i] : 0u;
             kk[q] = i < m ? a.key[n0 + 1u + i] : 0ull;
+            ha[q] = !FG && i < m ? a.hanc[i] : 0u;
         }
         uint32_t bad = 0;
 #pragma unroll
@@ -216,14 +216,13 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
                 li = m;
                 A[i] = PR[i] = a.rank[pp[q]];
                 if (kk[q] <= maxkey0) {
-                    // some old sibling may sort above it: its place comes from a search below
+                    // some old sibling may sort above it: its place came from k_inc_search,
+                    // which searched the first kIncHard such roots
                     const uint32_t h = atomicAdd(&nhard, 1u);
-                    if (h < kIncHard) {
-                        hp[h] = pp[q];
-                        hx[h] = (uint16_t)i;
-                    } else {
+                    if (h < kIncHard && ha[q] != 0xFFFFFFFFu)
+                        A[i] = ha[q];
+                    else
                         bad |= (uint32_t)F_KEY;
-                    }
                 }
             } else {
                 const uint32_t l = pp[q] - (n0 + 1u);
@@ -239,43 +238,7 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     }
     INC_TS(1);
     __syncthreads();
-    // ---- the places of the roots that may sort below an old sibling (concurrent inserts): in
-    // the RGA pre-order a root x of key k under old parent p follows p's old children that sort
-    // above it, with their subtrees, so it goes before the first rank after p that holds an old
-    // child of p with a key <= k (x's id is greater than every old one: equal keys put x first)
-    // or that leaves p's subtree (an item whose parent ranks before p); its anchor is the rank
-    // before that.  The block searches 1024 ranks at a time, one root after the other.
-    {
-        const uint32_t nh = min(nhard, kIncHard);
-        for (uint32_t h = 0; h < nh && !flag; ++h) {
-            const uint32_t i = hx[h], p = hp[h], r0 = PR[i];
-            const uint64_t k = keys[i];
-            if (t == 0) found = 0xFFFFFFFFu;
-            __syncthreads();
-            for (uint32_t c = 0;; c += kIncThreads) {
-                const uint32_t r = r0 + 1u + c + t;
-                bool stop = r > n0;  // (the document's end)
-                if (!stop) {
-                    const uint32_t sl = a.seq[r], pr = a.parent[sl];
-                    stop = pr == p ? a.key[sl] <= k : a.rank[pr] < r0;
-                }
-                if (stop) atomicMin(&found, r);
-                __syncthreads();
-                const uint32_t f = found;
-                __syncthreads();
-                if (f != 0xFFFFFFFFu) {
-                    if (t == 0) A[i] = f - 1u;
-                    break;
-                }
-                if (c + kIncThreads >= kIncScan) {
-                    if (t == 0) atomicOr(&flag, (uint32_t)F_KEY);
-                    break;
-                }
-            }
-        }
-    }
     INC_TS(2);
-    __syncthreads();
     // ---- segment starts: exclusive scan over nodes 0..m (m + 1 <= kIncMax + 1 counts) ----
     {
         constexpr uint32_t P = (Q * kIncThreads + 1u + kIncThreads - 1u) / kIncThreads + 1u;
@@ -712,6 +675,68 @@ __device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint2 range, uin
     }
 }
 
+// ---- k_inc_search: the places of the roots that may sort below an old sibling (concurrent
+// inserts), once per call, before k_inc.  In the RGA pre-order a root x of key k under old parent
+// p follows p's old children that sort above it, with their subtrees, so it goes before the first
+// rank after p that holds an old child of p with a key <= k (x's id is greater than every old one:
+// equal keys put x first) or that leaves p's subtree (an item whose parent ranks before p); its
+// anchor is the rank before that.  Workgroup b searches the b-th such root in item order (at most
+// kIncHard workgroups), kSearchRound ranks per round; k_inc reads the anchors from hanc (a search
+// that ran kIncScan ranks without an answer leaves 0xFFFFFFFF: k_inc then merges in full).
+constexpr uint32_t kSearchThreads = 1024;
+constexpr uint32_t kSearchPer = kIncMax / kSearchThreads;       // items (and ranks) per thread
+constexpr uint32_t kSearchRound = kSearchThreads * kSearchPer;  // ranks per round
+static_assert(kIncScan % kSearchRound == 0, "search rounds");
+__global__ __launch_bounds__(kSearchThreads) void k_inc_search(IncArgs a) {
+    __shared__ uint32_t red[kSearchThreads / 64];
+    __shared__ uint32_t target, found;
+    const uint32_t t = threadIdx.x, b = blockIdx.x, m = a.m, n0 = a.n0;
+    const uint64_t maxkey0 = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
+    // this workgroup's root: the b-th new item with an old parent and a key not above every old one
+    uint32_t hard = 0;
+#pragma unroll
+    for (int q = 0; q < (int)kSearchPer; ++q) {
+        const uint32_t i = t * kSearchPer + (uint32_t)q;
+        if (i < m && a.parent[n0 + 1u + i] <= n0 && a.key[n0 + 1u + i] <= maxkey0) hard |= 1u << q;
+    }
+    if (t == 0) {
+        target = 0xFFFFFFFFu;
+        found = 0xFFFFFFFFu;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<kSearchThreads / 64>((uint32_t)__popc(hard), red, tot);
+    if (b >= ex && b < ex + (uint32_t)__popc(hard)) {
+        uint32_t h = hard;
+        for (uint32_t k = b - ex; k; --k) h &= h - 1u;  // (the (b - ex)-th set bit)
+        target = t * kSearchPer + (uint32_t)__ffs(h) - 1u;
+    }
+    __syncthreads();
+    const uint32_t i = target;
+    if (i == 0xFFFFFFFFu) return;  // (fewer such roots than workgroups: block-uniform)
+    const uint32_t p = a.parent[n0 + 1u + i], r0 = a.rank[p];
+    const uint64_t k = a.key[n0 + 1u + i];
+    uint32_t f = 0xFFFFFFFFu;
+    for (uint32_t c = 0; c < kIncScan; c += kSearchRound) {
+        uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < (int)kSearchPer; ++q) {
+            const uint32_t r = r0 + 1u + c + (uint32_t)q * kSearchThreads + t;
+            bool stop = r > n0;  // (the document's end)
+            if (!stop) {
+                const uint32_t sl = a.seq[r], pr = a.parent[sl];
+                stop = pr == p ? a.key[sl] <= k : a.rank[pr] < r0;
+            }
+            if (stop) best = min(best, r);
+        }
+        if (best != 0xFFFFFFFFu) atomicMin(&found, best);
+        __syncthreads();
+        f = found;
+        __syncthreads();  // (every thread has read it before the next round's atomics)
+        if (f != 0xFFFFFFFFu) break;  // (block-uniform)
+    }
+    if (t == 0) a.hanc[i] = f != 0xFFFFFFFFu ? f - 1u : 0xFFFFFFFFu;
+}
+
 // ---- the whole incremental merge in one launch: one workgroup per tile of old ranks ------------
 // Every workgroup orders the new items itself (the forest is small: the same result in each, no
 // grid-wide barrier), splices its tile, takes its byte offset by look-back and writes its text.
@@ -721,7 +746,7 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     __shared__ uint32_t red[kIncThreads / 64];
     __shared__ uint32_t rsum[2 * (kIncThreads / 64)];
     __shared__ uint32_t cb[2];
-    __shared__ uint32_t flag, nhard, found;
+    __shared__ uint32_t flag, nhard;
     __shared__ uint64_t excl_lds;
     const uint32_t b = blockIdx.x;
     // the tile's old order, loaded before the forest so that the round trip overlaps it
@@ -735,18 +760,18 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     uint32_t cwq[kSpliceRanks];
     if (a.m && a.hasl) {  // (Fugue)
         if (a.m <= kIncThreads)
-            inc_forest<1, true>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<1, true>(a, lds, red, flag, nhard, sl, cwq);
         else if (a.m <= 2u * kIncThreads)
-            inc_forest<2, true>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<2, true>(a, lds, red, flag, nhard, sl, cwq);
         else
-            inc_forest<kIncMax / kIncThreads, true>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<kIncMax / kIncThreads, true>(a, lds, red, flag, nhard, sl, cwq);
     } else if (a.m) {
         if (a.m <= kIncThreads)
-            inc_forest<1, false>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<1, false>(a, lds, red, flag, nhard, sl, cwq);
         else if (a.m <= 2u * kIncThreads)
-            inc_forest<2, false>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<2, false>(a, lds, red, flag, nhard, sl, cwq);
         else
-            inc_forest<kIncMax / kIncThreads, false>(a, lds, red, flag, nhard, found, sl, cwq);
+            inc_forest<kIncMax / kIncThreads, false>(a, lds, red, flag, nhard, sl, cwq);
     } else {
 #pragma unroll
         for (int q = 0; q < (int)kSpliceRanks; ++q) cwq[q] = slot_word(a.cp, sl[q]);
@@ -908,6 +933,7 @@ int inc_reserve(Engine& E, IncState& s, uint64_t items, uint64_t bytes) {
     const uint64_t tcap = bytes + 64;
     if (tcap > s.text_cap)
         ICHK(igrow(&s.text, s.text_cap, std::max<uint64_t>(tcap, 2 * s.text_cap)), "hipMalloc text");
+    if (!s.hanc) ICHK(dalloc(&s.hanc, (uint64_t)kIncMax), "hipMalloc search anchors");
     if (!s.ctl) {
         ICHK(dalloc(&s.ctl, (uint64_t)I_N), "hipMalloc counters");
         ICHK(hipMemset(s.ctl, 0, I_N * 8), "clear counters");
@@ -943,6 +969,7 @@ IncArgs make_args(Replica& r, IncState& s, uint32_t n0, uint32_t m) {
     a.hres = s.dres;
     a.call = ++s.calls;
     a.hasl = r.logs.fugue ? s.hasl : nullptr;  // (selects the Fugue forest)
+    a.hanc = s.hanc;
     return a;
 }
 
@@ -979,6 +1006,10 @@ int inc_run(Engine& E, IncState& s, IncArgs& a, bool sync) {
     a.tsp = prof ? tsp : nullptr;
     const auto h0 = std::chrono::steady_clock::now();
     if (prof) ICHK(hipEventRecord(ev[0], st), "event");
+    if (a.m && !a.hasl) {  // (RGA: the searched roots' anchors, once per call)
+        k_inc_search<<<std::min(a.m, kIncHard), kSearchThreads, 0, st>>>(a);
+        ICHK(hipGetLastError(), "incremental merge search launch");
+    }
     k_inc<<<std::max<uint32_t>(1, a.nblk), kIncThreads, inc_forest_lds(kIncMax), st>>>(a);
     ICHK(hipGetLastError(), "incremental merge launch");
     if (prof) ICHK(hipEventRecord(ev[1], st), "event");
@@ -1081,6 +1112,7 @@ IncState::~IncState() {
     for (hipEvent_t e : pev)
         if (e) (void)hipEventDestroy(e);
     dfree(hasl);
+    dfree(hanc);
     dfree(lb_flag);
     dfree(lb_agg);
     dfree(lb_inc);

@@ -767,7 +767,10 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
             if (rc) return rc;
             const std::vector<uint64_t> key = {
                 E.generation(), w.gen, init.gen, (uint64_t)(uintptr_t)&init, init.n, init.vis_bytes,
-                cap, (uint64_t)(uintptr_t)&ub, ub.len, ub.n, st.n_after, b_plan};
+                cap, (uint64_t)(uintptr_t)&ub, ub.len, ub.n, st.n_after, b_plan,
+                // (knobs that change what is captured: a closure captured under other settings
+                // is not replayed)
+                (uint64_t)E.nsq_list, (uint64_t)E.contraction};
             hipStream_t s = E.stream;
             if (key != st.key || !st.exec) {
                 drop_graph(st);

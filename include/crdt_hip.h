@@ -147,7 +147,8 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * flag: 1 (default) = resident batches, and replicas of at least 2^22 slots, whose merges rebuild
  * it; 2 = every replica too; 0 = never), "contraction" (run contraction of RGA waves, decided
  * when a batch is built or logs are uploaded: 0 = by the input (default: no contraction when at
- * least 3/4 of a wave's items lack the previous-slot flag), 1 = always, 2 = never), "l1_group"
+ * least 3/4 of a wave's items lack the previous-slot flag), 1 = always, 2 = never; replica
+ * merges, which count no flags, contract under 0 and 1 and never under 2), "l1_group"
  * (sibling grouping of the global level 1: 0 = by counting when the wave's largest document has
  * at most 2^16 runs or the wave at most 2^23, else by radix sorts (default), 1 = always
  * counting, 2 = always radix sorts), "rs_digit_bits" (digit width of the radix sort by parent:

@@ -227,6 +227,63 @@ def test_concurrent_roots_placed_by_search_match_oracle(ctx, oracle):
     assert paths[0] == 0 and paths[1:].count(1) >= len(paths) - 5, paths
 
 
+def test_concurrent_root_whose_search_runs_out_of_range_falls_back(ctx, oracle):
+    """A concurrent root under the document start of a 70,000-item document: its place would be
+    after the whole document (one typing chain under the first item), beyond the search's 65,536
+    ranks (incr.hip kIncScan), so the call merges in full; the next local edit is incremental."""
+    a = crdt_hip.OpLog(agent=1)
+    h = crdt_hip.OpLog(agent=1)
+    r = crdt_hip.Replica(ctx)
+
+    def ship(u):
+        r.apply_updates([u])
+        h.apply_update(u)
+
+    a.insert(0, "".join(chr(ord("a") + i % 26) for i in range(70_000)))
+    ship(a.encode_from(0))
+    assert r.merge_inc()[2] == 0
+    v = a.version()
+    a.insert(0, "XY")
+    ship(_with_item_id(a.encode_from(v), 0, 1, 0))  # X sorts below the first item (1, agent 1)
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 0
+    assert text == oracle.merge(to_anchor(h.arrays()))
+    assert text.endswith(b"XY")
+    v = h.version()
+    h.insert(5, "--")
+    r.apply_updates([h.encode_from(v)])
+    cps, nb, path, text = r.merge_inc(text=True)
+    assert path == 1 and text == oracle.merge(to_anchor(h.arrays()))
+
+
+@pytest.mark.parametrize("nroots,path", [(200, 1), (300, 0)])
+def test_many_concurrent_roots_in_one_batch(ctx, oracle, nroots, path):
+    """One batch of `nroots` concurrent inserts, each a new child of a different old item with a
+    key below every old one: up to 256 of them (incr.hip kIncHard) are placed by the searches, one
+    workgroup each (k_inc_search); more than that merges in full."""
+    log = crdt_hip.OpLog(agent=1)
+    log.insert(0, "abcdefghijklmnopqrstuvwxyz" * 80)
+    base = log.encode_from(0)
+    r = crdt_hip.Replica(ctx)
+    r.apply_updates([base])
+    assert r.merge_inc()[2] == 0
+    v = log.version()
+    for k in range(nroots):  # descending positions: every new item's parent is an old item
+        log.insert(6 * (nroots - k), "XYZ"[k % 3])
+    u = log.encode_from(v)
+    n = struct.unpack_from("<I", u, 12)[0]
+    assert n == nroots
+    for k in range(n):
+        u = _with_item_id(u, k, 1 + k, 0)
+    h = crdt_hip.OpLog(agent=1)
+    h.apply_update(base)
+    h.apply_update(u)
+    r.apply_updates([u])
+    cps, nb, p, text = r.merge_inc(text=True)
+    assert p == path
+    assert text == oracle.merge(to_anchor(h.arrays()))
+
+
 @pytest.mark.parametrize("name,K", [("sveltecomponent", 300), ("automerge-paper", 1000)])
 def test_fugue_incremental_len_matches_oracle(ctx, oracle, name, K):
     """Fugue replicas on the incremental path: the trace replayed on a Fugue upstream, its

@@ -296,6 +296,37 @@ def _replay_closure(ctx, golden, py_trace, name):
     init.close()
 
 
+@pytest.mark.parametrize("mode", [2, 1, 0])
+def test_replica_merges_follow_the_contraction_knob(ctx, golden, py_trace, mode):
+    """Replica merges (merge_len, the replay closure, the incremental state's full merge) honour
+    "contraction": 2 merges without run contraction (every item its own run), 0 and 1 contract.
+    Switching the knob between replays recaptures the closure (the graph key holds it); every
+    result is the trace's document."""
+    name = "sveltecomponent"
+    t = crdt_hip.Trace(trace_path(name))
+    patches = [t.patch(i) for i in range(len(t))]
+    up, updates = crdt_hip.HipMerge.upstream_updates(t.start_content, patches)
+    end = py_trace(name).end_content
+    want = (len(end), len(end.encode()), int(golden[name]["tree_digest"], 16))
+    init = crdt_hip.Replica(ctx)
+    ub = crdt_hip.UpdateBatch(ctx, *crdt_hip.pack_updates(updates))
+    try:
+        assert init.replay(ub) == want
+        ctx.set_param("contraction", mode)
+        for _ in range(3):
+            assert init.replay(ub) == want
+        r = init.clone()
+        r.apply_resident(ub)
+        assert r.merge_len() == want
+        cps, nb, path, text = r.merge_inc(text=True)
+        assert path == 0 and text.decode() == end
+        r.close()
+    finally:
+        ctx.set_param("contraction", 0)
+        ub.close()
+        init.close()
+
+
 def test_replay_falls_back_when_sizes_change(ctx, golden):
     """Speculated sizes that no longer hold (forced with the plan_shrink hook) are caught by the
     device check and the closure is merged again with the real ones; a changed init starts over."""
