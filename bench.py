@@ -536,6 +536,8 @@ def traces_workload(args) -> int:
         ctx.set_param("xcd_order", args.xcd_order)
     if args.stile_text != 1:  # (likewise)
         ctx.set_param("stile_text", args.stile_text)
+    if args.runs_slots != 32:  # (likewise)
+        ctx.set_param("runs_slots", args.runs_slots)
     if args.nsq_list != 1:  # (likewise)
         ctx.set_param("nsq_list", args.nsq_list)
     ctx.set_param("lane_gate", args.lane_gate)
@@ -999,9 +1001,11 @@ def parse_args(argv=None):
                     help="0: k_doctree leaves the text to k_expand (smaller LDS footprint)")
     ap.add_argument("--xcd-order", type=int, default=1, choices=[0, 1],
                     help="1: level-0 tiles in XCD-aware order (each XCD one contiguous range)")
-    ap.add_argument("--stile-text", type=int, default=1, choices=[0, 1],
-                    help="1: fused level 1 stages text from the tile segments (k_runs skips the "
-                         "slot-order copy)")
+    ap.add_argument("--stile-text", type=int, default=2, choices=[0, 1, 2],
+                    help="fused level 1 stages text from the tile segments (k_runs skips the "
+                         "slot-order copy): 1 by loads and shifts, 2 by LDS-DMA per tile")
+    ap.add_argument("--runs-slots", type=int, default=32, choices=[16, 32],
+                    help="k_runs slots per thread (16: 256 threads per tile, 32: 128)")
     ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1, 2],
                     help="1: resident batches (input encoding) and replicas of 2^22+ slots (every "
                          "merge) carry the compact list of the non-seq items' parents and keys; "

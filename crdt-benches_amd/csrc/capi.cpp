@@ -208,9 +208,15 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.xcd_order = value == 1;
         return 0;
     }
-    if (k == "stile_text") {  // 1: fused plans stage text from the tile segments (L1Plan)
-        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "stile_text must be 0 or 1");
-        ctx->eng.stile_text = value == 1;
+    if (k == "runs_slots") {  // k_runs slots per thread: 16 or 32
+        if (value != 16 && value != 32) return set_err(ctx, CRDT_HIP_EINVAL, "runs_slots must be 16 or 32");
+        ctx->eng.runs_slots = (uint32_t)value;
+        return CRDT_HIP_OK;
+    }
+    if (k == "stile_text") {  // fused plans stage text from the tile segments (L1Plan): 1 by
+                              // loads and shifts, 2 by LDS-DMA per tile
+        if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "stile_text must be 0, 1 or 2");
+        ctx->eng.stile_text = (uint32_t)value;
         return 0;
     }
     if (k == "contraction") {  // run contraction: 0 by the input, 1 always, 2 never (Wave::nocon)

@@ -424,7 +424,8 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 
 // k_heads: one thread per 64-slot word of the rank bitvector (a word is inside one document),
 // one wave per tile.  head(g) = document start, or an item that does not continue the run of
-// the slot before it: continue(g) = seq(g) && !jump(g-1).  Besides the words: the heads before
+// the slot before it: continue(g) = seq(g) && !jump(g-1) && g is not a tile's first slot (runs
+// never cross tiles: +1 run per 4096 slots at most).  Besides the words: the heads before
 // each word inside its tile (hrec .z), so that the run of any slot s is
 // tile_hw[s / 4096].x + hrec[s / 64].z + popcount(bits of hrec[s / 64] up to s) - 1 once the tile
 // prefixes are scanned.
@@ -454,8 +455,13 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint2 jr = *reinterpret_cast<const uint2*>(a.jbits + (gs >> 5));
             const uint2 jq = *reinterpret_cast<const uint2*>(a.jloc + (gs >> 5));
             const uint64_t jw = ((uint64_t)(jr.y | jq.y) << 32) | (uint64_t)(jr.x | jq.x);
+            // (a tile's first slot always heads a run: no run crosses a tile, so the text of every
+            // run lies inside one tile's stile segment, which k_doctree stages tile by tile)
             uint64_t pj = 0;
-            if (l0 > 0) pj = ((a.jbits[(gs >> 5) - 1] | a.jloc[(gs >> 5) - 1]) >> 31) & 1u;
+            if (l0 > 0)
+                pj = (gs % kScanTile) == 0u
+                         ? 1u
+                         : ((a.jbits[(gs >> 5) - 1] | a.jloc[(gs >> 5) - 1]) >> 31) & 1u;
             const uint64_t prevj = (jw << 1) | pj;  // bit k = jump(gs + k - 1)
             const uint64_t item = low_mask64(n + 1u - l0) & ~low_mask64(l0 == 0 ? 1u : 0u);
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
@@ -592,23 +598,37 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
 // FUGUE: the wave has left children.  A head with left children then numbers two rows; the
 // tile still keeps one record per head (kRecTree marks those heads) and the per-head loop finds
 // each head's first row by a block scan of the rows per head.
-template <bool FUGUE>
-__global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
-    constexpr int NW = kBlock / 64;
+// SL = slots per thread (16: 256 threads per tile; 32: 128 threads per tile).  With 32, a wave
+// covers two 1024-slot stretches and a CU holds 16 tiles at once instead of 8 (32 waves per CU
+// either way): the per-head phase is a chain of dependent gathers (list entry, then the parent's
+// head record) with ~100 heads per tile on the traces, so the tiles a CU holds at once bound the
+// gathers in flight.  The records are staged in an LDS window of kRunsWin heads (+1), filled and
+// drained as often as the tile needs (nearly always once), which keeps the 128-thread block at
+// ~6 KiB of LDS.
+constexpr uint32_t kRunsWin = 1024;
+template <bool FUGUE, int SL>
+__global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(8))) void k_runs(L0Args a) {
+    static_assert(SL == 16 || SL == 32, "slots per thread");
+    constexpr int NT = kScanTile / SL;  // threads per tile
+    constexpr int NW = NT / 64;
+    constexpr int NQ = SL / 16;         // weight-nibble words per thread
+    constexpr uint32_t kWin = SL == 16 ? (uint32_t)kScanTile : kRunsWin;
     __shared__ uint32_t lsum[NW];
     __shared__ uint32_t lrow[NW];
-    __shared__ uint32_t rec[kScanTile];
-    __shared__ uint16_t lnsq[kBlock];  // nsq bits of every thread's 16 slots
-    __shared__ uint2 ldoc[kBlock];     // every thread's document {base slot, items}
+    __shared__ uint32_t rec[kWin + 1];
+    __shared__ uint32_t lnsq[NT];      // nsq bits of every thread's slots
+    __shared__ uint2 ldoc[NT];         // every thread's document {base slot, items}
     __shared__ uint32_t lsq[NW];
-    __shared__ uint16_t lnpf[kBlock];  // non-seq items of the tile before every thread
-    __shared__ uint16_t ldp[FUGUE ? kBlock : 1];  // Fugue: two-row heads before every thread
-    __shared__ uint16_t ldm[FUGUE ? kBlock : 1];  //   and every thread's two-row head bits
+    __shared__ uint16_t lnpf[NT];      // non-seq items of the tile before every thread
+    __shared__ uint16_t ldp[FUGUE ? NT : 1];  // Fugue: two-row heads before every thread
+    __shared__ uint32_t ldm[FUGUE ? NT : 1];  //   and every thread's two-row head bits
     const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t gs = tile * kScanTile + threadIdx.x * kScanItems;
+    const uint32_t gs = tile * kScanTile + threadIdx.x * SL;
     uint32_t hm = 0, nsq = 0, dm = 0;
-    uint64_t nib = 0;
+    uint64_t nib[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) nib[q] = 0;
     uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
     // the parents of the tile's nsq items: the compact list of a resident batch, else the tile's
@@ -617,15 +637,22 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     const uint32_t* pls = a.nsq_par ? a.nsq_par + nlo : a.plist + (uint64_t)tile * kScanTile;
     if (gs < a.nslots) {
         const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
-        hm = (((gs & 63u) < 32u ? hb.x : hb.y) >> (gs & 31u)) & 0xFFFFu;
+        const uint32_t hw32 = (gs & 63u) < 32u ? hb.x : hb.y;
+        hm = SL == 32 ? hw32 : (hw32 >> (gs & 31u)) & 0xFFFFu;
         if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
-        nib = a.wnib[gs >> 4];
+        if (SL == 32) {
+            const uint4 q = *reinterpret_cast<const uint4*>(a.wnib + (gs >> 4));
+            nib[0] = ((uint64_t)q.y << 32) | q.x;
+            nib[NQ - 1] = ((uint64_t)q.w << 32) | q.z;
+        } else {
+            nib[0] = a.wnib[gs >> 4];
+        }
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        nsq = a.nsqb[gs >> 4];
-        lnsq[threadIdx.x] = (uint16_t)nsq;
+        nsq = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.nsqb + (gs >> 4)) : a.nsqb[gs >> 4];
     }
+    lnsq[threadIdx.x] = nsq;
     ldoc[threadIdx.x] = doc;
-    // The first 4*kBlock bytes of the tile's text are loaded with the rest, before the tile's
+    // The first 4*NT bytes of the tile's text are loaded with the rest, before the tile's
     // offset is known: thread t's destination dword needs source dwords t and t+1 whatever the
     // offset's alignment (the segment is kTileBytes long, so both are in bounds).
     const uint8_t* src = a.stile + (uint64_t)tile * kTileBytes;
@@ -638,7 +665,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     }
     uint32_t W = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) W += (uint32_t)(nib >> (4 * j)) & 15u;
+    for (int j = 0; j < SL; ++j) W += (uint32_t)(nib[j >> 4] >> (4 * (j & 15))) & 15u;
     const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;  // heads (records) << 16 | weight
     const uint32_t inc = wave_incl_scan(x);
     const uint32_t cq = (uint32_t)__popc(nsq), incq = wave_incl_scan(cq);
@@ -665,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     const uint32_t dpre = offd + incd - cd;  // (Fugue) two-row heads of the tile before the thread
     if (FUGUE) {
         ldp[threadIdx.x] = (uint16_t)dpre;
-        ldm[threadIdx.x] = (uint16_t)dm;
+        ldm[threadIdx.x] = dm;
     }
     const uint32_t ex = off + inc - x;
     const uint32_t nh = tot >> 16;
@@ -680,17 +707,6 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     // tiles and written bytewise.
     const uint32_t D = pre.y, lo = (D + 3u) & ~3u, hi = (D + tw) & ~3u, sh = (lo - D) & 3u;
     uint32_t m = lo + 4u * threadIdx.x;
-    {
-        uint32_t r = ex >> 16, p = ex & 0xFFFFu;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (hm & (1u << j)) {
-                rec[r++] = ((threadIdx.x * kScanItems + (uint32_t)j) << 16) | p |
-                           ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
-            }
-            p += (uint32_t)(nib >> (4 * j)) & 15u;
-        }
-    }
     if ((hm & 1u) && (gs & 63u) == 0 && doc.x == gs) {  // document starts are 64-aligned
         const uint32_t d = a.chunk_doc[gs >> a.log2m];
         a.doc_root[d] = pre.x + (ex >> 16) + dpre;  // (rows: heads + two-row heads before)
@@ -700,7 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
     if (copy) {
         uint32_t* d32 = reinterpret_cast<uint32_t*>(a.sbytes);
         if (m < hi) d32[m >> 2] = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * sh)) : w0;
-        for (m += 4u * kBlock; m < hi; m += 4u * kBlock) {
+        for (m += 4u * NT; m < hi; m += 4u * NT) {
             const uint32_t o = m - D;
             const uint32_t v0 = s32[o >> 2], v1 = sh ? s32[(o >> 2) + 1] : 0u;
             d32[m >> 2] = sh ? (uint32_t)((((uint64_t)v1 << 32) | v0) >> (8 * sh)) : v0;
@@ -710,85 +726,111 @@ __global__ __launch_bounds__(kBlock) void k_runs(L0Args a) {
         if (tw && threadIdx.x == 1)
             for (uint32_t g = max(hi, lo); g < D + tw; ++g) a.sbytes[g] = src[g - D];
     }
-    __syncthreads();
     const uint32_t tbase = tile * kScanTile;
-    // one thread per head: every gather of a stage issued before any is used
-    for (uint32_t i = threadIdx.x; i < nh; i += kBlock) {
-        const uint32_t rv = rec[i];
-        const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
-        const bool two = (rv & kRecTree) != 0u;  // Fugue: a content row, then the tree row
-        // the head's first row: heads before it, plus (Fugue) the two-row heads before it
-        const uint32_t rho = pre.x + i +
-            (FUGUE ? ldp[li >> 4] + (uint32_t)__popc(ldm[li >> 4] & ((1u << (li & 15u)) - 1u)) : 0u);
-        const uint32_t rt = rho + (two ? 1u : 0u);  // the row with the run's parent and key
-        const uint2 dc = ldoc[li >> 4];
-        const bool root = g == dc.x;
-        const bool sq = !root && !((lnsq[li >> 4] >> (li & 15u)) & 1u);
-        // a non-seq head's parent from the tile's list: its index = the non-seq items before it;
-        // (resident batches) its key from the same index of the key list, a seq head's gathered
-        const uint32_t nw = lnsq[li >> 4];
-        const uint32_t lix = lnpf[li >> 4] + __popc(nw & ((1u << (li & 15u)) - 1u));
-        const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
-        if (!FUGUE && a.nocon) {
-            // no contraction: the run's parent and key from the columns (heads are every slot of
-            // the tile's items, so these reads are in slot order); parent run = the document
-            // start's run + the parent's item index
-            uint32_t pr = kNil;
-            uint64_t k = 0;
-            if (!root) {
-                uint32_t p = a.in_parent[g];
-                k = a.in_key[g];
-                if (p > dc.y || p == g - dc.x) {
-                    atomicOr(&a.ctl[C_ERR], 1u);
-                    p = 0;
+    // the records of heads [h0, h0 + kWin] (the one past the window: a two-row head reads the
+    // next head's weight prefix), then one thread per head of the window; block-uniform loop
+    for (uint32_t h0 = 0;; h0 += kWin) {
+        {
+            uint32_t r = ex >> 16, p = ex & 0xFFFFu;
+            if (r <= h0 + kWin && r + (uint32_t)__popc(hm) > h0) {
+#pragma unroll
+                for (int j = 0; j < SL; ++j) {
+                    if (hm & (1u << j)) {
+                        if (r >= h0 && r - h0 <= kWin)
+                            rec[r - h0] = ((threadIdx.x * SL + (uint32_t)j) << 16) | p |
+                                          ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
+                        ++r;
+                    }
+                    p += (uint32_t)(nib[j >> 4] >> (4 * (j & 15))) & 15u;
                 }
-                pr = rho - (g - dc.x) + p;
             }
+        }
+        __syncthreads();
+        // one thread per head: every gather of a stage issued before any is used
+        const uint32_t hend = min(nh, h0 + kWin);
+        for (uint32_t i = h0 + threadIdx.x; i < hend; i += NT) {
+            const uint32_t rv = rec[i - h0];
+            const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
+            const uint32_t th = li / SL, bl = li % SL;
+            const uint32_t below = (1u << bl) - 1u;
+            const bool two = (rv & kRecTree) != 0u;  // Fugue: a content row, then the tree row
+            // the head's first row: heads before it, plus (Fugue) the two-row heads before it
+            const uint32_t rho =
+                pre.x + i + (FUGUE ? ldp[th] + (uint32_t)__popc(ldm[th] & below) : 0u);
+            const uint32_t rt = rho + (two ? 1u : 0u);  // the row with the run's parent and key
+            const uint2 dc = ldoc[th];
+            const bool root = g == dc.x;
+            const uint32_t nw = lnsq[th];
+            const bool sq = !root && !((nw >> bl) & 1u);
+            // a non-seq head's parent from the tile's list: its index = the non-seq items before
+            // it; (resident batches) its key from the same index of the key list, a seq head's
+            // gathered
+            const uint32_t lix = lnpf[th] + (uint32_t)__popc(nw & below);
+            const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
+            if (!FUGUE && a.nocon) {
+                // no contraction: the run's parent and key from the columns (heads are every
+                // slot of the tile's items, so these reads are in slot order); parent run = the
+                // document start's run + the parent's item index
+                uint32_t pr = kNil;
+                uint64_t k = 0;
+                if (!root) {
+                    uint32_t p = a.in_parent[g];
+                    k = a.in_key[g];
+                    if (p > dc.y || p == g - dc.x) {
+                        atomicOr(&a.ctl[C_ERR], 1u);
+                        p = 0;
+                    }
+                    pr = rho - (g - dc.x) + p;
+                }
+                a.r_head[rho] = g;
+                a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
+                if (rho < a.cap_rows) {
+                    a.r_parent[rho] = pr;
+                    a.r_key[rho] = k;
+                }
+                continue;
+            }
+            uint32_t ps = (!sq && !root) ? pls[lix] : 0u;  // (the parent as a wave slot)
             a.r_head[rho] = g;
             a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
-            if (rho < a.cap_rows) {
-                a.r_parent[rho] = pr;
-                a.r_key[rho] = k;
-            }
-            continue;
-        }
-        uint32_t ps = (!sq && !root) ? pls[lix] : 0u;  // (the parent as a wave slot)
-        a.r_head[rho] = g;
-        a.r_pstart[rho] = pre.y + (rv & 0xFFFFu);
-        if (two) {
-            // the tree row weighs nothing: its prefix is the next head's (the content row's end)
-            a.r_head[rt] = g;
-            a.r_pstart[rt] = pre.y + (i + 1u < nh ? rec[i + 1u] & 0xFFFFu : tw_all);
-        }
-        uint32_t pr = kNil;
-        if (sq) {
-            pr = rho - 1u;  // the parent is the slot before the head: the previous run's last row
-        } else if (!root) {
-            const uint32_t p = ps - dc.x;
-            if (p > dc.y || p == g - dc.x) ps = dc.x;  // flagged by k_classify
-            const uint4 hr = a.hrec[ps >> 6];
-            const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
-            const uint32_t hl = hr.z;
-            const uint32_t tp = a.tile_hw[ps / kScanTile].x;
-            const uint32_t b = ps & 63u;
-            const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
-            uint32_t rows = (uint32_t)__popcll(hb & mask);
-            if (FUGUE) {  // (rows of the parent slot's run: its tree row is its last)
-                const uint64_t lw = *reinterpret_cast<const uint64_t*>(a.lbits + ((ps >> 5) & ~1u));
-                rows += (uint32_t)__popcll(hb & lw & mask);
-            }
-            pr = tp + hl + rows - 1u;
-        }
-        if (rt < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
-            a.r_parent[rt] = pr;
-            a.r_key[rt] = root ? 0ull : key;
             if (two) {
-                // the run's text: a child of its tree row between the left and the right
-                // children (kMidKey)
-                a.r_parent[rho] = rt;
-                a.r_key[rho] = kMidKey;
+                // the tree row weighs nothing: its prefix is the next head's (the content row's
+                // end)
+                a.r_head[rt] = g;
+                a.r_pstart[rt] = pre.y + (i + 1u < nh ? rec[i + 1u - h0] & 0xFFFFu : tw_all);
+            }
+            uint32_t pr = kNil;
+            if (sq) {
+                pr = rho - 1u;  // the parent is the slot before the head: the previous run's last row
+            } else if (!root) {
+                const uint32_t p = ps - dc.x;
+                if (p > dc.y || p == g - dc.x) ps = dc.x;  // flagged by k_classify
+                const uint4 hr = a.hrec[ps >> 6];
+                const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
+                const uint32_t hl = hr.z;
+                const uint32_t tp = a.tile_hw[ps / kScanTile].x;
+                const uint32_t b = ps & 63u;
+                const uint64_t mask = (b == 63u) ? ~0ull : ((2ull << b) - 1ull);
+                uint32_t rows = (uint32_t)__popcll(hb & mask);
+                if (FUGUE) {  // (rows of the parent slot's run: its tree row is its last)
+                    const uint64_t lw = *reinterpret_cast<const uint64_t*>(a.lbits + ((ps >> 5) & ~1u));
+                    rows += (uint32_t)__popcll(hb & lw & mask);
+                }
+                pr = tp + hl + rows - 1u;
+            }
+            if (rt < a.cap_rows) {  // (beyond: the wave outgrew its plan, C_REPLAN follows)
+                a.r_parent[rt] = pr;
+                a.r_key[rt] = root ? 0ull : key;
+                if (two) {
+                    // the run's text: a child of its tree row between the left and the right
+                    // children (kMidKey)
+                    a.r_parent[rho] = rt;
+                    a.r_key[rho] = kMidKey;
+                }
             }
         }
+        if (h0 + kWin >= nh) break;
+        __syncthreads();  // (the window is read before the next one is written)
     }
 }
 
@@ -2321,35 +2363,104 @@ __device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, 
     }
 }
 
+// Staging by LDS-DMA (DocArgs::stile_text == 2).  No run crosses a tile (k_heads), so the text
+// need not be contiguous across tiles: tile k's share of the document is staged as the aligned
+// 16-byte chunks of its segment that cover it, verbatim (chunks before it: cpx[k]; the first one at
+// segment offset akt[k]).  Chunk c is one lane of a global_load_lds_dwordx4 (the LDS image of a
+// wave instruction is lane-linear: 64 consecutive chunks); its tile comes from a binary search of
+// cpx, four chunks per thread at once, and every load of the staging is in flight before the one
+// wait at the barrier.  A run of tile k then reads its text at staging offset
+// 16 cpx[k] + (ps - tpx[k]) - akt[k].  No register holds the bytes, no byte is shifted, and no
+// chunk is partly copied.  Table: tpx, cpx, akt (nt + 2 u32 each) at `tab`.
+__device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32_t tl, uint32_t t0,
+                                           uint32_t nt, uint32_t tpx_reg, uint8_t* st,
+                                           uint32_t* tab, uint32_t* scan_lds) {
+    const uint32_t t = threadIdx.x;
+    uint32_t* tpx = tab;
+    uint32_t* cpx = tab + (nt + 2u);
+    uint32_t* akt = cpx + (nt + 2u);
+    if (t <= nt + 1u) tpx[t] = tpx_reg;
+    __syncthreads();
+    uint32_t nk = 0, ak = 0;
+    if (t <= nt) {
+        const uint32_t x0 = tpx[t];
+        const uint32_t lo = max(x0, p0), hi = min(tpx[t + 1u], p0 + tl);
+        if (hi > lo) {
+            ak = (lo - x0) & ~15u;
+            nk = ((hi - x0 + 15u) >> 4) - (ak >> 4);
+        }
+    }
+    uint32_t C;
+    const uint32_t ex = block_excl_scan<kDocThreads / 64>(nk, scan_lds, C);
+    if (t <= nt) {
+        cpx[t] = ex;
+        akt[t] = ak;
+    }
+    __syncthreads();
+    const uint32_t lane = t & 63u, wv = t >> 6;
+    constexpr int kG = 4;  // chunks per thread per round (their tile searches interleave)
+    for (uint32_t c0 = 64u * wv; c0 < C; c0 += 64u * 16u * kG) {
+        uint32_t k[kG];
+#pragma unroll
+        for (int e = 0; e < kG; ++e) k[e] = 0;
+#pragma unroll
+        for (uint32_t step = 512; step; step >>= 1) {
+#pragma unroll
+            for (int e = 0; e < kG; ++e) {
+                const uint32_t c = c0 + 1024u * (uint32_t)e + lane;
+                if (k[e] + step <= nt && cpx[k[e] + step] <= c) k[e] += step;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kG; ++e) {
+            const uint32_t cb = c0 + 1024u * (uint32_t)e;  // (wave-uniform: the LDS base)
+            const uint32_t c = cb + lane;
+            if (c < C) {
+                const uint8_t* src = a.stile + (uint64_t)(t0 + k[e]) * kTileBytes + akt[k[e]] +
+                                     16u * (c - cpx[k[e]]);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)src,
+                    (__attribute__((address_space(3))) void*)(st + 16u * cb), 16, 0, 0);
+            }
+        }
+    }
+}
+
 template <int J>
 __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t p0, uint64_t toff,
                                          uint32_t tiles, uint32_t tpx_reg,
                                          const uint32_t (&ro)[J], const uint32_t (&ps)[J],
                                          uint8_t* st, uint32_t* scan_lds, uint64_t* tprobe) {
     const uint32_t t = threadIdx.x;
-    const uint32_t sh = p0 & 15u;
-    const uint32_t nq = (sh + tl + 15u) >> 4;  // staged 16-byte pieces
+    const bool glds = a.stile_text == 2u;
+    const uint32_t sh = glds ? 0u : p0 & 15u;
+    const uint32_t t0 = tiles & 0xFFFFFu, nt = tiles >> 20;
+    // staged 16-byte pieces (glds: every tile share's covering chunks, at most two partly used
+    // per tile)
+    const uint32_t nq = glds ? ((tl + 15u) >> 4) + 2u * (nt + 1u) : (sh + tl + 15u) >> 4;
     const uint32_t nw = (tl + 31u) >> 5;       // bitvector words
     const uint32_t o_bits = 16u * nq + 16u, o_pref = o_bits + 4u * nw;
     const uint32_t o_delta = (o_pref + 2u * nw + 15u) & ~15u;
-    const uint32_t t0 = tiles & 0xFFFFFu, nt = tiles >> 20;
     uint32_t mine = 0;
 #pragma unroll
     for (int j = 0; j < J; ++j) mine += ro[j] != kNil ? 1u : 0u;
     uint32_t Rw;
     (void)block_excl_scan<kDocThreads / 64>(mine, scan_lds, Rw);
     const uint32_t o_tab = (o_delta + 4u * Rw + 15u) & ~15u;
-    if (o_tab + (a.stile_text ? 8u * (nt + 2u) : 0u) > a.lds_bytes ||
-        nq > (uint32_t)(kDocQ * kDocThreads))
+    if (o_tab + (a.stile_text ? (glds ? 12u : 8u) * (nt + 2u) : 0u) > a.lds_bytes ||
+        (!glds && nq > (uint32_t)(kDocQ * kDocThreads)))
         return false;
     uint32_t* bits = reinterpret_cast<uint32_t*>(st + o_bits);
     uint16_t* pref = reinterpret_cast<uint16_t*>(st + o_pref);
     uint32_t* delta = reinterpret_cast<uint32_t*>(st + o_delta);
+    uint32_t* tab = reinterpret_cast<uint32_t*>(st + o_tab);
     // 1) staging (every load first; the run prefixes ps were loaded before the offsets)
     if (a.stile_text) {
         for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
-        stage_from_tiles(a, p0, tl, sh, t0, nt, tpx_reg, st,
-                         reinterpret_cast<uint32_t*>(st + o_tab), scan_lds);
+        if (glds)
+            stage_glds(a, p0, tl, t0, nt, tpx_reg, st, tab, scan_lds);
+        else
+            stage_from_tiles(a, p0, tl, sh, t0, nt, tpx_reg, st, tab, scan_lds);
     }
     {
         if (!a.stile_text) {
@@ -2387,12 +2498,28 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
             }
         }
         __syncthreads();
+        // (glds) the tile of every owned run's text: the last tile whose weight prefix is at or
+        // below the run's (runs do not cross tiles), ten interleaved search steps
+        uint32_t kt[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) kt[j] = 0;
+        if (glds) {
+#pragma unroll
+            for (uint32_t step = 512; step; step >>= 1) {
+#pragma unroll
+                for (int j = 0; j < J; ++j)
+                    if (ro[j] != kNil && kt[j] + step <= nt && tab[kt[j] + step] <= ps[j]) kt[j] += step;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             if (ro[j] == kNil) continue;
             const uint32_t wd = ro[j] >> 5;
             const uint32_t rank = pref[wd] + (uint32_t)__popc(bits[wd] & ((1u << (ro[j] & 31u)) - 1u));
-            delta[rank] = (ps[j] - p0 + sh) - ro[j];
+            const uint32_t so = glds ? 16u * tab[nt + 2u + kt[j]] + (ps[j] - tab[kt[j]]) -
+                                           tab[2u * (nt + 2u) + kt[j]]
+                                     : ps[j] - p0 + sh;
+            delta[rank] = so - ro[j];
         }
     }
     __syncthreads();
@@ -3811,8 +3938,10 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     p.fuse = fuse_text && p.lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
     // (a document spans at most max_doc_slots / 4096 + 2 tiles)
     p.stile_text = p.fuse && stile_text && w.max_doc_slots / kScanTile + 2u <= kDocTiles;
+    // (+ the glds staging's partly used chunks and tile table: 44 B per tile)
     p.dyn_bytes = p.fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
-                               dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u + 15u) & ~15ull))
+                               dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u +
+                                        44ull * (w.max_doc_slots / kScanTile + 3u) + 15u) & ~15ull))
                          : dbytes;
     if (doctree_lds_max && p.lds1) p.dyn_bytes = kDocLds;  // experiment: one workgroup per CU
     return p;
@@ -3905,6 +4034,21 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.wtmp = wtmp_;                                                                   \
     a.ovf = ovf_
 
+// k_runs with 16 or 32 slots per thread (Engine::runs_slots)
+void launch_k_runs(const L0Args& a0, uint32_t ntiles, hipStream_t s, uint32_t slots) {
+    if (a0.fugue) {
+        if (slots == 32)
+            k_runs<true, 32><<<ntiles, kScanTile / 32, 0, s>>>(a0);
+        else
+            k_runs<true, 16><<<ntiles, kScanTile / 16, 0, s>>>(a0);
+    } else {
+        if (slots == 32)
+            k_runs<false, 32><<<ntiles, kScanTile / 32, 0, s>>>(a0);
+        else
+            k_runs<false, 16><<<ntiles, kScanTile / 16, 0, s>>>(a0);
+    }
+}
+
 int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text,
                           uint32_t cap_runs, uint32_t cap_rmax, StageClock& ck) {
     hipStream_t s = cur_;
@@ -3924,10 +4068,7 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text
     k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
     k_tiles_top<<<1, 1024, 0, s>>>(a0, nsums);
     k_tiles_apply<<<nsums, kBlock, 0, s>>>(a0);
-    if (L.fugue)
-        k_runs<true><<<ntiles, kBlock, 0, s>>>(a0);
-    else
-        k_runs<false><<<ntiles, kBlock, 0, s>>>(a0);
+    launch_k_runs(a0, ntiles, s, runs_slots);
     k_docmax<<<1, 1024, 0, s>>>(a0);
     MARK(S_RUNS);
     HIPCHK(hipGetLastError(), "level-0 launch");
@@ -3937,10 +4078,7 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text
 // k_runs alone (run_wave: the run rows did not fit the rows allocated when level 0 ran).
 int Engine::launch_runs(DeviceLogs& L, const Wave& w, bool ord) {
     L0ARGS(a0);
-    if (L.fugue)
-        k_runs<true><<<a0.ntiles, kBlock, 0, cur_>>>(a0);
-    else
-        k_runs<false><<<a0.ntiles, kBlock, 0, cur_>>>(a0);
+    launch_k_runs(a0, a0.ntiles, cur_, runs_slots);
     HIPCHK(hipGetLastError(), "k_runs launch");
     return CRDT_HIP_OK;
 }
@@ -3972,7 +4110,7 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.probe = probe_doc_;
     da.wg = wgtab_;
     da.keyoff = doctree_key_off(p.rcap, p.scap);
-    da.stile_text = stile ? 1u : 0u;
+    da.stile_text = stile ? (stile_text == 2u ? 2u : 1u) : 0u;
     da.ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
     da.stile = stile_;
     da.tile_hw = tile_hw_;
@@ -4447,6 +4585,7 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         m.eng[i]->fuse_text = fuse_text;
         m.eng[i]->xcd_order = xcd_order;
         m.eng[i]->stile_text = stile_text;
+        m.eng[i]->runs_slots = runs_slots;
         m.eng[i]->l1_split = l1_split;
         m.eng[i]->probe_doc_ = probe_doc_;
     }
@@ -4647,6 +4786,7 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         eng[i]->fuse_text = fuse_text;
         eng[i]->xcd_order = xcd_order;
         eng[i]->stile_text = stile_text;
+        eng[i]->runs_slots = runs_slots;
         eng[i]->probe_doc_ = probe_doc_;
     }
     std::vector<int> rc(K, CRDT_HIP_OK);

@@ -215,7 +215,10 @@ public:
     // bumped by every (re)allocation of scratch, this engine's or a lane engine's (a graph that
     // captured a multi-lane merge holds the lane engines' pointers too)
     bool xcd_order = true;  // XCD-aware tile order in k_classify / k_runs (engine.hip xcd_block)
-    bool stile_text = true;  // fused plans stage text from the tile segments (L1Plan::stile_text)
+    // fused plans stage text from the tile segments (L1Plan::stile_text): 1 by 16-byte loads and
+    // funnel shifts into one contiguous image, 2 by LDS-DMA, tile by tile (engine.hip stage_glds)
+    uint32_t stile_text = 2;
+    uint32_t runs_slots = 32;  // k_runs slots per thread: 16 (256 threads per tile) or 32 (128)
     uint64_t generation() const {
         uint64_t g = gen_;
         for (const auto& e : lane_eng_) g += e->generation() + 1;

@@ -142,7 +142,9 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * lane, so that the next wave's level 0 is favoured when the two compete for the CUs),
  * "tail_wave_div" (default 0; k: a merge of several waves ends with a wave of at most
  * max_wave_slots / k slots), "xcd_order" (default 1: XCD-aware tile order in level 0),
- * "stile_text" (default 1: the per-document merge stages text from the per-tile segments),
+ * "stile_text" (default 2: the per-document merge stages text from the per-tile segments by
+ * LDS-DMA, tile by tile; 1: by loads and shifts into one contiguous image; 0: from the slot-order
+ * text k_runs then writes),
  * "nsq_list" (the compact list of the parents and keys of the items without the previous-slot
  * flag: 1 (default) = resident batches, and replicas of at least 2^22 slots, whose merges rebuild
  * it; 2 = every replica too; 0 = never), "contraction" (run contraction of RGA waves, decided

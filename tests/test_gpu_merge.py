@@ -291,9 +291,10 @@ def test_level1_lds_path_is_taken_for_trace_batches(ctx):
     assert st["stage_launches"]["expand"] == 0
     # dead runs (no visible item, no child) are dropped at level 0: the four traces number
     # 44,844 runs without the drop and ~27,160 with it (the drop is conservative at wave
-    # boundaries, so the exact count moves a little with each replica's relabelling shift); a
+    # boundaries, so the exact count moves a little with each replica's relabelling shift), plus
+    # at most one per 4096-slot tile (247 per replica of the four) since runs never cross tiles; a
     # regression that kept them would still merge correctly, so the count is checked here
-    assert 2 * 27000 < st["runs"] < 2 * 27400
+    assert 2 * 27000 < st["runs"] < 2 * 27650
 
 
 @pytest.mark.parametrize("shape", ["typing", "tree"])
