@@ -2309,8 +2309,8 @@ __device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, 
         for (uint32_t step = 512; step; step >>= 1) {
 #pragma unroll
             for (int e = 0; e < kE; ++e) {
-                const uint32_t c = kk[e] + step;
-                if (c <= nt && itp[c] <= ii[e]) kk[e] = c;
+                const uint32_t c = min(kk[e] + step, nt);  // (branch-free: reads issue together)
+                kk[e] = itp[c] <= ii[e] ? c : kk[e];
             }
         }
         uint4 q0[kE], q1[kE];
@@ -2403,12 +2403,15 @@ __device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32
         uint32_t k[kG];
 #pragma unroll
         for (int e = 0; e < kG; ++e) k[e] = 0;
+        // (branch-free: the clamped probe and a select, so that the kG reads of a step issue
+        // together instead of one exec-masked read and wait each)
 #pragma unroll
         for (uint32_t step = 512; step; step >>= 1) {
 #pragma unroll
             for (int e = 0; e < kG; ++e) {
                 const uint32_t c = c0 + 1024u * (uint32_t)e + lane;
-                if (k[e] + step <= nt && cpx[k[e] + step] <= c) k[e] += step;
+                const uint32_t q = min(k[e] + step, nt);
+                k[e] = cpx[q] <= c ? q : k[e];
             }
         }
 #pragma unroll
@@ -2454,6 +2457,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     uint16_t* pref = reinterpret_cast<uint16_t*>(st + o_pref);
     uint32_t* delta = reinterpret_cast<uint32_t*>(st + o_delta);
     uint32_t* tab = reinterpret_cast<uint32_t*>(st + o_tab);
+    if (tprobe) tprobe[1] = wall_clock64();
     // 1) staging (every load first; the run prefixes ps were loaded before the offsets)
     if (a.stile_text) {
         for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
@@ -2480,11 +2484,13 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
             }
         }
         __syncthreads();
+        if (tprobe) tprobe[2] = wall_clock64();
         // 2) run starts -> ranks in document order -> staging offset minus document offset
 #pragma unroll
         for (int j = 0; j < J; ++j)
             if (ro[j] != kNil) atomicOr(&bits[ro[j] >> 5], 1u << (ro[j] & 31u));
         __syncthreads();
+        if (tprobe) tprobe[3] = wall_clock64();
         {
             const uint32_t K = (nw + kDocThreads - 1) / kDocThreads;
             const uint32_t lo = min(nw, t * K), hi = min(nw, lo + K);
@@ -2498,29 +2504,41 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
             }
         }
         __syncthreads();
+        if (tprobe) tprobe[4] = wall_clock64();
         // (glds) the tile of every owned run's text: the last tile whose weight prefix is at or
         // below the run's (runs do not cross tiles), ten interleaved search steps
-        uint32_t kt[J];
+        // dv[j]: the run's staging offset minus its document offset (glds: the tile search
+        // result first, then turned into the delta in place)
+        uint32_t dv[J];
 #pragma unroll
-        for (int j = 0; j < J; ++j) kt[j] = 0;
+        for (int j = 0; j < J; ++j) dv[j] = 0;
         if (glds) {
 #pragma unroll
             for (uint32_t step = 512; step; step >>= 1) {
 #pragma unroll
-                for (int j = 0; j < J; ++j)
-                    if (ro[j] != kNil && kt[j] + step <= nt && tab[kt[j] + step] <= ps[j]) kt[j] += step;
+                for (int j = 0; j < J; ++j) {
+                    const uint32_t q = min(dv[j] + step, nt);  // (branch-free, as in stage_glds)
+                    dv[j] = tab[q] <= ps[j] ? q : dv[j];
+                }
             }
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                dv[j] = 16u * tab[nt + 2u + dv[j]] + (ps[j] - tab[dv[j]]) -
+                        tab[2u * (nt + 2u) + dv[j]] - ro[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < J; ++j) dv[j] = ps[j] - p0 + sh - ro[j];
         }
+        uint32_t rk[J];
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            if (ro[j] == kNil) continue;
-            const uint32_t wd = ro[j] >> 5;
-            const uint32_t rank = pref[wd] + (uint32_t)__popc(bits[wd] & ((1u << (ro[j] & 31u)) - 1u));
-            const uint32_t so = glds ? 16u * tab[nt + 2u + kt[j]] + (ps[j] - tab[kt[j]]) -
-                                           tab[2u * (nt + 2u) + kt[j]]
-                                     : ps[j] - p0 + sh;
-            delta[rank] = so - ro[j];
+            const uint32_t y = ro[j] != kNil ? ro[j] : 0u;
+            const uint32_t wd = y >> 5;
+            rk[j] = pref[wd] + (uint32_t)__popc(bits[wd] & ((1u << (y & 31u)) - 1u));
         }
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+            if (ro[j] != kNil) delta[rk[j]] = dv[j];
     }
     __syncthreads();
     if (tprobe) *tprobe = wall_clock64();
@@ -2529,7 +2547,9 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     // The run of the piece's first byte (the last start at or before it) comes from the bitvector
     // and its prefix count; every later start inside the piece (bit b of m) moves to the next run
     // in document order, whose delta is read then (an LDS read only in the lanes that have a
-    // start at b: ~1 in 11 bytes on the traces, instead of one read per byte).
+    // start at b: ~1 in 11 bytes on the traces, instead of one read per byte).  (A branch-free
+    // form that reads the first four runs' deltas up front and picks one per byte by selects
+    // made k_doctree 10 % slower: its per-byte VALU work costs more than the waits it saves.)
     for (uint32_t i = t; i < (tl + 15u) >> 4; i += kDocThreads) {
         const uint32_t y0 = 16u * i, wd = y0 >> 5, b0 = y0 & 31u;
         const uint32_t bw = bits[wd], pr = pref[wd];
@@ -2667,10 +2687,17 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     __syncthreads();
     PROBE(3);
     // ---- placement: segment start + the place the count handed out ---------------------------
+    // (every read first, unconditionally with a clamped index, then the stores: an LDS read
+    // inside a per-run branch is waited for before the next run's; here and below)
+    {
+        uint32_t dp[J];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const uint32_t p = pk[j] & 0xFFFFu;
-        if (p != kNil16) ch[D[p] + (pk[j] >> 16)] = (uint16_t)(t + (uint32_t)j * kDocThreads);
+        for (int j = 0; j < J; ++j) dp[j] = D[min(pk[j] & 0xFFFFu, R)];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const uint32_t p = pk[j] & 0xFFFFu;
+            if (p != kNil16) ch[dp[j] + (pk[j] >> 16)] = (uint16_t)(t + (uint32_t)j * kDocThreads);
+        }
     }
     __syncthreads();
     PROBE(4);
@@ -2710,7 +2737,8 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             // as a child
             const uint32_t s0 = cw[j] & 0xFFFFu, cnt = (cw[j] >> 16) - s0;
             const bool child = (pk[j] & 0xFFFFu) != kNil16;
-            const uint32_t o = (child && cnt == 2u) ? ch[s0 + ((pk[j] >> 16) ^ 1u)] : 0u;
+            const uint32_t oc = ch[min(s0 + ((pk[j] >> 16) ^ 1u), R)];
+            const uint32_t o = (child && cnt == 2u) ? oc : 0u;
             cw[j] = s0 | (child && cnt == 1u ? 1u << 14 : 0u) | (child && cnt == 2u ? 1u << 15 : 0u) |
                     (o << 16);
         }
@@ -2824,10 +2852,11 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
+            const uint32_t fch = ch[min(fcs[j] & 0xFFFFu, R)], nn = nx[min(v, R)];
             uint32_t f = fcs[j], n = 0;
             if (v < R) {
-                if (f & 0x10000u) f = ch[f & 0xFFFFu];
-                n = nx[v];
+                if (f & 0x10000u) f = fch;
+                n = nn;
                 if ((n & kUp16) && n != kNil16) act |= 1u << j;
             }
             fx[j] = (f & 0xFFFFu) | (n << 16);
@@ -2993,11 +3022,11 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            uint32_t pk = 0xFFFFFFFFu;
-            if (v < R) pk = rec32[2u * v + 1u];
+            const uint32_t pk = v < R ? rec32[2u * min(v, R) + 1u] : 0xFFFFFFFFu;
             const uint32_t sid = pk >> 18;
+            const uint32_t sr = srec[min(sid, S - 1u)];
             // weightless (or never reached: flagged below)
-            ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (srec[sid] >> 14) : kNil;
+            ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (sr >> 14) : kNil;
         }
         if (!a.text) {  // offsets for k_expand
 #pragma unroll
@@ -3048,13 +3077,15 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     if (probe) {
         printf("[doctree] doc %u R %u S %u us: load %.1f count %.1f scan %.1f place %.1f "
                "glist %.1f pairs %.1f net3-8 %.1f wide9-64 %.1f fc %.1f uplinks %.1f walk1 %.1f "
-               "jump %.1f offsets %.1f text-stage %.1f text-out %.1f total %.1f | visited %u "
-               "steps max %u sum %u\n", d, R, S,
+               "jump %.1f offsets %.1f text-stage %.1f (scan %.1f load %.1f bits %.1f pref %.1f "
+               "delta %.1f) text-out %.1f total %.1f | visited %u steps max %u sum %u\n", d, R, S,
                (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
                (tp[4] - tp[3]) / 100.0, (tp[12] - tp[4]) / 100.0, (tp[11] - tp[12]) / 100.0,
                (tp[5] - tp[11]) / 100.0, (tp[13] - tp[5]) / 100.0, (tp[14] - tp[13]) / 100.0,
                (tp[6] - tp[14]) / 100.0, (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0,
-               (tp[9] - tp[8]) / 100.0, (tp[15] - tp[9]) / 100.0, (tp[10] - tp[15]) / 100.0,
+               (tp[9] - tp[8]) / 100.0, (tp[15] - tp[9]) / 100.0, (tp[16] - tp[9]) / 100.0,
+               (tp[17] - tp[16]) / 100.0, (tp[18] - tp[17]) / 100.0, (tp[19] - tp[18]) / 100.0,
+               (tp[15] - tp[19]) / 100.0, (tp[10] - tp[15]) / 100.0,
                (tp[10] - tp[0]) / 100.0, visited_lds, probe_max, probe_sum);
     }
 #endif
