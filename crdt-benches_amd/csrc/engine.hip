@@ -132,8 +132,13 @@ struct L0Args {
     uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
     uint16_t* nsqb;             // per slot bit, 16 per thread: an item whose parent is not the
                                 //   previous slot (no previous-slot flag)
-    uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item)
+    uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item), written
+                                //   only for the 16-slot groups escm marks
     uint16_t* visb;             // per slot bit, 16 per thread: an item with a nonzero weight
+    uint64_t* escm;             // per 1024 slots: bit i = the group of slots [16 i, 16 i + 16)
+                                //   weighs other than its visible bits (a multi-byte character):
+                                //   its weights are in wnib; every other group weighs 1 byte per
+                                //   visible slot, so its nibbles are visb spread out
     uint32_t* lbits;            // Fugue: per slot bit, has a left child (its run gets a content
                                 //   node; see k_runs)
     uint32_t fugue;             // the wave holds Fugue logs (left children)
@@ -185,6 +190,18 @@ constexpr uint32_t kTileBytes = kScanTile * 4;  // worst case: every slot a 4-by
 __host__ __device__ constexpr uint64_t jbits_words(uint64_t slots) { return (slots / 32 + 8 + 3) & ~3ull; }
 constexpr uint64_t kMidKey = (1ull << 48) - 1ull;
 constexpr uint32_t kRecTree = 1u << 31;  // k_runs record of a head with two rows
+
+// 16 bits -> 16 nibbles (bit k to bit 4k), each half by three shift-or-mask steps
+__device__ __forceinline__ uint64_t spread_nib16(uint32_t v) {
+    uint32_t l8 = v & 0xFFu, h8 = (v >> 8) & 0xFFu;
+    l8 = (l8 | (l8 << 12)) & 0x000F000Fu;
+    h8 = (h8 | (h8 << 12)) & 0x000F000Fu;
+    l8 = (l8 | (l8 << 6)) & 0x03030303u;
+    h8 = (h8 | (h8 << 6)) & 0x03030303u;
+    l8 = (l8 | (l8 << 3)) & 0x11111111u;
+    h8 = (h8 | (h8 << 3)) & 0x11111111u;
+    return ((uint64_t)h8 << 32) | l8;
+}
 
 // k_classify: the characters of 16 slots per thread (3 x 16-byte loads of the codepoint column:
 // codepoint, tombstone, "parent is the previous slot" flag), then the parents of the tile's
@@ -271,15 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     if (a.mode || hi == 0u) {
         vis = a.mode ? itm : (itm & ~dm);
         W = (uint32_t)__popc(vis);
-        // 16 bits -> 16 nibbles (bit k to bit 4k), each half by three shift-or-mask steps
-        uint32_t l8 = vis & 0xFFu, h8 = vis >> 8;
-        l8 = (l8 | (l8 << 12)) & 0x000F000Fu;
-        h8 = (h8 | (h8 << 12)) & 0x000F000Fu;
-        l8 = (l8 | (l8 << 6)) & 0x03030303u;
-        h8 = (h8 | (h8 << 6)) & 0x03030303u;
-        l8 = (l8 | (l8 << 3)) & 0x11111111u;
-        h8 = (h8 | (h8 << 3)) & 0x11111111u;
-        nib = ((uint64_t)h8 << 32) | l8;
+        nib = spread_nib16(vis);
     } else {
         W = 0;
         vis = 0;
@@ -293,12 +302,16 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
             vis |= (w ? 1u : 0u) << k;
         }
     }
+    // the weight nibbles only of a group that weighs other than its visible bits (a visible
+    // multi-byte character: rare), marked in the wave's escape word; k_runs spreads the visible
+    // bits of every other group itself (the nibbles were 0.5 B per slot written and read back)
+    const bool esc = live && W != (uint32_t)__popc(vis);
+    const uint64_t em = __ballot(esc);
     if (live) {
         a.nsqb[gs >> 4] = (uint16_t)nsq;
-        // (sparse: only the groups with an escaped codepoint can weigh more than one byte per
-        // visible slot; k_runs reads the nibbles of exactly those, by the same escape bits)
-        a.wnib[gs >> 4] = nib;
+        if (esc) a.wnib[gs >> 4] = nib;
         a.visb[gs >> 4] = (uint16_t)vis;
+        if ((threadIdx.x & 63u) == 0u) a.escm[gs >> 10] = em;  // (a wave: 1024 aligned slots)
     }
     // one scan for both: nsq items << 16 | weight (a tile holds at most 4096 and 16,384)
     uint32_t tot;
@@ -640,13 +653,13 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
         const uint32_t hw32 = (gs & 63u) < 32u ? hb.x : hb.y;
         hm = SL == 32 ? hw32 : (hw32 >> (gs & 31u)) & 0xFFFFu;
         if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
-        if (SL == 32) {
-            const uint4 q = *reinterpret_cast<const uint4*>(a.wnib + (gs >> 4));
-            nib[0] = ((uint64_t)q.y << 32) | q.x;
-            nib[NQ - 1] = ((uint64_t)q.w << 32) | q.z;
-        } else {
-            nib[0] = a.wnib[gs >> 4];
-        }
+        // weights: the visible bits spread to nibbles, or (a group escm marks) its nibbles
+        const uint32_t vw = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.visb + (gs >> 4))
+                                     : (uint32_t)a.visb[gs >> 4];
+        const uint32_t e = (uint32_t)(a.escm[gs >> 10] >> ((gs >> 4) & 63u)) & ((1u << NQ) - 1u);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            nib[q] = (e >> q) & 1u ? a.wnib[(gs >> 4) + (uint32_t)q] : spread_nib16(vw >> (16 * q));
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         nsq = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.nsqb + (gs >> 4)) : a.nsqb[gs >> 4];
     }
@@ -3527,7 +3540,7 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
+    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(escm_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_); dfree(wgtab_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(rloc_); dfree(r_key_);
@@ -3796,7 +3809,7 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(hrec_); dfree(stile_); dfree(plist_);
+        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(escm_); dfree(hrec_); dfree(stile_); dfree(plist_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         // jump bits, then (Fugue) the left-child bits: jbits_words(slots) words each
@@ -3805,6 +3818,7 @@ int Engine::ensure_scratch(const Wave& w) {
         HIPCHK(dalloc(&nsqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
         HIPCHK(dalloc(&visb_, slots / 16 + 4), "hipMalloc visible bits");
+        HIPCHK(dalloc(&escm_, slots / 1024 + 4), "hipMalloc escape words");
         HIPCHK(dalloc(&hrec_, slots / 64 + 2), "hipMalloc head records");
         HIPCHK(dalloc(&stile_, tiles * kTileBytes), "hipMalloc tile text");
         HIPCHK(dalloc(&plist_, tiles * kScanTile), "hipMalloc parent lists");
@@ -4011,6 +4025,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.nsqb = nsqb_;                                                \
     a0.wnib = wnib_;                                                \
     a0.visb = visb_;                                                \
+    a0.escm = escm_;                                                \
     a0.lbits = jbits_ + jbits_words(w.nslots);                      \
     a0.fugue = L.fugue ? 1u : 0u;                                   \
     a0.stile = stile_;                                              \

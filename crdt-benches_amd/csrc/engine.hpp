@@ -259,6 +259,7 @@ private:
     uint16_t* nsqb_ = nullptr;
     uint64_t* wnib_ = nullptr;
     uint16_t* visb_ = nullptr;
+    uint64_t* escm_ = nullptr;
     uint4* hrec_ = nullptr;
     uint8_t *stile_ = nullptr, *sbytes_ = nullptr;
     uint32_t* plist_ = nullptr;
