@@ -538,6 +538,9 @@ def traces_workload(args) -> int:
         ctx.set_param("stile_text", args.stile_text)
     if args.runs_slots != 32:  # (likewise)
         ctx.set_param("runs_slots", args.runs_slots)
+    group = args.group_docs if args.group_docs >= 0 else int(args.order == "fugue")
+    if group:
+        ctx.set_param("group_docs", group)
     if args.nsq_list != 1:  # (likewise)
         ctx.set_param("nsq_list", args.nsq_list)
     ctx.set_param("lane_gate", args.lane_gate)
@@ -1004,6 +1007,9 @@ def parse_args(argv=None):
     ap.add_argument("--stile-text", type=int, default=2, choices=[0, 1, 2],
                     help="fused level 1 stages text from the tile segments (k_runs skips the "
                          "slot-order copy): 1 by loads and shifts, 2 by LDS-DMA per tile")
+    ap.add_argument("--group-docs", type=int, default=-1, choices=[-1, 0, 1],
+                    help="replica batches placed base by base, each base in waves of its own "
+                         "(-1: only for --order fugue, whose seph-blog1 rows exceed the LDS level 1)")
     ap.add_argument("--runs-slots", type=int, default=32, choices=[16, 32],
                     help="k_runs slots per thread (16: 256 threads per tile, 32: 128)")
     ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1, 2],

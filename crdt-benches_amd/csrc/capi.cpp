@@ -208,6 +208,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.xcd_order = value == 1;
         return 0;
     }
+    if (k == "group_docs") {  // replica batches: documents placed base by base (waves per base)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "group_docs must be 0 or 1");
+        ctx->eng.group_docs = value == 1;
+        return CRDT_HIP_OK;
+    }
     if (k == "runs_slots") {  // k_runs slots per thread: 16 or 32
         if (value != 16 && value != 32) return set_err(ctx, CRDT_HIP_EINVAL, "runs_slots must be 16 or 32");
         ctx->eng.runs_slots = (uint32_t)value;

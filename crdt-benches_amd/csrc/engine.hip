@@ -2180,7 +2180,7 @@ constexpr int kDocThreads = 1024;
 // dropped.  Every per-run loop is unrolled kDocJ times (the per-thread arrays live in VGPRs), so
 // kDocJ sets the code size: 20 made k_doctree 60 KB of code, 12 makes it 42 KB and the kernel
 // ~8 % faster (A/B at the headline config; an instruction cache is shared by two CUs).
-#define CRDT_DOC_J 12
+#define CRDT_DOC_J 14
 #endif
 constexpr int kDocJ = CRDT_DOC_J;  // runs per thread: documents of up to kDocJ * 1024 runs
 #ifndef CRDT_DOC_LOG2S
@@ -2244,7 +2244,7 @@ struct DocArgs {
 };
 
 // LDS bytes of a document with up to rcap - 2 runs: D, nx, ch (2 B/run each), the sibling keys
-// (8 B/run; the 8-byte run records later take D, nx, ch and the front of the keys) and the gl
+// (4 B/run, doc_key32; the 8-byte run records later take D, nx, ch and the keys) and the gl
 // region: the work list of sibling groups of three or more (at most one per three runs), later
 // the splitter records (4 B per splitter).
 __host__ __device__ constexpr uint32_t doctree_ch_bytes(uint32_t rcap, uint32_t) {
@@ -2259,15 +2259,35 @@ __host__ __device__ constexpr uint32_t doctree_gl_bytes(uint32_t rcap, uint32_t 
 __host__ __device__ constexpr uint32_t doctree_key_off(uint32_t rcap, uint32_t scap) {
     return (4u * rcap + doctree_ch_bytes(rcap, scap) + 15u) & ~15u;
 }
-__host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap) {
-    return (uint64_t)doctree_key_off(rcap, scap) + 8ull * rcap + doctree_gl_bytes(rcap, scap);
+// kb: bytes per sibling key, 8 (k_doctree) or 4 (k_doctree_wide, doc_key32)
+__host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap, uint32_t kb) {
+    return (uint64_t)doctree_key_off(rcap, scap) + (uint64_t)kb * rcap + doctree_gl_bytes(rcap, scap);
 }
 
-// Sort key: (lamport, agent) of the run's head (48 bits; Fugue: 49, with the left-child bit) and
-// the local run index (15 bits), so that equal timestamps still order deterministically (greater
-// run first, as the oracle does).  The keys were staged in LDS by the load phase.
-__device__ __forceinline__ uint64_t doc_key(const uint64_t* keys, uint32_t v) {
-    return (keys[v] << 15) | v;
+// Sort key: the run head's (lamport, agent) (Fugue: and the left-child bit) compressed to 32
+// bits for this document (doc_key32), and the local run index (15 bits), so that equal
+// timestamps still order deterministically (greater run first, as the oracle does).  The keys
+// were staged in LDS by the load phase.
+template <bool K32>
+__device__ __forceinline__ uint64_t doc_key(const void* keys, uint32_t v) {
+    if (K32) return ((uint64_t) reinterpret_cast<const uint32_t*>(keys)[v] << 15) | v;
+    return (reinterpret_cast<const uint64_t*>(keys)[v] << 15) | v;
+}
+// A run key (lamport << 16 | agent, bit 48 = a Fugue left child, kMidKey = a Fugue content row)
+// as 32 bits that order siblings the same way: left children above everything (bit 31), then
+// the content row (0x7FFFFFFF), then lamport << 8 | agent.  That holds for lamports below 2^23
+// and agents below 256 (the traces: lamport < 2^20, one agent); a document with a wider key
+// (key32_fits, checked in the load phase) goes to the global level 1, which sorts the 64-bit
+// keys.  (A per-document layout from the document's largest lamport and agent cost k_doctree 6 %:
+// the reduction kept every 64-bit key live across a barrier.)
+constexpr uint32_t kKey32Agent = 8;
+__device__ __forceinline__ bool key32_fits(uint64_t k) {  // (lamport < 2^23 - 1, agent < 256)
+    return (k & 0xFF00u) == 0u && ((k >> 16) & 0xFFFFFFFFull) < (1ull << (31 - kKey32Agent)) - 1u;
+}
+__device__ __forceinline__ uint32_t doc_key32(uint64_t k) {
+    if (k == kMidKey) return 0x7FFFFFFFu;
+    const uint32_t c = ((uint32_t)(k >> 16) << kKey32Agent) | (uint32_t)(k & 0xFFu);
+    return (k & kLeftKey) ? (c | 0x80000000u) : c;
 }
 
 // Phase C of k_doctree: expansion fused, when the document's text and its run-start index fit
@@ -2580,8 +2600,9 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     return true;
 }
 
-// One document (workgroup descriptor widx); the kernel below runs it once per descriptor.
-template <int J>
+// One document (workgroup descriptor widx); the kernel below runs it once per descriptor.  K32:
+// the sibling keys are held in LDS as doc_key32 (4 bytes per run instead of 8).
+template <int J, bool K32>
 __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     constexpr int KK = (J + (1 << kDocLog2S) - 1) >> kDocLog2S;
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
@@ -2601,8 +2622,8 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
     uint16_t* nx = D + a.rcap;
     uint16_t* ch = nx + a.rcap;
-    uint64_t* keys = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(dyn) + a.keyoff);
-    uint16_t* glist = reinterpret_cast<uint16_t*>(keys + a.rcap);  // groups of 3..64
+    uint8_t* keys = reinterpret_cast<uint8_t*>(dyn) + a.keyoff;
+    uint16_t* glist = reinterpret_cast<uint16_t*>(keys + (K32 ? 4u : 8u) * a.rcap);  // groups of 3..64
     uint32_t* srec = reinterpret_cast<uint32_t*>(glist);  // splitter records, once gl is dead
     uint2* rec = reinterpret_cast<uint2*>(dyn);           // run records, once D..keys are dead
     uint32_t* rec32 = dyn;
@@ -2651,22 +2672,29 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             gk[j] = v < R ? a.r_key[base + v] : 0ull;
         }
         for (uint32_t i = t; i < (R + 2u) / 2u; i += kDocThreads) D32[i] = 0;
-        uint32_t bad = 0;
+        uint32_t bad = 0, wide = 0;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
             uint32_t p = kNil16;
-            if (v < R) {
-                if (v) {
-                    const uint32_t lp = gp[j] - base;
-                    if (lp >= R || lp == v) bad = 1;
-                    else p = lp;
-                }
-                keys[v] = gk[j];
+            if (v < R && v) {
+                const uint32_t lp = gp[j] - base;
+                if (lp >= R || lp == v) bad = 1;
+                else p = lp;
             }
             pk[j] = p;
+            if (v < R) {
+                if (K32) {
+                    reinterpret_cast<uint32_t*>(keys)[v] = doc_key32(gk[j]);
+                    // (a key beyond the 32-bit layout: the document takes the global level 1)
+                    if (v && gk[j] != kMidKey && !key32_fits(gk[j])) wide = 1;
+                } else {
+                    reinterpret_cast<uint64_t*>(keys)[v] = gk[j];
+                }
+            }
         }
         if (bad) atomicOr(&flags, 1u);
+        if (wide) atomicOr(&flags, 2u);
     }
     __syncthreads();
     PROBE(1);
@@ -2763,7 +2791,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
                 nx[v] = (uint16_t)up;
             } else if (cw[j] & (1u << 15)) {
                 const uint32_t o = cw[j] >> 16;
-                const bool first = doc_key(keys, v) > doc_key(keys, o);
+                const bool first = doc_key<K32>(keys, v) > doc_key<K32>(keys, o);
                 ch[s0 + (first ? 0u : 1u)] = (uint16_t)v;
                 nx[v] = (uint16_t)(first ? o : up);
             }
@@ -2807,7 +2835,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) c[q] = (uint32_t)q < cnt ? ch[b + q] : 0u;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) k[q] = (uint32_t)q < cnt ? doc_key(keys, c[q]) : 0ull;
+        for (int q = 0; q < 8; ++q) k[q] = (uint32_t)q < cnt ? doc_key<K32>(keys, c[q]) : 0ull;
         cx(k[0], c[0], k[1], c[1]); cx(k[2], c[2], k[3], c[3]);
         cx(k[4], c[4], k[5], c[5]); cx(k[6], c[6], k[7], c[7]);
         cx(k[0], c[0], k[2], c[2]); cx(k[1], c[1], k[3], c[3]);
@@ -2836,7 +2864,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             if (cnt <= 8u) continue;  // wave-uniform
             const bool on = lane < cnt;
             const uint32_t c = on ? ch[s0 + lane] : 0u;
-            const uint64_t k = on ? doc_key(keys, c) : 0ull;
+            const uint64_t k = on ? doc_key<K32>(keys, c) : 0ull;
             uint32_t rank = 0;
             for (uint32_t j = 0; j < cnt; ++j) {
                 const uint64_t kj = ((uint64_t)(uint32_t)__shfl((int)(k >> 32), (int)j) << 32) |
@@ -3128,28 +3156,27 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 // walks several descriptors per workgroup spilled 34 VGPRs: not used.)
 // The document's run count picks the instance: every per-run loop is unrolled J times, so a
 // document of at most 4096 / 8192 runs skips the empty slots of the 12-run instance.
-#ifndef CRDT_DOC_JSET
-#define CRDT_DOC_JSET 1
-#endif
-template <int J>
+// Two kernels, so that the instance set of the common case stays small (every per-run loop is
+// unrolled J times; one more instance in the same kernel made k_doctree 5 % slower on the
+// traces, instruction fetch): k_doctree for documents of up to 12 runs per thread (instances
+// 4 / 8 / 12), k_doctree_wide for waves whose largest document needs more (instances 8 / 14:
+// Fugue automerge-paper and rustcode, 13.5 k and 12.6 k rows).
+constexpr int kDocJNarrow = 12;
+template <int J, bool K32>
 __device__ __forceinline__ bool doctree_try(const DocArgs& a, uint32_t R) {
-    if (J > kDocJ || R > (uint32_t)J * kDocThreads) return false;
-    doctree_doc<(J > kDocJ ? kDocJ : J)>(a, blockIdx.x);
+    if (R > (uint32_t)J * kDocThreads) return false;
+    doctree_doc<J, K32>(a, blockIdx.x);
     return true;
 }
 __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
-    (void)R;
-#if CRDT_DOC_JSET == 1
-    if (doctree_try<4>(a, R) || doctree_try<8>(a, R)) return;
-#elif CRDT_DOC_JSET == 2
-    if (doctree_try<3>(a, R) || doctree_try<7>(a, R) || doctree_try<8>(a, R) ||
-        doctree_try<10>(a, R))
-        return;
-#elif CRDT_DOC_JSET == 3
-    if (doctree_try<4>(a, R) || doctree_try<8>(a, R) || doctree_try<10>(a, R)) return;
-#endif
-    doctree_doc<kDocJ>(a, blockIdx.x);
+    if (doctree_try<4, false>(a, R) || doctree_try<8, false>(a, R)) return;
+    doctree_doc<kDocJNarrow, false>(a, blockIdx.x);
+}
+__global__ __launch_bounds__(kDocThreads) void k_doctree_wide(DocArgs a) {
+    const uint32_t R = a.wg[2u * blockIdx.x].z;
+    if (doctree_try<8, true>(a, R)) return;
+    doctree_doc<kDocJ, true>(a, blockIdx.x);
 }
 // ---------------------------------------------------------------------------------------------
 // digest: xxh64 of 4 KiB leaves, then xxh64 of the leaf digests seeded with the length
@@ -3602,16 +3629,22 @@ std::string Engine::init(int dev) {
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
         hipSuccess)
         return std::string("k_doctree LDS: ") + hipGetErrorString(e);
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree_wide),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
+        hipSuccess)
+        return std::string("k_doctree_wide LDS: ") + hipGetErrorString(e);
     return "";
 }
 
-int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
+int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs,
+                 const std::vector<uint8_t>* brk) {
     const uint64_t M = 1ull << kDocAlignLog2;  // documents start on 64-slot boundaries
     // (a new slot layout: the compact nsq list, if any, no longer matches it)
     L.nsq_ok = false;
     L.nsq_items = 0;
     L.log2m = kDocAlignLog2;
     L.docs = docs;
+    L.api_doc.clear();  // (replicate sets it again for a grouped layout)
     L.doc_slot.resize(docs.size());
     L.waves.clear();
     L.items = 0;
@@ -3641,7 +3674,7 @@ int Engine::plan(DeviceLogs& L, const std::vector<DocInfo>& docs) {
         }
         const uint64_t dt = (docs[d].text_cap + 15) & ~15ull;
         if (L.waves.empty() || (uint64_t)L.waves.back().nslots + ds > max_wave_slots ||
-            L.waves.back().text_cap + dt > kMaxWaveText || d == tail0) {
+            L.waves.back().text_cap + dt > kMaxWaveText || d == tail0 || (brk && (*brk)[d])) {
             Wave w{};
             w.first_doc = d;
             w.slot0 = slot;
@@ -3973,9 +4006,12 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     p.rmax = rmax;
     p.rcap = (rmax + 2u + 7u) & ~7u;
     p.scap = (((rmax + (1u << kDocLog2S) - 1u) >> kDocLog2S) + 8u) & ~7u;
-    const uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap);
     // per-document LDS path when the largest document's run tree fits one workgroup (sublist
-    // offsets are packed in 18 bits inside the walk: documents below 256 KiB of text)
+    // offsets are packed in 18 bits inside the walk: documents below 256 KiB of text):
+    // k_doctree (8-byte keys, 12 runs per thread), else k_doctree_wide (32-bit keys, 14)
+    uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap, 8u);
+    p.wide = rmax > (uint32_t)(kDocJNarrow * kDocThreads) || dbytes > kDocLds;
+    if (p.wide) dbytes = doctree_lds_bytes(p.rcap, p.scap, 4u);
     p.lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
              dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
     // expansion + digest fused into k_doctree when every document's text fits LDS: text staging
@@ -4162,7 +4198,10 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.tile_hw = tile_hw_;
     a.wg = wgtab_;  // (k_doctotals writes the k_doctree workgroup descriptors)
     k_doctotals<<<1, 1024, 0, s>>>(a);
-    k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+    if (p.wide)
+        k_doctree_wide<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+    else
+        k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
     MARK(S_DOCTREE);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
@@ -4528,7 +4567,8 @@ void Engine::collect(const DeviceLogs& L, uint32_t wi, uint64_t* digests, uint64
     const Wave& w = L.waves[wi];
     const uint4* r = reinterpret_cast<const uint4*>(host_block(L, wi) + 16);
     for (uint32_t k = 0; k < w.ndocs; ++k) {
-        const uint32_t d = w.first_doc + k;
+        // (a grouped replica batch: the caller's document of slot-order document first_doc + k)
+        const uint32_t d = L.api_doc.empty() ? w.first_doc + k : L.api_doc[w.first_doc + k];
         if (lens) lens[d] = r[k].x;
         if (cps) cps[d] = r[k].y;
         if (digests) digests[d] = ((uint64_t)r[k].w << 32) | r[k].z;
@@ -4921,11 +4961,31 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     if (total > 0xFFFFFFFFull) { err = "too many documents"; return CRDT_HIP_ERANGE; }
     docs.reserve(total);
     uint32_t nmax = 0;
-    for (uint64_t r = 0; r < total; ++r) docs.push_back(B.docs[r % nb]);
+    // Replica r of base r % nb is the caller's document r.  Grouped (group_docs): the documents
+    // lie in slots base by base, each base's replicas in waves of their own, so that a base whose
+    // run trees do not fit the per-document LDS level 1 (Fugue seph-blog1) sends only its own
+    // waves to the global level 1; results still come back in the caller's order (api_doc).
+    const bool grp = group_docs && nb > 1 && replicas > 1;
+    std::vector<uint32_t> order;  // slot-order document k -> the caller's document
+    std::vector<uint8_t> brk;
+    if (grp) {
+        order.reserve(total);
+        brk.assign(total, 0);
+        for (uint32_t b = 0; b < nb; ++b) {
+            brk[order.size()] = 1;
+            for (uint32_t q = 0; q < replicas; ++q) order.push_back(q * nb + b);
+        }
+    }
+    for (uint64_t k = 0; k < total; ++k) docs.push_back(B.docs[(grp ? order[k] : k) % nb]);
     for (uint32_t b = 0; b < nb; ++b) nmax = std::max(nmax, B.docs[b].n);
-    int rc = plan(R, docs);
+    int rc = plan(R, docs, grp ? &brk : nullptr);
     if (rc) return rc;
     R.fugue = B.fugue;
+    std::vector<uint64_t> rslot(R.doc_slot);  // (by the caller's document)
+    if (grp) {
+        R.api_doc = order;
+        for (uint64_t k = 0; k < total; ++k) rslot[order[k]] = R.doc_slot[k];
+    }
     std::vector<uint32_t> bn(nb);
     for (uint32_t b = 0; b < nb; ++b) bn[b] = B.docs[b].n;
     uint64_t *dbslot = nullptr, *drslot = nullptr;
@@ -4936,7 +4996,7 @@ int Engine::replicate(DeviceLogs& B, DeviceLogs& R, uint32_t replicas, uint32_t 
     hipError_t e = hipMemcpyAsync(dbslot, B.doc_slot.data(), nb * 8ull, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(dbn, bn.data(), nb * 4ull, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(drslot, R.doc_slot.data(), total * 8ull, hipMemcpyHostToDevice, stream);
+        e = hipMemcpyAsync(drslot, rslot.data(), total * 8ull, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess && nmax) {
         // one launch for the whole batch (a launch per replica made setup, and a profiler
         // serialising every dispatch, slow at 16,384 replicas)

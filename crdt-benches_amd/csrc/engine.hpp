@@ -59,6 +59,7 @@ struct StageClock {
 struct L1Plan {
     uint32_t R = 0, rmax = 0;
     bool lds1 = false, fuse = false;
+    bool wide = false;  // k_doctree_wide (32-bit keys, 14 runs per thread) instead of k_doctree
     // k_doctree stages each document's text from the per-tile segments k_classify wrote (stile),
     // so k_runs does not copy them into the slot-order text (sbytes): fused plans whose
     // documents span at most kDocTiles tiles
@@ -95,6 +96,8 @@ struct DeviceLogs {
     uint32_t log2m = 6;
     uint64_t total_slots = 0, cap_slots = 0;
     std::vector<DocInfo> docs;
+    // (grouped replica batches) slot-order document -> the caller's document; empty: the same
+    std::vector<uint32_t> api_doc;
     std::vector<uint64_t> doc_slot;  // global slot base per doc
     std::vector<Wave> waves;
     uint64_t items = 0;
@@ -178,7 +181,9 @@ public:
     std::string err;
 
     // Plan docs into waves and (re)allocate `L`'s arrays for them (contents undefined).
-    int plan(DeviceLogs& L, const std::vector<DocInfo>& docs);
+    // brk (optional, per document): 1 = start a new wave at this document
+    int plan(DeviceLogs& L, const std::vector<DocInfo>& docs,
+             const std::vector<uint8_t>* brk = nullptr);
     // Upload host views into `L` (plan first).  Synchronous.
     int upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n);
     // Build docs_rel / chunk_doc tables for L's plan.
@@ -218,7 +223,8 @@ public:
     // fused plans stage text from the tile segments (L1Plan::stile_text): 1 by 16-byte loads and
     // funnel shifts into one contiguous image, 2 by LDS-DMA, tile by tile (engine.hip stage_glds)
     uint32_t stile_text = 2;
-    uint32_t runs_slots = 32;  // k_runs slots per thread: 16 (256 threads per tile) or 32 (128)
+    uint32_t runs_slots = 32;
+    bool group_docs = false;  // replicate(): documents in slots base by base (waves per base)  // k_runs slots per thread: 16 (256 threads per tile) or 32 (128)
     uint64_t generation() const {
         uint64_t g = gen_;
         for (const auto& e : lane_eng_) g += e->generation() + 1;

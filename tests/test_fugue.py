@@ -322,6 +322,32 @@ def test_gpu_fugue_multi_wave_lanes(golden, lanes):
     c.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_gpu_fugue_grouped_batch_takes_the_lds_level1(golden, lanes):
+    """group_docs: the replicas are placed base by base, each base in waves of its own.  The
+    Fugue rows of automerge-paper (~13.5 k), rustcode (~12.6 k) and sveltecomponent fit the
+    per-document LDS level 1 (k_doctree: 14 rows per thread, 32-bit sibling keys); seph-blog1's
+    ~19 k rows take the global level 1, in their own wave only.  Results come back in the
+    caller's (replica-major) order, equal to every trace's endContent digest."""
+    c = crdt_hip.Context(0)
+    c.set_param("lanes", lanes)
+    c.set_param("group_docs", 1)
+    bases = [fugue_resolved(n) for n in TRACES]
+    b = c.batch(bases, replicas=3, relabel="rotate", seed=21)
+    for _ in range(2):  # (the second merge runs on the learnt plans)
+        dig, lens, st = b.merge()
+    for r in range(b.docs):
+        name = TRACES[r % 4]
+        assert "%016x" % dig[r] == golden[name]["tree_digest"], r
+        assert lens[r] == golden[name]["end_bytes"], r
+    assert st["waves"] == 4
+    # (two launches per LDS wave: k_doctotals and k_doctree)
+    assert st["stage_launches"]["doctree"] == 2 * 3 and st["stage_launches"]["walk1"] >= 1, st
+    b.close()
+    c.close()
+
+
 # ---- GPU: Fugue replicas (device decode of version-2 updates) --------------------------------
 _FUPD = {}
 

@@ -297,6 +297,28 @@ def test_level1_lds_path_is_taken_for_trace_batches(ctx):
     assert 2 * 27000 < st["runs"] < 2 * 27650
 
 
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_grouped_batch_returns_results_in_the_callers_order(lanes):
+    """group_docs places a replica batch base by base (each base in waves of its own); the
+    digests and lengths still come back in the caller's replica-major order, equal to the
+    ungrouped batch's, over several waves and lanes."""
+    bases = [resolved(n) for n in TRACES]
+    out = []
+    for grp in (0, 1):
+        c = crdt_hip.Context(0)
+        c.set_param("lanes", lanes)
+        c.set_param("group_docs", grp)
+        c.set_param("max_wave_slots", 1 << 20)
+        b = c.batch(bases, replicas=3, relabel="rotate", seed=8)
+        for _ in range(2):
+            dig, lens, st = b.merge()
+        out.append((dig.copy(), lens.copy(), st["waves"]))
+        b.close()
+        c.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert out[1][2] >= 4
+
+
 @pytest.mark.parametrize("shape", ["typing", "tree"])
 def test_tiles_above_the_lds_text_stage(ctx, oracle, shape):
     """Tiles holding more than k_classify's 8 KiB LDS text stage (4-byte characters, nearly all
