@@ -409,19 +409,15 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
                 bad = 1u;  // (the document start has no left children)
             } else {
                 const uint32_t ps = d.x + pj;
-                if (ps / kScanTile == tile)
-                    atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
-                else
-                    atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
                 if (left) {
                     // Fugue: the parent's run node holds its left children, so the parent must
-                    // head its run: a jump bit on the slot before it cuts the run there
+                    // head its run (k_heads cuts before every slot with a left-child bit), and
+                    // nothing more: the run goes on after it
                     atomicOr(&a.lbits[ps >> 5], 1u << (ps & 31u));
-                    const uint32_t pv = ps - 1u;
-                    if (pv / kScanTile == tile)
-                        atomicOr(&jl[(pv % kScanTile) >> 5], 1u << (pv & 31u));
-                    else
-                        atomicOr(&a.jbits[pv >> 5], 1u << (pv & 31u));
+                } else if (ps / kScanTile == tile) {
+                    atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
+                } else {
+                    atomicOr(&a.jbits[ps >> 5], 1u << (ps & 31u));
                 }
             }
         }
@@ -458,7 +454,7 @@ __device__ __forceinline__ uint64_t low_mask64(uint32_t b) {
 __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
-    uint64_t hw = 0, lv = 0, lb = 0, vs = 0;
+    uint64_t hw = 0, lv = 0, lb = 0, vs = 0, sqh = 0;
     if (gs < a.nslots) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         const uint32_t l0 = gs - doc.x, n = doc.y;
@@ -478,10 +474,15 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             const uint64_t prevj = (jw << 1) | pj;  // bit k = jump(gs + k - 1)
             const uint64_t item = low_mask64(n + 1u - l0) & ~low_mask64(l0 == 0 ? 1u : 0u);
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
-            hw = root | (item & (nsq | prevj));
-            lv = root | vis | (item & jw);
-            vs = vis;
+            // (Fugue) a slot with left children heads its run and is live: its run node holds them
             if (a.fugue) lb = *reinterpret_cast<const uint64_t*>(a.lbits + (gs >> 5));
+            hw = root | (item & (nsq | prevj | lb));
+            lv = root | vis | (item & (jw | lb));
+            vs = vis;
+            // a head whose parent is the slot before it (a seq head) makes that slot live: it is
+            // the last item of the head's parent run (RGA: that slot has a jump bit anyway)
+            sqh = hw & item & ~nsq;
+            lv |= sqh >> 1;
         }
     }
     const uint64_t hw0 = hw;  // the run boundaries (before the dead-run drop)
@@ -494,9 +495,11 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
             if (l0 <= n) hw = low_mask64(n + 1u - l0);  // (the document start and its items)
         }
     } else {
-        // the next word's live slots before its first head keep this word's last run
+        // the next word's live slots before its first head keep this word's last run, and so
+        // does a seq head in its first slot
         const uint64_t hn = (uint64_t)__shfl_down((long long)hw, 1);
         const uint64_t ln = (uint64_t)__shfl_down((long long)lv, 1);
+        lv |= (uint64_t)__shfl_down((long long)sqh, 1) << 63;
         const bool carry = (threadIdx.x & 63u) == 63u || hn == 0ull ||
                            (ln & low_mask64((uint32_t)__builtin_ctzll(hn))) != 0ull;
         uint64_t z = lv | (carry ? (1ull << 63) : 0ull);

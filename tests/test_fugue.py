@@ -326,9 +326,9 @@ def test_gpu_fugue_multi_wave_lanes(golden, lanes):
 @pytest.mark.parametrize("lanes", [1, 2])
 def test_gpu_fugue_grouped_batch_takes_the_lds_level1(golden, lanes):
     """group_docs: the replicas are placed base by base, each base in waves of its own.  The
-    Fugue rows of automerge-paper (~13.5 k), rustcode (~12.6 k) and sveltecomponent fit the
-    per-document LDS level 1 (k_doctree: 14 rows per thread, 32-bit sibling keys); seph-blog1's
-    ~19 k rows take the global level 1, in their own wave only.  Results come back in the
+    Fugue rows of automerge-paper (11.8 k), rustcode (10.7 k) and sveltecomponent (4.5 k) fit the
+    per-document LDS level 1 (k_doctree_wide: 32-bit sibling keys, up to 14 rows per thread);
+    seph-blog1's 16.6 k rows take the global level 1, in their own wave only (tools/fugue_rows.py).  Results come back in the
     caller's (replica-major) order, equal to every trace's endContent digest."""
     c = crdt_hip.Context(0)
     c.set_param("lanes", lanes)
