@@ -2183,7 +2183,7 @@ constexpr int kDocThreads = 1024;
 // dropped.  Every per-run loop is unrolled kDocJ times (the per-thread arrays live in VGPRs), so
 // kDocJ sets the code size: 20 made k_doctree 60 KB of code, 12 makes it 42 KB and the kernel
 // ~8 % faster (A/B at the headline config; an instruction cache is shared by two CUs).
-#define CRDT_DOC_J 14
+#define CRDT_DOC_J 17
 #endif
 constexpr int kDocJ = CRDT_DOC_J;  // runs per thread: documents of up to kDocJ * 1024 runs
 #ifndef CRDT_DOC_LOG2S
@@ -2259,13 +2259,21 @@ __host__ __device__ constexpr uint32_t doctree_gl_bytes(uint32_t rcap, uint32_t 
     return ((2u * doctree_defer_cap(rcap) > 4u * scap ? 2u * doctree_defer_cap(rcap) : 4u * scap) +
             15u) & ~15u;
 }
-__host__ __device__ constexpr uint32_t doctree_key_off(uint32_t rcap, uint32_t scap) {
-    return (4u * rcap + doctree_ch_bytes(rcap, scap) + 15u) & ~15u;
+// k32 (k_doctree_wide): 4-byte keys, and no nx array of its own: a run's up-arc successor is
+// written into its key slot once the key is dead (D, ch, keys: 8 B per run, + gl)
+__host__ __device__ constexpr uint32_t doctree_key_off(uint32_t rcap, uint32_t scap, bool k32) {
+    return ((k32 ? 2u : 4u) * rcap + doctree_ch_bytes(rcap, scap) + 15u) & ~15u;
 }
-// kb: bytes per sibling key, 8 (k_doctree) or 4 (k_doctree_wide, doc_key32)
-__host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap, uint32_t kb) {
-    return (uint64_t)doctree_key_off(rcap, scap) + (uint64_t)kb * rcap + doctree_gl_bytes(rcap, scap);
+__host__ __device__ constexpr uint64_t doctree_lds_bytes(uint32_t rcap, uint32_t scap, bool k32) {
+    return (uint64_t)doctree_key_off(rcap, scap, k32) + (k32 ? 4ull : 8ull) * rcap +
+           doctree_gl_bytes(rcap, scap);
 }
+// the nx array: its own u16 array, or (k32) the low half of every run's 4-byte key slot
+struct NxRef {
+    uint16_t* p;
+    uint32_t stride;
+    __device__ __forceinline__ uint16_t& operator[](uint32_t v) const { return p[stride * v]; }
+};
 
 // Sort key: the run head's (lamport, agent) (Fugue: and the left-child bit) compressed to 32
 // bits for this document (doc_key32), and the local run index (15 bits), so that equal
@@ -2623,9 +2631,9 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     (void)d;
     const uint32_t S = (R + (1u << kDocLog2S) - 1u) >> kDocLog2S;
     uint16_t* D = reinterpret_cast<uint16_t*>(dyn);
-    uint16_t* nx = D + a.rcap;
-    uint16_t* ch = nx + a.rcap;
     uint8_t* keys = reinterpret_cast<uint8_t*>(dyn) + a.keyoff;
+    const NxRef nx{K32 ? reinterpret_cast<uint16_t*>(keys) : D + a.rcap, K32 ? 2u : 1u};
+    uint16_t* ch = D + (K32 ? 1u : 2u) * a.rcap;
     uint16_t* glist = reinterpret_cast<uint16_t*>(keys + (K32 ? 4u : 8u) * a.rcap);  // groups of 3..64
     uint32_t* srec = reinterpret_cast<uint32_t*>(glist);  // splitter records, once gl is dead
     uint2* rec = reinterpret_cast<uint2*>(dyn);           // run records, once D..keys are dead
@@ -2758,9 +2766,9 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     uint32_t fcs[J];
     if (t == 0) nx[0] = kNil16;
     {
-        // cw[j]: as a child, its group's start | (1 << 14: an only child) | (1 << 15: a pair) |
-        // (the pair's other member << 16)
-        uint32_t cw[J], pw[J];
+        // cw[j]: as a child, its group's start | (the pair's other member << 16); bit j of onlym /
+        // pairm: an only child / a member of a pair (segment starts take 15 bits: up to 32 k runs)
+        uint32_t cw[J], pw[J], onlym = 0, pairm = 0;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const uint32_t p = pk[j] & 0xFFFFu, v = t + (uint32_t)j * kDocThreads;
@@ -2783,18 +2791,32 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             const bool child = (pk[j] & 0xFFFFu) != kNil16;
             const uint32_t oc = ch[min(s0 + ((pk[j] >> 16) ^ 1u), R)];
             const uint32_t o = (child && cnt == 2u) ? oc : 0u;
-            cw[j] = s0 | (child && cnt == 1u ? 1u << 14 : 0u) | (child && cnt == 2u ? 1u << 15 : 0u) |
-                    (o << 16);
+            cw[j] = s0 | (o << 16);
+            onlym |= (child && cnt == 1u ? 1u : 0u) << j;
+            pairm |= (child && cnt == 2u ? 1u : 0u) << j;
+        }
+        // (K32: nx lives in the key slots, so both members of every pair read both keys before
+        // any nx is written)
+        uint32_t firstm = 0;
+        if (K32) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const uint32_t v = t + (uint32_t)j * kDocThreads;
+                if ((pairm >> j) & 1u)
+                    firstm |= (doc_key<K32>(keys, v) > doc_key<K32>(keys, cw[j] >> 16) ? 1u : 0u) << j;
+            }
+            __syncthreads();
         }
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const uint32_t v = t + (uint32_t)j * kDocThreads;
-            const uint32_t up = (pk[j] & 0xFFFFu) | kUp16, s0 = cw[j] & 0x3FFFu;
-            if (cw[j] & (1u << 14)) {
+            const uint32_t up = (pk[j] & 0xFFFFu) | kUp16, s0 = cw[j] & 0xFFFFu;
+            if ((onlym >> j) & 1u) {
                 nx[v] = (uint16_t)up;
-            } else if (cw[j] & (1u << 15)) {
+            } else if ((pairm >> j) & 1u) {
                 const uint32_t o = cw[j] >> 16;
-                const bool first = doc_key<K32>(keys, v) > doc_key<K32>(keys, o);
+                const bool first = K32 ? ((firstm >> j) & 1u) != 0u
+                                       : doc_key<K32>(keys, v) > doc_key<K32>(keys, o);
                 ch[s0 + (first ? 0u : 1u)] = (uint16_t)v;
                 nx[v] = (uint16_t)(first ? o : up);
             }
@@ -3178,7 +3200,9 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 }
 __global__ __launch_bounds__(kDocThreads) void k_doctree_wide(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
-    if (doctree_try<8, true>(a, R)) return;
+#ifndef CRDT_WIDE_ONLY
+    if (doctree_try<12, true>(a, R)) return;
+#endif
     doctree_doc<kDocJ, true>(a, blockIdx.x);
 }
 // ---------------------------------------------------------------------------------------------
@@ -4012,9 +4036,9 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     // per-document LDS path when the largest document's run tree fits one workgroup (sublist
     // offsets are packed in 18 bits inside the walk: documents below 256 KiB of text):
     // k_doctree (8-byte keys, 12 runs per thread), else k_doctree_wide (32-bit keys, 14)
-    uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap, 8u);
+    uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap, false);
     p.wide = rmax > (uint32_t)(kDocJNarrow * kDocThreads) || dbytes > kDocLds;
-    if (p.wide) dbytes = doctree_lds_bytes(p.rcap, p.scap, 4u);
+    if (p.wide) dbytes = doctree_lds_bytes(p.rcap, p.scap, true);
     p.lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
              dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
     // expansion + digest fused into k_doctree when every document's text fits LDS: text staging
@@ -4194,7 +4218,7 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.lds_bytes = (uint32_t)p.dyn_bytes;
     da.probe = probe_doc_;
     da.wg = wgtab_;
-    da.keyoff = doctree_key_off(p.rcap, p.scap);
+    da.keyoff = doctree_key_off(p.rcap, p.scap, p.wide);
     da.stile_text = stile ? (stile_text == 2u ? 2u : 1u) : 0u;
     da.ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
     da.stile = stile_;
