@@ -3181,11 +3181,14 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 // walks several descriptors per workgroup spilled 34 VGPRs: not used.)
 // The document's run count picks the instance: every per-run loop is unrolled J times, so a
 // document of at most 4096 / 8192 runs skips the empty slots of the 12-run instance.
-// Two kernels, so that the instance set of the common case stays small (every per-run loop is
-// unrolled J times; one more instance in the same kernel made k_doctree 5 % slower on the
-// traces, instruction fetch): k_doctree for documents of up to 12 runs per thread (instances
-// 4 / 8 / 12), k_doctree_wide for waves whose largest document needs more (instances 8 / 14:
-// Fugue automerge-paper and rustcode, 13.5 k and 12.6 k rows).
+// Three kernels, so that the instance set of the common case stays small (every per-run loop is
+// unrolled J times; one more instance in the same kernel made k_doctree 5 % slower on the traces,
+// instruction fetch): k_doctree for documents of up to 12 runs per thread with 8-byte keys
+// (instances 4 / 8 / 12: the RGA traces), k_doctree_wide for waves whose largest document does
+// not fit those 15 bytes of LDS per run (32-bit keys and nx in the key slots: 9 bytes; instances
+// 8 / 12: Fugue automerge-paper and rustcode, 11.8 k and 10.7 k rows), k_doctree_wide17 for up to
+// 17 rows per thread (Fugue seph-blog1, 16.6 k rows; 8 VGPRs spill on its own, ~40 inside
+// k_doctree_wide).
 constexpr int kDocJNarrow = 12;
 template <int J, bool K32>
 __device__ __forceinline__ bool doctree_try(const DocArgs& a, uint32_t R) {
@@ -3200,9 +3203,12 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
 }
 __global__ __launch_bounds__(kDocThreads) void k_doctree_wide(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
-#ifndef CRDT_WIDE_ONLY
-    if (doctree_try<12, true>(a, R)) return;
-#endif
+    if (doctree_try<8, true>(a, R)) return;
+    doctree_doc<kDocJNarrow, true>(a, blockIdx.x);
+}
+// (its own kernel: the 17 runs per thread spill ~40 VGPRs, which the 12-run instance beside them
+// would pay for in scratch allocation and register pressure)
+__global__ __launch_bounds__(kDocThreads) void k_doctree_wide17(DocArgs a) {
     doctree_doc<kDocJ, true>(a, blockIdx.x);
 }
 // ---------------------------------------------------------------------------------------------
@@ -3660,6 +3666,10 @@ std::string Engine::init(int dev) {
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
         hipSuccess)
         return std::string("k_doctree_wide LDS: ") + hipGetErrorString(e);
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree_wide17),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
+        hipSuccess)
+        return std::string("k_doctree_wide17 LDS: ") + hipGetErrorString(e);
     return "";
 }
 
@@ -4225,7 +4235,9 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.tile_hw = tile_hw_;
     a.wg = wgtab_;  // (k_doctotals writes the k_doctree workgroup descriptors)
     k_doctotals<<<1, 1024, 0, s>>>(a);
-    if (p.wide)
+    if (p.wide && p.rmax > (uint32_t)(kDocJNarrow * kDocThreads))
+        k_doctree_wide17<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+    else if (p.wide)
         k_doctree_wide<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
     else
         k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
