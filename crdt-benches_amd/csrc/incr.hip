@@ -55,10 +55,11 @@ constexpr uint32_t kSpliceTile = kIncThreads * kSpliceRanks;        // old ranks
 constexpr uint32_t kIncGroupMax = 1024;  // largest sibling group ranked in inc_forest
 constexpr uint32_t kIncThinGroup = 32;   // more roots than this: ranked one wave per root
 // Roots that do not sort above every old item (a concurrent insert) take their place from a
-// search of their parent's old subtree (k_inc_search, one workgroup per root, before k_inc): at
-// most kIncHard of them per call, each search over at most kIncScan ranks (else the call merges
-// in full)
+// search of their parent's old subtree (inc_search, by k_inc's first kIncSearchers workgroups):
+// at most kIncHard of them per call, each search over at most kIncScan ranks (else the call
+// merges in full)
 constexpr uint32_t kIncHard = 256;
+constexpr uint32_t kIncSearchers = 16;
 constexpr uint32_t kIncScan = 1u << 16;
 #ifndef CRDT_INC_RUNS
 #define CRDT_INC_RUNS 1
@@ -94,7 +95,8 @@ struct IncArgs {
     uint64_t* tsp;              // (CRDT_INC_PROFILE) phase timestamps of the forest, or null
     uint64_t call;              // this call's number (a stale result block is detected)
     const uint32_t* hasl;       // (Fugue) 1 bit per old slot: it has a left child
-    uint32_t* hanc;             // per new item: a searched root's anchor rank (k_inc_search)
+    uint64_t* hanc;             // per new item: a searched root's anchor rank | call << 32
+    uint32_t nsearch;           // leading workgroups of k_inc that search (0: none, Fugue)
 };
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32i_t;
@@ -176,15 +178,15 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     // parent's children).  The counts are cleared while the loads are in flight ----
     uint32_t plc[Q];
     uint64_t kmax = 0;
+    uint32_t hq = 0;  // (RGA) this thread's roots whose place a search gives
     {
-        uint32_t pp[Q], ha[Q];
+        uint32_t pp[Q];
         uint64_t kk[Q];
 #pragma unroll
         for (int q = 0; q < (int)Q; ++q) {
             const uint32_t i = t + (uint32_t)q * kIncThreads;
             pp[q] = i < m ? a.parent[n0 + 1u + i] : 0u;
             kk[q] = i < m ? a.key[n0 + 1u + i] : 0ull;
-            ha[q] = !FG && i < m ? a.hanc[i] : 0u;
         }
         uint32_t bad = 0;
 #pragma unroll
@@ -216,13 +218,10 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
                 li = m;
                 A[i] = PR[i] = a.rank[pp[q]];
                 if (kk[q] <= maxkey0) {
-                    // some old sibling may sort above it: its place came from k_inc_search,
-                    // which searched the first kIncHard such roots
-                    const uint32_t h = atomicAdd(&nhard, 1u);
-                    if (h < kIncHard && ha[q] != 0xFFFFFFFFu)
-                        A[i] = ha[q];
-                    else
-                        bad |= (uint32_t)F_KEY;
+                    // some old sibling may sort above it: its place comes from the search
+                    // workgroups (taken below, once every such root is counted)
+                    hq |= 1u << q;
+                    atomicAdd(&nhard, 1u);
                 }
             } else {
                 const uint32_t l = pp[q] - (n0 + 1u);
@@ -238,6 +237,27 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
     }
     INC_TS(1);
     __syncthreads();
+    if (!FG && nhard) {
+        // the searched anchors (published by the leading workgroups, stamped with the call);
+        // more roots than kIncHard: none was searched, the call merges in full
+        if (nhard > kIncHard) {
+            if (t == 0) atomicOr(&flag, (uint32_t)F_KEY);
+        } else {
+#pragma unroll
+            for (int q = 0; q < (int)Q; ++q) {
+                if (!((hq >> q) & 1u)) continue;
+                const uint32_t i = t + (uint32_t)q * kIncThreads;
+                uint64_t v;
+                while ((uint32_t)((v = __hip_atomic_load(&a.hanc[i], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (uint32_t)a.call)
+                    __builtin_amdgcn_s_sleep(2);
+                if ((uint32_t)v != 0xFFFFFFFFu)
+                    A[i] = (uint32_t)v;
+                else
+                    atomicOr(&flag, (uint32_t)F_KEY);
+            }
+        }
+    }
     INC_TS(2);
     // ---- segment starts: exclusive scan over nodes 0..m (m + 1 <= kIncMax + 1 counts) ----
     {
@@ -490,9 +510,9 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
         }
     }
     INC_TS(9);
-    // the largest key now held, for the next call's check (workgroup 0; the slot this call
-    // writes is not the one any workgroup of it reads)
-    if (blockIdx.x == 0) {
+    // the largest key now held, for the next call's check (tile 0; the slot this call writes is
+    // not the one any workgroup of it reads)
+    if (blockIdx.x == a.nsearch) {
         uint64_t km = max(kmax, maxkey0);
 #pragma unroll
         for (int o = 32; o; o >>= 1) {
@@ -675,66 +695,67 @@ __device__ __forceinline__ void inc_text_tile(const IncArgs& a, uint2 range, uin
     }
 }
 
-// ---- k_inc_search: the places of the roots that may sort below an old sibling (concurrent
-// inserts), once per call, before k_inc.  In the RGA pre-order a root x of key k under old parent
-// p follows p's old children that sort above it, with their subtrees, so it goes before the first
+// ---- the places of the roots that may sort below an old sibling (concurrent inserts), by the
+// first a.nsearch workgroups of k_inc.  In the RGA pre-order a root x of key k under old parent p
+// follows p's old children that sort above it, with their subtrees, so it goes before the first
 // rank after p that holds an old child of p with a key <= k (x's id is greater than every old one:
 // equal keys put x first) or that leaves p's subtree (an item whose parent ranks before p); its
-// anchor is the rank before that.  Workgroup b searches the b-th such root in item order (at most
-// kIncHard workgroups), kSearchRound ranks per round; k_inc reads the anchors from hanc (a search
-// that ran kIncScan ranks without an answer leaves 0xFFFFFFFF: k_inc then merges in full).
-constexpr uint32_t kSearchThreads = 1024;
+// anchor is the rank before that.  Search workgroup b takes the roots b, b + nsearch, ... in item
+// order, kSearchRound ranks per round, and publishes each anchor stamped with the call (a search
+// that ran kIncScan ranks without an answer publishes 0xFFFFFFFF: the call merges in full).  The
+// tile workgroups wait for the stamps only when they hold such roots; the searchers come first in
+// the grid and wait for nothing, so they are dispatched before any tile that waits on them.
+constexpr uint32_t kSearchThreads = kIncThreads;
 constexpr uint32_t kSearchPer = kIncMax / kSearchThreads;       // items (and ranks) per thread
 constexpr uint32_t kSearchRound = kSearchThreads * kSearchPer;  // ranks per round
 static_assert(kIncScan % kSearchRound == 0, "search rounds");
-__global__ __launch_bounds__(kSearchThreads) void k_inc_search(IncArgs a) {
-    __shared__ uint32_t red[kSearchThreads / 64];
-    __shared__ uint32_t target, found;
-    const uint32_t t = threadIdx.x, b = blockIdx.x, m = a.m, n0 = a.n0;
+__device__ __forceinline__ void inc_search(const IncArgs& a, uint32_t sb, uint32_t* red,
+                                           uint32_t& target, uint32_t& found) {
+    const uint32_t t = threadIdx.x, m = a.m, n0 = a.n0;
     const uint64_t maxkey0 = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
-    // this workgroup's root: the b-th new item with an old parent and a key not above every old one
     uint32_t hard = 0;
 #pragma unroll
     for (int q = 0; q < (int)kSearchPer; ++q) {
         const uint32_t i = t * kSearchPer + (uint32_t)q;
         if (i < m && a.parent[n0 + 1u + i] <= n0 && a.key[n0 + 1u + i] <= maxkey0) hard |= 1u << q;
     }
-    if (t == 0) {
-        target = 0xFFFFFFFFu;
-        found = 0xFFFFFFFFu;
-    }
     uint32_t tot;
     const uint32_t ex = block_excl_scan<kSearchThreads / 64>((uint32_t)__popc(hard), red, tot);
-    if (b >= ex && b < ex + (uint32_t)__popc(hard)) {
-        uint32_t h = hard;
-        for (uint32_t k = b - ex; k; --k) h &= h - 1u;  // (the (b - ex)-th set bit)
-        target = t * kSearchPer + (uint32_t)__ffs(h) - 1u;
-    }
-    __syncthreads();
-    const uint32_t i = target;
-    if (i == 0xFFFFFFFFu) return;  // (fewer such roots than workgroups: block-uniform)
-    const uint32_t p = a.parent[n0 + 1u + i], r0 = a.rank[p];
-    const uint64_t k = a.key[n0 + 1u + i];
-    uint32_t f = 0xFFFFFFFFu;
-    for (uint32_t c = 0; c < kIncScan; c += kSearchRound) {
-        uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-        for (int q = 0; q < (int)kSearchPer; ++q) {
-            const uint32_t r = r0 + 1u + c + (uint32_t)q * kSearchThreads + t;
-            bool stop = r > n0;  // (the document's end)
-            if (!stop) {
-                const uint32_t sl = a.seq[r], pr = a.parent[sl];
-                stop = pr == p ? a.key[sl] <= k : a.rank[pr] < r0;
-            }
-            if (stop) best = min(best, r);
+    if (tot > kIncHard) return;  // (block-uniform: the tiles merge in full without waiting)
+    for (uint32_t b = sb; b < tot; b += a.nsearch) {
+        if (b >= ex && b < ex + (uint32_t)__popc(hard)) {  // (the (b - ex)-th set bit: one thread)
+            uint32_t h = hard;
+            for (uint32_t k = b - ex; k; --k) h &= h - 1u;
+            target = t * kSearchPer + (uint32_t)__ffs(h) - 1u;
+            found = 0xFFFFFFFFu;
         }
-        if (best != 0xFFFFFFFFu) atomicMin(&found, best);
         __syncthreads();
-        f = found;
-        __syncthreads();  // (every thread has read it before the next round's atomics)
-        if (f != 0xFFFFFFFFu) break;  // (block-uniform)
+        const uint32_t i = target;
+        const uint32_t p = a.parent[n0 + 1u + i], r0 = a.rank[p];
+        const uint64_t k = a.key[n0 + 1u + i];
+        uint32_t f = 0xFFFFFFFFu;
+        for (uint32_t c = 0; c < kIncScan; c += kSearchRound) {
+            uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+            for (int q = 0; q < (int)kSearchPer; ++q) {
+                const uint32_t r = r0 + 1u + c + (uint32_t)q * kSearchThreads + t;
+                bool stop = r > n0;  // (the document's end)
+                if (!stop) {
+                    const uint32_t sl = a.seq[r], pr = a.parent[sl];
+                    stop = pr == p ? a.key[sl] <= k : a.rank[pr] < r0;
+                }
+                if (stop) best = min(best, r);
+            }
+            if (best != 0xFFFFFFFFu) atomicMin(&found, best);
+            __syncthreads();
+            f = found;
+            __syncthreads();  // (every thread has read it before the next round's atomics)
+            if (f != 0xFFFFFFFFu) break;  // (block-uniform)
+        }
+        if (t == 0)
+            __hip_atomic_store(&a.hanc[i], ((uint64_t)(uint32_t)a.call << 32) | (f != 0xFFFFFFFFu ? f - 1u : 0xFFFFFFFFu),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (t == 0) a.hanc[i] = f != 0xFFFFFFFFu ? f - 1u : 0xFFFFFFFFu;
 }
 
 // ---- the whole incremental merge in one launch: one workgroup per tile of old ranks ------------
@@ -748,7 +769,11 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     __shared__ uint32_t cb[2];
     __shared__ uint32_t flag, nhard;
     __shared__ uint64_t excl_lds;
-    const uint32_t b = blockIdx.x;
+    if (blockIdx.x < a.nsearch) {  // (block-uniform: a search workgroup)
+        inc_search(a, blockIdx.x, red, flag, nhard);
+        return;
+    }
+    const uint32_t b = blockIdx.x - a.nsearch;  // the tile
     // the tile's old order, loaded before the forest so that the round trip overlaps it
     uint32_t sl[kSpliceRanks];
     {
@@ -778,7 +803,7 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
     }
     if (!a.m && threadIdx.x == 0) {
         flag = 0;
-        if (blockIdx.x == 0) {  // (carry the largest key over to this call's slot)
+        if (b == 0) {  // (carry the largest key over to this call's slot)
             const uint64_t km = a.ctl[I_MAXKEY + ((a.call & 1u) ^ 1u)];
             atomicMax(reinterpret_cast<unsigned long long*>(&a.ctl[I_MAXKEY + (a.call & 1u)]),
                       (unsigned long long)km);
@@ -800,7 +825,7 @@ __global__ __launch_bounds__(kIncThreads) void k_inc(IncArgs a) {
         if (base + agg.x <= a.text_cap) inc_text_tile(a, range, base, cwl, red);
         tot = excl + agg64;
     }
-    if (b + 1u == gridDim.x && threadIdx.x == 0) {
+    if (b + 1u == a.nblk && threadIdx.x == 0) {
         const uint64_t bytes = (uint32_t)tot, cps = tot >> 32;
         a.hres[0] = f ? f : (bytes > a.text_cap ? F_TEXT : 0u);
         a.hres[1] = bytes;
@@ -933,7 +958,10 @@ int inc_reserve(Engine& E, IncState& s, uint64_t items, uint64_t bytes) {
     const uint64_t tcap = bytes + 64;
     if (tcap > s.text_cap)
         ICHK(igrow(&s.text, s.text_cap, std::max<uint64_t>(tcap, 2 * s.text_cap)), "hipMalloc text");
-    if (!s.hanc) ICHK(dalloc(&s.hanc, (uint64_t)kIncMax), "hipMalloc search anchors");
+    if (!s.hanc) {  // (stamps of call 0: no call reads them)
+        ICHK(dalloc(&s.hanc, (uint64_t)kIncMax), "hipMalloc search anchors");
+        ICHK(hipMemset(s.hanc, 0, kIncMax * 8ull), "clear search anchors");
+    }
     if (!s.ctl) {
         ICHK(dalloc(&s.ctl, (uint64_t)I_N), "hipMalloc counters");
         ICHK(hipMemset(s.ctl, 0, I_N * 8), "clear counters");
@@ -1006,11 +1034,9 @@ int inc_run(Engine& E, IncState& s, IncArgs& a, bool sync) {
     a.tsp = prof ? tsp : nullptr;
     const auto h0 = std::chrono::steady_clock::now();
     if (prof) ICHK(hipEventRecord(ev[0], st), "event");
-    if (a.m && !a.hasl) {  // (RGA: the searched roots' anchors, once per call)
-        k_inc_search<<<std::min(a.m, kIncHard), kSearchThreads, 0, st>>>(a);
-        ICHK(hipGetLastError(), "incremental merge search launch");
-    }
-    k_inc<<<std::max<uint32_t>(1, a.nblk), kIncThreads, inc_forest_lds(kIncMax), st>>>(a);
+    // (RGA: leading search workgroups for the roots an old sibling may precede)
+    a.nsearch = a.m && !a.hasl ? std::min(a.m, kIncSearchers) : 0u;
+    k_inc<<<a.nsearch + a.nblk, kIncThreads, inc_forest_lds(kIncMax), st>>>(a);
     ICHK(hipGetLastError(), "incremental merge launch");
     if (prof) ICHK(hipEventRecord(ev[1], st), "event");
     const auto h1 = std::chrono::steady_clock::now();

@@ -34,7 +34,7 @@ struct IncState {
     uint32_t* hasl = nullptr;
     // per new item (kIncMax): the anchor rank found by k_inc_search for a root whose key is not
     // above every old key (0xFFFFFFFF: the search ran out of range)
-    uint32_t* hanc = nullptr;
+    uint64_t* hanc = nullptr;
     uint32_t* lb_flag = nullptr;     // per tile of the order: look-back status, aggregate and
     uint64_t* lb_agg = nullptr;      //   inclusive prefix of the text (incr.hip inc_lookback)
     uint64_t* lb_inc = nullptr;
