@@ -642,9 +642,12 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * SL;
     uint32_t hm = 0, nsq = 0, dm = 0;
-    uint64_t nib[NQ];
+    // weights: the visible bits (vw) of groups without a visible multi-byte character; a thread
+    // holding an escaped group (e) takes its slots' nibbles: 8 slots per word nwd
+    uint32_t vw = 0, e = 0;
+    uint32_t nwd[2 * NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) nib[q] = 0;
+    for (int q = 0; q < 2 * NQ; ++q) nwd[q] = 0;
     uint2 doc = make_uint2(0, 0);
     const uint2 pre = a.tile_hw[tile];
     // the parents of the tile's nsq items: the compact list of a resident batch, else the tile's
@@ -656,13 +659,16 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
         const uint32_t hw32 = (gs & 63u) < 32u ? hb.x : hb.y;
         hm = SL == 32 ? hw32 : (hw32 >> (gs & 31u)) & 0xFFFFu;
         if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
-        // weights: the visible bits spread to nibbles, or (a group escm marks) its nibbles
-        const uint32_t vw = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.visb + (gs >> 4))
-                                     : (uint32_t)a.visb[gs >> 4];
-        const uint32_t e = (uint32_t)(a.escm[gs >> 10] >> ((gs >> 4) & 63u)) & ((1u << NQ) - 1u);
+        vw = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.visb + (gs >> 4)) : (uint32_t)a.visb[gs >> 4];
+        e = (uint32_t)(a.escm[gs >> 10] >> ((gs >> 4) & 63u)) & ((1u << NQ) - 1u);
+        if (e) {  // (rare: the nibbles of the escaped groups, the visible bits spread for the rest)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q)
-            nib[q] = (e >> q) & 1u ? a.wnib[(gs >> 4) + (uint32_t)q] : spread_nib16(vw >> (16 * q));
+            for (int q = 0; q < NQ; ++q) {
+                const uint64_t nb = (e >> q) & 1u ? a.wnib[(gs >> 4) + (uint32_t)q] : spread_nib16(vw >> (16 * q));
+                nwd[2 * q] = (uint32_t)nb;
+                nwd[2 * q + 1] = (uint32_t)(nb >> 32);
+            }
+        }
         doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         nsq = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.nsqb + (gs >> 4)) : a.nsqb[gs >> 4];
     }
@@ -679,9 +685,15 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
         w0 = s32[threadIdx.x];
         w1 = s32[threadIdx.x + 1];
     }
+    // the weight before each nibble word (v_dot8 sums eight nibbles), and the thread's weight
+    uint32_t nwc[2 * NQ];
     uint32_t W = 0;
 #pragma unroll
-    for (int j = 0; j < SL; ++j) W += (uint32_t)(nib[j >> 4] >> (4 * (j & 15))) & 15u;
+    for (int q = 0; q < 2 * NQ; ++q) {
+        nwc[q] = W;
+        W = __builtin_amdgcn_udot8(nwd[q], 0x11111111u, W, false);
+    }
+    if (!e) W = (uint32_t)__popc(vw);
     const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;  // heads (records) << 16 | weight
     const uint32_t inc = wave_incl_scan(x);
     const uint32_t cq = (uint32_t)__popc(nsq), incq = wave_incl_scan(cq);
@@ -747,17 +759,31 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
     // next head's weight prefix), then one thread per head of the window; block-uniform loop
     for (uint32_t h0 = 0;; h0 += kWin) {
         {
-            uint32_t r = ex >> 16, p = ex & 0xFFFFu;
+            // the thread's heads one by one (a lane holds ~1 on the traces), each record's weight
+            // prefix = the thread's prefix + the weight of its slots below the head
+            uint32_t r = ex >> 16;
+            const uint32_t p0 = ex & 0xFFFFu;
             if (r <= h0 + kWin && r + (uint32_t)__popc(hm) > h0) {
+                for (uint32_t m = hm; m; m &= m - 1u) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(m);
+                    uint32_t p;
+                    if (!e) {
+                        p = (uint32_t)__popc(vw & ((1u << j) - 1u));
+                    } else {
+                        const uint32_t wi = j >> 3;
+                        uint32_t xw = nwd[0], cw = nwc[0];
 #pragma unroll
-                for (int j = 0; j < SL; ++j) {
-                    if (hm & (1u << j)) {
-                        if (r >= h0 && r - h0 <= kWin)
-                            rec[r - h0] = ((threadIdx.x * SL + (uint32_t)j) << 16) | p |
-                                          ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
-                        ++r;
+                        for (int q = 1; q < 2 * NQ; ++q)
+                            if (wi == (uint32_t)q) {
+                                xw = nwd[q];
+                                cw = nwc[q];
+                            }
+                        p = __builtin_amdgcn_udot8(xw & ((1u << (4u * (j & 7u))) - 1u), 0x11111111u, cw, false);
                     }
-                    p += (uint32_t)(nib[j >> 4] >> (4 * (j & 15))) & 15u;
+                    if (r >= h0 && r - h0 <= kWin)
+                        rec[r - h0] = ((threadIdx.x * SL + j) << 16) | (p0 + p) |
+                                      ((dm >> j) & 1u ? kRecTree : 0u);  // (Fugue: two rows)
+                    ++r;
                 }
             }
         }
