@@ -455,8 +455,10 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     const uint32_t wi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t gs = wi * 64u;
     uint64_t hw = 0, lv = 0, lb = 0, vs = 0, sqh = 0;
+    uint32_t dbase = 0;  // the word's document start (hrec .w: k_runs reads it there)
     if (gs < a.nslots) {
         const uint2 doc = a.docs[a.chunk_doc[gs >> a.log2m]];
+        dbase = doc.x;
         const uint32_t l0 = gs - doc.x, n = doc.y;
         if (l0 <= n) {
             const uint64_t nsq = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
@@ -534,7 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
     // Fugue: a head with left children numbers two run rows (k_runs)
     const uint32_t c = (uint32_t)__popcll(hw) + (uint32_t)__popcll(hw & lb);
     const uint32_t inc = wave_incl_scan(c);
-    if (gs < a.nslots) a.hrec[wi] = make_uint4((uint32_t)hw, (uint32_t)(hw >> 32), inc - c, 0u);
+    if (gs < a.nslots) a.hrec[wi] = make_uint4((uint32_t)hw, (uint32_t)(hw >> 32), inc - c, dbase);
     const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     const uint32_t tile = wi >> 6;  // 64 words per tile: one wave
     if ((threadIdx.x & 63u) == 0 && tile < a.ntiles) a.tile_hw[tile].x = th;
@@ -655,8 +657,12 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
     const uint32_t nlo = a.nsq_par ? a.nsq_pre[tile * (kScanTile / 64)] : 0u;
     const uint32_t* pls = a.nsq_par ? a.nsq_par + nlo : a.plist + (uint64_t)tile * kScanTile;
     if (gs < a.nslots) {
-        const uint2 hb = *reinterpret_cast<const uint2*>(a.hrec + (gs >> 6));
+        // the head bits and (.w) the document start from the word's head record; the document's
+        // item count only where the parents are checked here (no contraction)
+        const uint4 hb = a.hrec[gs >> 6];
         const uint32_t hw32 = (gs & 63u) < 32u ? hb.x : hb.y;
+        doc = make_uint2(hb.w, 0xFFFFFFFFu);
+        if (a.nocon) doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         hm = SL == 32 ? hw32 : (hw32 >> (gs & 31u)) & 0xFFFFu;
         if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
         vw = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.visb + (gs >> 4)) : (uint32_t)a.visb[gs >> 4];
@@ -669,7 +675,6 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
                 nwd[2 * q + 1] = (uint32_t)(nb >> 32);
             }
         }
-        doc = a.docs[a.chunk_doc[gs >> a.log2m]];
         nsq = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.nsqb + (gs >> 4)) : a.nsqb[gs >> 4];
     }
     lnsq[threadIdx.x] = nsq;
@@ -845,8 +850,7 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
             if (sq) {
                 pr = rho - 1u;  // the parent is the slot before the head: the previous run's last row
             } else if (!root) {
-                const uint32_t p = ps - dc.x;
-                if (p > dc.y || p == g - dc.x) ps = dc.x;  // flagged by k_classify
+                if (ps >= a.nslots) ps = dc.x;  // (a bad parent, flagged by k_classify: any in-range read)
                 const uint4 hr = a.hrec[ps >> 6];
                 const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
                 const uint32_t hl = hr.z;
