@@ -64,12 +64,15 @@ MIN_B_PER_TEXT = 1.0
 # Per-kernel algorithmic bytes: each kernel's declared inputs read once +
 # outputs written once, as (bytes per item slot, bytes per run, bytes per visible UTF-8 byte).
 KERNEL_BYTES = {
-    # 3-byte cp|flags in; nsq + visible bits, weight nibbles, jump bits out; parents of the nsq
-    # items read + listed (counted per run); tile UTF-8
-    "classify": (3.875, 8.0, 1.0),
-    # head stage (k_heads: nsq/visible/jump bits in, head records out) and k_runs: head records,
-    # nibbles; per run: key + parent slot + rank lookup in, record row out; text move
-    "runs": (0.875, 38.0, 2.0),
+    # 3-byte cp|flags in; nsq + visible bits, jump bits, the escape word (1/128 B) out (weight
+    # nibbles only for 16-slot groups with a visible multi-byte character: ~0 on the traces);
+    # parents of the nsq items read + listed (counted per run); tile UTF-8 (stile) out
+    "classify": (3.3828125, 8.0, 1.0),
+    # head stage (k_heads: nsq, visible and both jump bitvectors in, head records out) and k_runs
+    # (head records, visible and nsq bits in); per run: key + parent slot + rank lookup in, record
+    # row out; the tile text moved to sbytes only when a later kernel reads it there (k_expand,
+    # or stile_text 0): k_doctree's default staging reads the stile segments themselves
+    "runs": (1.25, 38.0, 2.0),
     # global level 1, sibling groups by counting: parent in + child count (count), placement
     # (place), keys and links (link); the radix form is priced in level1_run_bytes below
     "count": (0.0, 4.0, 0.0),
@@ -434,10 +437,11 @@ def traces_rank(args, comm, make_batch, inputs) -> dict | None:
     return res if rank == 0 else None
 
 
-def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> dict:
+def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True, stile_text: int = 2) -> dict:
     """Per-kernel algorithmic GB/s, the dominant kernel's roofline, the pipeline's fraction.
     pmc: the PMC traffic file describes this workload (the headline config); else traffic is
-    null rather than another workload's bytes."""
+    null rather than another workload's bytes.  stile_text: the engine parameter (0: k_runs
+    copies every tile's text to sbytes for k_doctree)."""
     stage_ns = {k: float(np.mean([s["stage_ns"][k] for s in stats])) for k in stats[0]["stage_ns"]}
     launches = stats[0]["stage_launches"]
     slots = items_per_gpu + batch.docs  # items + one document-start slot per document
@@ -457,6 +461,9 @@ def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True) -> di
         per_slot, per_run, per_text = KERNEL_BYTES[k]
         if k == "doctree" and launches.get("expand", 1):
             per_text = 0.0  # expansion left to k_expand: no text in or out of k_doctree
+        if (k == "runs" and stile_text and launches.get("doctree") and not launches.get("expand")
+                and not launches.get("walk1")):
+            per_text = 0.0  # (k_doctree stages the text from the stile segments: no copy)
         if k == "expand" and launches.get("walk1"):
             per_run = 20.0
         if radix and level1_run_bytes(k, per_wave, text_mode) is not None:
@@ -573,7 +580,8 @@ def traces_workload(args) -> int:
         # (the committed PMC bytes per item were measured at the headline config)
         headline = (args.relabel == "rotate" and args.order != "fugue" and args.replicas == 4096
                     and args.nsq_list == 1)
-        rf = roofline_fields(iso_stats, batch, items_per_gpu, res["step_s"], pmc=headline)
+        rf = roofline_fields(iso_stats, batch, items_per_gpu, res["step_s"], pmc=headline,
+                             stile_text=args.stile_text)
         rf_lanes = None
         if args.lanes > 1:
             rf_lanes = {k: round(float(np.mean([s["stage_ns"][k] for s in stats])) / 1e6, 4)
@@ -657,7 +665,7 @@ def traces_workload(args) -> int:
                                {k: float(np.mean([s["stage_ns"][k] for s in cs]))
                                 for k in cs[0]["stage_ns"]}.items() if v > 2e4},
             }
-            crf = roofline_fields(cs, cb, cb.items, cres["step_s"], pmc=False)
+            crf = roofline_fields(cs, cb, cb.items, cres["step_s"], pmc=False, stile_text=args.stile_text)
             out["companion_shuffle"]["rooflines"] = {
                 k: {"kernel": v["kernel"], "frac": v["frac"], "achieved_gbps": v["achieved"],
                     "launch_us": v["launch_us"]} for k, v in crf["rooflines"].items()}
@@ -765,7 +773,8 @@ def side_workload(args) -> int:
             "text_bytes": int(lens[0]), "digest": "%016x" % int(dig[0]), "digests_ok": ok,
         }
         # every stage's roofline by its algorithmic bytes (DESIGN.md §7 pricing; no PMC here)
-        rf = roofline_fields(stats, batch, batch.items, el / args.steps, pmc=False)
+        rf = roofline_fields(stats, batch, batch.items, el / args.steps, pmc=False,
+                             stile_text=getattr(args, "stile_text", 2))
         out["rooflines"] = {k: {"kernel": v["kernel"], "frac": v["frac"],
                                 "achieved_gbps": v["achieved"], "launch_us": v["launch_us"]}
                             for k, v in rf["rooflines"].items()}

@@ -2348,6 +2348,9 @@ constexpr int kDocQ = 10;  // 16-byte pieces per thread: texts up to 160 KiB
 // item over the table in LDS).  A chunk wholly inside one share is two aligned 16-byte loads from
 // the segment, a funnel shift and one 16-byte LDS store; a chunk a share only partly covers (at
 // most two per tile) stores its bytes one by one (the neighbouring tile stores the rest).
+// First step of a power-of-two search over table entries 0..n (the steps sum to at least n):
+// the document's tiles, not the kernel's 1024 at most
+__device__ __forceinline__ uint32_t search_step0(uint32_t n) { return n ? 1u << (31 - __builtin_clz(n)) : 0u; }
 __device__ __forceinline__ uint32_t funnel_byte(uint32_t lo, uint32_t hi, uint32_t b) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * b));
 }
@@ -2378,9 +2381,9 @@ __device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, 
             ii[e] = i0 + t + (uint32_t)e * kDocThreads;
             kk[e] = 0;
         }
-        // the last tile whose first item is at or before the item (10 steps: nt + 1 <= 1024)
+        // the last tile whose first item is at or before the item (log2(nt) + 1 steps)
 #pragma unroll
-        for (uint32_t step = 512; step; step >>= 1) {
+        for (uint32_t step = search_step0(nt); step; step >>= 1) {
 #pragma unroll
             for (int e = 0; e < kE; ++e) {
                 const uint32_t c = min(kk[e] + step, nt);  // (branch-free: reads issue together)
@@ -2480,7 +2483,7 @@ __device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32
         // (branch-free: the clamped probe and a select, so that the kG reads of a step issue
         // together instead of one exec-masked read and wait each)
 #pragma unroll
-        for (uint32_t step = 512; step; step >>= 1) {
+        for (uint32_t step = search_step0(nt); step; step >>= 1) {
 #pragma unroll
             for (int e = 0; e < kG; ++e) {
                 const uint32_t c = c0 + 1024u * (uint32_t)e + lane;
@@ -2588,7 +2591,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
         for (int j = 0; j < J; ++j) dv[j] = 0;
         if (glds) {
 #pragma unroll
-            for (uint32_t step = 512; step; step >>= 1) {
+            for (uint32_t step = search_step0(nt); step; step >>= 1) {
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const uint32_t q = min(dv[j] + step, nt);  // (branch-free, as in stage_glds)

@@ -30,9 +30,15 @@ def test_lds_path_prices_the_headline_stages():
                 {"classify": 1, "runs": 6, "doctree": 1, "digest": 2}, runs=30_000, text=250_000)
     rf = bench.roofline_fields(st, _Batch(), items, 1e-3, pmc=False)
     slots = items + _Batch.docs
-    want = 3.875 * slots + 8.0 * 30_000 + 1.0 * 250_000
+    want = 3.3828125 * slots + 8.0 * 30_000 + 1.0 * 250_000
     assert rf["rooflines"]["classify"]["alg_bytes_per_launch"] == pytest.approx(want)
     assert rf["roofline"]["kernel"] == "k_classify"  # the most device time
+    # k_doctree stages the text from the tile segments: k_runs moves no text (stile_text 2), and
+    # with stile_text 0 it copies every tile's text to sbytes
+    assert rf["rooflines"]["runs"]["alg_bytes_per_launch"] == pytest.approx(1.25 * slots + 38.0 * 30_000)
+    rf0 = bench.roofline_fields(st, _Batch(), items, 1e-3, pmc=False, stile_text=0)
+    assert rf0["rooflines"]["runs"]["alg_bytes_per_launch"] == pytest.approx(
+        1.25 * slots + 38.0 * 30_000 + 2.0 * 250_000)
     assert set(rf["rooflines"]) == {"classify", "runs", "doctree", "digest"}
     assert all(r["traffic"] is None for r in rf["rooflines"].values())  # (pmc=False)
 
@@ -53,7 +59,9 @@ def test_radix_passes_priced_per_pass():
     assert r["link"]["alg_bytes_per_launch"] == pytest.approx(28.0 * runs)
     # waves without contraction (runs > half the slots): classify reads no parents
     slots = items + _Batch.docs
-    assert r["classify"]["alg_bytes_per_launch"] == pytest.approx(3.875 * slots + 100_000)
+    assert r["classify"]["alg_bytes_per_launch"] == pytest.approx(3.3828125 * slots + 100_000)
+    # (the global level 1 reads the text from sbytes: k_runs copies it)
+    assert r["runs"]["alg_bytes_per_launch"] == pytest.approx(1.25 * slots + 32.0 * runs + 2.0 * 100_000)
     assert rf["roofline"]["kernel"] == "place"
 
 
