@@ -2382,7 +2382,6 @@ __device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, 
             kk[e] = 0;
         }
         // the last tile whose first item is at or before the item (log2(nt) + 1 steps)
-#pragma unroll
         for (uint32_t step = search_step0(nt); step; step >>= 1) {
 #pragma unroll
             for (int e = 0; e < kE; ++e) {
@@ -2482,7 +2481,6 @@ __device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32
         for (int e = 0; e < kG; ++e) k[e] = 0;
         // (branch-free: the clamped probe and a select, so that the kG reads of a step issue
         // together instead of one exec-masked read and wait each)
-#pragma unroll
         for (uint32_t step = search_step0(nt); step; step >>= 1) {
 #pragma unroll
             for (int e = 0; e < kG; ++e) {
@@ -2590,7 +2588,6 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
 #pragma unroll
         for (int j = 0; j < J; ++j) dv[j] = 0;
         if (glds) {
-#pragma unroll
             for (uint32_t step = search_step0(nt); step; step >>= 1) {
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
