@@ -364,6 +364,30 @@ def test_malformed_logs_are_rejected(ctx):
     assert ctx.merge(ok)[0] == b"ab"  # the engine recovers after an error
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("level1", [0, 1])
+def test_parent_in_another_document_of_the_wave_is_rejected(level1):
+    """A parent index past its document's items that lands on an item of the NEXT document of the
+    same wave (documents are 64-slot aligned: index 70 of a 2-item document is slot 6 of the next
+    one).  k_classify flags it; k_runs (which takes each word's document start from its head
+    record and no longer clamps such a parent into its own document) then finds a run of the other
+    document, which the level 1 must not follow into a wrong order or an endless walk.  The batch
+    fails with EBADLOG on both level-1 paths, and the same engine merges a well-formed batch right
+    after."""
+    c = crdt_hip.Context(0)
+    c.set_param("level1", level1)
+    n = 10
+    good = crdt_hip.LogArrays(list(range(n)), list(range(1, n + 1)), [0] * n, [0] * n,
+                              [97 + i for i in range(n)])
+    bad = crdt_hip.LogArrays([0, 70], [1, 2], [0, 0], [0, 0], [97, 98])
+    with pytest.raises(crdt_hip.CrdtHipError) as e:
+        c.merge_batch([bad, good])
+    assert e.value.code == -5
+    dig, lens = c.merge_batch([good, good])
+    assert list(lens) == [n, n] and dig[0] == dig[1]
+    c.close()
+
+
 def test_repeated_merges_are_deterministic(ctx):
     log = crdt_hip.OpLog.synth_agents(300000, 64, 42).arrays()
     d0 = ctx.merge_digest(log)
