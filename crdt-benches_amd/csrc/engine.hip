@@ -2655,6 +2655,9 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     const uint32_t t = threadIdx.x;
     // the plan check and the workgroup's document (written by k_doctotals in LPT order: document,
     // first run, runs, text offset / length) in one round of loads
+#ifdef CRDT_HIP_PROBE
+    const uint64_t tdesc = wall_clock64();  // (before the descriptor's round trip)
+#endif
     const uint4 wg = a.wg[2u * widx], wg1 = a.wg[2u * widx + 1u];
     if (replan(a.ctl)) return;
     const uint32_t d = wg.x, base = wg.y, R = wg.z;
@@ -3171,11 +3174,11 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     PROBE(10);
 #ifdef CRDT_HIP_PROBE
     if (probe) {
-        printf("[doctree] doc %u R %u S %u us: load %.1f count %.1f scan %.1f place %.1f "
+        printf("[doctree] doc %u R %u S %u us: desc %.1f load %.1f count %.1f scan %.1f place %.1f "
                "glist %.1f pairs %.1f net3-8 %.1f wide9-64 %.1f fc %.1f uplinks %.1f walk1 %.1f "
                "jump %.1f offsets %.1f text-stage %.1f (scan %.1f load %.1f bits %.1f pref %.1f "
                "delta %.1f) text-out %.1f total %.1f | visited %u steps max %u sum %u\n", d, R, S,
-               (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
+               (tp[0] - tdesc) / 100.0, (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, (tp[3] - tp[2]) / 100.0,
                (tp[4] - tp[3]) / 100.0, (tp[12] - tp[4]) / 100.0, (tp[11] - tp[12]) / 100.0,
                (tp[5] - tp[11]) / 100.0, (tp[13] - tp[5]) / 100.0, (tp[14] - tp[13]) / 100.0,
                (tp[6] - tp[14]) / 100.0, (tp[7] - tp[6]) / 100.0, (tp[8] - tp[7]) / 100.0,
