@@ -68,11 +68,11 @@ KERNEL_BYTES = {
     # nibbles only for 16-slot groups with a visible multi-byte character: ~0 on the traces);
     # parents of the nsq items read + listed (counted per run); tile UTF-8 (stile) out
     "classify": (3.3828125, 8.0, 1.0),
-    # head stage (k_heads: nsq, visible and both jump bitvectors in, head records out) and k_runs
-    # (head records, visible and nsq bits in); per run: key + parent slot + rank lookup in, record
+    # head stage (k_heads: nsq, visible and jump bits in, head records out) and k_runs (head
+    # records, visible and nsq bits in); per run: key + parent slot + rank lookup in, record
     # row out; the tile text moved to sbytes only when a later kernel reads it there (k_expand,
     # or stile_text 0): k_doctree's default staging reads the stile segments themselves
-    "runs": (1.25, 38.0, 2.0),
+    "runs": (1.125, 38.0, 2.0),
     # global level 1, sibling groups by counting: parent in + child count (count), placement
     # (place), keys and links (link); the radix form is priced in level1_run_bytes below
     "count": (0.0, 4.0, 0.0),

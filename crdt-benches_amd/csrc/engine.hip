@@ -128,8 +128,7 @@ struct L0Args {
     const uint32_t* in_parent;
     const uint64_t* in_key;     // lamport << 16 | agent (one gather per run head)
     const uint8_t* in_cp;       // 3 bytes per slot (cp3_get)
-    uint32_t* jbits;            // per slot bit: has a non-consecutive child in a later tile
-    uint32_t* jloc;             // per slot bit: has a non-consecutive child in its own tile
+    uint32_t* jbits;            // per slot bit: has a non-consecutive child (a jump)
     uint16_t* nsqb;             // per slot bit, 16 per thread: an item whose parent is not the
                                 //   previous slot (no previous-slot flag)
     uint64_t* wnib;             // per slot 4-bit weight (visible UTF-8 bytes / 1 per item), written
@@ -213,7 +212,8 @@ __device__ __forceinline__ uint64_t spread_nib16(uint32_t v) {
 //    parents read by the whole block, four loads per thread in flight at a time (the items
 //    cluster; listing them spreads the loads over the block);
 //  * the jump bit of every parent that has a non-consecutive child: parents inside the tile in
-//    LDS (stored whole to jloc), parents in earlier tiles by agent-scope atomicOr on jbits;
+//    LDS (ORed into jbits word by word at the end), parents in other tiles by agent-scope
+//    atomicOr on jbits;
 //  * a parent out of range (or an item that is its own parent) is flagged; such an item becomes
 //    a run head under the document start, and the merge reports CRDT_HIP_EBADLOG;
 //  * the parents themselves (as wave slots), in slot order, to the tile's plist segment: every
@@ -365,10 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     }
     if (cl && T != nhi - nlo && threadIdx.x == 0) atomicOr(&a.ctl[C_ERR], 1u);  // list != flags
     if (a.nocon) return;  // (no contraction: no jump bits; k_runs checks the parents)
-    if (T == 0) {  // (block-uniform) no nsq item: no jump bit from this tile
-        if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = 0u;
-        return;
-    }
+    if (T == 0) return;  // (block-uniform) no nsq item: no jump bit from this tile
     __syncthreads();  // the text stage is stored: its LDS holds the list
     // list entries: tile-local slot, bit 15 = a left child (Fugue)
     uint16_t* lst = reinterpret_cast<uint16_t*>(sb);
@@ -423,7 +420,11 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
         }
     }
     __syncthreads();
-    if (threadIdx.x < kScanTile / 32) a.jloc[tile * (kScanTile / 32) + threadIdx.x] = jl[threadIdx.x];
+    // the tile's own jump words join the bits later tiles set, by one atomic OR per nonzero word
+    // (a plain store could overwrite another tile's OR into the same word): k_heads then reads
+    // a single jump bitvector
+    if (threadIdx.x < kScanTile / 32 && jl[threadIdx.x])
+        atomicOr(&a.jbits[tile * (kScanTile / 32) + threadIdx.x], jl[threadIdx.x]);
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
@@ -463,16 +464,14 @@ __global__ __launch_bounds__(kBlock) void k_heads(L0Args a) {
         if (l0 <= n) {
             const uint64_t nsq = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
             const uint64_t vis = *reinterpret_cast<const uint64_t*>(a.visb + (gs >> 4));
-            const uint2 jr = *reinterpret_cast<const uint2*>(a.jbits + (gs >> 5));
-            const uint2 jq = *reinterpret_cast<const uint2*>(a.jloc + (gs >> 5));
-            const uint64_t jw = ((uint64_t)(jr.y | jq.y) << 32) | (uint64_t)(jr.x | jq.x);
+            const uint64_t jw = *reinterpret_cast<const uint64_t*>(a.jbits + (gs >> 5));
             // (a tile's first slot always heads a run: no run crosses a tile, so the text of every
             // run lies inside one tile's stile segment, which k_doctree stages tile by tile)
             uint64_t pj = 0;
             if (l0 > 0)
                 pj = (gs % kScanTile) == 0u
                          ? 1u
-                         : ((a.jbits[(gs >> 5) - 1] | a.jloc[(gs >> 5) - 1]) >> 31) & 1u;
+                         : (a.jbits[(gs >> 5) - 1] >> 31) & 1u;
             const uint64_t prevj = (jw << 1) | pj;  // bit k = jump(gs + k - 1)
             const uint64_t item = low_mask64(n + 1u - l0) & ~low_mask64(l0 == 0 ? 1u : 0u);
             const uint64_t root = l0 == 0 ? 1ull : 0ull;
@@ -3633,7 +3632,7 @@ void DeviceLogs::release() {
 
 Engine::~Engine() {
     if (stream) (void)hipStreamSynchronize(stream);
-    dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(escm_); dfree(hrec_); dfree(stile_); dfree(plist_);
+    dfree(jbits_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(escm_); dfree(hrec_); dfree(stile_); dfree(plist_);
     dfree(tile_hw_); dfree(tile_sums_); dfree(sbytes_);
     dfree(doc_root_); dfree(doc_p0_); dfree(doc_fused_); dfree(wgtab_);
     dfree(r_head_); dfree(r_pstart_); dfree(r_parent_); dfree(roff_); dfree(rloc_); dfree(r_key_);
@@ -3912,12 +3911,11 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
 int Engine::ensure_scratch(const Wave& w) {
     const uint64_t slots = w.nslots;
     if (slots > cap_slots0_) {
-        dfree(jbits_); dfree(jloc_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(escm_); dfree(hrec_); dfree(stile_); dfree(plist_);
+        dfree(jbits_); dfree(nsqb_); dfree(visb_); dfree(wnib_); dfree(escm_); dfree(hrec_); dfree(stile_); dfree(plist_);
         dfree(tile_hw_); dfree(tile_sums_);
         const uint64_t tiles = slots / kScanTile + 2;
         // jump bits, then (Fugue) the left-child bits: jbits_words(slots) words each
         HIPCHK(dalloc(&jbits_, 2 * jbits_words(slots)), "hipMalloc jump bits");
-        HIPCHK(dalloc(&jloc_, tiles * (kScanTile / 32)), "hipMalloc local jump bits");
         HIPCHK(dalloc(&nsqb_, slots / 16 + 4), "hipMalloc seq bits");
         HIPCHK(dalloc(&wnib_, slots / 16 + 4), "hipMalloc weight nibbles");
         HIPCHK(dalloc(&visb_, slots / 16 + 4), "hipMalloc visible bits");
@@ -4127,7 +4125,6 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a0.in_key = L.key + w.slot0;                                    \
     a0.in_cp = L.cp + 3ull * w.slot0;                               \
     a0.jbits = jbits_;                                              \
-    a0.jloc = jloc_;                                                \
     a0.nsqb = nsqb_;                                                \
     a0.wnib = wnib_;                                                \
     a0.visb = visb_;                                                \

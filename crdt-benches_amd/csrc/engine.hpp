@@ -261,7 +261,7 @@ private:
     bool l1_pending_ = false;  // ev_l1_ marks this merge's last level 1 on stream_l1
     // level-0 scratch (per slot / per tile), grown on demand
     uint64_t cap_slots0_ = 0, cap_docs_ = 0, cap_text_ = 0, cap_leaves_ = 0;
-    uint32_t *jbits_ = nullptr, *jloc_ = nullptr;
+    uint32_t* jbits_ = nullptr;
     uint16_t* nsqb_ = nullptr;
     uint64_t* wnib_ = nullptr;
     uint16_t* visb_ = nullptr;

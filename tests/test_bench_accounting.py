@@ -35,10 +35,10 @@ def test_lds_path_prices_the_headline_stages():
     assert rf["roofline"]["kernel"] == "k_classify"  # the most device time
     # k_doctree stages the text from the tile segments: k_runs moves no text (stile_text 2), and
     # with stile_text 0 it copies every tile's text to sbytes
-    assert rf["rooflines"]["runs"]["alg_bytes_per_launch"] == pytest.approx(1.25 * slots + 38.0 * 30_000)
+    assert rf["rooflines"]["runs"]["alg_bytes_per_launch"] == pytest.approx(1.125 * slots + 38.0 * 30_000)
     rf0 = bench.roofline_fields(st, _Batch(), items, 1e-3, pmc=False, stile_text=0)
     assert rf0["rooflines"]["runs"]["alg_bytes_per_launch"] == pytest.approx(
-        1.25 * slots + 38.0 * 30_000 + 2.0 * 250_000)
+        1.125 * slots + 38.0 * 30_000 + 2.0 * 250_000)
     assert set(rf["rooflines"]) == {"classify", "runs", "doctree", "digest"}
     assert all(r["traffic"] is None for r in rf["rooflines"].values())  # (pmc=False)
 
@@ -61,7 +61,7 @@ def test_radix_passes_priced_per_pass():
     slots = items + _Batch.docs
     assert r["classify"]["alg_bytes_per_launch"] == pytest.approx(3.3828125 * slots + 100_000)
     # (the global level 1 reads the text from sbytes: k_runs copies it)
-    assert r["runs"]["alg_bytes_per_launch"] == pytest.approx(1.25 * slots + 32.0 * runs + 2.0 * 100_000)
+    assert r["runs"]["alg_bytes_per_launch"] == pytest.approx(1.125 * slots + 32.0 * runs + 2.0 * 100_000)
     assert rf["roofline"]["kernel"] == "place"
 
 
