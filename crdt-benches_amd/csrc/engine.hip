@@ -2501,6 +2501,8 @@ __device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32
             }
         }
     }
+    // (the loads land while the run starts, prefix counts and deltas are computed; doc_text
+    // waits for them before the barrier in front of the text output)
 }
 
 template <int J>
@@ -2613,6 +2615,10 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
         for (int j = 0; j < J; ++j)
             if (ro[j] != kNil) delta[rk[j]] = dv[j];
     }
+    // (LDS-DMA staging) the DMA writes LDS as a global load, and a workgroup barrier waits only
+    // for LDS operations (lgkmcnt): every wave waits for its own staging loads (vmcnt) before the
+    // barrier after which any wave reads any staged chunk
+    if (glds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tprobe) *tprobe = wall_clock64();
     // 3) the document in order, 16 bytes per lane per step (one bitvector word covers them)
