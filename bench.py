@@ -1019,7 +1019,7 @@ def parse_args(argv=None):
     ap.add_argument("--group-docs", type=int, default=-1, choices=[-1, 0, 1],
                     help="replica batches placed base by base, each base in waves of its own "
                          "(-1: only for --order fugue, whose seph-blog1 rows exceed the LDS level 1)")
-    ap.add_argument("--runs-slots", type=int, default=32, choices=[16, 32],
+    ap.add_argument("--runs-slots", type=int, default=32, choices=[16, 32, 64],
                     help="k_runs slots per thread (16: 256 threads per tile, 32: 128)")
     ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1, 2],
                     help="1: resident batches (input encoding) and replicas of 2^22+ slots (every "

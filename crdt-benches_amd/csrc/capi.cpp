@@ -213,8 +213,9 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.group_docs = value == 1;
         return CRDT_HIP_OK;
     }
-    if (k == "runs_slots") {  // k_runs slots per thread: 16 or 32
-        if (value != 16 && value != 32) return set_err(ctx, CRDT_HIP_EINVAL, "runs_slots must be 16 or 32");
+    if (k == "runs_slots") {  // k_runs slots per thread: 16, 32 or 64
+        if (value != 16 && value != 32 && value != 64)
+            return set_err(ctx, CRDT_HIP_EINVAL, "runs_slots must be 16, 32 or 64");
         ctx->eng.runs_slots = (uint32_t)value;
         return CRDT_HIP_OK;
     }

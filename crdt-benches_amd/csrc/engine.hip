@@ -623,29 +623,33 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
 // drained as often as the tile needs (nearly always once), which keeps the 128-thread block at
 // ~6 KiB of LDS.
 constexpr uint32_t kRunsWin = 1024;
+__device__ __forceinline__ uint32_t mpop(uint32_t x) { return (uint32_t)__popc(x); }
+__device__ __forceinline__ uint32_t mpop(uint64_t x) { return (uint32_t)__popcll(x); }
 template <bool FUGUE, int SL>
 __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(8))) void k_runs(L0Args a) {
-    static_assert(SL == 16 || SL == 32, "slots per thread");
+    static_assert(SL == 16 || SL == 32 || SL == 64, "slots per thread");
+    using MT = typename std::conditional<SL == 64, uint64_t, uint32_t>::type;  // a thread's slot masks
     constexpr int NT = kScanTile / SL;  // threads per tile
     constexpr int NW = NT / 64;
     constexpr int NQ = SL / 16;         // weight-nibble words per thread
-    constexpr uint32_t kWin = SL == 16 ? (uint32_t)kScanTile : kRunsWin;
+    constexpr uint32_t kWin = SL == 16 ? (uint32_t)kScanTile : SL == 32 ? kRunsWin : kRunsWin / 2;
     __shared__ uint32_t lsum[NW];
     __shared__ uint32_t lrow[NW];
     __shared__ uint32_t rec[kWin + 1];
-    __shared__ uint32_t lnsq[NT];      // nsq bits of every thread's slots
+    __shared__ MT lnsq[NT];            // nsq bits of every thread's slots
     __shared__ uint2 ldoc[NT];         // every thread's document {base slot, items}
     __shared__ uint32_t lsq[NW];
     __shared__ uint16_t lnpf[NT];      // non-seq items of the tile before every thread
     __shared__ uint16_t ldp[FUGUE ? NT : 1];  // Fugue: two-row heads before every thread
-    __shared__ uint32_t ldm[FUGUE ? NT : 1];  //   and every thread's two-row head bits
+    __shared__ MT ldm[FUGUE ? NT : 1];        //   and every thread's two-row head bits
     const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gs = tile * kScanTile + threadIdx.x * SL;
-    uint32_t hm = 0, nsq = 0, dm = 0;
+    MT hm = 0, nsq = 0, dm = 0;
     // weights: the visible bits (vw) of groups without a visible multi-byte character; a thread
     // holding an escaped group (e) takes its slots' nibbles: 8 slots per word nwd
-    uint32_t vw = 0, e = 0;
+    MT vw = 0;
+    uint32_t e = 0;
     uint32_t nwd[2 * NQ];
 #pragma unroll
     for (int q = 0; q < 2 * NQ; ++q) nwd[q] = 0;
@@ -662,19 +666,28 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
         const uint32_t hw32 = (gs & 63u) < 32u ? hb.x : hb.y;
         doc = make_uint2(hb.w, 0xFFFFFFFFu);
         if (a.nocon) doc = a.docs[a.chunk_doc[gs >> a.log2m]];
-        hm = SL == 32 ? hw32 : (hw32 >> (gs & 31u)) & 0xFFFFu;
-        if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
-        vw = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.visb + (gs >> 4)) : (uint32_t)a.visb[gs >> 4];
+        if constexpr (SL == 64) {
+            hm = ((uint64_t)hb.y << 32) | hb.x;
+            if (FUGUE) dm = hm & *reinterpret_cast<const uint64_t*>(a.lbits + (gs >> 5));
+            vw = *reinterpret_cast<const uint64_t*>(a.visb + (gs >> 4));
+        } else {
+            hm = SL == 32 ? hw32 : (hw32 >> (gs & 31u)) & 0xFFFFu;
+            if (FUGUE) dm = hm & (a.lbits[gs >> 5] >> (gs & 31u));
+            vw = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.visb + (gs >> 4)) : (uint32_t)a.visb[gs >> 4];
+        }
         e = (uint32_t)(a.escm[gs >> 10] >> ((gs >> 4) & 63u)) & ((1u << NQ) - 1u);
         if (e) {  // (rare: the nibbles of the escaped groups, the visible bits spread for the rest)
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                const uint64_t nb = (e >> q) & 1u ? a.wnib[(gs >> 4) + (uint32_t)q] : spread_nib16(vw >> (16 * q));
+                const uint64_t nb = (e >> q) & 1u ? a.wnib[(gs >> 4) + (uint32_t)q] : spread_nib16((uint32_t)(vw >> (16 * q)));
                 nwd[2 * q] = (uint32_t)nb;
                 nwd[2 * q + 1] = (uint32_t)(nb >> 32);
             }
         }
-        nsq = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.nsqb + (gs >> 4)) : a.nsqb[gs >> 4];
+        if constexpr (SL == 64)
+            nsq = *reinterpret_cast<const uint64_t*>(a.nsqb + (gs >> 4));
+        else
+            nsq = SL == 32 ? *reinterpret_cast<const uint32_t*>(a.nsqb + (gs >> 4)) : a.nsqb[gs >> 4];
     }
     lnsq[threadIdx.x] = nsq;
     ldoc[threadIdx.x] = doc;
@@ -697,11 +710,11 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
         nwc[q] = W;
         W = __builtin_amdgcn_udot8(nwd[q], 0x11111111u, W, false);
     }
-    if (!e) W = (uint32_t)__popc(vw);
-    const uint32_t x = ((uint32_t)__popc(hm) << 16) | W;  // heads (records) << 16 | weight
+    if (!e) W = mpop(vw);
+    const uint32_t x = (mpop(hm) << 16) | W;  // heads (records) << 16 | weight
     const uint32_t inc = wave_incl_scan(x);
-    const uint32_t cq = (uint32_t)__popc(nsq), incq = wave_incl_scan(cq);
-    const uint32_t cd = FUGUE ? (uint32_t)__popc(dm) : 0u, incd = FUGUE ? wave_incl_scan(cd) : 0u;
+    const uint32_t cq = mpop(nsq), incq = wave_incl_scan(cq);
+    const uint32_t cd = FUGUE ? mpop(dm) : 0u, incd = FUGUE ? wave_incl_scan(cd) : 0u;
     if (lane == 63u) {
         lsum[wv] = inc;
         lsq[wv] = incq;
@@ -767,12 +780,12 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
             // prefix = the thread's prefix + the weight of its slots below the head
             uint32_t r = ex >> 16;
             const uint32_t p0 = ex & 0xFFFFu;
-            if (r <= h0 + kWin && r + (uint32_t)__popc(hm) > h0) {
-                for (uint32_t m = hm; m; m &= m - 1u) {
-                    const uint32_t j = (uint32_t)__builtin_ctz(m);
+            if (r <= h0 + kWin && r + mpop(hm) > h0) {
+                for (MT m = hm; m; m &= m - 1u) {
+                    const uint32_t j = SL == 64 ? (uint32_t)__builtin_ctzll((uint64_t)m) : (uint32_t)__builtin_ctz((uint32_t)m);
                     uint32_t p;
                     if (!e) {
-                        p = (uint32_t)__popc(vw & ((1u << j) - 1u));
+                        p = mpop(vw & ((MT(1) << j) - 1u));
                     } else {
                         const uint32_t wi = j >> 3;
                         uint32_t xw = nwd[0], cw = nwc[0];
@@ -798,20 +811,20 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
             const uint32_t rv = rec[i - h0];
             const uint32_t li = (rv >> 16) & 0xFFFu, g = tbase + li;
             const uint32_t th = li / SL, bl = li % SL;
-            const uint32_t below = (1u << bl) - 1u;
+            const MT below = (MT(1) << bl) - 1u;
             const bool two = (rv & kRecTree) != 0u;  // Fugue: a content row, then the tree row
             // the head's first row: heads before it, plus (Fugue) the two-row heads before it
             const uint32_t rho =
-                pre.x + i + (FUGUE ? ldp[th] + (uint32_t)__popc(ldm[th] & below) : 0u);
+                pre.x + i + (FUGUE ? ldp[th] + mpop(ldm[th] & below) : 0u);
             const uint32_t rt = rho + (two ? 1u : 0u);  // the row with the run's parent and key
             const uint2 dc = ldoc[th];
             const bool root = g == dc.x;
-            const uint32_t nw = lnsq[th];
+            const MT nw = lnsq[th];
             const bool sq = !root && !((nw >> bl) & 1u);
             // a non-seq head's parent from the tile's list: its index = the non-seq items before
             // it; (resident batches) its key from the same index of the key list, a seq head's
             // gathered
-            const uint32_t lix = lnpf[th] + (uint32_t)__popc(nw & below);
+            const uint32_t lix = lnpf[th] + mpop(nw & below);
             const uint64_t key = (a.nsq_key && !sq && !root) ? a.nsq_key[nlo + lix] : a.in_key[g];
             if (!FUGUE && a.nocon) {
                 // no contraction: the run's parent and key from the columns (heads are every
@@ -4192,12 +4205,16 @@ int Engine::clock_mark(StageClock& c, int stage) {
 // k_runs with 16 or 32 slots per thread (Engine::runs_slots)
 void launch_k_runs(const L0Args& a0, uint32_t ntiles, hipStream_t s, uint32_t slots) {
     if (a0.fugue) {
-        if (slots == 32)
+        if (slots == 64)
+            k_runs<true, 64><<<ntiles, kScanTile / 64, 0, s>>>(a0);
+        else if (slots == 32)
             k_runs<true, 32><<<ntiles, kScanTile / 32, 0, s>>>(a0);
         else
             k_runs<true, 16><<<ntiles, kScanTile / 16, 0, s>>>(a0);
     } else {
-        if (slots == 32)
+        if (slots == 64)
+            k_runs<false, 64><<<ntiles, kScanTile / 64, 0, s>>>(a0);
+        else if (slots == 32)
             k_runs<false, 32><<<ntiles, kScanTile / 32, 0, s>>>(a0);
         else
             k_runs<false, 16><<<ntiles, kScanTile / 16, 0, s>>>(a0);

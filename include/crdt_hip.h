@@ -145,7 +145,7 @@ const char* crdt_hip_last_error(const crdt_hip_ctx* ctx);
  * "group_docs" (replica batches: 1 = documents placed in slots base by base, each base's
  * replicas in waves of their own, so that only the waves of a base whose run trees exceed the
  * per-document LDS level 1 take the global one; results stay in the caller's order; default 0),
- * "runs_slots" (k_runs slots per thread, 16 or 32; default 32),
+ * "runs_slots" (k_runs slots per thread, 16, 32 or 64; default 32),
  * "stile_text" (default 2: the per-document merge stages text from the per-tile segments by
  * LDS-DMA, tile by tile; 1: by loads and shifts into one contiguous image; 0: from the slot-order
  * text k_runs then writes),

@@ -323,8 +323,8 @@ def test_gpu_fugue_multi_wave_lanes(golden, lanes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_gpu_fugue_grouped_batch_takes_the_lds_level1(golden, lanes):
+@pytest.mark.parametrize("lanes,slots", [(1, 32), (2, 32), (2, 64)])
+def test_gpu_fugue_grouped_batch_takes_the_lds_level1(golden, lanes, slots):
     """group_docs: the replicas are placed base by base, each base in waves of its own.  The
     Fugue rows of every trace fit the per-document LDS level 1: sveltecomponent (4.5 k rows) in
     k_doctree, automerge-paper (11.8 k), rustcode (10.7 k) and seph-blog1 (16.6 k) in
@@ -334,6 +334,7 @@ def test_gpu_fugue_grouped_batch_takes_the_lds_level1(golden, lanes):
     c = crdt_hip.Context(0)
     c.set_param("lanes", lanes)
     c.set_param("group_docs", 1)
+    c.set_param("runs_slots", slots)  # (k_runs<true>: 32 or 64 slots per thread)
     bases = [fugue_resolved(n) for n in TRACES]
     b = c.batch(bases, replicas=3, relabel="rotate", seed=21)
     for _ in range(2):  # (the second merge runs on the learnt plans)

@@ -255,6 +255,33 @@ def _level1_cases():
     return logs
 
 
+@pytest.mark.parametrize("slots", [16, 32, 64])
+def test_runs_slots_per_thread_agree(oracle, golden, slots):
+    """k_runs with 16, 32 (default) and 64 slots per thread (64: one wave per 4096-slot tile,
+    64-bit slot masks): the level-1 cases against the oracle, a rotated trace batch (contracted,
+    compact nsq list) and a shuffled one (no contraction) against the golden digests, with the
+    synchronous merge and the learnt-plan merge."""
+    c = crdt_hip.Context(0)
+    c.set_param("runs_slots", slots)
+    logs = _level1_cases()
+    dig, lens = c.merge_batch(logs)
+    for i, lg in enumerate(logs):
+        ref = oracle.merge(to_anchor(lg)) if lg.n else b""
+        assert lens[i] == len(ref), i
+        assert dig[i] == oracle.tree_digest(ref), i
+    bases = [resolved(n) for n in TRACES]
+    for relabel in ("rotate", "shuffle"):
+        b = c.batch(bases, replicas=2, relabel=relabel, seed=5)
+        for _ in range(2):
+            dig, lens, st = b.merge()
+            for r in range(b.docs):
+                name = TRACES[r % 4]
+                assert "%016x" % dig[r] == golden[name]["tree_digest"], (relabel, r)
+                assert lens[r] == golden[name]["end_bytes"], (relabel, r)
+        b.close()
+    c.close()
+
+
 @pytest.mark.parametrize("level1,group,dbits", [(0, 0, 0), (1, 1, 0), (1, 2, 0), (1, 2, 10)])
 def test_level1_paths_match_oracle(oracle, level1, group, dbits):
     """Per-document LDS level 1 (k_doctree, default) and the global level-1 kernels, with their
