@@ -1,6 +1,6 @@
 """Level-1 rows (runs) per document of each trace, RGA and Fugue anchors: one document per merge
 (crdt_hip stats "runs"); the capacity of k_doctree is 12 runs per thread (12,288), of
-k_doctree_wide 14 (14,336).  GPU."""
+k_doctree_wide 12 and of k_doctree_wide17 17 (17,408).  GPU."""
 import os
 import sys
 

@@ -1,4 +1,6 @@
 #!/bin/bash
+# k_doctree phase times (probe build) of automerge-paper and seph-blog1 documents with one lane
+# and with two lanes (the other lane's level 0 beside it); $ARGS: extra bench arguments.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 for L in 1 2; do for p in 0 3; do
