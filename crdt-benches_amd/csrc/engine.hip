@@ -600,6 +600,34 @@ __global__ __launch_bounds__(kBlock) void k_tiles_apply(L0Args a) {
             ew += v[k].y;
         }
 }
+// A wave of at most kScanTile tiles (16 M slots: single documents, replicas, the downstream
+// closure) scans its tile pairs in one workgroup: the three launches above in one.
+__global__ __launch_bounds__(kBlock) void k_tiles_one(L0Args a) {
+    __shared__ uint32_t lh[kBlock / 64], lw[kBlock / 64];
+    const uint32_t base = threadIdx.x * kScanItems;
+    uint2 v[kScanItems];
+    uint32_t h = 0, w = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = base + k < a.ntiles ? a.tile_hw[base + k] : make_uint2(0, 0);
+        h += v[k].x;
+        w += v[k].y;
+    }
+    uint32_t th, tw;
+    uint32_t eh = block_excl_scan<kBlock / 64>(h, lh, th);
+    uint32_t ew = block_excl_scan<kBlock / 64>(w, lw, tw);
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < a.ntiles) {
+            a.tile_hw[base + k] = make_uint2(eh, ew);
+            eh += v[k].x;
+            ew += v[k].y;
+        }
+    if (threadIdx.x == 0) {
+        a.ctl[C_RTOTAL] = th;
+        a.ctl[C_WTOTAL] = tw;
+    }
+}
 
 // k_runs: one record per run head and the tile's UTF-8 moved from its stile segment to its place
 // in sbytes.  One packed scan, heads << 16 | weight (a tile holds at most 4096 heads and 16,384
@@ -4237,9 +4265,13 @@ int Engine::launch_level0(DeviceLogs& L, const Wave& w, bool ord, bool copy_text
     k_classify<<<ntiles, kBlock, 0, s>>>(a0);
     MARK(S_CLASSIFY);
     k_heads<<<grid_for(w.nslots / 64), kBlock, 0, s>>>(a0);
-    k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
-    k_tiles_top<<<1, 1024, 0, s>>>(a0, nsums);
-    k_tiles_apply<<<nsums, kBlock, 0, s>>>(a0);
+    if (nsums == 1) {
+        k_tiles_one<<<1, kBlock, 0, s>>>(a0);
+    } else {
+        k_tiles_reduce<<<nsums, kBlock, 0, s>>>(a0);
+        k_tiles_top<<<1, 1024, 0, s>>>(a0, nsums);
+        k_tiles_apply<<<nsums, kBlock, 0, s>>>(a0);
+    }
     launch_k_runs(a0, ntiles, s, runs_slots);
     k_docmax<<<1, 1024, 0, s>>>(a0);
     MARK(S_RUNS);
@@ -4515,7 +4547,10 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
     const bool wt = walk_text(w, ord, p);
     const bool expand_run = !p.fuse && !wt;
     const uint32_t rs = l1_csr_ ? 0u : 1u;
-    const uint32_t launches[S_N] = {1, 6, (rs_npassB_ + 2) * g1 * rs, g1, (rs ? 1u : 3u) * g1,
+    // (the runs stage: k_heads, the tile scan in one launch or three, k_runs, k_docmax)
+    const uint64_t ntiles = (w.nslots + kScanTile - 1) / kScanTile;
+    const uint32_t runs_launches = ntiles <= (uint64_t)kScanTile ? 4u : 6u;
+    const uint32_t launches[S_N] = {1, runs_launches, (rs_npassB_ + 2) * g1 * rs, g1, (rs ? 1u : 3u) * g1,
                                     (rs ? rs_npass_ : 1u) * g1, (rs ? 2u : 3u) * g1, g1,
                                     (3 + rounds) * g1, (wt ? 4u : 1u) * g1,
                                     expand_run ? 1u : 0u,
