@@ -88,6 +88,10 @@ KERNEL_BYTES = {
     "expand": (0.0, 16.0, 2.0),
     "digest": (0.0, 0.0, 1.0),
     "doctree": (0.0, 20.0, 2.0),     # parent run, weight, key in; slot-order text in, document out
+    # k_tscatter (after k_doctree in scatter mode, which then moves no text and writes the run's
+    # place, 4 B, inside its 20 B/run): per tile its {rows, weight} prefix (8 B per 4096 slots),
+    # per run its weight prefix and place in, the tiles' text in and the documents out
+    "text": (8.0 / 4096, 8.0, 2.0),
 }
 
 
@@ -107,7 +111,8 @@ def level1_run_bytes(k: str, per_wave: dict, text_mode: bool):
 
 
 STAGE_KERNEL = {"classify": "k_classify", "runs": "k_runs",
-                "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash"}
+                "doctree": "k_doctree", "expand": "k_expand", "digest": "k_leafhash",
+                "text": "k_tscatter"}
 # HBM bytes per item of each kernel from rocprofv3 PMC passes of this build (FETCH_SIZE x2 for
 # gfx950 wide reads + WRITE_SIZE, one pass each: tools/profile.sh + tools/pmc_summary.py).
 PMC_FILE = "profiles/pmc_per_item.json"
@@ -459,8 +464,8 @@ def roofline_fields(stats, batch, items_per_gpu, step_s, pmc: bool = True, stile
 
     def alg_bytes(k):
         per_slot, per_run, per_text = KERNEL_BYTES[k]
-        if k == "doctree" and launches.get("expand", 1):
-            per_text = 0.0  # expansion left to k_expand: no text in or out of k_doctree
+        if k == "doctree" and (launches.get("expand", 1) or launches.get("text")):
+            per_text = 0.0  # text left to k_expand / k_tscatter: no text in or out of k_doctree
         if (k == "runs" and stile_text and launches.get("doctree") and not launches.get("expand")
                 and not launches.get("walk1")):
             per_text = 0.0  # (k_doctree stages the text from the stile segments: no copy)
@@ -539,12 +544,12 @@ def traces_workload(args) -> int:
     if not args.fuse_text:  # (the engine's default is 1; builds before the parameter lack it)
         ctx.set_param("fuse_text", 0)
     ctx.set_param("lanes", args.lanes)
-    if args.xcd_order != 1:  # (the engine's default; builds before the parameter lack it)
-        ctx.set_param("xcd_order", args.xcd_order)
-    if args.stile_text != 1:  # (likewise)
-        ctx.set_param("stile_text", args.stile_text)
-    if args.runs_slots != 32:  # (likewise)
-        ctx.set_param("runs_slots", args.runs_slots)
+    # (every knob the line reports is sent, defaults included: the JSON labels what ran)
+    ctx.set_param("xcd_order", args.xcd_order)
+    ctx.set_param("stile_text", args.stile_text)
+    ctx.set_param("text_scatter", args.text_scatter)
+    ctx.set_param("doctree_k32", args.doctree_k32)
+    ctx.set_param("runs_slots", args.runs_slots)
     group = args.group_docs if args.group_docs >= 0 else int(args.order == "fugue")
     if group:
         ctx.set_param("group_docs", group)
@@ -696,6 +701,33 @@ def traces_workload(args) -> int:
             out["digests_ok"] = out["digests_ok"] and pres["digests_ok"]
         if rank == 0:
             pres["batch"].close()
+    # companion line: the headline batch in raw SoA mode: every merge first
+    # derives the key, the codepoint word with its flags and the compact nsq list on the device
+    # from reference-shaped columns (lamport, agent, deleted, codepoint beside the parents), so
+    # the step is priced over the raw SoA, the untimed input encoding included
+    if args.raw_companion:
+        def make_raw(bases, replicas, relabel, seed):
+            b = make_batch(bases, replicas, relabel, seed)
+            b.set_raw(True)
+            return b
+        ra = argparse.Namespace(replicas=args.replicas, relabel=args.relabel, warmup=1, steps=3)
+        rres = traces_rank(ra, comm, make_raw, inputs)
+        if rank == 0:
+            rb, rs = rres["batch"], rres["stats"]
+            kms = {k: float(np.mean([s_["stage_ns"][k] for s_ in rs])) / 1e6 for k in rs[0]["stage_ns"]}
+            out["companion_raw_soa"] = {
+                "workload": "config 3 (%d replicas per GPU, relabel=%s) over the raw SoA: the "
+                            "input encoding (key, flags, nsq list) derived on the device inside "
+                            "every timed merge" % (ra.replicas, ra.relabel),
+                "value": rres["value"], "unit": "patches/s", "ms_per_step": rres["step_s"] * 1e3,
+                "steps": ra.steps, "digests_ok": rres["digests_ok"],
+                "encode_ms": kms.get("encode", 0.0),
+                "raw_bytes_per_slot": 15, "encoded_bytes_per_slot_written": 11,
+                "kernels_ms": {k: v for k, v in kms.items() if v > 0.02},
+            }
+            out["digests_ok"] = out["digests_ok"] and rres["digests_ok"]
+        if rank == 0:
+            rres["batch"].close()
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:  # (the CPU lines belong to the N=1 run)
             threads = args.cpu_threads or host_cpus()["threads"]
@@ -721,6 +753,8 @@ def side_workload(args) -> int:
     ctx.set_param("level1", args.level1)
     ctx.set_param("contraction", args.contraction)
     ctx.set_param("l1_group", args.l1_group)
+    ctx.set_param("stile_text", args.stile_text)
+    ctx.set_param("text_scatter", args.text_scatter)
     if args.splitter_stride:
         ctx.set_param("splitter_stride", args.splitter_stride)
     t_setup = time.perf_counter()
@@ -774,7 +808,7 @@ def side_workload(args) -> int:
         }
         # every stage's roofline by its algorithmic bytes (DESIGN.md §7 pricing; no PMC here)
         rf = roofline_fields(stats, batch, batch.items, el / args.steps, pmc=False,
-                             stile_text=getattr(args, "stile_text", 2))
+                             stile_text=args.stile_text)
         out["rooflines"] = {k: {"kernel": v["kernel"], "frac": v["frac"],
                                 "achieved_gbps": v["achieved"], "launch_us": v["launch_us"]}
                             for k, v in rf["rooflines"].items()}
@@ -1016,11 +1050,20 @@ def parse_args(argv=None):
     ap.add_argument("--stile-text", type=int, default=2, choices=[0, 1, 2],
                     help="fused level 1 stages text from the tile segments (k_runs skips the "
                          "slot-order copy): 1 by loads and shifts, 2 by LDS-DMA per tile")
+    ap.add_argument("--raw-companion", type=int, default=1, choices=[0, 1],
+                    help="1: also time the headline batch in raw SoA mode (the input encoding "
+                         "derived on the device inside every merge)")
+    ap.add_argument("--doctree-k32", type=int, default=0, choices=[0, 1],
+                    help="1: every LDS level 1 on k_doctree_wide (32-bit sibling keys, 9 B of "
+                         "LDS per run instead of 15)")
+    ap.add_argument("--text-scatter", type=int, default=1, choices=[0, 1],
+                    help="1: k_doctree stops at the run offsets and k_tscatter streams the tiles' "
+                         "text to the documents; 0: k_doctree writes the text itself (phase C)")
     ap.add_argument("--group-docs", type=int, default=-1, choices=[-1, 0, 1],
                     help="replica batches placed base by base, each base in waves of its own "
                          "(-1: only for --order fugue, whose seph-blog1 rows exceed the LDS level 1)")
     ap.add_argument("--runs-slots", type=int, default=32, choices=[16, 32, 64],
-                    help="k_runs slots per thread (16: 256 threads per tile, 32: 128)")
+                    help="k_runs slots per thread (16: 256 threads per tile, 32: 128, 64: one wave)")
     ap.add_argument("--nsq-list", type=int, default=1, choices=[0, 1, 2],
                     help="1: resident batches (input encoding) and replicas of 2^22+ slots (every "
                          "merge) carry the compact list of the non-seq items' parents and keys; "

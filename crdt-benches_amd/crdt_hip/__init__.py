@@ -25,7 +25,7 @@ ERRORS = {
     -7: "EIO", -8: "ECOMM",
 }
 STAGES = ["classify", "runs", "sortb", "count", "scan", "place", "link", "walk1", "rank",
-          "walk2", "expand", "digest", "doctree"]
+          "walk2", "expand", "digest", "doctree", "text", "encode"]
 
 # Every symbol include/crdt_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -44,7 +44,7 @@ EXPORTS = [
     "crdt_hip_logfile_close", "crdt_hip_synth_agents",
     "crdt_hip_synth_tree", "crdt_hip_synth_tree_visible", "crdt_hip_merge", "crdt_hip_merge_batch", "crdt_hip_merge_order",
     "crdt_hip_batch_create", "crdt_hip_batch_synth_tree", "crdt_hip_batch_free", "crdt_hip_batch_info",
-    "crdt_hip_batch_merge", "crdt_hip_replica_new", "crdt_hip_replica_clone",
+    "crdt_hip_batch_merge", "crdt_hip_batch_raw", "crdt_hip_replica_new", "crdt_hip_replica_clone",
     "crdt_hip_replica_free", "crdt_hip_replica_apply_updates", "crdt_hip_replica_info",
     "crdt_hip_updates_upload", "crdt_hip_updates_free", "crdt_hip_replica_apply_resident",
     "crdt_hip_replica_merge", "crdt_hip_comm_unique_id", "crdt_hip_comm_init",
@@ -156,6 +156,7 @@ def lib() -> C.CDLL:
         "crdt_hip_batch_free": (i32, [vp]),
         "crdt_hip_batch_info": (i32, [vp, P(u64), P(u64), P(u64)]),
         "crdt_hip_batch_merge": (i32, [vp, vp, vp, vp, P(Stats)]),
+        "crdt_hip_batch_raw": (i32, [vp, vp, i32]),
         "crdt_hip_replica_new": (i32, [vp, P(View), P(vp)]),
         "crdt_hip_replica_clone": (i32, [vp, vp, P(vp)]),
         "crdt_hip_replica_free": (i32, [vp]),
@@ -607,6 +608,11 @@ class Batch:
         _check(lib().crdt_hip_batch_merge(self.ctx._h, self._h, dig.ctypes.data,
                                           lens.ctypes.data, C.byref(st)), self.ctx._h)
         return dig, lens, st.as_dict()
+
+    def set_raw(self, on: bool = True) -> None:
+        """Raw SoA mode (crdt_hip_batch_raw): every merge derives its input encoding on the device
+        from reference-shaped columns (lamport, agent, deleted, codepoint beside the parents)."""
+        _check(lib().crdt_hip_batch_raw(self.ctx._h, self._h, int(bool(on))), self.ctx._h)
 
 
 def pack_updates(updates) -> tuple:

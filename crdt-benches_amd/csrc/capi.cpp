@@ -225,6 +225,11 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
         ctx->eng.stile_text = (uint32_t)value;
         return 0;
     }
+    if (k == "text_scatter") {  // stile plans: 1 k_doctree + k_tscatter, 0 k_doctree phase C
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "text_scatter must be 0 or 1");
+        ctx->eng.text_scatter = (uint32_t)value;
+        return CRDT_HIP_OK;
+    }
     if (k == "contraction") {  // run contraction: 0 by the input, 1 always, 2 never (Wave::nocon)
         if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "contraction must be 0, 1 or 2");
         ctx->eng.contraction = (uint32_t)value;
@@ -244,6 +249,15 @@ int crdt_hip_set_param(crdt_hip_ctx* ctx, const char* key, uint64_t value) {
     if (k == "nsq_list") {  // the compact nsq parent list (Engine::build_nsq, nsq_launch)
         if (value > 2) return set_err(ctx, CRDT_HIP_EINVAL, "nsq_list must be 0, 1 or 2");
         ctx->eng.nsq_list = (uint32_t)value;
+        return 0;
+    }
+    if (k == "doctree_k32") {  // LDS level 1 with 32-bit sibling keys (Engine::doctree_k32)
+        if (value > 1) return set_err(ctx, CRDT_HIP_EINVAL, "doctree_k32 must be 0 or 1");
+        ctx->eng.doctree_k32 = value == 1;
+        return CRDT_HIP_OK;
+    }
+    if (k == "glds_late") {  // test hook (see Engine::glds_late)
+        ctx->eng.glds_late = value != 0;
         return 0;
     }
     if (k == "plan_shrink") {  // test hook (see Engine::plan_shrink)
@@ -689,6 +703,22 @@ int crdt_hip_batch_merge(crdt_hip_ctx* ctx, crdt_hip_batch* b, uint64_t* digests
     if (b->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "batch belongs to another context");
     return guard(ctx, [&] {
         return from_engine(ctx, ctx->eng.merge(b->logs, crdt::Engine::TEXT, digests, lens, stats));
+    });
+}
+
+int crdt_hip_batch_raw(crdt_hip_ctx* ctx, crdt_hip_batch* b, int on) {
+    if (!ctx || !b) return set_err(ctx, CRDT_HIP_EINVAL, "null argument");
+    if (b->ctx != ctx) return set_err(ctx, CRDT_HIP_EINVAL, "batch belongs to another context");
+    return guard(ctx, [&] {
+        if (!on) {
+            b->logs.raw = false;
+            return 0;
+        }
+        if (b->logs.raw_lam) {
+            b->logs.raw = true;
+            return 0;
+        }
+        return from_engine(ctx, ctx->eng.raw_keep(b->logs));
     });
 }
 

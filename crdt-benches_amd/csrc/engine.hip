@@ -108,7 +108,7 @@ __device__ __forceinline__ bool replan(const uint32_t* ctl) { return ctl[C_REPLA
 
 // Stages = event intervals of crdt_hip_stats (include/crdt_hip.h CRDT_HIP_STAGE_*).
 enum Stage { S_CLASSIFY, S_RUNS, S_SORTB, S_COUNT, S_SCAN, S_PLACE, S_LINK, S_WALK1, S_RANK,
-             S_WALK2, S_EXPAND, S_DIGEST, S_DOCTREE, S_N };
+             S_WALK2, S_EXPAND, S_DIGEST, S_DOCTREE, S_TEXT, S_ENCODE, S_N };
 
 
 // ---------------------------------------------------------------------------------------------
@@ -890,7 +890,10 @@ __global__ __launch_bounds__(kScanTile / SL) __attribute__((amdgpu_waves_per_eu(
             if (sq) {
                 pr = rho - 1u;  // the parent is the slot before the head: the previous run's last row
             } else if (!root) {
-                if (ps >= a.nslots) ps = dc.x;  // (a bad parent, flagged by k_classify: any in-range read)
+                // (a bad parent, flagged by k_classify: out of range, or the item itself, whose
+                // row would be its own parent, a self-loop for the global level 1; any in-range
+                // read that names another row does)
+                if (ps >= a.nslots || ps == g) ps = dc.x;
                 const uint4 hr = a.hrec[ps >> 6];
                 const uint64_t hb = ((uint64_t)hr.y << 32) | hr.x;
                 const uint32_t hl = hr.z;
@@ -2314,6 +2317,10 @@ struct DocArgs {
     uint8_t* text;
     uint8_t* fused;       // per document: 1 = text written by k_doctree
     uint32_t lds_bytes;   // dynamic LDS of the launch
+    // scatter mode (text == nullptr): roff[run] = the run's place in the wave's text (its
+    // document's output offset + its document offset, u32) for k_tscatter, which moves the text
+    uint32_t scatter;
+    uint32_t glds_late;  // test hook: LDS-DMA staging loads issued last (doc_text)
 };
 
 // LDS bytes of a document with up to rcap - 2 runs: D, nx, ch (2 B/run each), the sibling keys
@@ -2488,9 +2495,10 @@ __device__ __forceinline__ void stage_from_tiles(const DocArgs& a, uint32_t p0, 
 // wait at the barrier.  A run of tile k then reads its text at staging offset
 // 16 cpx[k] + (ps - tpx[k]) - akt[k].  No register holds the bytes, no byte is shifted, and no
 // chunk is partly copied.  Table: tpx, cpx, akt (nt + 2 u32 each) at `tab`.
-__device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32_t tl, uint32_t t0,
-                                           uint32_t nt, uint32_t tpx_reg, uint8_t* st,
-                                           uint32_t* tab, uint32_t* scan_lds) {
+// The table (returns the chunk count C); stage_glds_issue then issues the loads.
+__device__ __forceinline__ uint32_t stage_glds_table(uint32_t p0, uint32_t tl, uint32_t nt,
+                                                     uint32_t tpx_reg, uint32_t* tab,
+                                                     uint32_t* scan_lds) {
     const uint32_t t = threadIdx.x;
     uint32_t* tpx = tab;
     uint32_t* cpx = tab + (nt + 2u);
@@ -2513,6 +2521,13 @@ __device__ __forceinline__ void stage_glds(const DocArgs& a, uint32_t p0, uint32
         akt[t] = ak;
     }
     __syncthreads();
+    return C;
+}
+__device__ __forceinline__ void stage_glds_issue(const DocArgs& a, uint32_t C, uint32_t t0,
+                                                 uint32_t nt, uint8_t* st, const uint32_t* tab) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t* cpx = tab + (nt + 2u);
+    const uint32_t* akt = cpx + (nt + 2u);
     const uint32_t lane = t & 63u, wv = t >> 6;
     constexpr int kG = 4;  // chunks per thread per round (their tile searches interleave)
     for (uint32_t c0 = 64u * wv; c0 < C; c0 += 64u * 16u * kG) {
@@ -2575,13 +2590,19 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
     uint32_t* delta = reinterpret_cast<uint32_t*>(st + o_delta);
     uint32_t* tab = reinterpret_cast<uint32_t*>(st + o_tab);
     if (tprobe) tprobe[1] = wall_clock64();
-    // 1) staging (every load first; the run prefixes ps were loaded before the offsets)
+    // 1) staging (every load first; the run prefixes ps were loaded before the offsets).  Test
+    // hook glds_late: the LDS-DMA loads are issued after the deltas instead, right in front of
+    // the wait and barrier before the output, so that the output reads chunks still in flight
+    // unless that wait holds (tests/test_gpu_merge.py pins the engine.hip vmcnt wait with it)
+    uint32_t gC = 0;
     if (a.stile_text) {
         for (uint32_t i = t; i < nw; i += kDocThreads) bits[i] = 0;
-        if (glds)
-            stage_glds(a, p0, tl, t0, nt, tpx_reg, st, tab, scan_lds);
-        else
+        if (glds) {
+            gC = stage_glds_table(p0, tl, nt, tpx_reg, tab, scan_lds);
+            if (!a.glds_late) stage_glds_issue(a, gC, t0, nt, st, tab);
+        } else {
             stage_from_tiles(a, p0, tl, sh, t0, nt, tpx_reg, st, tab, scan_lds);
+        }
     }
     {
         if (!a.stile_text) {
@@ -2656,6 +2677,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
         for (int j = 0; j < J; ++j)
             if (ro[j] != kNil) delta[rk[j]] = dv[j];
     }
+    if (glds && a.glds_late) stage_glds_issue(a, gC, t0, nt, st, tab);
     // (LDS-DMA staging) the DMA writes LDS as a global load, and a workgroup barrier waits only
     // for LDS operations (lgkmcnt): every wave waits for its own staging loads (vmcnt) before the
     // barrier after which any wave reads any staged chunk
@@ -3173,10 +3195,11 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             // weightless (or never reached: flagged below)
             ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (sr >> 14) : kNil;
         }
-        if (!a.text) {  // offsets for k_expand
+        if (!a.text) {  // offsets for k_expand (document-relative) or k_tscatter (wave-relative)
+            const uint32_t ob = a.scatter ? wg1.y : 0u;  // (scatter: the wave's text is < 4 GiB)
 #pragma unroll
             for (int j = 0; j < J; ++j)
-                if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ro[j];
+                if (ro[j] != kNil) a.roff[base + t + (uint32_t)j * kDocThreads] = ob + ro[j];
         }
     }
     const uint32_t wsum = wave_sum(runs);
@@ -3269,18 +3292,23 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 // 17 rows per thread (Fugue seph-blog1, 16.6 k rows; 8 VGPRs spill on its own, ~40 inside
 // k_doctree_wide).
 constexpr int kDocJNarrow = 12;
+#ifdef CRDT_DOC_WPE  // (experiment: cap k_doctree's registers so other kernels' waves fit beside it)
+#define DOC_WPE __attribute__((amdgpu_waves_per_eu(CRDT_DOC_WPE)))
+#else
+#define DOC_WPE
+#endif
 template <int J, bool K32>
 __device__ __forceinline__ bool doctree_try(const DocArgs& a, uint32_t R) {
     if (R > (uint32_t)J * kDocThreads) return false;
     doctree_doc<J, K32>(a, blockIdx.x);
     return true;
 }
-__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
+__global__ __launch_bounds__(kDocThreads) DOC_WPE void k_doctree(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
     if (doctree_try<4, false>(a, R) || doctree_try<8, false>(a, R)) return;
     doctree_doc<kDocJNarrow, false>(a, blockIdx.x);
 }
-__global__ __launch_bounds__(kDocThreads) void k_doctree_wide(DocArgs a) {
+__global__ __launch_bounds__(kDocThreads) DOC_WPE void k_doctree_wide(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
     if (doctree_try<8, true>(a, R)) return;
     doctree_doc<kDocJNarrow, true>(a, blockIdx.x);
@@ -3290,6 +3318,194 @@ __global__ __launch_bounds__(kDocThreads) void k_doctree_wide(DocArgs a) {
 __global__ __launch_bounds__(kDocThreads) void k_doctree_wide17(DocArgs a) {
     doctree_doc<kDocJ, true>(a, blockIdx.x);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Text scatter (k_tscatter): the documents of a wave whose k_doctree ran in scatter mode
+// ---------------------------------------------------------------------------------------------
+// k_doctree in scatter mode ends with the run offsets: every weighted row's place in the wave's
+// text (its document's output offset + its offset in the document; u32, the host takes this mode
+// only for waves with less than 4 GiB of text) goes to roff, and no text is staged in LDS.  This
+// kernel then writes the text as a grid-wide stream, one wave per 4096-slot tile.  Runs never
+// cross tiles (k_heads), so the tile's rows [tile_hw[k].x, tile_hw[k + 1].x) have their visible
+// UTF-8 in row order in the tile's stile segment (k_classify), one contiguous range.  The wave
+// takes the rows 64 at a time (a chunk): their bytes are one contiguous stretch of the segment.
+// Per chunk one round of loads: the rows' weight prefixes and places, and (LDS-DMA, 16 B per lane)
+// the first kScatterWin bytes of the stretch, whose start is the previous chunk's end; longer
+// stretches take more windows.  Then 64 bytes per step, one per lane, each stored at its row's
+// place.  The row of a byte: the starts of the chunk's weighted rows are bits of an LDS bitmap
+// over the window (one ds_or each), a step reads its 64 bits with one broadcast read, and a
+// lane's row is the starts at or before its byte (mbcnt) plus the starts of the earlier steps;
+// the weighted rows' bases (place - start in the stretch) are compacted in LDS in start order.
+// A step's 64 bytes land in the few rows they belong to (~9 bytes per row on the traces), each a
+// contiguous destination range, so its stores touch a few lines.
+#ifndef CRDT_TSC_WIN
+#define CRDT_TSC_WIN 1024
+#endif
+#ifndef CRDT_TSC_RQ
+#define CRDT_TSC_RQ 1
+#endif
+constexpr uint32_t kScatterWin = CRDT_TSC_WIN;  // stretch bytes staged per window (1 KiB per DMA)
+static_assert(kScatterWin / 32 + 2 <= 64, "a window's bitmap words fit one VGPR of the wave");
+constexpr uint32_t kScatterRows = 64 * CRDT_TSC_RQ;  // rows per round of loads
+#ifndef CRDT_TSC_TPW
+#define CRDT_TSC_TPW 4
+#endif
+constexpr uint32_t kScatterTiles = CRDT_TSC_TPW;  // consecutive tiles per wave (<= 63)
+struct ScatterArgs {
+    uint32_t ntiles, xcd;
+    const uint2* tile_hw;      // per tile {rows before it, weight before it}
+    const uint32_t* r_pstart;  // per row: weight prefix ([R] = the wave's weight)
+    const uint32_t* roff;      // per weighted row: its place in the wave's text (k_doctree)
+    const uint8_t* stile;      // per tile: its visible UTF-8 in row order (kTileBytes each)
+    uint8_t* text;
+    uint64_t text_cap;
+    uint32_t* ctl;
+};
+// One window of the stretch: segment bytes [a0, min(a1, a0 + kScatterWin)) (a0 16-aligned) into
+// buf, 16 B per lane and KiB, through registers: an LDS-DMA would leave a write to LDS pending on
+// the vector-memory counter, and the compiler then waits for every outstanding store (the same
+// counter) before each LDS read of the steps below.
+__device__ __forceinline__ void scatter_window(const uint8_t* seg, uint32_t a0, uint32_t a1,
+                                               uint8_t* buf, uint32_t lane) {
+    uint4 v[kScatterWin / 1024u];
+#pragma unroll
+    for (uint32_t i = 0; i < kScatterWin / 1024u; ++i) {
+        const uint32_t o = a0 + 1024u * i + 16u * lane;
+        v[i] = o < a1 ? *reinterpret_cast<const uint4*>(seg + o) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kScatterWin / 1024u; ++i)
+        *reinterpret_cast<uint4*>(buf + 1024u * i + 16u * lane) = v[i];
+}
+__device__ __forceinline__ uint32_t uni(uint32_t x) {  // (a wave-uniform value, as an SGPR)
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__global__ __launch_bounds__(kBlock) void k_tscatter(ScatterArgs a) {
+    constexpr uint32_t NW = kBlock / 64;
+    constexpr uint32_t BW = kScatterWin / 32 + 2;  // bitmap words (+2: a step's second word)
+    constexpr int RQ = kScatterRows / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t tb[NW][kScatterWin];
+    __shared__ uint32_t bm[NW][BW];
+    __shared__ uint32_t lb[NW][kScatterRows];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    // (no barrier below: every wave works alone on its own LDS)
+    if (replan(a.ctl) || a.ctl[C_ERR]) return;  // (an error: the host redoes or rejects the wave)
+    const uint32_t tile0 = (xcd_block(blockIdx.x, gridDim.x, a.xcd) * NW + wv) * kScatterTiles;
+    if (tile0 >= a.ntiles) return;
+    uint8_t* buf = tb[wv];
+    uint32_t* bmw = bm[wv];
+    uint32_t* lbw = lb[wv];
+    for (uint32_t i = lane; i < BW; i += 64u) bmw[i] = 0;
+    // the {rows, weight} prefixes of the wave's tiles and of the one after them, one per lane
+    // (the wave's last: ctl's totals)
+    const uint2 hl = a.tile_hw[min(tile0 + lane, a.ntiles - 1u)];
+    const uint2 hc = make_uint2(a.ctl[C_RTOTAL], a.ctl[C_WTOTAL]);
+    const uint2 hv = tile0 + lane < a.ntiles ? hl : hc;
+    bool oob = false;
+#ifdef CRDT_TSC_NOSTORE
+    uint32_t sink = 0;
+#endif
+    for (uint32_t tk = 0; tk < kScatterTiles && tile0 + tk < a.ntiles; ++tk) {
+    const uint32_t tile = tile0 + tk;
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, (int)tk);
+    const uint32_t h1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, (int)tk + 1);
+    const uint32_t wt0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, (int)tk);
+    // (the tile's text: segment bytes [0, te); no load reaches past it)
+    const uint32_t te = min((uint32_t)__builtin_amdgcn_readlane((int)hv.y, (int)tk + 1) - wt0,
+                            kTileBytes);
+    const uint8_t* seg = a.stile + (uint64_t)tile * kTileBytes;
+    uint32_t p0 = wt0;  // the rows' stretch start (weight position): the previous round's end
+    for (uint32_t c = r0; c < h1; c += kScatterRows) {
+        const uint32_t nr = min(kScatterRows, h1 - c);
+        // one round of loads: prefixes, places, the stretch's first window
+        const uint32_t sh = (p0 - wt0) & 15u, a0 = (p0 - wt0) & ~15u;
+        uint32_t ps[RQ], ro[RQ];
+        const uint32_t pe = a.r_pstart[c + nr];  // (the stretch's end)
+#pragma unroll
+        for (int i = 0; i < RQ; ++i) {
+            const uint32_t r = lane + 64u * (uint32_t)i;
+            ps[i] = r < nr ? a.r_pstart[c + r] : 0u;
+            ro[i] = r < nr ? a.roff[c + r] : 0u;  // (weightless rows: unused)
+        }
+        scatter_window(seg, a0, te, buf, lane);  // (every load of the round issued before a use)
+        const uint32_t pend = uni(pe);
+#pragma unroll
+        for (int i = 0; i < RQ; ++i) ps[i] = lane + 64u * (uint32_t)i < nr ? ps[i] : pend;
+        const uint32_t T = pend - p0, U = T + sh;
+        uint32_t w[RQ], u[RQ];
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < RQ; ++i) {
+            const uint32_t nx = (uint32_t)__shfl_down((int)ps[i], 1);
+            const uint32_t n63 = i + 1 < RQ ? uni(ps[i + 1 < RQ ? i + 1 : i]) : pend;
+            w[i] = (lane == 63u ? n63 : nx) - ps[i];
+            u[i] = ps[i] - p0 + sh;  // (the row's start in window coordinates)
+            bad |= w[i] && (uint64_t)ro[i] + w[i] > a.text_cap;
+        }
+        // a place beyond the text buffer (only a malformed wave, which k_doctree flags): no store
+        if (__ballot(bad)) {
+            oob = true;
+            p0 = pend;
+            continue;
+        }
+        // compacted bases of the weighted rows, in start order: the byte at window coordinate x
+        // goes to lbw[its row] + x
+        uint32_t kb = 0;
+#pragma unroll
+        for (int i = 0; i < RQ; ++i) {
+            const uint64_t wm = __ballot(w[i] != 0u);
+            const uint32_t k = kb + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
+            if (w[i]) lbw[k] = ro[i] - u[i];
+            kb += (uint32_t)__popcll(wm);
+        }
+        uint32_t cnt = 0;  // weighted starts before the step
+        for (uint32_t w0 = 0; w0 < U; w0 += kScatterWin) {
+            if (w0) scatter_window(seg, a0 + w0, te, buf, lane);  // (a longer stretch)
+#pragma unroll
+            for (int i = 0; i < RQ; ++i)
+                if (w[i] && u[i] >= w0 && u[i] - w0 < kScatterWin)
+                    atomicOr(&bmw[(u[i] - w0) >> 5], 1u << ((u[i] - w0) & 31u));
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // (lgkmcnt(0): the wave's bits are in)
+            const uint32_t w1 = min(U, w0 + kScatterWin) - w0;
+            // the window's bitmap in one VGPR (lane j: word j): a step reads its two words by
+            // v_readlane, no LDS round trip
+            const uint32_t bwd = lane < BW ? bmw[lane] : 0u;
+            // A step: the row of lane L's byte is (starts at or before it) - 1 = cnt + M_0 - 1
+            // + (bits of M >> 1 below L): the uniform part in SGPRs, one mbcnt pair per lane.
+            const uint32_t lo = w0 ? 0u : sh;  // (the first window starts at sh)
+            const uint32_t* lbx = lbw;
+            uint32_t x = lane;  // (this lane's byte, window coordinate)
+#pragma unroll 4
+            for (uint32_t b = 0; b < w1; b += 64u, x += 64u) {
+                const int q = (int)(b >> 5);
+                const uint64_t M = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)bwd, q + 1) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)bwd, q);
+                const uint32_t base = cnt + (uint32_t)(M & 1u) - 1u;
+                const uint64_t Ms = M >> 1;
+                cnt += (uint32_t)__popcll(M);
+                const uint32_t own = __builtin_amdgcn_mbcnt_hi((uint32_t)(Ms >> 32),
+                                         __builtin_amdgcn_mbcnt_lo((uint32_t)Ms, base));
+#ifdef CRDT_TSC_NOSTORE
+                if (x < w1 && x >= lo) sink ^= lbx[own] + w0 + x + buf[x];
+#else
+                if (x < w1 && x >= lo) a.text[lbx[own] + w0 + x] = buf[x];
+#endif
+            }
+            // (clear for the next window / round; the reads above are done first)
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            for (uint32_t i = lane; i < (w1 + 31u) / 32u + 2u && i < BW; i += 64u) bmw[i] = 0u;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        p0 = pend;
+    }
+    }
+    if (oob) atomicOr(&a.ctl[C_ERR], 8u);
+#ifdef CRDT_TSC_NOSTORE
+    if (sink == 0x12345678u) a.text[lane] = 0;  // (keeps the work)
+#endif
+}
+
 // ---------------------------------------------------------------------------------------------
 // digest: xxh64 of 4 KiB leaves, then xxh64 of the leaf digests seeded with the length
 // ---------------------------------------------------------------------------------------------
@@ -3673,6 +3889,8 @@ void DeviceLogs::release() {
     nsq_ok = false;
     nsq_cap = nsq_pre_cap = nsq_sums_cap = 0;
     dfree(docs_rel); dfree(doc_rank); dfree(chunk_doc);
+    dfree(raw_lam); dfree(raw_agent); dfree(raw_del); dfree(raw_cp);
+    raw = false;
     cap_slots = cap_docs = cap_chunks = 0;
     tab_sig.clear();
 }
@@ -3695,6 +3913,8 @@ Engine::~Engine() {
     if (host_out_) (void)hipHostFree(host_out_);
     for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : wev_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : raw_ev_)
+        if (e) (void)hipEventDestroy(e);
     if (ev_l0_) (void)hipEventDestroy(ev_l0_);
     if (ev_l1_) (void)hipEventDestroy(ev_l1_);
     if (stream_l1) {
@@ -4125,7 +4345,7 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     // offsets are packed in 18 bits inside the walk: documents below 256 KiB of text):
     // k_doctree (8-byte keys, 12 runs per thread), else k_doctree_wide (32-bit keys, 14)
     uint64_t dbytes = doctree_lds_bytes(p.rcap, p.scap, false);
-    p.wide = rmax > (uint32_t)(kDocJNarrow * kDocThreads) || dbytes > kDocLds;
+    p.wide = rmax > (uint32_t)(kDocJNarrow * kDocThreads) || dbytes > kDocLds || doctree_k32;
     if (p.wide) dbytes = doctree_lds_bytes(p.rcap, p.scap, true);
     p.lds1 = !level1_global && !force_global && rmax <= (uint32_t)(kDocJ * kDocThreads) &&
              dbytes <= kDocLds && w.max_doc_text < (1ull << 18);
@@ -4134,6 +4354,9 @@ L1Plan Engine::plan_level1(const Wave& w, uint32_t R, uint32_t rmax, bool ord,
     p.fuse = fuse_text && p.lds1 && !ord && w.max_doc_text + 512u <= kDocLds;
     // (a document spans at most max_doc_slots / 4096 + 2 tiles)
     p.stile_text = p.fuse && stile_text && w.max_doc_slots / kScanTile + 2u <= kDocTiles;
+    // (roff holds u32 places in the wave's text)
+    p.scatter = p.stile_text && text_scatter && w.text_cap + 64u < (1ull << 32);
+    p.dyn_scatter = dbytes;
     // (+ the glds staging's partly used chunks and tile table: 44 B per tile)
     p.dyn_bytes = p.fuse ? std::min<uint64_t>(kDocLds, std::max<uint64_t>(
                                dbytes, (w.max_doc_text * 5 / 4 + 4ull * rmax + 512u +
@@ -4230,7 +4453,7 @@ int Engine::clock_mark(StageClock& c, int stage) {
     a.wtmp = wtmp_;                                                                   \
     a.ovf = ovf_
 
-// k_runs with 16 or 32 slots per thread (Engine::runs_slots)
+// k_runs with 16, 32 or 64 slots per thread (Engine::runs_slots)
 void launch_k_runs(const L0Args& a0, uint32_t ntiles, hipStream_t s, uint32_t slots) {
     if (a0.fugue) {
         if (slots == 64)
@@ -4293,6 +4516,8 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     hipStream_t s = cur_;
     TREEARGS(a);
     tail_nspl_ = 0;  // (k_doctree leaves any offsets k_expand needs in roff)
+    const bool scatter = stile && p.scatter;
+    tail_scatter_ = scatter;
     DocArgs da{};
     da.ndocs = w.ndocs;
     da.rcap = p.rcap;
@@ -4308,24 +4533,26 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.tlen = tlen_;
     da.toff = toff_;
     da.sbytes = sbytes_;
-    da.text = p.fuse ? text_ : nullptr;
+    da.text = p.fuse && !scatter ? text_ : nullptr;
     da.fused = doc_fused_;
-    da.lds_bytes = (uint32_t)p.dyn_bytes;
+    da.scatter = scatter ? 1u : 0u;
+    da.glds_late = glds_late ? 1u : 0u;
+    da.lds_bytes = (uint32_t)(scatter ? p.dyn_scatter : p.dyn_bytes);
     da.probe = probe_doc_;
     da.wg = wgtab_;
     da.keyoff = doctree_key_off(p.rcap, p.scap, p.wide);
-    da.stile_text = stile ? (stile_text == 2u ? 2u : 1u) : 0u;
+    da.stile_text = stile && !scatter ? (stile_text == 2u ? 2u : 1u) : 0u;
     da.ntiles = (uint32_t)((w.nslots + kScanTile - 1) / kScanTile);
     da.stile = stile_;
     da.tile_hw = tile_hw_;
     a.wg = wgtab_;  // (k_doctotals writes the k_doctree workgroup descriptors)
     k_doctotals<<<1, 1024, 0, s>>>(a);
     if (p.wide && p.rmax > (uint32_t)(kDocJNarrow * kDocThreads))
-        k_doctree_wide17<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+        k_doctree_wide17<<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
     else if (p.wide)
-        k_doctree_wide<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+        k_doctree_wide<<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
     else
-        k_doctree<<<w.ndocs, kDocThreads, (uint32_t)p.dyn_bytes, s>>>(da);
+        k_doctree<<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
     MARK(S_DOCTREE);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;
@@ -4337,6 +4564,7 @@ int Engine::launch_global_level1(DeviceLogs& L, const Wave& w, bool ord, const L
                                  StageClock& ck, uint32_t& rounds) {
     hipStream_t s = cur_;
     TREEARGS(a);
+    tail_scatter_ = false;
     const uint32_t R = p.R;
     // splitter stride: longer sublists once the pointer jumping over the splitter lists
     // dominates (measured on config 5: 182 M runs, stride 16 -> 64 took 72 -> 59 ms)
@@ -4524,6 +4752,20 @@ int Engine::launch_tail(DeviceLogs& L, const Wave& w, bool ord, bool fused, Stag
         k_expand<<<4096, kBlock, 0, s>>>(ea);
         MARK(S_EXPAND);
     }
+    if (tail_scatter_) {  // (k_doctree in scatter mode left the text to k_tscatter)
+        ScatterArgs sa{};
+        sa.ntiles = a0.ntiles;
+        sa.xcd = a0.xcd;
+        sa.tile_hw = tile_hw_;
+        sa.r_pstart = r_pstart_;
+        sa.roff = roff_;
+        sa.stile = stile_;
+        sa.text = text_;
+        sa.text_cap = cap_text_ - 64;
+        sa.ctl = ctl_;
+        k_tscatter<<<grid_for(sa.ntiles, (kBlock / 64) * kScatterTiles), kBlock, 0, s>>>(sa);
+        MARK(S_TEXT);
+    }
     if (!ord) {
         k_leafhash<<<grid_for(w.leaf_cap + 1, (kBlock / 64) * kLeafGroup), kBlock, 0, s>>>(
             a, (uint32_t)(w.leaf_cap + 1));
@@ -4555,7 +4797,7 @@ int Engine::finish_wave(const Wave& w, bool ord, const L1Plan& p, uint32_t round
                                     (3 + rounds) * g1, (wt ? 4u : 1u) * g1,
                                     expand_run ? 1u : 0u,
                                     ord ? 0u : (w.max_doc_text > (uint64_t)kLeaf * kGroup ? 3u : 2u),
-                                    p.lds1 ? 2u : 0u};
+                                    p.lds1 ? 2u : 0u, p.lds1 && p.scatter ? 1u : 0u, 0u};
     for (uint32_t i = 0; i + 1 < ck.n; ++i) {
         if (ck.stage[i] >= S_N) continue;  // not a stage (a host wait between two launches)
         float ms = 0;
@@ -4604,7 +4846,8 @@ int Engine::run_wave(DeviceLogs& L, uint32_t wi, Mode mode, std::vector<float>& 
                                : "malformed op log: parent id out of range";
         return CRDT_HIP_EBADLOG;
     }
-    const L1Plan p = plan_level1(w, hctl[C_RTOTAL], hctl[C_RMAX], ord, force_global);
+    L1Plan p = plan_level1(w, hctl[C_RTOTAL], hctl[C_RMAX], ord, force_global);
+    p.scatter = false;  // (no stile here: k_runs writes the slot-order text, k_doctree stages it)
     const uint32_t lg = log2m_set ? log2m : (p.R > (1u << 24) ? 6u : 4u);
     const uint32_t Sreg = 2 * ((p.R + (1u << lg) - 1) >> lg);
     const uint64_t rows = cap_runs_;  // run rows k_runs could write
@@ -4712,6 +4955,29 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
         return CRDT_HIP_EINVAL;
     }
     if (const char* pe = getenv("CRDT_HIP_PROBE")) probe_doc_ = 1u + (uint32_t)atoi(pe);
+    if (L.raw) {  // (raw SoA mode: the input encoding is part of every merge)
+        if (!raw_ev_[0]) {
+            HIPCHK(hipEventCreate(&raw_ev_[0]), "event create");
+            HIPCHK(hipEventCreate(&raw_ev_[1]), "event create");
+        }
+        HIPCHK(hipEventRecord(raw_ev_[0], stream), "event record");
+        if (const int rc = raw_encode(L)) return rc;
+        HIPCHK(hipEventRecord(raw_ev_[1], stream), "event record");
+        const int rc = merge_inner(L, mode, digests, lens, st, text_out, text_offsets, cps);
+        if (rc || !st) return rc;
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, raw_ev_[0], raw_ev_[1]), "event time");
+        st->stage_ns[S_ENCODE] += (uint64_t)((double)ms * 1e6);
+        st->stage_launches[S_ENCODE] += (uint32_t)L.waves.size() + (L.nsq_ok ? 3u + (uint32_t)L.waves.size() : 0u);
+        st->total_ns += (uint64_t)((double)ms * 1e6);
+        return rc;
+    }
+    return merge_inner(L, mode, digests, lens, st, text_out, text_offsets, cps);
+}
+
+int Engine::merge_inner(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+                        crdt_hip_stats* st, std::vector<uint8_t>* text_out,
+                        std::vector<uint64_t>* text_offsets, uint64_t* cps) {
     bool hinted = plan_cache && mode == TEXT && !text_out && !text_offsets && !L.waves.empty();
     for (const Wave& w : L.waves) hinted = hinted && w.hint_lds;
     if (hinted) return merge_async(L, digests, lens, cps, st);
@@ -4798,6 +5064,9 @@ int Engine::merge_async_prepare(DeviceLogs& L, AsyncMerge& m, bool timed) {
         m.eng[i]->fuse_text = fuse_text;
         m.eng[i]->xcd_order = xcd_order;
         m.eng[i]->stile_text = stile_text;
+        m.eng[i]->text_scatter = text_scatter;
+        m.eng[i]->glds_late = glds_late;
+        m.eng[i]->doctree_k32 = doctree_k32;
         m.eng[i]->runs_slots = runs_slots;
         m.eng[i]->l1_split = l1_split;
         m.eng[i]->probe_doc_ = probe_doc_;
@@ -4999,6 +5268,9 @@ int Engine::merge_lanes(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* l
         eng[i]->fuse_text = fuse_text;
         eng[i]->xcd_order = xcd_order;
         eng[i]->stile_text = stile_text;
+        eng[i]->text_scatter = text_scatter;
+        eng[i]->glds_late = glds_late;
+        eng[i]->doctree_k32 = doctree_k32;
         eng[i]->runs_slots = runs_slots;
         eng[i]->probe_doc_ = probe_doc_;
     }
@@ -5216,16 +5488,132 @@ int Engine::nsq_reserve_prefix(DeviceLogs& L) {
 // Counts of the nsq items per 64-slot chunk, scanned in place into L.nsq_pre (launches only).
 void Engine::nsq_count_scan(DeviceLogs& L) {
     const bool ord = false;  // (L0ARGS)
-    const uint32_t n = (uint32_t)(L.total_slots / 64 + 64), nb = (n + kScanTile - 1) / kScanTile;
+    const uint32_t n = (uint32_t)(L.total_slots / 64 + 64);
     (void)hipMemsetAsync(L.nsq_pre, 0, (n + 1ull) * 4, stream);
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
         k_nsq_count<<<grid_for((w.nslots + 15) / 16), kBlock, 0, stream>>>(a0, L.nsq_pre + (w.slot0 >> 6),
                                                                    L.nsq_mask + (w.slot0 >> 6));
     }
+    nsq_scan(L);
+}
+void Engine::nsq_scan(DeviceLogs& L) {
+    const uint32_t n = (uint32_t)(L.total_slots / 64 + 64), nb = (n + kScanTile - 1) / kScanTile;
     k_scan_reduce<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, L.nsq_sums);
     k_scan_top<<<1, 1024, 0, stream>>>(L.nsq_sums, nb, L.nsq_pre, n);
     k_scan_apply<<<nb, kBlock, 0, stream>>>(L.nsq_pre, n, L.nsq_sums, L.nsq_pre);
+}
+
+// Raw SoA mode (DeviceLogs::raw).  k_raw_fill keeps the reference-shaped columns of resident logs
+// once (lamport, agent, deleted, codepoint per slot, from the encoded key and codepoint word);
+// k_raw_encode derives the encoded input from them and the parent column at every merge: 16
+// slots per thread, the key (lamport << 16 | agent), the 3-byte codepoint word with the tombstone
+// and the previous-slot flag (parent == index - 1), and the nsq count and mask of each 64-slot
+// chunk (what k_nsq_count reads back from the codepoint words otherwise).  Item slots only: a
+// document start and the padding keep their words.  RGA logs.
+__global__ __launch_bounds__(kBlock) void k_raw_fill(L0Args a, uint32_t* __restrict__ lam,
+                                                     uint16_t* __restrict__ agent,
+                                                     uint8_t* __restrict__ del,
+                                                     uint32_t* __restrict__ cpw) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.nslots) return;
+    const uint64_t k = a.in_key[g];
+    const uint32_t c = cp3_get(a.in_cp, g);
+    lam[g] = (uint32_t)(k >> 16);
+    agent[g] = (uint16_t)k;
+    del[g] = (c & kDelBit) ? 1u : 0u;
+    cpw[g] = c & 0x1FFFFFu;
+}
+__global__ __launch_bounds__(kBlock) void k_raw_encode(L0Args a, const uint32_t* __restrict__ lam,
+                                                       const uint16_t* __restrict__ agent,
+                                                       const uint8_t* __restrict__ del,
+                                                       const uint32_t* __restrict__ cpw,
+                                                       uint64_t* __restrict__ key,
+                                                       uint8_t* __restrict__ cp3,
+                                                       uint32_t* __restrict__ cnt,
+                                                       uint64_t* __restrict__ mask) {
+    // one slot per lane (every column read and the key written coalesced); a wave = one 64-slot
+    // chunk (its nsq mask is a ballot); the block's 256 codepoint words are assembled in LDS and
+    // stored as 48 16-byte pieces
+    __shared__ __attribute__((aligned(16))) uint8_t cb[3 * kBlock];
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    bool nsq = false;
+    uint32_t c = 0;
+    if (g < a.nslots) {
+        const uint2 doc = a.docs[a.chunk_doc[g >> a.log2m]];
+        const uint32_t l = g - doc.x;  // (the slot's item index; 0: the document start)
+        const uint32_t p = a.in_parent[g], lm = lam[g], cw = cpw[g];
+        const uint16_t ag = agent[g];
+        const uint8_t dl = del[g];
+        if (l - 1u < doc.y) {
+            const bool sq = p == l - 1u;
+            nsq = !sq;
+            c = (cw & 0x1FFFFFu) | (dl ? kDelBit : 0u) | (sq ? kSeqBit : 0u);
+            key[g] = ((uint64_t)lm << 16) | ag;
+        } else {
+            c = cp3_get(a.in_cp, g);  // (a document start or padding keeps its word)
+        }
+    }
+    cb[3 * threadIdx.x] = (uint8_t)c;
+    cb[3 * threadIdx.x + 1] = (uint8_t)(c >> 8);
+    cb[3 * threadIdx.x + 2] = (uint8_t)(c >> 16);
+    const uint64_t m = __ballot(nsq);
+    if ((threadIdx.x & 63u) == 0u && g < a.nslots && cnt) {
+        cnt[g >> 6] = (uint32_t)__popcll(m);
+        mask[g >> 6] = m;
+    }
+    __syncthreads();
+    const uint32_t g0 = blockIdx.x * kBlock;
+    if (threadIdx.x < 3 * kBlock / 16 && g0 + 16u * threadIdx.x / 3u < a.nslots)
+        reinterpret_cast<uint4*>(cp3 + 3ull * g0)[threadIdx.x] =
+            reinterpret_cast<const uint4*>(cb)[threadIdx.x];
+}
+
+int Engine::raw_keep(DeviceLogs& L) {
+    if (L.fugue) {
+        err = "raw SoA mode needs RGA logs";
+        return CRDT_HIP_EINVAL;
+    }
+    if (L.raw) return CRDT_HIP_OK;
+    const uint64_t n = L.total_slots + 64;
+    HIPCHK(dalloc(&L.raw_lam, n), "hipMalloc raw lamport");
+    HIPCHK(dalloc(&L.raw_agent, n), "hipMalloc raw agent");
+    HIPCHK(dalloc(&L.raw_del, n), "hipMalloc raw deleted");
+    HIPCHK(dalloc(&L.raw_cp, n), "hipMalloc raw codepoint");
+    const bool ord = false;  // (L0ARGS)
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_raw_fill<<<grid_for(w.nslots), kBlock, 0, stream>>>(a0, L.raw_lam + w.slot0,
+                                                               L.raw_agent + w.slot0,
+                                                               L.raw_del + w.slot0,
+                                                               L.raw_cp + w.slot0);
+    }
+    HIPCHK(hipGetLastError(), "raw fill launch");
+    HIPCHK(hipStreamSynchronize(stream), "raw fill");
+    L.raw = true;
+    gen_++;
+    return CRDT_HIP_OK;
+}
+
+// The merge's input encoding from the raw columns (launches only, on the engine's stream): keys,
+// codepoint words and nsq counts per wave, then the nsq scan and list (when the batch keeps one).
+int Engine::raw_encode(DeviceLogs& L) {
+    const bool ord = false;  // (L0ARGS)
+    const bool nsq = L.nsq_ok && L.nsq_pre;
+    if (nsq) (void)hipMemsetAsync(L.nsq_pre, 0, (L.total_slots / 64 + 65) * 4ull, stream);
+    for (const Wave& w : L.waves) {
+        L0ARGS(a0);
+        k_raw_encode<<<grid_for(w.nslots), kBlock, 0, stream>>>(
+            a0, L.raw_lam + w.slot0, L.raw_agent + w.slot0, L.raw_del + w.slot0,
+            L.raw_cp + w.slot0, L.key + w.slot0, L.cp + 3ull * w.slot0,
+            nsq ? L.nsq_pre + (w.slot0 >> 6) : nullptr, nsq ? L.nsq_mask + (w.slot0 >> 6) : nullptr);
+    }
+    if (nsq) {
+        nsq_scan(L);
+        nsq_scatter(L);
+    }
+    HIPCHK(hipGetLastError(), "raw encode launch");
+    return CRDT_HIP_OK;
 }
 
 // The list itself, every wave's tiles (launches only).

@@ -64,8 +64,12 @@ struct L1Plan {
     // so k_runs does not copy them into the slot-order text (sbytes): fused plans whose
     // documents span at most kDocTiles tiles
     bool stile_text = false;
+    // k_doctree stops at the run offsets (wave-relative, in roff) and k_tscatter writes the text
+    // from the tile segments: stile plans of waves with less than 4 GiB of text
+    // (Engine::text_scatter); k_doctree then needs only the run tree's LDS (dyn_scatter)
+    bool scatter = false;
     uint32_t rcap = 0, scap = 0;
-    uint64_t dyn_bytes = 0;
+    uint64_t dyn_bytes = 0, dyn_scatter = 0;
 };
 
 // The codepoint column: 3 bytes per slot, the codepoint (bits 0-20), the tombstone flag (bit 23)
@@ -128,6 +132,15 @@ struct DeviceLogs {
     uint64_t nsq_cap = 0, nsq_pre_cap = 0, nsq_sums_cap = 0;
     uint32_t* nsq_sums = nullptr;  // (scan scratch)
     uint64_t* nsq_mask = nullptr;  // (the nsq items of every 64-slot chunk, for the scatter)
+    // Raw SoA mode (Engine::raw_keep, the companion line that prices the input encoding): the
+    // reference-shaped columns beside the parent column, lamport u32, agent u16, deleted u8 and
+    // codepoint u32 per slot; every merge first derives the key, the codepoint word with its
+    // tombstone and previous-slot flags, and the compact nsq list from them on the device
+    bool raw = false;
+    uint32_t* raw_lam = nullptr;
+    uint16_t* raw_agent = nullptr;
+    uint8_t* raw_del = nullptr;
+    uint32_t* raw_cp = nullptr;
     void release();
     ~DeviceLogs() { release(); }
 };
@@ -197,6 +210,9 @@ public:
     int merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, crdt_hip_stats* st,
               std::vector<uint8_t>* text_out = nullptr,
               std::vector<uint64_t>* text_offsets = nullptr, uint64_t* cps = nullptr);
+    int merge_inner(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
+                    crdt_hip_stats* st, std::vector<uint8_t>* text_out,
+                    std::vector<uint64_t>* text_offsets, uint64_t* cps);
 
     // merge() of logs whose every wave has a learnt plan, in three phases so that the launches
     // can be captured in a graph: prepare (every allocation), enqueue (launches and copies only;
@@ -223,8 +239,15 @@ public:
     // fused plans stage text from the tile segments (L1Plan::stile_text): 1 by 16-byte loads and
     // funnel shifts into one contiguous image, 2 by LDS-DMA, tile by tile (engine.hip stage_glds)
     uint32_t stile_text = 2;
+    // 1: stile plans leave the text to k_tscatter (L1Plan::scatter); 0: k_doctree phase C
+    uint32_t text_scatter = 1;
+    bool glds_late = false;  // test hook: k_doctree issues its LDS-DMA staging loads last
+    // every LDS level 1 on k_doctree_wide (32-bit keys, 9 B of LDS per run instead of 15)
+    bool doctree_k32 = false;
+    // k_runs slots per thread: 16 (256 threads per tile), 32 (128) or 64 (one wave per tile,
+    // 64-bit slot masks)
     uint32_t runs_slots = 32;
-    bool group_docs = false;  // replicate(): documents in slots base by base (waves per base)  // k_runs slots per thread: 16 (256 threads per tile) or 32 (128)
+    bool group_docs = false;  // replicate(): documents in slots base by base (waves per base)
     uint64_t generation() const {
         uint64_t g = gen_;
         for (const auto& e : lane_eng_) g += e->generation() + 1;
@@ -237,8 +260,13 @@ public:
 
     // The compact nsq parent list of L (after its last plan; see DeviceLogs::nsq_par).
     int build_nsq(DeviceLogs& L);
+    // raw SoA mode of resident logs (DeviceLogs::raw): keep the raw columns (once, untimed) /
+    // derive the engine's input format from them (every merge, on the device)
+    int raw_keep(DeviceLogs& L);
+    int raw_encode(DeviceLogs& L);
     int nsq_reserve_prefix(DeviceLogs& L);
     void nsq_count_scan(DeviceLogs& L);
+    void nsq_scan(DeviceLogs& L);
     void nsq_scatter(DeviceLogs& L);
     // Wave::nocon of every wave of L from its nsq_items and the contraction parameter.
     void set_contraction(DeviceLogs& L) const;
@@ -301,6 +329,8 @@ private:
     uint64_t cap_wtmp_ = 0;    // (bytes)
     uint32_t wtmp_log2_ = 7;
     uint32_t tail_nspl_ = 0;   // splitters of the last global level 1 whose offsets are in rloc_
+    bool tail_scatter_ = false;
+    hipEvent_t raw_ev_[2] = {nullptr, nullptr};  // (raw SoA mode: the encoding's interval)  // the last level 1 was k_doctree in scatter mode: k_tscatter next
                                //   (0: k_expand reads roff_)
     uint32_t* ovf_ = nullptr;  // text mode: splitters whose sublist holds more than its slot
     uint64_t cap_ovf_ = 0;

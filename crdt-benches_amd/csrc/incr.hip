@@ -247,10 +247,19 @@ __device__ __forceinline__ void inc_forest(const IncArgs& a, uint8_t* lds, uint3
             for (int q = 0; q < (int)Q; ++q) {
                 if (!((hq >> q) & 1u)) continue;
                 const uint32_t i = t + (uint32_t)q * kIncThreads;
+                // (bounded: the searchers lead the grid and are dispatched first, so they are
+                // resident or done; should they not be, the wait gives up after ~50 ms and the
+                // call merges in full instead of hanging on the dispatch order)
                 uint64_t v;
+                uint32_t spins = 0;
                 while ((uint32_t)((v = __hip_atomic_load(&a.hanc[i], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (uint32_t)a.call)
+                                                         __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (uint32_t)a.call) {
+                    if (++spins > (1u << 20)) {
+                        v = 0xFFFFFFFFull;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(2);
+                }
                 if ((uint32_t)v != 0xFFFFFFFFu)
                     A[i] = (uint32_t)v;
                 else

@@ -770,7 +770,9 @@ int replica_replay(Engine& E, const Replica& init, const UpdateBatch& ub, Replay
                 cap, (uint64_t)(uintptr_t)&ub, ub.len, ub.n, st.n_after, b_plan,
                 // (knobs that change what is captured: a closure captured under other settings
                 // is not replayed)
-                (uint64_t)E.nsq_list, (uint64_t)E.contraction};
+                (uint64_t)E.nsq_list, (uint64_t)E.contraction, (uint64_t)E.runs_slots,
+                (uint64_t)E.stile_text, (uint64_t)E.xcd_order, (uint64_t)E.text_scatter,
+                (uint64_t)E.fuse_text, (uint64_t)E.lanes};
             hipStream_t s = E.stream;
             if (key != st.key || !st.exec) {
                 drop_graph(st);

@@ -121,7 +121,12 @@ enum {
     CRDT_HIP_STAGE_DIGEST = 11,  /* per-document tree digest                                  */
     CRDT_HIP_STAGE_DOCTREE = 12, /* level 1 in LDS: whole run tree of a document per workgroup
                                     (replaces stages 3-9 when every document fits)           */
-    CRDT_HIP_NSTAGES = 13
+    CRDT_HIP_STAGE_TEXT = 13,    /* text scatter after a k_doctree in scatter mode: the tiles'
+                                    slot-order text to the documents (k_tscatter)            */
+    CRDT_HIP_STAGE_ENCODE = 14,  /* raw SoA mode (crdt_hip_batch_raw): the input encoding derived
+                                    from the raw columns inside the merge (k_raw_encode + the
+                                    compact nsq list)                                        */
+    CRDT_HIP_NSTAGES = 15
 };
 
 /* ---- library / context ----------------------------------------------------------------- */
@@ -282,6 +287,15 @@ int crdt_hip_batch_info(const crdt_hip_batch* b, uint64_t* docs, uint64_t* items
  * NULL). */
 int crdt_hip_batch_merge(crdt_hip_ctx* ctx, crdt_hip_batch* b, uint64_t* digests,
                          uint64_t* lens, crdt_hip_stats* stats);
+/* Raw SoA mode of a resident RGA batch (the companion line that prices the input encoding): keep
+ * the reference-shaped columns (lamport u32, agent u16, deleted u8, codepoint u32 per item, beside
+ * the parent column) and derive the engine's input format from them on the device at every
+ * crdt_hip_batch_merge: the sibling key, the 3-byte codepoint word with its tombstone and
+ * previous-slot flags, and the compact list of the items without that flag (stage
+ * CRDT_HIP_STAGE_ENCODE).  on = 0 leaves the mode (the columns are kept until the batch is freed).
+ * Replaces no reference interface: the reference's op log is its own in-memory format
+ * (rope.rs:116-130 builds it). */
+int crdt_hip_batch_raw(crdt_hip_ctx* ctx, crdt_hip_batch* b, int on);
 
 /* ---- device-resident replicas: Downstream on the device ------------------------------------
  * A replica is an op log resident in HBM that receives encoded updates and is merged where it

@@ -371,24 +371,35 @@ def test_tiles_above_the_lds_text_stage(ctx, oracle, shape):
     b.close()
 
 
-def test_malformed_logs_are_rejected(ctx):
+@pytest.mark.parametrize("level1", [0, 1])
+def test_malformed_logs_are_rejected(level1):
+    """Out-of-range parents, an item that is its own parent and parent cycles fail with EBADLOG on
+    the per-document (LDS) and on the global level 1, as single merges and as resident batches
+    (learnt plans on the second merge), and the engine merges a good log right after."""
+    ctx = crdt_hip.Context(0)
+    ctx.set_param("level1", level1)
     bad_parent = crdt_hip.LogArrays([0, 5], [1, 2], [0, 0], [0, 0], [97, 98])
-    with pytest.raises(crdt_hip.CrdtHipError) as e:
-        ctx.merge(bad_parent)
-    assert e.value.code == -5
+    # item 2 is its own parent: k_runs must not give its row itself as parent (a self-loop the
+    # global walks would follow), it clamps it to the document start and the merge is rejected
+    self_parent = crdt_hip.LogArrays([0, 2], [1, 2], [0, 0], [0, 0], [97, 98])
     cycle = crdt_hip.LogArrays([0, 3, 2], [1, 2, 3], [0, 0, 0], [0, 0, 0], [97, 98, 99])
-    with pytest.raises(crdt_hip.CrdtHipError) as e:
-        ctx.merge(cycle)
-    assert e.value.code == -5
     # two runs that are each other's parent (neither reachable from the document start): their
     # up links never resolve, so the LDS path's pointer jumping has to give up, not spin
     cycle2 = crdt_hip.LogArrays([0, 4, 1, 2], [1, 2, 3, 4], [0, 0, 0, 0], [0, 0, 0, 0],
                                 [97, 98, 99, 100])
-    with pytest.raises(crdt_hip.CrdtHipError) as e:
-        ctx.merge(cycle2)
-    assert e.value.code == -5
     ok = crdt_hip.LogArrays([0, 1], [1, 2], [0, 0], [0, 0], [97, 98])
+    for bad in (bad_parent, self_parent, cycle, cycle2):
+        with pytest.raises(crdt_hip.CrdtHipError) as e:
+            ctx.merge(bad)
+        assert e.value.code == -5
+        b = ctx.batch([ok, bad, ok], replicas=2, relabel="none")
+        for _ in range(2):
+            with pytest.raises(crdt_hip.CrdtHipError) as e:
+                b.merge()
+            assert e.value.code == -5
+        b.close()
     assert ctx.merge(ok)[0] == b"ab"  # the engine recovers after an error
+    ctx.close()
 
 
 @pytest.mark.gpu
@@ -470,7 +481,13 @@ def test_learnt_plan_merges_match_synchronous_ones(golden, lanes):
                 name = TRACES[r % 4]
                 assert "%016x" % dig[r] == golden[name]["tree_digest"], (cache, r)
                 assert lens[r] == golden[name]["end_bytes"], (cache, r)
-        out[cache] = [(d.tolist(), l.tolist(), st["runs"], st["stage_launches"]) for d, l, st in res]
+        # (the learnt-plan merges write the text with k_tscatter, the synchronous ones in
+        # k_doctree: the text stage's launches differ, every other stage's match)
+        for i, (_, _, st) in enumerate(res):
+            assert (st["stage_launches"]["text"] > 0) == (cache == 1 and i > 0)
+        out[cache] = [(d.tolist(), l.tolist(), st["runs"],
+                       {k: v for k, v in st["stage_launches"].items() if k != "text"})
+                      for d, l, st in res]
         b.close()
         c.close()
     assert out[0] == out[1]
@@ -667,5 +684,145 @@ def test_level0_knobs_off_match_golden(golden, knob):
             name = TRACES[r % 4]
             assert "%016x" % dig[r] == golden[name]["tree_digest"], (knob, r)
             assert lens[r] == golden[name]["end_bytes"], (knob, r)
+    b.close()
+    c.close()
+
+
+def _mixed_logs(seed=11):
+    """Documents with multi-byte codepoints among ASCII, some deleted, one spanning ~20 tiles
+    (small enough in runs and text for k_doctree's LDS)."""
+    rng = np.random.default_rng(seed)
+    logs = []
+    for n, p_esc, p_seq in ((30_000, 0.02, 0.9), (5_000, 0.3, 0.9), (80_000, 0.001, 0.97)):
+        ids = np.arange(1, n + 1, dtype=np.uint32)
+        parent = np.where(rng.random(n) < p_seq, ids - 1, rng.integers(0, ids, dtype=np.uint32))
+        deleted = (rng.random(n) < 0.1).astype(np.uint8)
+        cp = rng.integers(0x20, 0x7F, n, dtype=np.uint32)
+        esc = rng.random(n) < p_esc
+        cp[esc] = rng.choice([0xE9, 0x4E2D, 0x1F600, 0x7FF, 0x800, 0xFFFF, 0x10000],
+                             int(esc.sum())).astype(np.uint32)
+        logs.append(crdt_hip.LogArrays(parent, ids, np.zeros(n, np.uint16), deleted, cp))
+    return logs
+
+
+@pytest.mark.parametrize("scatter,stile,lanes", [(1, 2, 2), (1, 2, 1), (1, 1, 1), (0, 2, 2),
+                                                  (0, 1, 1)])
+def test_text_paths_match_golden(golden, scatter, stile, lanes):
+    """The document text of the learnt-plan merges is written either by k_doctree itself
+    (text_scatter 0: phase C, staged by loads and shifts or by LDS-DMA) or by k_tscatter from the
+    tiles' text segments once k_doctree has left every run's place in roff (text_scatter 1, the
+    default): the same digests and lengths as the synchronous first merge and the traces', and
+    the text stage runs exactly when scatter mode is on."""
+    bases = [resolved(n) for n in TRACES]
+    c = crdt_hip.Context(0)
+    c.set_param("text_scatter", scatter)
+    c.set_param("stile_text", stile)
+    c.set_param("lanes", lanes)
+    c.set_param("max_wave_slots", 1 << 21)  # several waves
+    b = c.batch(bases, replicas=5, relabel="rotate", seed=13)
+    for it in range(3):
+        dig, lens, st = b.merge()
+        for r in range(b.docs):
+            name = TRACES[r % 4]
+            assert "%016x" % dig[r] == golden[name]["tree_digest"], (it, r)
+            assert lens[r] == golden[name]["end_bytes"], (it, r)
+        if it:  # (learnt plans: stile staging, and the text kernel in scatter mode)
+            assert (st["stage_launches"]["text"] > 0) == bool(scatter), st["stage_launches"]
+            assert st["stage_launches"]["text"] in (0, st["waves"])
+    b.close()
+    c.close()
+
+
+@pytest.mark.parametrize("scatter", [1, 0])
+def test_text_paths_multibyte_match_oracle(oracle, scatter):
+    """Multi-byte UTF-8 (2-4 bytes, escaped groups) in learnt-plan merges, both text paths, against
+    the oracle's bytes and digests; one document spans ~20 tiles."""
+    logs = _mixed_logs()
+    refs = [oracle.merge(to_anchor(lg)) for lg in logs]
+    c = crdt_hip.Context(0)
+    c.set_param("text_scatter", scatter)
+    b = c.batch(logs, replicas=4, relabel="rotate", seed=3)
+    for it in range(3):
+        d, l, st = b.merge()
+        for i, (x, y) in enumerate(zip(d, l)):
+            ref = refs[i % 3]
+            assert int(y) == len(ref) and int(x) == oracle.tree_digest(ref), (it, i)
+    assert (st["stage_launches"]["text"] > 0) == bool(scatter)
+    b.close()
+    c.close()
+
+
+def test_glds_staging_wait_is_pinned(golden, oracle):
+    """Guard of the s_waitcnt vmcnt(0) in front of k_doctree's text-output barrier (engine.hip
+    doc_text): the LDS-DMA staging writes LDS as a global load, which a barrier does not wait for.
+    With the glds_late hook every staging load is issued after the prefix and delta phases, right
+    in front of that wait, so without it the output would read chunks still in flight; phase C
+    (text_scatter 0) with LDS-DMA staging (stile_text 2) must still give the traces' digests and
+    the oracle's for a document spanning more than 16 tiles."""
+    bases = [resolved(n) for n in TRACES]
+    logs = _mixed_logs(5)
+    refs = [oracle.merge(to_anchor(lg)) for lg in logs]
+    c = crdt_hip.Context(0)
+    c.set_param("text_scatter", 0)
+    c.set_param("stile_text", 2)
+    c.set_param("glds_late", 1)
+    b = c.batch(bases, replicas=3, relabel="rotate", seed=9)
+    m = c.batch(logs, replicas=2, relabel="rotate", seed=9)
+    for _ in range(3):
+        dig, lens, st = b.merge()
+        for r in range(b.docs):
+            name = TRACES[r % 4]
+            assert "%016x" % dig[r] == golden[name]["tree_digest"], r
+            assert lens[r] == golden[name]["end_bytes"], r
+        d, l, _ = m.merge()
+        for i, (x, y) in enumerate(zip(d, l)):
+            assert int(y) == len(refs[i % 3]) and int(x) == oracle.tree_digest(refs[i % 3]), i
+    assert st["stage_launches"]["doctree"] > 0 and st["stage_launches"]["text"] == 0
+    b.close()
+    m.close()
+    c.close()
+
+
+@pytest.mark.parametrize("relabel", ["rotate", "shuffle"])
+def test_raw_soa_mode_matches_encoded(golden, oracle, relabel):
+    """Raw SoA mode (crdt_hip_batch_raw): every merge derives the key, the codepoint word with its
+    tombstone and previous-slot flags and the compact nsq list on the device from the raw
+    columns; the digests and lengths equal the encoded batch's and the golden / oracle ones, the
+    encode stage runs, and leaving the mode merges the (now re-derived) encoded columns."""
+    bases = [resolved(n) for n in TRACES]
+    agents = crdt_hip.OpLog.synth_agents(50_000, 64, 0x5EED0007).arrays()  # (agent bits in keys)
+    mixed = _mixed_logs(3)
+    others = [agents] + mixed
+    refs = [oracle.merge(to_anchor(lg)) for lg in others]
+    c = crdt_hip.Context(0)
+    for logs, check in ((bases, "golden"), (others, "oracle")):
+        b = c.batch(logs, replicas=3, relabel=relabel, seed=17)
+        d0, l0, _ = b.merge()
+        b.set_raw(True)
+        for it in range(3):
+            d, l, st = b.merge()
+            assert np.array_equal(d, d0) and np.array_equal(l, l0), it
+            assert st["stage_launches"]["encode"] > 0 and st["stage_ns"]["encode"] > 0
+        for r in range(b.docs):
+            if check == "golden":
+                name = TRACES[r % 4]
+                assert "%016x" % d[r] == golden[name]["tree_digest"], r
+                assert l[r] == golden[name]["end_bytes"], r
+            else:
+                ref = refs[r % len(others)]
+                assert int(l[r]) == len(ref) and int(d[r]) == oracle.tree_digest(ref), r
+        b.set_raw(False)
+        d, l, st = b.merge()
+        assert np.array_equal(d, d0) and st["stage_launches"]["encode"] == 0
+        b.close()
+    c.close()
+
+
+def test_raw_soa_mode_rejects_fugue():
+    c = crdt_hip.Context(0)
+    lg = crdt_hip.Trace(trace_path("sveltecomponent")).resolve(fugue=True).arrays()
+    b = c.batch([lg], replicas=2, relabel="rotate", seed=1)
+    with pytest.raises(crdt_hip.CrdtHipError):
+        b.set_raw(True)
     b.close()
     c.close()
