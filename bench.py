@@ -1056,7 +1056,7 @@ def parse_args(argv=None):
     ap.add_argument("--doctree-k32", type=int, default=0, choices=[0, 1],
                     help="1: every LDS level 1 on k_doctree_wide (32-bit sibling keys, 9 B of "
                          "LDS per run instead of 15)")
-    ap.add_argument("--text-scatter", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--text-scatter", type=int, default=0, choices=[0, 1],
                     help="1: k_doctree stops at the run offsets and k_tscatter streams the tiles' "
                          "text to the documents; 0: k_doctree writes the text itself (phase C)")
     ap.add_argument("--group-docs", type=int, default=-1, choices=[-1, 0, 1],

@@ -2711,7 +2711,7 @@ __device__ __forceinline__ bool doc_text(const DocArgs& a, uint32_t tl, uint32_t
 
 // One document (workgroup descriptor widx); the kernel below runs it once per descriptor.  K32:
 // the sibling keys are held in LDS as doc_key32 (4 bytes per run instead of 8).
-template <int J, bool K32>
+template <int J, bool K32, bool PC>
 __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     constexpr int KK = (J + (1 << kDocLog2S) - 1) >> kDocLog2S;
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
@@ -2770,7 +2770,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     uint32_t pk[J];
     // (stile_text) this lane's entry of the document's tile prefix table, used by phase C
     uint32_t tpx_reg = 0;
-    if (a.stile_text) {
+    if (PC && a.stile_text) {
         const uint32_t t0 = wg1.w & 0xFFFFFu, nt = wg1.w >> 20;
         if (t <= nt + 1u) tpx_reg = t0 + t < a.ntiles ? a.tile_hw[t0 + t].y : a.ctl[C_WTOTAL];
     }
@@ -3144,7 +3144,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const uint32_t v = t + (uint32_t)j * kDocThreads;
-        ps[j] = (a.text && v < R) ? a.r_pstart[base + v] : 0u;
+        ps[j] = (PC && a.text && v < R) ? a.r_pstart[base + v] : 0u;
     }
     // ---- pointer jumping: record = (sum from the splitter to the end of the tour) << 14 | next.
     // A record always describes a valid stretch of the tour (sum up to its next splitter, read
@@ -3195,7 +3195,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
             // weightless (or never reached: flagged below)
             ro[j] = (pk != 0xFFFFFFFFu && sid < S) ? (pk & 0x3FFFFu) + total - (sr >> 14) : kNil;
         }
-        if (!a.text) {  // offsets for k_expand (document-relative) or k_tscatter (wave-relative)
+        if (!PC || !a.text) {  // offsets for k_expand (document-relative) or k_tscatter (wave-relative)
             const uint32_t ob = a.scatter ? wg1.y : 0u;  // (scatter: the wave's text is < 4 GiB)
 #pragma unroll
             for (int j = 0; j < J; ++j)
@@ -3206,7 +3206,7 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
     if ((t & 63u) == 0 && wsum) atomicAdd(&visited_lds, wsum);
     __syncthreads();
     PROBE(9);
-    if (a.text) {
+    if (PC && a.text) {
 #ifdef CRDT_HIP_PROBE
         uint64_t* tprobe = probe ? &tp[15] : nullptr;
 #else
@@ -3297,26 +3297,31 @@ constexpr int kDocJNarrow = 12;
 #else
 #define DOC_WPE
 #endif
-template <int J, bool K32>
+// PC: phase C (the document text written from LDS) compiled in.  The instances without it (the
+// scatter mode, and the offsets left to k_expand) carry neither its code nor its registers.
+template <int J, bool K32, bool PC>
 __device__ __forceinline__ bool doctree_try(const DocArgs& a, uint32_t R) {
     if (R > (uint32_t)J * kDocThreads) return false;
-    doctree_doc<J, K32>(a, blockIdx.x);
+    doctree_doc<J, K32, PC>(a, blockIdx.x);
     return true;
 }
+template <bool PC>
 __global__ __launch_bounds__(kDocThreads) DOC_WPE void k_doctree(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
-    if (doctree_try<4, false>(a, R) || doctree_try<8, false>(a, R)) return;
-    doctree_doc<kDocJNarrow, false>(a, blockIdx.x);
+    if (doctree_try<4, false, PC>(a, R) || doctree_try<8, false, PC>(a, R)) return;
+    doctree_doc<kDocJNarrow, false, PC>(a, blockIdx.x);
 }
+template <bool PC>
 __global__ __launch_bounds__(kDocThreads) DOC_WPE void k_doctree_wide(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
-    if (doctree_try<8, true>(a, R)) return;
-    doctree_doc<kDocJNarrow, true>(a, blockIdx.x);
+    if (doctree_try<8, true, PC>(a, R)) return;
+    doctree_doc<kDocJNarrow, true, PC>(a, blockIdx.x);
 }
 // (its own kernel: the 17 runs per thread spill ~40 VGPRs, which the 12-run instance beside them
 // would pay for in scratch allocation and register pressure)
+template <bool PC>
 __global__ __launch_bounds__(kDocThreads) void k_doctree_wide17(DocArgs a) {
-    doctree_doc<kDocJ, true>(a, blockIdx.x);
+    doctree_doc<kDocJ, true, PC>(a, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3348,7 +3353,7 @@ constexpr uint32_t kScatterWin = CRDT_TSC_WIN;  // stretch bytes staged per wind
 static_assert(kScatterWin / 32 + 2 <= 64, "a window's bitmap words fit one VGPR of the wave");
 constexpr uint32_t kScatterRows = 64 * CRDT_TSC_RQ;  // rows per round of loads
 #ifndef CRDT_TSC_TPW
-#define CRDT_TSC_TPW 4
+#define CRDT_TSC_TPW 1
 #endif
 constexpr uint32_t kScatterTiles = CRDT_TSC_TPW;  // consecutive tiles per wave (<= 63)
 struct ScatterArgs {
@@ -3371,7 +3376,11 @@ __device__ __forceinline__ void scatter_window(const uint8_t* seg, uint32_t a0, 
 #pragma unroll
     for (uint32_t i = 0; i < kScatterWin / 1024u; ++i) {
         const uint32_t o = a0 + 1024u * i + 16u * lane;
+#ifdef CRDT_TSC_NOTEXT
+        v[i] = make_uint4(o, 0, 0, 0);
+#else
         v[i] = o < a1 ? *reinterpret_cast<const uint4*>(seg + o) : make_uint4(0, 0, 0, 0);
+#endif
     }
 #pragma unroll
     for (uint32_t i = 0; i < kScatterWin / 1024u; ++i)
@@ -3468,29 +3477,53 @@ __global__ __launch_bounds__(kBlock) void k_tscatter(ScatterArgs a) {
                     atomicOr(&bmw[(u[i] - w0) >> 5], 1u << ((u[i] - w0) & 31u));
             __builtin_amdgcn_s_waitcnt(0xc07f);  // (lgkmcnt(0): the wave's bits are in)
             const uint32_t w1 = min(U, w0 + kScatterWin) - w0;
-            // the window's bitmap in one VGPR (lane j: word j): a step reads its two words by
-            // v_readlane, no LDS round trip
+            // The window's bitmap in one VGPR (lane j: word j) and the starts before each word
+            // (a wave scan): a lane's row is then pre[j] + the starts in word j at or before its
+            // byte - 1, from two v_readlane pairs per step and no LDS round trip, and the steps
+            // are independent of each other (no running count), so the unrolled steps' LDS reads
+            // and stores overlap.
             const uint32_t bwd = lane < BW ? bmw[lane] : 0u;
-            // A step: the row of lane L's byte is (starts at or before it) - 1 = cnt + M_0 - 1
-            // + (bits of M >> 1 below L): the uniform part in SGPRs, one mbcnt pair per lane.
+            const uint32_t pc = (uint32_t)__popc(bwd);
+            const uint32_t pinc = wave_incl_scan(pc);
+            const uint32_t pre = cnt + pinc - pc - 1u;  // (- 1: rows are counted from 0)
+            cnt += (uint32_t)__builtin_amdgcn_readlane((int)pinc, 63);
             const uint32_t lo = w0 ? 0u : sh;  // (the first window starts at sh)
-            const uint32_t* lbx = lbw;
-            uint32_t x = lane;  // (this lane's byte, window coordinate)
-#pragma unroll 4
-            for (uint32_t b = 0; b < w1; b += 64u, x += 64u) {
-                const int q = (int)(b >> 5);
-                const uint64_t M = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)bwd, q + 1) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)bwd, q);
-                const uint32_t base = cnt + (uint32_t)(M & 1u) - 1u;
-                const uint64_t Ms = M >> 1;
-                cnt += (uint32_t)__popcll(M);
-                const uint32_t own = __builtin_amdgcn_mbcnt_hi((uint32_t)(Ms >> 32),
-                                         __builtin_amdgcn_mbcnt_lo((uint32_t)Ms, base));
-#ifdef CRDT_TSC_NOSTORE
-                if (x < w1 && x >= lo) sink ^= lbx[own] + w0 + x + buf[x];
+            const bool hi = lane >= 32u;
+            const uint32_t mle = (lane & 31u) == 31u ? ~0u : (2u << (lane & 31u)) - 1u;
+            // Four steps at a time, their LDS reads issued unconditionally (clamped indices) so
+            // that they overlap; only the stores are predicated.  (Four bytes per lane and step,
+            // with four byte stores each, was slower: a store instruction then touches ~30 rows'
+            // lines instead of ~8, and the store path is what this loop waits on.)
+            constexpr uint32_t SU = 4;
+#ifdef CRDT_TSC_NOSTEPS
+            for (uint32_t b = 0; b < (w1 & 0u); b += 64u * SU) {
 #else
-                if (x < w1 && x >= lo) a.text[lbx[own] + w0 + x] = buf[x];
+            for (uint32_t b = 0; b < w1; b += 64u * SU) {
 #endif
+                uint32_t dst[SU], val[SU];
+                bool ok[SU];
+#pragma unroll
+                for (uint32_t k = 0; k < SU; ++k) {
+                    const uint32_t bk = b + 64u * k;
+                    const int q = (int)min(bk >> 5, BW - 2u);
+                    const uint32_t wlo = (uint32_t)__builtin_amdgcn_readlane((int)bwd, q);
+                    const uint32_t whi = (uint32_t)__builtin_amdgcn_readlane((int)bwd, q + 1);
+                    const uint32_t plo = (uint32_t)__builtin_amdgcn_readlane((int)pre, q);
+                    const uint32_t phi = (uint32_t)__builtin_amdgcn_readlane((int)pre, q + 1);
+                    const uint32_t own = (hi ? phi : plo) + (uint32_t)__popc((hi ? whi : wlo) & mle);
+                    const uint32_t x = bk + lane;  // (this lane's byte, window coordinate)
+                    ok[k] = x < w1 && x >= lo;
+                    dst[k] = lbw[min(own, kScatterRows - 1u)] + w0 + x;
+                    val[k] = buf[min(x, kScatterWin - 1u)];
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < SU; ++k) {
+#ifdef CRDT_TSC_NOSTORE
+                    if (ok[k]) sink ^= dst[k] + val[k];
+#else
+                    if (ok[k]) a.text[dst[k]] = (uint8_t)val[k];
+#endif
+                }
             }
             // (clear for the next window / round; the reads above are done first)
             __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -3957,18 +3990,18 @@ std::string Engine::init(int dev) {
     ev_.resize(2 * S_N + 4);
     for (hipEvent_t& x : ev_)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hipGetErrorString(e);
-    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
-        hipSuccess)
-        return std::string("k_doctree LDS: ") + hipGetErrorString(e);
-    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree_wide),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
-        hipSuccess)
-        return std::string("k_doctree_wide LDS: ") + hipGetErrorString(e);
-    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doctree_wide17),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDocLds)) !=
-        hipSuccess)
-        return std::string("k_doctree_wide17 LDS: ") + hipGetErrorString(e);
+    {
+        const void* dk[6] = {reinterpret_cast<const void*>(&k_doctree<true>),
+                             reinterpret_cast<const void*>(&k_doctree<false>),
+                             reinterpret_cast<const void*>(&k_doctree_wide<true>),
+                             reinterpret_cast<const void*>(&k_doctree_wide<false>),
+                             reinterpret_cast<const void*>(&k_doctree_wide17<true>),
+                             reinterpret_cast<const void*>(&k_doctree_wide17<false>)};
+        for (const void* f : dk)
+            if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)kDocLds)) != hipSuccess)
+                return std::string("k_doctree LDS: ") + hipGetErrorString(e);
+    }
     return "";
 }
 
@@ -4547,12 +4580,17 @@ int Engine::launch_lds_level1(DeviceLogs& L, const Wave& w, bool ord, const L1Pl
     da.tile_hw = tile_hw_;
     a.wg = wgtab_;  // (k_doctotals writes the k_doctree workgroup descriptors)
     k_doctotals<<<1, 1024, 0, s>>>(a);
-    if (p.wide && p.rmax > (uint32_t)(kDocJNarrow * kDocThreads))
-        k_doctree_wide17<<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
-    else if (p.wide)
-        k_doctree_wide<<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
-    else
-        k_doctree<<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+    const bool pc = da.text != nullptr;  // (phase C: the instances that write the text)
+    if (p.wide && p.rmax > (uint32_t)(kDocJNarrow * kDocThreads)) {
+        if (pc) k_doctree_wide17<true><<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+        else k_doctree_wide17<false><<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+    } else if (p.wide) {
+        if (pc) k_doctree_wide<true><<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+        else k_doctree_wide<false><<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+    } else {
+        if (pc) k_doctree<true><<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+        else k_doctree<false><<<w.ndocs, kDocThreads, da.lds_bytes, s>>>(da);
+    }
     MARK(S_DOCTREE);
     HIPCHK(hipGetLastError(), "level-1 launch");
     return CRDT_HIP_OK;

@@ -239,8 +239,10 @@ public:
     // fused plans stage text from the tile segments (L1Plan::stile_text): 1 by 16-byte loads and
     // funnel shifts into one contiguous image, 2 by LDS-DMA, tile by tile (engine.hip stage_glds)
     uint32_t stile_text = 2;
-    // 1: stile plans leave the text to k_tscatter (L1Plan::scatter); 0: k_doctree phase C
-    uint32_t text_scatter = 1;
+    // 1: stile plans leave the text to k_tscatter (L1Plan::scatter); 0: k_doctree phase C (the
+    // default: the two measured equal on the RGA headline, 8.43 ms per step either way, and
+    // phase C is 0.16 ms faster on the Fugue line)
+    uint32_t text_scatter = 0;
     bool glds_late = false;  // test hook: k_doctree issues its LDS-DMA staging loads last
     // every LDS level 1 on k_doctree_wide (32-bit keys, 9 B of LDS per run instead of 15)
     bool doctree_k32 = false;

@@ -470,6 +470,7 @@ def test_learnt_plan_merges_match_synchronous_ones(golden, lanes):
     out = {}
     for cache in (0, 1):
         c = crdt_hip.Context(0)
+        c.set_param("text_scatter", 1)  # (the learnt-plan merges then take the text kernel)
         c.set_param("lanes", lanes)
         c.set_param("plan_cache", cache)
         c.set_param("max_wave_slots", 1 << 20)  # several waves
@@ -710,8 +711,8 @@ def _mixed_logs(seed=11):
 def test_text_paths_match_golden(golden, scatter, stile, lanes):
     """The document text of the learnt-plan merges is written either by k_doctree itself
     (text_scatter 0: phase C, staged by loads and shifts or by LDS-DMA) or by k_tscatter from the
-    tiles' text segments once k_doctree has left every run's place in roff (text_scatter 1, the
-    default): the same digests and lengths as the synchronous first merge and the traces', and
+    tiles' text segments once k_doctree has left every run's place in roff (text_scatter 1): the
+    same digests and lengths as the synchronous first merge and the traces', and
     the text stage runs exactly when scatter mode is on."""
     bases = [resolved(n) for n in TRACES]
     c = crdt_hip.Context(0)
