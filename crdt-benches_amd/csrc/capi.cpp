@@ -432,11 +432,10 @@ int trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out, bool fugue) {
         // from_str(start_content), then replace() every patch (main.rs:29-33, rope.rs:21-32)
         if (!T.start_content.empty())
             e = L->log.insert_utf8(0, T.start_content.data(), T.start_content.size());
-        for (size_t i = 0; e.empty() && i < T.patches.size(); ++i) {
-            const crdt::Patch& p = T.patches[i];
-            if (p.del) e = L->log.remove(p.pos, p.pos + p.del);
-            if (e.empty() && p.ins_len) e = L->log.insert_utf8(p.pos, T.ins.data() + p.ins_off, p.ins_len);
-        }
+        static_assert(sizeof(crdt::Patch) == 4 * sizeof(uint64_t), "Patch = {pos, del, ins_off, ins_len}");
+        if (e.empty())
+            e = L->log.replay(reinterpret_cast<const uint64_t*>(T.patches.data()), T.patches.size(),
+                              T.ins.data());
         if (!e.empty()) {
             delete L;
             return set_err(nullptr, CRDT_HIP_ERANGE, e);

@@ -356,6 +356,134 @@ std::string OpLog::remove_rga(uint64_t start, uint64_t end) {
     return "";
 }
 
+// The resolver's hot loop for RGA logs (the upstream closure, main.rs:28-36).  The same steps as
+// remove_rga + insert_rga, fused: every column is sized once to the trace's bound and written by
+// index (no per-item push_back), a one-byte insert (typing) and a one-codepoint delete
+// (backspace) take straight-line paths, and no std::string is made per patch.
+std::string OpLog::replay(const uint64_t* pt, size_t np, const char* ins) {
+    if (fugue || stale_) {
+        for (size_t i = 0; i < np; ++i) {
+            const uint64_t* q = pt + 4 * i;
+            std::string e;
+            if (q[1]) e = remove(q[0], q[0] + q[1]);
+            if (e.empty() && q[3]) e = insert_utf8(q[0], ins + q[2], q[3]);
+            if (!e.empty()) return e;
+        }
+        return "";
+    }
+    size_t ib = 0, db = 0;  // bounds: items <= inserted bytes, deletes = deleted codepoints
+    for (size_t i = 0; i < np; ++i) {
+        ib += pt[4 * i + 3];
+        db += pt[4 * i + 1];
+    }
+    size_t n = parent.size(), m = del_ops.size();
+    if ((uint64_t)n + ib >= 0x7FFFFFF0ull) return "op log too large";
+    parent.resize(n + ib);
+    oright.resize(n + ib);
+    lamport.resize(n + ib);
+    agent.resize(n + ib);
+    deleted.resize(n + ib);
+    cp.resize(n + ib);
+    nxt_.resize(n + 1 + ib);
+    del_ops.resize(m + db);
+    uint32_t *P = parent.data(), *O = oright.data(), *L = lamport.data(), *C = cp.data();
+    uint16_t* A = agent.data();
+    uint8_t* Dl = deleted.data();
+    uint32_t *N = nxt_.data(), *Do = del_ops.data();
+    const char* err = nullptr;
+    for (size_t i = 0; i < np && !err; ++i) {
+        const uint64_t pos = pt[4 * i], del = pt[4 * i + 1], ioff = pt[4 * i + 2], ilen = pt[4 * i + 3];
+        if (del) {  // (remove_rga)
+            if (pos + del > nvis_) {
+                err = "remove range out of range";
+                break;
+            }
+            gb_reserve(1);
+            gb_move(pos);
+            nvis_ -= del;
+            uint64_t left = del;
+            while (left) {
+                GSpan& sp = gb_[g1_];
+                const uint32_t take = (uint32_t)std::min<uint64_t>(left, sp.len);
+                for (uint32_t j = 0; j < take; ++j) Do[m + j] = sp.id + j;
+                m += take;
+                std::memset(Dl + sp.id - 1, 1, take);
+                if (take == sp.len) {
+                    ++g1_;
+                } else {
+                    sp.id += take;
+                    sp.len -= take;
+                }
+                left -= take;
+            }
+        }
+        if (!ilen) continue;
+        // (insert_rga) the codepoints: one ASCII byte while typing, else decoded
+        const unsigned char* s8 = reinterpret_cast<const unsigned char*>(ins + ioff);
+        uint32_t c1;
+        const uint32_t* cps;
+        size_t k;
+        if (ilen == 1 && s8[0] < 0x80u) {
+            c1 = s8[0];
+            cps = &c1;
+            k = 1;
+        } else {
+            cps_.clear();
+            if (!utf8_decode(reinterpret_cast<const char*>(s8), ilen, cps_)) {
+                err = "invalid UTF-8";
+                break;
+            }
+            cps = cps_.data();
+            k = cps_.size();
+        }
+        if (pos > nvis_) {
+            err = "insert position out of range";
+            break;
+        }
+        const uint32_t first = (uint32_t)n + 1;
+        gb_reserve(2);
+        gb_move(pos);
+        const uint32_t lft = pos ? gb_[g0_ - 1].id + gb_[g0_ - 1].len - 1u : 0u;
+        const uint32_t rgt = N[lft];
+        N[lft] = first;
+        if (k == 1) {  // (typing)
+            P[n] = lft;
+            O[n] = rgt;
+            L[n] = max_lamport + 1u;
+            A[n] = local_agent;
+            Dl[n] = 0;
+            C[n] = cps[0];
+        } else {  // (a paste: column by column, each loop vectorises)
+            P[n] = lft;
+            for (size_t j = 1; j < k; ++j) P[n + j] = first + (uint32_t)j - 1u;
+            std::fill(O + n, O + n + k, rgt);
+            for (size_t j = 0; j < k; ++j) L[n + j] = max_lamport + 1u + (uint32_t)j;
+            std::fill(A + n, A + n + k, local_agent);
+            std::memset(Dl + n, 0, k);
+            std::memcpy(C + n, cps, k * sizeof(uint32_t));
+            for (size_t j = 0; j + 1 < k; ++j) N[n + 1 + j] = first + (uint32_t)j + 1u;
+        }
+        N[n + k] = rgt;
+        max_lamport += (uint32_t)k;
+        n += k;
+        if (g0_ && gb_[g0_ - 1].id + gb_[g0_ - 1].len == first)
+            gb_[g0_ - 1].len += (uint32_t)k;  // typing on: the span before the gap grows
+        else
+            gb_[g0_++] = GSpan{first, (uint32_t)k};
+        gvis_ += k;
+        nvis_ += k;
+    }
+    parent.resize(n);
+    oright.resize(n);
+    lamport.resize(n);
+    agent.resize(n);
+    deleted.resize(n);
+    cp.resize(n);
+    nxt_.resize(n + 1);
+    del_ops.resize(m);
+    return err ? std::string(err) : std::string();
+}
+
 // The gap buffer and the successors from the full document order (ids, tombstones included).
 std::string OpLog::rebuild_index_rga(const std::vector<uint32_t>& order) {
     nxt_.assign((size_t)size() + 1, NIL);

@@ -49,6 +49,12 @@ public:
     std::string insert_utf8(uint64_t pos, const char* s, size_t nbytes);
     std::string remove(uint64_t start, uint64_t end);
 
+    // The upstream loop of one editing trace (main.rs:28-36: replace = remove then insert per
+    // patch, rope.rs:21-32) as one call: patches as (pos, del, ins_off, ins_len) in codepoints,
+    // ins the concatenated inserted UTF-8.  RGA logs run a fused loop over columns sized once;
+    // Fugue (or stale) logs take insert / remove per patch.  "" or an error message.
+    std::string replay(const uint64_t* patches, size_t n, const char* ins);
+
     // Downstream wire format (see oplog.cpp for the layout).
     uint64_t version() const { return ((uint64_t)size() << 32) | (uint32_t)del_ops.size(); }
     std::vector<uint8_t> encode_from(uint64_t version) const;
