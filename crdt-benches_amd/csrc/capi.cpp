@@ -423,19 +423,14 @@ int trace_resolve(const crdt_hip_trace* t, crdt_hip_oplog** out, bool fugue) {
         L->log.fugue = fugue;
         const crdt::Trace& T = t->t;
         std::string e;
-        size_t ins_bytes = T.start_content.size(), dels = 0;
-        for (const crdt::Patch& p : T.patches) {
-            ins_bytes += p.ins_len;
-            dels += p.del;
-        }
-        L->log.reserve(ins_bytes, dels);  // >= items (one per codepoint), = delete ops
+        // (OpLog::replay sizes the columns to the patches' bounds itself)
         // from_str(start_content), then replace() every patch (main.rs:29-33, rope.rs:21-32)
         if (!T.start_content.empty())
             e = L->log.insert_utf8(0, T.start_content.data(), T.start_content.size());
         static_assert(sizeof(crdt::Patch) == 4 * sizeof(uint64_t), "Patch = {pos, del, ins_off, ins_len}");
         if (e.empty())
             e = L->log.replay(reinterpret_cast<const uint64_t*>(T.patches.data()), T.patches.size(),
-                              T.ins.data());
+                              T.ins.data(), T.ins.size());
         if (!e.empty()) {
             delete L;
             return set_err(nullptr, CRDT_HIP_ERANGE, e);

@@ -5016,9 +5016,31 @@ int Engine::merge(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens, c
 int Engine::merge_inner(DeviceLogs& L, Mode mode, uint64_t* digests, uint64_t* lens,
                         crdt_hip_stats* st, std::vector<uint8_t>* text_out,
                         std::vector<uint64_t>* text_offsets, uint64_t* cps) {
-    bool hinted = plan_cache && mode == TEXT && !text_out && !text_offsets && !L.waves.empty();
+    // learnt plans: every wave enqueued without a host wait; with text out for a one-wave merge
+    // too (a document merged again and again, the upstream closure of config 1), the text then
+    // copied back from this engine, which ran the one wave
+    const bool want_text = text_out || text_offsets;
+    bool hinted = plan_cache && mode == TEXT && !L.waves.empty() && (!want_text || L.waves.size() == 1);
     for (const Wave& w : L.waves) hinted = hinted && w.hint_lds;
-    if (hinted) return merge_async(L, digests, lens, cps, st);
+    if (hinted) {
+        const int rc = merge_async(L, digests, lens, cps, st);
+        if (rc || !want_text) return rc;
+        const Wave& w = L.waves[0];
+        std::vector<uint64_t> offs(w.ndocs + 1);
+        HIPCHK(hipMemcpyAsync(offs.data(), toff_, (w.ndocs + 1) * 8ull, hipMemcpyDeviceToHost, stream),
+               "copy offsets");
+        HIPCHK(hipStreamSynchronize(stream), "copy offsets");
+        if (text_out) {
+            text_out->resize(offs[w.ndocs]);
+            if (offs[w.ndocs]) {
+                HIPCHK(hipMemcpyAsync(text_out->data(), text_, offs[w.ndocs], hipMemcpyDeviceToHost,
+                                      stream), "copy text");
+                HIPCHK(hipStreamSynchronize(stream), "copy text");
+            }
+        }
+        if (text_offsets) *text_offsets = offs;
+        return CRDT_HIP_OK;
+    }
     if (lanes > 1 && L.waves.size() > 1 && !text_out) return merge_lanes(L, mode, digests, lens, cps, st);
     std::vector<float> stage_ms(S_N, 0.f);
     std::vector<uint32_t> stage_launches(S_N, 0);

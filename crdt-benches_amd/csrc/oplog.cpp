@@ -360,7 +360,7 @@ std::string OpLog::remove_rga(uint64_t start, uint64_t end) {
 // remove_rga + insert_rga, fused: every column is sized once to the trace's bound and written by
 // index (no per-item push_back), a one-byte insert (typing) and a one-codepoint delete
 // (backspace) take straight-line paths, and no std::string is made per patch.
-std::string OpLog::replay(const uint64_t* pt, size_t np, const char* ins) {
+std::string OpLog::replay(const uint64_t* pt, size_t np, const char* ins, size_t ins_total) {
     if (fugue || stale_) {
         for (size_t i = 0; i < np; ++i) {
             const uint64_t* q = pt + 4 * i;
@@ -371,12 +371,10 @@ std::string OpLog::replay(const uint64_t* pt, size_t np, const char* ins) {
         }
         return "";
     }
-    size_t ib = 0, db = 0;  // bounds: items <= inserted bytes, deletes = deleted codepoints
-    for (size_t i = 0; i < np; ++i) {
-        ib += pt[4 * i + 3];
-        db += pt[4 * i + 1];
-    }
+    // bounds without a pass over the patches: items <= the inserted bytes, and every item is
+    // deleted at most once (the columns are default-initialised: the slack costs no writes)
     size_t n = parent.size(), m = del_ops.size();
+    const size_t ib = ins_total, db = n + ib;
     if ((uint64_t)n + ib >= 0x7FFFFFF0ull) return "op log too large";
     parent.resize(n + ib);
     oright.resize(n + ib);

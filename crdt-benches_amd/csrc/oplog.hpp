@@ -11,10 +11,37 @@
 // resolver's sequence equals the merged document order at every step.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace crdt {
+
+// Op-log columns: vectors whose growth leaves new elements default-initialised (uninitialised
+// for these integer types) instead of zero-filled: the resolver sizes every column once to the
+// trace's bound and writes each item by index (OpLog::replay), so a zero fill would be a second
+// pass over the columns.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using Column = std::vector<T, DefaultInitAlloc<T>>;
 
 // Update wire format (OpLog::encode_from / apply_update, decoded on the device by replica.hip).
 constexpr uint32_t kUpdateMagic = 0x55445243u;  // "CRDU"
@@ -27,10 +54,10 @@ constexpr uint32_t kUpdateSideBit = 0x80000000u;
 class OpLog {
 public:
     // ---- SoA (index k holds item id k+1) ----
-    std::vector<uint32_t> parent, oright, lamport, cp;
-    std::vector<uint16_t> agent;
-    std::vector<uint8_t> deleted;
-    std::vector<uint32_t> del_ops;  // target id of every delete op, in op order
+    Column<uint32_t> parent, oright, lamport, cp;
+    Column<uint16_t> agent;
+    Column<uint8_t> deleted;
+    Column<uint32_t> del_ops;  // target id of every delete op, in op order
     // Fugue mode (set on an empty log): side[k] = 1 if item k+1 is a LEFT child of parent[k].
     // An insert after left neighbour a (full-list successor b) is a right child of a when a has
     // no right child yet, else a left child of b (the leftmost node of a's right subtree): the
@@ -51,9 +78,10 @@ public:
 
     // The upstream loop of one editing trace (main.rs:28-36: replace = remove then insert per
     // patch, rope.rs:21-32) as one call: patches as (pos, del, ins_off, ins_len) in codepoints,
-    // ins the concatenated inserted UTF-8.  RGA logs run a fused loop over columns sized once;
-    // Fugue (or stale) logs take insert / remove per patch.  "" or an error message.
-    std::string replay(const uint64_t* patches, size_t n, const char* ins);
+    // ins the concatenated inserted UTF-8 (ins_total bytes: every patch's text lies inside).
+    // RGA logs run a fused loop over columns sized once; Fugue (or stale) logs take insert /
+    // remove per patch.  "" or an error message.
+    std::string replay(const uint64_t* patches, size_t n, const char* ins, size_t ins_total);
 
     // Downstream wire format (see oplog.cpp for the layout).
     uint64_t version() const { return ((uint64_t)size() << 32) | (uint32_t)del_ops.size(); }
@@ -83,7 +111,7 @@ private:
     std::vector<GSpan> gb_;        // gap [g0_, g1_)
     size_t g0_ = 0, g1_ = 0;
     uint64_t gvis_ = 0;            // visible items in gb_[0, g0_)
-    std::vector<uint32_t> nxt_;    // per id 0..n: next item in the full list (NIL: last)
+    Column<uint32_t> nxt_;         // per id 0..n: next item in the full list (NIL: last)
     void gb_move(uint64_t pos);    // the gap at visible position pos (a span split if needed)
     void gb_reserve(size_t k);
     std::string insert_rga(uint64_t pos, const uint32_t* cps, size_t k);

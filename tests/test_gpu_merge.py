@@ -49,6 +49,24 @@ def test_trace_merge_byte_exact(ctx, oracle, golden, name):
     assert dig == oracle.tree_digest(text)
 
 
+@pytest.mark.parametrize("scatter", [0, 1])
+def test_repeated_text_merges_take_the_learnt_plan(golden, scatter):
+    """The upstream closure of config 1 merges a document of the same shape again and again: from
+    the second merge on the single wave runs on its learnt plan (no host wait inside the merge)
+    and the text is copied back from the engine that ran it; the bytes stay endContent's, with
+    the text from phase C or from the text kernel."""
+    import hashlib
+    c = crdt_hip.Context(0)
+    c.set_param("text_scatter", scatter)
+    for name in TRACES:
+        log = resolved(name)
+        for _ in range(3):
+            text, dig = c.merge(log)
+            assert hashlib.sha256(text).hexdigest() == golden[name]["sha256"], name
+            assert "%016x" % dig == golden[name]["tree_digest"]
+    c.close()
+
+
 @pytest.mark.parametrize("name", ["sveltecomponent", "automerge-paper"])
 def test_merge_order_matches_oracle_preorder(ctx, oracle, name):
     log = resolved(name)
