@@ -83,9 +83,13 @@ int guard(crdt_hip_ctx* ctx, F&& f) {
 }
 
 uint64_t visible_bytes(const crdt_hip_oplog_view& v) {
+    // (branch-free, so that it vectorises: part of every crdt_hip_merge of a host view)
     uint64_t b = 0;
-    for (uint32_t i = 0; i < v.n; ++i)
-        if (!v.deleted[i]) b += crdt::utf8_len_cp(v.cp[i] & 0x1FFFFFu);
+    for (uint32_t i = 0; i < v.n; ++i) {
+        const uint32_t c = v.cp[i] & 0x1FFFFFu;
+        const uint32_t len = 1u + (c >= 0x80u) + (c >= 0x800u) + (c >= 0x10000u);
+        b += v.deleted[i] ? 0u : len;
+    }
     return b;
 }
 

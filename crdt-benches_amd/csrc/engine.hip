@@ -3944,6 +3944,7 @@ Engine::~Engine() {
     dfree(leafh_); dfree(ghash_); dfree(text_);
     dfree(leafcp_); dfree(gcp_); dfree(tab_slot_); dfree(tab_local_);
     if (host_out_) (void)hipHostFree(host_out_);
+    if (up_pin_) (void)hipHostFree(up_pin_);
     for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : wev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : raw_ev_)
@@ -4161,17 +4162,38 @@ int Engine::upload_tables(DeviceLogs& L) {
 
 int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) {
     const uint64_t S = L.total_slots;
-    std::vector<uint32_t> par(S, 0);
-    std::vector<uint8_t> c(cp3_bytes(S), 0);
-    for (uint64_t g = 0; g < S; ++g) cp3_put(c.data(), g, kDelBit);
-    std::vector<uint64_t> key(S, 0);
+    // the encoded columns are written into a pinned staging buffer (kept and grown by the engine)
+    // and copied by DMA: a pageable source is copied through the driver's own staging at a
+    // fraction of the rate, and fresh host vectors cost a zero fill of every column (the upload
+    // of a one-document merge, config 1's len(), was ~2/3 of that merge)
+    const uint64_t need = S * 12ull + cp3_bytes(S) + 64;
+    if (need > cap_up_pin_) {
+        if (up_pin_) (void)hipHostFree(up_pin_);
+        up_pin_ = nullptr;
+        cap_up_pin_ = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&up_pin_), need), "pinned upload staging");
+        cap_up_pin_ = need;
+    }
+    uint64_t* key = reinterpret_cast<uint64_t*>(up_pin_);
+    uint32_t* par = reinterpret_cast<uint32_t*>(up_pin_ + S * 8ull);
+    uint8_t* c = up_pin_ + S * 12ull;
+    // every slot that holds no item (document starts, padding): parent 0, key 0, deleted
+    for (uint32_t d = 0; d <= n; ++d) {
+        const uint64_t lo = d ? L.doc_slot[d - 1] + 1 + views[d - 1].n : 0;
+        const uint64_t hi = d < n ? L.doc_slot[d] + 1 : S;  // (through the start slot of doc d)
+        for (uint64_t g = lo; g < hi; ++g) {
+            par[g] = 0;
+            key[g] = 0;
+            cp3_put(c, g, kDelBit);
+        }
+    }
     L.fugue = false;
     std::vector<uint64_t> nsq_doc(n, 0);
     for (uint32_t d = 0; d < n; ++d) {
         const crdt_hip_oplog_view& v = views[d];
         const uint64_t b = L.doc_slot[d] + 1;
         if (v.n == 0) continue;
-        std::memcpy(&par[b], v.parent, v.n * 4ull);
+        std::memcpy(par + b, v.parent, v.n * 4ull);
         if (v.side) {  // Fugue: left children carry kLeftBit / kLeftKey, never the seq flag
             for (uint32_t i = 0; i < v.n; ++i) {
                 const bool left = v.side[i] != 0;
@@ -4182,15 +4204,15 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
                 }
                 L.fugue |= left;
                 key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i] | (left ? kLeftKey : 0ull);
-                cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
-                                             (left ? kLeftBit : (v.parent[i] == i ? kSeqBit : 0u)));
+                cp3_put(c, b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
+                                      (left ? kLeftBit : (v.parent[i] == i ? kSeqBit : 0u)));
             }
             continue;
         }
         for (uint32_t i = 0; i < v.n; ++i) {
             key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
-            cp3_put(c.data(), b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
-                                         (v.parent[i] == i ? kSeqBit : 0u));
+            cp3_put(c, b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
+                                  (v.parent[i] == i ? kSeqBit : 0u));
             nsq_doc[d] += v.parent[i] != i;
         }
     }
@@ -4201,9 +4223,10 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
     set_contraction(L);
     // on the engine's stream (a null-stream copy does not wait for the non-blocking streams the
     // kernels run on, nor they for it), then waited for: the host columns are freed on return
-    HIPCHK(hipMemcpyAsync(L.parent, par.data(), S * 4, hipMemcpyHostToDevice, stream), "upload parent");
-    HIPCHK(hipMemcpyAsync(L.key, key.data(), S * 8, hipMemcpyHostToDevice, stream), "upload key");
-    HIPCHK(hipMemcpyAsync(L.cp, c.data(), c.size(), hipMemcpyHostToDevice, stream), "upload cp");
+    // (the staging is reused by the next upload: waited for here)
+    HIPCHK(hipMemcpyAsync(L.parent, par, S * 4, hipMemcpyHostToDevice, stream), "upload parent");
+    HIPCHK(hipMemcpyAsync(L.key, key, S * 8, hipMemcpyHostToDevice, stream), "upload key");
+    HIPCHK(hipMemcpyAsync(L.cp, c, cp3_bytes(S), hipMemcpyHostToDevice, stream), "upload cp");
     HIPCHK(hipStreamSynchronize(stream), "upload sync");
     return CRDT_HIP_OK;
 }

@@ -344,6 +344,8 @@ private:
     uint2* sup_ = nullptr;     // super-splitters (engine.hip k_sup1): {weight, next}
     uint32_t* spred_ = nullptr;
     uint2* svp_[2] = {nullptr, nullptr};
+    uint8_t* up_pin_ = nullptr;          // pinned staging of upload(): the encoded columns
+    uint64_t cap_up_pin_ = 0;
     uint32_t* host_out_ = nullptr;       // pinned image of every wave's result block
     uint64_t cap_host_out_ = 0;          // bytes
     uint32_t probe_doc_ = 0;             // 1 + document whose k_doctree phases are printed
