@@ -388,26 +388,65 @@ std::string OpLog::replay(const uint64_t* pt, size_t np, const char* ins, size_t
     uint16_t* A = agent.data();
     uint8_t* Dl = deleted.data();
     uint32_t *N = nxt_.data(), *Do = del_ops.data();
+    // the gap buffer's state and the counters in locals for the whole loop (the byte stores to
+    // the deleted column may alias any member, which would reload them after every store)
+    // (a patch adds at most three spans: a split at its delete, a split at its insert and the
+    // new span; the gap buffer is default-initialised, so the room costs no writes)
+    gb_reserve(3 * np + 64);
+    GSpan* G = gb_.data();
+    size_t g0 = g0_, g1 = g1_;
+    uint64_t gvis = gvis_, nvis = nvis_;
+    uint32_t maxl = max_lamport;
+    const uint16_t agent0 = local_agent;
+    // the gap to visible position pos (gb_move on the locals)
+    auto move_to = [&](uint64_t pos) {
+        while (gvis > pos) {
+            GSpan& sp = G[g0 - 1];
+            if (gvis - sp.len >= pos) {
+                G[--g1] = sp;
+                --g0;
+                gvis -= sp.len;
+            } else {  // split: the part after pos goes right of the gap
+                const uint32_t o = (uint32_t)(pos - (gvis - sp.len));
+                G[--g1] = GSpan{sp.id + o, sp.len - o};
+                sp.len = o;
+                gvis = pos;
+            }
+        }
+        while (gvis < pos) {
+            GSpan& sp = G[g1];
+            if (gvis + sp.len <= pos) {
+                G[g0++] = sp;
+                ++g1;
+                gvis += sp.len;
+            } else {
+                const uint32_t o = (uint32_t)(pos - gvis);
+                G[g0++] = GSpan{sp.id, o};
+                sp.id += o;
+                sp.len -= o;
+                gvis = pos;
+            }
+        }
+    };
     const char* err = nullptr;
     for (size_t i = 0; i < np && !err; ++i) {
         const uint64_t pos = pt[4 * i], del = pt[4 * i + 1], ioff = pt[4 * i + 2], ilen = pt[4 * i + 3];
         if (del) {  // (remove_rga)
-            if (pos + del > nvis_) {
+            if (pos + del > nvis) {
                 err = "remove range out of range";
                 break;
             }
-            gb_reserve(1);
-            gb_move(pos);
-            nvis_ -= del;
+            move_to(pos);
+            nvis -= del;
             uint64_t left = del;
             while (left) {
-                GSpan& sp = gb_[g1_];
+                GSpan& sp = G[g1];
                 const uint32_t take = (uint32_t)std::min<uint64_t>(left, sp.len);
                 for (uint32_t j = 0; j < take; ++j) Do[m + j] = sp.id + j;
                 m += take;
                 std::memset(Dl + sp.id - 1, 1, take);
                 if (take == sp.len) {
-                    ++g1_;
+                    ++g1;
                 } else {
                     sp.id += take;
                     sp.len -= take;
@@ -434,43 +473,47 @@ std::string OpLog::replay(const uint64_t* pt, size_t np, const char* ins, size_t
             cps = cps_.data();
             k = cps_.size();
         }
-        if (pos > nvis_) {
+        if (pos > nvis) {
             err = "insert position out of range";
             break;
         }
         const uint32_t first = (uint32_t)n + 1;
-        gb_reserve(2);
-        gb_move(pos);
-        const uint32_t lft = pos ? gb_[g0_ - 1].id + gb_[g0_ - 1].len - 1u : 0u;
+        move_to(pos);
+        const uint32_t lft = pos ? G[g0 - 1].id + G[g0 - 1].len - 1u : 0u;
         const uint32_t rgt = N[lft];
         N[lft] = first;
         if (k == 1) {  // (typing)
             P[n] = lft;
             O[n] = rgt;
-            L[n] = max_lamport + 1u;
-            A[n] = local_agent;
+            L[n] = maxl + 1u;
+            A[n] = agent0;
             Dl[n] = 0;
             C[n] = cps[0];
         } else {  // (a paste: column by column, each loop vectorises)
             P[n] = lft;
             for (size_t j = 1; j < k; ++j) P[n + j] = first + (uint32_t)j - 1u;
             std::fill(O + n, O + n + k, rgt);
-            for (size_t j = 0; j < k; ++j) L[n + j] = max_lamport + 1u + (uint32_t)j;
-            std::fill(A + n, A + n + k, local_agent);
+            for (size_t j = 0; j < k; ++j) L[n + j] = maxl + 1u + (uint32_t)j;
+            std::fill(A + n, A + n + k, agent0);
             std::memset(Dl + n, 0, k);
             std::memcpy(C + n, cps, k * sizeof(uint32_t));
             for (size_t j = 0; j + 1 < k; ++j) N[n + 1 + j] = first + (uint32_t)j + 1u;
         }
         N[n + k] = rgt;
-        max_lamport += (uint32_t)k;
+        maxl += (uint32_t)k;
         n += k;
-        if (g0_ && gb_[g0_ - 1].id + gb_[g0_ - 1].len == first)
-            gb_[g0_ - 1].len += (uint32_t)k;  // typing on: the span before the gap grows
+        if (g0 && G[g0 - 1].id + G[g0 - 1].len == first)
+            G[g0 - 1].len += (uint32_t)k;  // typing on: the span before the gap grows
         else
-            gb_[g0_++] = GSpan{first, (uint32_t)k};
-        gvis_ += k;
-        nvis_ += k;
+            G[g0++] = GSpan{first, (uint32_t)k};
+        gvis += k;
+        nvis += k;
     }
+    g0_ = g0;
+    g1_ = g1;
+    gvis_ = gvis;
+    nvis_ = nvis;
+    max_lamport = maxl;
     parent.resize(n);
     oright.resize(n);
     lamport.resize(n);

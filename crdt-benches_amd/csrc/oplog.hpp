@@ -108,7 +108,7 @@ private:
     struct GSpan {
         uint32_t id, len;
     };
-    std::vector<GSpan> gb_;        // gap [g0_, g1_)
+    Column<GSpan> gb_;             // gap [g0_, g1_)
     size_t g0_ = 0, g1_ = 0;
     uint64_t gvis_ = 0;            // visible items in gb_[0, g0_)
     Column<uint32_t> nxt_;         // per id 0..n: next item in the full list (NIL: last)
