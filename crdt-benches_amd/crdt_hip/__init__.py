@@ -485,12 +485,12 @@ class Context:
         """Merged document: (utf8 bytes, tree digest)."""
         v, keep = _as_view(log)
         cap = 4 * v.n + 16
-        buf = C.create_string_buffer(cap)
+        buf = np.empty(cap, np.uint8)  # (not zeroed: the engine writes the n bytes returned)
         n, dig = C.c_size_t(), C.c_uint64()
-        _check(lib().crdt_hip_merge(self._h, C.byref(v), buf, cap, C.byref(n), C.byref(dig)),
-               self._h)
+        _check(lib().crdt_hip_merge(self._h, C.byref(v), buf.ctypes.data, cap, C.byref(n),
+                                    C.byref(dig)), self._h)
         del keep
-        return buf.raw[: n.value], int(dig.value)
+        return buf[: n.value].tobytes(), int(dig.value)
 
     def merge_digest(self, log) -> tuple:
         v, keep = _as_view(log)
