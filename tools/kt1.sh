@@ -7,7 +7,7 @@ R=${ROUND:-kt}
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${R} -o run \
     -- python3 bench.py --steps 5 --warmup 2 --lanes ${LANES:-1} --no-cpu-baseline --companion-replicas 0 \
-    --config1-seconds 0 > gpurun_out/${R}_bench.json 2> gpurun_out/${R}.log
+    --config1-seconds 0 --raw-companion 0 > gpurun_out/${R}_bench.json 2> gpurun_out/${R}.log
 st=$?; echo "status $st"
 case $st in 0) ;; *) tail -5 gpurun_out/${R}.log; exit $st;; esac
 python3 - gpurun_out/${R} <<'PY'
