@@ -5589,7 +5589,7 @@ void Engine::nsq_scan(DeviceLogs& L) {
 
 // Raw SoA mode (DeviceLogs::raw).  k_raw_fill keeps the reference-shaped columns of resident logs
 // once (lamport, agent, deleted, codepoint per slot, from the encoded key and codepoint word);
-// k_raw_encode derives the encoded input from them and the parent column at every merge: 16
+// k_raw_encode derives the encoded input from them and the parent column at every merge: 4
 // slots per thread, the key (lamport << 16 | agent), the 3-byte codepoint word with the tombstone
 // and the previous-slot flag (parent == index - 1), and the nsq count and mask of each 64-slot
 // chunk (what k_nsq_count reads back from the codepoint words otherwise).  Item slots only: a
@@ -5615,41 +5615,62 @@ __global__ __launch_bounds__(kBlock) void k_raw_encode(L0Args a, const uint32_t*
                                                        uint8_t* __restrict__ cp3,
                                                        uint32_t* __restrict__ cnt,
                                                        uint64_t* __restrict__ mask) {
-    // one slot per lane (every column read and the key written coalesced); a wave = one 64-slot
-    // chunk (its nsq mask is a ballot); the block's 256 codepoint words are assembled in LDS and
-    // stored as 48 16-byte pieces
-    __shared__ __attribute__((aligned(16))) uint8_t cb[3 * kBlock];
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    bool nsq = false;
-    uint32_t c = 0;
-    if (g < a.nslots) {
-        const uint2 doc = a.docs[a.chunk_doc[g >> a.log2m]];
-        const uint32_t l = g - doc.x;  // (the slot's item index; 0: the document start)
-        const uint32_t p = a.in_parent[g], lm = lam[g], cw = cpw[g];
-        const uint16_t ag = agent[g];
-        const uint8_t dl = del[g];
-        if (l - 1u < doc.y) {
-            const bool sq = p == l - 1u;
-            nsq = !sq;
-            c = (cw & 0x1FFFFFu) | (dl ? kDelBit : 0u) | (sq ? kSeqBit : 0u);
-            key[g] = ((uint64_t)lm << 16) | ag;
-        } else {
-            c = cp3_get(a.in_cp, g);  // (a document start or padding keeps its word)
+    // four slots per lane (every column read with one vector load, the keys written as two
+    // 16-byte stores); a wave = four 64-slot chunks, 16 lanes each (their nsq masks joined by
+    // shuffles); the block's 1024 codepoint words are assembled in LDS and stored as 192 16-byte
+    // pieces.  Wave slot counts are multiples of 64 (documents start 64-aligned).
+    __shared__ __attribute__((aligned(16))) uint32_t cb[3 * kBlock];
+    const uint32_t g0 = (blockIdx.x * kBlock + threadIdx.x) * 4u;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t nsq = 0, c[4] = {0u, 0u, 0u, 0u};
+    const bool live = g0 < a.nslots;
+    uint4 lm = make_uint4(0, 0, 0, 0);
+    uint2 ag2 = make_uint2(0, 0);
+    if (live) lm = *reinterpret_cast<const uint4*>(lam + g0);
+    if (live) ag2 = *reinterpret_cast<const uint2*>(agent + g0);
+    if (live) {
+        const uint2 doc = a.docs[a.chunk_doc[g0 >> a.log2m]];  // (the four slots share a chunk)
+        const uint4 p4 = *reinterpret_cast<const uint4*>(a.in_parent + g0);
+        const uint4 cw4 = *reinterpret_cast<const uint4*>(cpw + g0);
+        const uint32_t dl4 = *reinterpret_cast<const uint32_t*>(del + g0);
+        const uint32_t P[4] = {p4.x, p4.y, p4.z, p4.w}, CW[4] = {cw4.x, cw4.y, cw4.z, cw4.w};
+        const uint32_t LM[4] = {lm.x, lm.y, lm.z, lm.w};
+        const uint32_t AG[4] = {ag2.x & 0xFFFFu, ag2.x >> 16, ag2.y & 0xFFFFu, ag2.y >> 16};
+        uint64_t K[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t l = g0 + (uint32_t)k - doc.x;  // (item index + 1; 0: the document start)
+            K[k] = ((uint64_t)LM[k] << 16) | AG[k];
+            if (l - 1u < doc.y) {
+                const bool sq = P[k] == l - 1u;
+                nsq |= (sq ? 0u : 1u) << k;
+                c[k] = (CW[k] & 0x1FFFFFu) | ((dl4 >> (8 * k)) & 0xFFu ? kDelBit : 0u) | (sq ? kSeqBit : 0u);
+            } else {
+                c[k] = cp3_get(a.in_cp, g0 + (uint32_t)k);  // (a document start or padding keeps its word)
+                K[k] = a.in_key[g0 + (uint32_t)k];
+            }
         }
+        uint4* kd = reinterpret_cast<uint4*>(key + g0);
+        kd[0] = make_uint4((uint32_t)K[0], (uint32_t)(K[0] >> 32), (uint32_t)K[1], (uint32_t)(K[1] >> 32));
+        kd[1] = make_uint4((uint32_t)K[2], (uint32_t)(K[2] >> 32), (uint32_t)K[3], (uint32_t)(K[3] >> 32));
     }
-    cb[3 * threadIdx.x] = (uint8_t)c;
-    cb[3 * threadIdx.x + 1] = (uint8_t)(c >> 8);
-    cb[3 * threadIdx.x + 2] = (uint8_t)(c >> 16);
-    const uint64_t m = __ballot(nsq);
-    if ((threadIdx.x & 63u) == 0u && g < a.nslots && cnt) {
-        cnt[g >> 6] = (uint32_t)__popcll(m);
-        mask[g >> 6] = m;
+    // the four 3-byte words as three dwords at the lane's 12 bytes
+    cb[3 * threadIdx.x] = c[0] | (c[1] << 24);
+    cb[3 * threadIdx.x + 1] = (c[1] >> 8) | (c[2] << 16);
+    cb[3 * threadIdx.x + 2] = (c[2] >> 16) | (c[3] << 8);
+    // the chunk's mask: 16 lanes' nibbles
+    uint64_t m = (uint64_t)nsq << (4u * (lane & 15u));
+#pragma unroll
+    for (int x = 1; x < 16; x <<= 1) m |= (uint64_t)__shfl_xor((long long)m, x);
+    if ((lane & 15u) == 0u && live && cnt) {
+        cnt[g0 >> 6] = (uint32_t)__popcll(m);
+        mask[g0 >> 6] = m;
     }
     __syncthreads();
-    const uint32_t g0 = blockIdx.x * kBlock;
-    if (threadIdx.x < 3 * kBlock / 16 && g0 + 16u * threadIdx.x / 3u < a.nslots)
-        reinterpret_cast<uint4*>(cp3 + 3ull * g0)[threadIdx.x] =
-            reinterpret_cast<const uint4*>(cb)[threadIdx.x];
+    const uint32_t b0 = blockIdx.x * kBlock * 4u;
+    for (uint32_t i = threadIdx.x; i < 3u * kBlock * 4u / 16u; i += kBlock)
+        if (b0 + 16u * i / 3u < a.nslots)
+            reinterpret_cast<uint4*>(cp3 + 3ull * b0)[i] = reinterpret_cast<const uint4*>(cb)[i];
 }
 
 int Engine::raw_keep(DeviceLogs& L) {
@@ -5686,7 +5707,7 @@ int Engine::raw_encode(DeviceLogs& L) {
     if (nsq) (void)hipMemsetAsync(L.nsq_pre, 0, (L.total_slots / 64 + 65) * 4ull, stream);
     for (const Wave& w : L.waves) {
         L0ARGS(a0);
-        k_raw_encode<<<grid_for(w.nslots), kBlock, 0, stream>>>(
+        k_raw_encode<<<grid_for((w.nslots + 3) / 4), kBlock, 0, stream>>>(
             a0, L.raw_lam + w.slot0, L.raw_agent + w.slot0, L.raw_del + w.slot0,
             L.raw_cp + w.slot0, L.key + w.slot0, L.cp + 3ull * w.slot0,
             nsq ? L.nsq_pre + (w.slot0 >> 6) : nullptr, nsq ? L.nsq_mask + (w.slot0 >> 6) : nullptr);
