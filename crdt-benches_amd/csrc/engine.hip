@@ -3944,7 +3944,9 @@ Engine::~Engine() {
     dfree(leafh_); dfree(ghash_); dfree(text_);
     dfree(leafcp_); dfree(gcp_); dfree(tab_slot_); dfree(tab_local_);
     if (host_out_) (void)hipHostFree(host_out_);
+    if (up_pending_) (void)hipEventSynchronize(up_ev_);
     if (up_pin_) (void)hipHostFree(up_pin_);
+    if (up_ev_) (void)hipEventDestroy(up_ev_);
     for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : wev_) (void)hipEventDestroy(e);
     for (hipEvent_t e : raw_ev_)
@@ -4166,6 +4168,10 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
     // and copied by DMA: a pageable source is copied through the driver's own staging at a
     // fraction of the rate, and fresh host vectors cost a zero fill of every column (the upload
     // of a one-document merge, config 1's len(), was ~2/3 of that merge)
+    if (up_pending_) {  // (the last upload's copies still read the staging)
+        HIPCHK(hipEventSynchronize(up_ev_), "upload staging");
+        up_pending_ = false;
+    }
     const uint64_t need = S * 12ull + cp3_bytes(S) + 64;
     if (need > cap_up_pin_) {
         if (up_pin_) (void)hipHostFree(up_pin_);
@@ -4177,57 +4183,85 @@ int Engine::upload(DeviceLogs& L, const crdt_hip_oplog_view* views, uint32_t n) 
     uint64_t* key = reinterpret_cast<uint64_t*>(up_pin_);
     uint32_t* par = reinterpret_cast<uint32_t*>(up_pin_ + S * 8ull);
     uint8_t* c = up_pin_ + S * 12ull;
-    // every slot that holds no item (document starts, padding): parent 0, key 0, deleted
+    // the slots that hold no item (document starts, padding) before document d, and after the
+    // last (d = n): parent 0, key 0, deleted
+    auto gap = [&](uint32_t d, uint64_t& lo, uint64_t& hi) {
+        lo = d ? L.doc_slot[d - 1] + 1 + views[d - 1].n : 0;
+        hi = d < n ? L.doc_slot[d] + 1 : S;  // (through the start slot of doc d)
+    };
+    // Column by column, each copied (on the engine's stream: a null-stream copy does not wait
+    // for the non-blocking streams the kernels run on, nor they for it) as soon as it is
+    // written, so that the DMA of one column overlaps the encoding of the next.
+    uint64_t lo, hi;
     for (uint32_t d = 0; d <= n; ++d) {
-        const uint64_t lo = d ? L.doc_slot[d - 1] + 1 + views[d - 1].n : 0;
-        const uint64_t hi = d < n ? L.doc_slot[d] + 1 : S;  // (through the start slot of doc d)
-        for (uint64_t g = lo; g < hi; ++g) {
-            par[g] = 0;
-            key[g] = 0;
-            cp3_put(c, g, kDelBit);
-        }
+        gap(d, lo, hi);
+        if (hi > lo) std::memset(par + lo, 0, (hi - lo) * 4);
+        if (d < n && views[d].n) std::memcpy(par + L.doc_slot[d] + 1, views[d].parent, views[d].n * 4ull);
     }
+    HIPCHK(hipMemcpyAsync(L.parent, par, S * 4, hipMemcpyHostToDevice, stream), "upload parent");
     L.fugue = false;
-    std::vector<uint64_t> nsq_doc(n, 0);
-    for (uint32_t d = 0; d < n; ++d) {
+    for (uint32_t d = 0; d <= n; ++d) {
+        gap(d, lo, hi);
+        if (hi > lo) std::memset(key + lo, 0, (hi - lo) * 8);
+        if (d == n) break;
         const crdt_hip_oplog_view& v = views[d];
         const uint64_t b = L.doc_slot[d] + 1;
-        if (v.n == 0) continue;
-        std::memcpy(par + b, v.parent, v.n * 4ull);
-        if (v.side) {  // Fugue: left children carry kLeftBit / kLeftKey, never the seq flag
+        if (v.side) {  // Fugue: left children carry kLeftKey (and kLeftBit, never the seq flag)
             for (uint32_t i = 0; i < v.n; ++i) {
                 const bool left = v.side[i] != 0;
                 if (v.lamport[i] == 0xFFFFFFFFu) {  // (kMidKey sorts above every right child)
                     // a malformed log, as replica_upload reports it (one code on every path)
                     err = "invalid Fugue log (lamport 0xFFFFFFFF)";
+                    (void)hipStreamSynchronize(stream);  // (the parent copy reads the staging)
                     return CRDT_HIP_EBADLOG;
                 }
                 L.fugue |= left;
                 key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i] | (left ? kLeftKey : 0ull);
+            }
+        } else {
+            for (uint32_t i = 0; i < v.n; ++i) key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
+        }
+    }
+    HIPCHK(hipMemcpyAsync(L.key, key, S * 8, hipMemcpyHostToDevice, stream), "upload key");
+    std::vector<uint64_t> nsq_doc(n, 0);
+    for (uint32_t d = 0; d <= n; ++d) {
+        gap(d, lo, hi);
+        for (uint64_t g = lo; g < hi; ++g) cp3_put(c, g, kDelBit);
+        if (d == n) break;
+        const crdt_hip_oplog_view& v = views[d];
+        const uint64_t b = L.doc_slot[d] + 1;
+        if (v.side) {
+            for (uint32_t i = 0; i < v.n; ++i) {
+                const bool left = v.side[i] != 0;
                 cp3_put(c, b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
                                       (left ? kLeftBit : (v.parent[i] == i ? kSeqBit : 0u)));
             }
             continue;
         }
+        uint64_t q = 0;
         for (uint32_t i = 0; i < v.n; ++i) {
-            key[b + i] = ((uint64_t)v.lamport[i] << 16) | v.agent[i];
             cp3_put(c, b + i, (v.cp[i] & kCpMask) | (v.deleted[i] ? kDelBit : 0u) |
                                   (v.parent[i] == i ? kSeqBit : 0u));
-            nsq_doc[d] += v.parent[i] != i;
+            q += v.parent[i] != i;
         }
+        nsq_doc[d] = q;
     }
+    HIPCHK(hipMemcpyAsync(L.cp, c, cp3_bytes(S), hipMemcpyHostToDevice, stream), "upload cp");
     for (Wave& w : L.waves) {
         w.nsq_items = 0;
         for (uint32_t k = 0; k < w.ndocs; ++k) w.nsq_items += nsq_doc[w.first_doc + k];
     }
     set_contraction(L);
-    // on the engine's stream (a null-stream copy does not wait for the non-blocking streams the
-    // kernels run on, nor they for it), then waited for: the host columns are freed on return
-    // (the staging is reused by the next upload: waited for here)
-    HIPCHK(hipMemcpyAsync(L.parent, par, S * 4, hipMemcpyHostToDevice, stream), "upload parent");
-    HIPCHK(hipMemcpyAsync(L.key, key, S * 8, hipMemcpyHostToDevice, stream), "upload key");
-    HIPCHK(hipMemcpyAsync(L.cp, c, cp3_bytes(S), hipMemcpyHostToDevice, stream), "upload cp");
-    HIPCHK(hipStreamSynchronize(stream), "upload sync");
+    // A one-wave upload (a single document: config 1's len()) is not waited for: its merge runs
+    // on this stream behind the copies, and the next upload waits before it rewrites the staging
+    // (up_ev_).  Merges of several waves may run on the lanes' streams: waited for here.
+    if (L.waves.size() == 1) {
+        if (!up_ev_) HIPCHK(hipEventCreateWithFlags(&up_ev_, hipEventDisableTiming), "event create");
+        HIPCHK(hipEventRecord(up_ev_, stream), "upload event");
+        up_pending_ = true;
+    } else {
+        HIPCHK(hipStreamSynchronize(stream), "upload sync");
+    }
     return CRDT_HIP_OK;
 }
 

@@ -331,9 +331,11 @@ private:
     uint64_t cap_wtmp_ = 0;    // (bytes)
     uint32_t wtmp_log2_ = 7;
     uint32_t tail_nspl_ = 0;   // splitters of the last global level 1 whose offsets are in rloc_
-    bool tail_scatter_ = false;
-    hipEvent_t raw_ev_[2] = {nullptr, nullptr};  // (raw SoA mode: the encoding's interval)  // the last level 1 was k_doctree in scatter mode: k_tscatter next
-                               //   (0: k_expand reads roff_)
+    bool tail_scatter_ = false;  // the last level 1 was k_doctree in scatter mode: k_tscatter
+                                 //   next (0: k_expand reads roff_)
+    hipEvent_t raw_ev_[2] = {nullptr, nullptr};  // (raw SoA mode: the encoding's interval)
+    hipEvent_t up_ev_ = nullptr;  // after the copies of a one-wave upload (Engine::upload)
+    bool up_pending_ = false;     //   not yet waited for: the staging is still being read
     uint32_t* ovf_ = nullptr;  // text mode: splitters whose sublist holds more than its slot
     uint64_t cap_ovf_ = 0;
     uint32_t rs_npass_ = 0, rs_npassB_ = 0;
