@@ -719,8 +719,9 @@ def traces_workload(args) -> int:
     # companion line: the headline batch in raw SoA mode: every merge first
     # derives the key, the codepoint word with its flags and the compact nsq list on the device
     # from reference-shaped columns (lamport, agent, deleted, codepoint beside the parents), so
-    # the step is priced over the raw SoA, the untimed input encoding included
-    if args.raw_companion:
+    # the step is priced over the raw SoA, the untimed input encoding included (RGA batches: the
+    # raw columns carry no Fugue side)
+    if args.raw_companion and args.order == "rga":
         def make_raw(bases, replicas, relabel, seed):
             b = make_batch(bases, replicas, relabel, seed)
             b.set_raw(True)
