@@ -3292,11 +3292,6 @@ __device__ __forceinline__ void doctree_doc(const DocArgs& a, uint32_t widx) {
 // 17 rows per thread (Fugue seph-blog1, 16.6 k rows; 8 VGPRs spill on its own, ~40 inside
 // k_doctree_wide).
 constexpr int kDocJNarrow = 12;
-#ifdef CRDT_DOC_WPE  // (experiment: cap k_doctree's registers so other kernels' waves fit beside it)
-#define DOC_WPE __attribute__((amdgpu_waves_per_eu(CRDT_DOC_WPE)))
-#else
-#define DOC_WPE
-#endif
 // PC: phase C (the document text written from LDS) compiled in.  The instances without it (the
 // scatter mode, and the offsets left to k_expand) carry neither its code nor its registers.
 template <int J, bool K32, bool PC>
@@ -3306,13 +3301,13 @@ __device__ __forceinline__ bool doctree_try(const DocArgs& a, uint32_t R) {
     return true;
 }
 template <bool PC>
-__global__ __launch_bounds__(kDocThreads) DOC_WPE void k_doctree(DocArgs a) {
+__global__ __launch_bounds__(kDocThreads) void k_doctree(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
     if (doctree_try<4, false, PC>(a, R) || doctree_try<8, false, PC>(a, R)) return;
     doctree_doc<kDocJNarrow, false, PC>(a, blockIdx.x);
 }
 template <bool PC>
-__global__ __launch_bounds__(kDocThreads) DOC_WPE void k_doctree_wide(DocArgs a) {
+__global__ __launch_bounds__(kDocThreads) void k_doctree_wide(DocArgs a) {
     const uint32_t R = a.wg[2u * blockIdx.x].z;
     if (doctree_try<8, true, PC>(a, R)) return;
     doctree_doc<kDocJNarrow, true, PC>(a, blockIdx.x);
@@ -3376,11 +3371,7 @@ __device__ __forceinline__ void scatter_window(const uint8_t* seg, uint32_t a0, 
 #pragma unroll
     for (uint32_t i = 0; i < kScatterWin / 1024u; ++i) {
         const uint32_t o = a0 + 1024u * i + 16u * lane;
-#ifdef CRDT_TSC_NOTEXT
-        v[i] = make_uint4(o, 0, 0, 0);
-#else
         v[i] = o < a1 ? *reinterpret_cast<const uint4*>(seg + o) : make_uint4(0, 0, 0, 0);
-#endif
     }
 #pragma unroll
     for (uint32_t i = 0; i < kScatterWin / 1024u; ++i)
@@ -3411,9 +3402,6 @@ __global__ __launch_bounds__(kBlock) void k_tscatter(ScatterArgs a) {
     const uint2 hc = make_uint2(a.ctl[C_RTOTAL], a.ctl[C_WTOTAL]);
     const uint2 hv = tile0 + lane < a.ntiles ? hl : hc;
     bool oob = false;
-#ifdef CRDT_TSC_NOSTORE
-    uint32_t sink = 0;
-#endif
     for (uint32_t tk = 0; tk < kScatterTiles && tile0 + tk < a.ntiles; ++tk) {
     const uint32_t tile = tile0 + tk;
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, (int)tk);
@@ -3495,11 +3483,7 @@ __global__ __launch_bounds__(kBlock) void k_tscatter(ScatterArgs a) {
             // with four byte stores each, was slower: a store instruction then touches ~30 rows'
             // lines instead of ~8, and the store path is what this loop waits on.)
             constexpr uint32_t SU = 4;
-#ifdef CRDT_TSC_NOSTEPS
-            for (uint32_t b = 0; b < (w1 & 0u); b += 64u * SU) {
-#else
             for (uint32_t b = 0; b < w1; b += 64u * SU) {
-#endif
                 uint32_t dst[SU], val[SU];
                 bool ok[SU];
 #pragma unroll
@@ -3518,11 +3502,7 @@ __global__ __launch_bounds__(kBlock) void k_tscatter(ScatterArgs a) {
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < SU; ++k) {
-#ifdef CRDT_TSC_NOSTORE
-                    if (ok[k]) sink ^= dst[k] + val[k];
-#else
                     if (ok[k]) a.text[dst[k]] = (uint8_t)val[k];
-#endif
                 }
             }
             // (clear for the next window / round; the reads above are done first)
@@ -3534,9 +3514,6 @@ __global__ __launch_bounds__(kBlock) void k_tscatter(ScatterArgs a) {
     }
     }
     if (oob) atomicOr(&a.ctl[C_ERR], 8u);
-#ifdef CRDT_TSC_NOSTORE
-    if (sink == 0x12345678u) a.text[lane] = 0;  // (keeps the work)
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------
