@@ -223,13 +223,17 @@ __device__ __forceinline__ uint64_t spread_nib16(uint32_t v) {
 __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     __shared__ uint32_t lds[kBlock / 64];
     __shared__ uint32_t jl[kScanTile / 32];
+    __shared__ uint32_t ll[kScanTile / 32];  // (Fugue) the tile's own left-child bits
     __shared__ uint2 ldoc[kBlock];  // per thread: its document {base slot, items}
     // (+64: one sink byte per lane for the branch-free ASCII stores below)
     __shared__ __attribute__((aligned(16))) uint8_t sb[kTileBytes + 64];
     const uint32_t tile = xcd_block(blockIdx.x, gridDim.x, a.xcd);
     const uint32_t t0 = tile * kScanTile, gs = t0 + threadIdx.x * kScanItems;
     const bool live = gs < a.nslots;
-    if (threadIdx.x < kScanTile / 32) jl[threadIdx.x] = 0;
+    if (threadIdx.x < kScanTile / 32) {
+        jl[threadIdx.x] = 0;
+        ll[threadIdx.x] = 0;
+    }
     // (resident batches) the tile's range of the compact nsq parent list, first: the loads of its
     // first entries are issued as soon as it arrives, behind the codepoint column, instead of a
     // gather round trip at the end of the block
@@ -409,8 +413,12 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
                 if (left) {
                     // Fugue: the parent's run node holds its left children, so the parent must
                     // head its run (k_heads cuts before every slot with a left-child bit), and
-                    // nothing more: the run goes on after it
-                    atomicOr(&a.lbits[ps >> 5], 1u << (ps & 31u));
+                    // nothing more: the run goes on after it.  A parent inside the tile (most:
+                    // text typed backwards) takes the bit in LDS
+                    if (ps / kScanTile == tile)
+                        atomicOr(&ll[(ps % kScanTile) >> 5], 1u << (ps & 31u));
+                    else
+                        atomicOr(&a.lbits[ps >> 5], 1u << (ps & 31u));
                 } else if (ps / kScanTile == tile) {
                     atomicOr(&jl[(ps % kScanTile) >> 5], 1u << (ps & 31u));
                 } else {
@@ -425,6 +433,8 @@ __global__ __launch_bounds__(kBlock) void k_classify(L0Args a) {
     // a single jump bitvector
     if (threadIdx.x < kScanTile / 32 && jl[threadIdx.x])
         atomicOr(&a.jbits[tile * (kScanTile / 32) + threadIdx.x], jl[threadIdx.x]);
+    if (threadIdx.x < kScanTile / 32 && ll[threadIdx.x])
+        atomicOr(&a.lbits[tile * (kScanTile / 32) + threadIdx.x], ll[threadIdx.x]);
     if (bad) atomicOr(&a.ctl[C_ERR], 1u);
 }
 
