@@ -845,3 +845,20 @@ def test_raw_soa_mode_rejects_fugue():
         b.set_raw(True)
     b.close()
     c.close()
+
+
+def test_one_wave_uploads_back_to_back(ctx, oracle):
+    """A one-wave upload is not waited for (Engine::upload): its merge runs behind the copies on
+    the engine's stream, and the next upload waits for them before it rewrites the pinned staging,
+    also when the staging grows and is reallocated.  Documents of different sizes, merged (text,
+    then len()) back to back in an order that grows and shrinks the staging, match the oracle
+    every time."""
+    logs = _mixed_logs(23)
+    refs = [oracle.merge(to_anchor(lg)) for lg in logs]
+    order = [1, 0, 2, 0, 1, 2, 2, 0]
+    for i in order:
+        text, dig = ctx.merge(logs[i])
+        assert text == refs[i] and dig == oracle.tree_digest(refs[i]), i
+        cps, nb, dig2 = ctx.merge_len(logs[i])
+        assert cps == len(refs[i].decode("utf-8")) and nb == len(refs[i]), i
+        assert dig2 == oracle.tree_digest(refs[i]), i
