@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 import bench  # noqa: E402
 
 STAGES = ["classify", "runs", "sortb", "count", "scan", "place", "link", "walk1", "rank", "walk2",
-          "expand", "digest", "doctree"]
+          "expand", "digest", "doctree", "text"]
 
 
 class _Batch:
@@ -78,3 +78,21 @@ def test_text_mode_prices_the_staged_walk():
     assert r["walk2"]["alg_bytes_per_launch"] == pytest.approx(0.5 * runs + 2.0 * text)
     assert r["sortb"]["alg_bytes_per_launch"] == pytest.approx((16.0 + 12 + 32 + 17) * runs)
     assert rf["batched_merge"]["frac"] > 0
+
+
+def test_text_scatter_mode_prices_the_text_kernel():
+    """text_scatter 1: k_doctree stops at the run offsets (no text in or out of it), and the text
+    stage (k_tscatter) is priced at its own in/out: the tiles' prefixes, per run its weight prefix
+    and place, the tiles' text in and the documents out."""
+    items, runs, text = 1_000_000, 30_000, 250_000
+    st = _stats({"classify": 1e5, "runs": 9e4, "doctree": 6e4, "text": 3e4, "digest": 1e4},
+                {"classify": 1, "runs": 6, "doctree": 1, "text": 1, "digest": 2}, runs=runs,
+                text=text)
+    rf = bench.roofline_fields(st, _Batch(), items, 1e-3, pmc=False)
+    slots = items + _Batch.docs
+    assert rf["rooflines"]["doctree"]["alg_bytes_per_launch"] == pytest.approx(20.0 * runs)
+    assert rf["rooflines"]["text"]["alg_bytes_per_launch"] == pytest.approx(
+        8.0 / 4096 * slots + 8.0 * runs + 2.0 * text)
+    assert rf["rooflines"]["text"]["kernel"] == "k_tscatter"
+    assert set(rf["rooflines"]) == {"classify", "runs", "doctree", "text", "digest"}
+
